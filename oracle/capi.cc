@@ -1,0 +1,245 @@
+// ORACLE / TEST INFRASTRUCTURE ONLY — never linked into the product.
+// extern "C" surface of the CPU restatement, loaded by tests/ and bench.py
+// (cpu_baseline) through ctypes.
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+
+#include "fft.h"
+#include "oracle.h"
+
+using namespace oracle;
+
+extern "C" {
+
+struct orc_set_desc {
+  uint64_t width, height, n_channels, n_pol;
+  const float* weights;
+  float pol_factor;
+  int32_t squared_joins;
+};
+
+struct orc_algo_settings {
+  double threshold, major_iteration_threshold, minor_loop_gain,
+      major_loop_gain, border_ratio, divergence_limit;
+  uint64_t max_iterations;
+  int32_t allow_negative, stop_on_negative, use_sub_minor, fast_sub_minor_loop;
+  double sub_minor_loop_gain, scale_bias;
+  uint64_t max_scales;
+  double convolution_padding;
+  int32_t shape, pad0;
+  double beam_size_in_pixels;
+  const double* scale_list;
+  uint64_t n_scale_list;
+  const uint8_t* clean_mask;
+};
+
+struct orc_result {
+  int32_t has_starting_peak;
+  float starting_peak;
+  float final_peak;
+  int32_t another_iteration_required;
+  int32_t is_diverging;
+  int32_t pad0;
+  uint64_t iteration_number;
+  uint64_t n_trace;
+};
+
+static thread_local std::string g_error;
+const char* orc_last_error() { return g_error.c_str(); }
+
+void orc_set_threads(uint64_t n) { SetNThreads(n); }
+
+int orc_find_peak(const float* img, uint64_t w, uint64_t h, int allow_neg,
+                  uint64_t start_y, uint64_t end_y, uint64_t hb, uint64_t vb,
+                  const uint8_t* mask, int simple, uint64_t* x, uint64_t* y,
+                  float* value) {
+  Peak p;
+  if (mask)
+    p = FindPeakWithMask(img, w, h, allow_neg, start_y, end_y,
+                         reinterpret_cast<const bool*>(mask), hb, vb);
+  else if (simple)
+    p = FindPeakSimple(img, w, h, allow_neg, start_y, end_y, hb, vb);
+  else
+    p = FindPeakAvx(img, w, h, allow_neg, start_y, end_y, hb, vb);
+  *x = p.x;
+  *y = p.y;
+  *value = p.value;
+  return p.has ? 1 : 0;
+}
+
+void orc_partial_subtract(float* img, const float* psf, uint64_t w, uint64_t h,
+                          uint64_t x, uint64_t y, float factor,
+                          uint64_t start_y, uint64_t end_y) {
+  PartialSubtractImage(img, psf, w, h, x, y, factor, start_y, end_y);
+}
+
+void orc_subtract(float* img, const float* psf, uint64_t w, uint64_t h,
+                  uint64_t x, uint64_t y, float factor) {
+  SubtractImage(img, psf, w, h, x, y, factor);
+}
+
+uint64_t orc_good_fft_size(uint64_t n) { return CalculateGoodFFTSize(n); }
+uint64_t orc_convolution_size(double scale, uint64_t n, double padding) {
+  return GetConvolutionSize(scale, n, padding);
+}
+
+void orc_convolve(float* image, const float* kernel, uint64_t w, uint64_t h) {
+  ConvolveCircular(image, kernel, w, h);
+}
+
+uint64_t orc_shape_function(float scale, uint64_t max_n, int shape,
+                            float* out) {
+  size_t n;
+  std::vector<float> k = MakeShapeFunction(scale, n, max_n, Shape(shape));
+  if (out) std::memcpy(out, k.data(), k.size() * sizeof(float));
+  return n;
+}
+
+float orc_kernel_peak(double scale, uint64_t max_n, int shape) {
+  return KernelPeakValue(scale, max_n, Shape(shape));
+}
+
+void orc_ms_transform(float* images, uint64_t n_images, uint64_t w, uint64_t h,
+                      float scale, int shape) {
+  std::vector<float*> l;
+  for (uint64_t i = 0; i != n_images; ++i) l.push_back(images + i * w * h);
+  MsTransform(l, w, h, scale, Shape(shape));
+}
+
+void orc_add_shape_component(float* image, uint64_t w, uint64_t h, float scale,
+                             uint64_t x, uint64_t y, float gain, int shape) {
+  AddShapeComponent(image, w, h, scale, x, y, gain, Shape(shape));
+}
+
+static SetDesc MakeDesc(const orc_set_desc* d) {
+  SetDesc desc;
+  desc.n_channels = d->n_channels;
+  desc.n_pol = d->n_pol;
+  desc.weights.assign(d->weights, d->weights + d->n_channels);
+  desc.pol_factor = d->pol_factor;
+  desc.squared_joins = d->squared_joins != 0;
+  return desc;
+}
+
+static ImageSet MakeSet(const SetDesc& desc, const orc_set_desc* d,
+                        float* data) {
+  ImageSet s;
+  s.desc = &desc;
+  s.width = d->width;
+  s.height = d->height;
+  for (uint64_t i = 0; i != d->n_channels * d->n_pol; ++i)
+    s.images.push_back(data + i * d->width * d->height);
+  return s;
+}
+
+void orc_integrate(const orc_set_desc* d, float* images, float* dest,
+                   int square) {
+  SetDesc desc = MakeDesc(d);
+  ImageSet s = MakeSet(desc, d, images);
+  if (square)
+    GetSquareIntegrated(s, dest);
+  else
+    GetLinearIntegrated(s, dest);
+}
+
+struct OrcAlgo {
+  int type;
+  AlgoSettings settings;
+  std::vector<double> scale_list;
+  size_t iteration_number = 0;
+  std::unique_ptr<MultiScale> ms;
+};
+
+static AlgoSettings MakeSettings(const orc_algo_settings* a) {
+  AlgoSettings s;
+  s.threshold = a->threshold;
+  s.major_iteration_threshold = a->major_iteration_threshold;
+  s.minor_loop_gain = a->minor_loop_gain;
+  s.major_loop_gain = a->major_loop_gain;
+  s.clean_border_ratio = a->border_ratio;
+  s.divergence_limit = a->divergence_limit;
+  s.max_iterations = a->max_iterations;
+  s.allow_negative = a->allow_negative;
+  s.stop_on_negative = a->stop_on_negative;
+  s.clean_mask = reinterpret_cast<const bool*>(a->clean_mask);
+  s.use_sub_minor_optimization = a->use_sub_minor;
+  s.fast_sub_minor_loop = a->fast_sub_minor_loop;
+  s.sub_minor_loop_gain = a->sub_minor_loop_gain;
+  s.scale_bias = a->scale_bias;
+  s.max_scales = a->max_scales;
+  s.convolution_padding = a->convolution_padding;
+  s.shape = Shape(a->shape);
+  s.beam_size_in_pixels = a->beam_size_in_pixels;
+  if (a->scale_list)
+    s.scale_list.assign(a->scale_list, a->scale_list + a->n_scale_list);
+  return s;
+}
+
+void* orc_algo_create(int type, const orc_algo_settings* a) {
+  auto* algo = new OrcAlgo();
+  algo->type = type;
+  algo->settings = MakeSettings(a);
+  if (type == 1) algo->ms = std::make_unique<MultiScale>(algo->settings);
+  return algo;
+}
+
+void orc_algo_destroy(void* h) { delete static_cast<OrcAlgo*>(h); }
+
+// Update the mutable per-call settings (threshold, max iterations, gains).
+void orc_algo_update(void* h, const orc_algo_settings* a) {
+  auto* algo = static_cast<OrcAlgo*>(h);
+  algo->settings = MakeSettings(a);
+  if (algo->ms) {
+    algo->ms->Settings() = algo->settings;
+    if (algo->ms->Settings().beam_size_in_pixels <= 0.0)
+      algo->ms->Settings().beam_size_in_pixels = 1.0;
+  }
+}
+
+int orc_algo_execute(void* h, const orc_set_desc* d, float* residual,
+                     float* model, const float* psfs, orc_result* out,
+                     uint32_t* trace, uint64_t trace_cap) {
+  try {
+    auto* algo = static_cast<OrcAlgo*>(h);
+    SetDesc desc = MakeDesc(d);
+    ImageSet res = MakeSet(desc, d, residual);
+    ImageSet mod = MakeSet(desc, d, model);
+    std::vector<const float*> psf_ptrs;
+    for (uint64_t c = 0; c != d->n_channels; ++c)
+      psf_ptrs.push_back(psfs + c * d->width * d->height);
+    std::vector<Component> tr;
+    Result r;
+    if (algo->type == 0) {
+      r = GenericCleanExecute(algo->settings, algo->iteration_number, res, mod,
+                              psf_ptrs, &tr);
+    } else {
+      algo->ms->iteration_number = algo->iteration_number;
+      r = algo->ms->Execute(res, mod, psf_ptrs, &tr);
+      algo->iteration_number = algo->ms->iteration_number;
+    }
+    out->has_starting_peak = r.has_starting_peak;
+    out->starting_peak = r.starting_peak;
+    out->final_peak = r.final_peak;
+    out->another_iteration_required = r.another_iteration_required;
+    out->is_diverging = r.is_diverging;
+    out->iteration_number = algo->iteration_number;
+    out->n_trace = tr.size();
+    if (trace) {
+      const size_t n = std::min<size_t>(tr.size(), trace_cap);
+      for (size_t i = 0; i != n; ++i) {
+        trace[3 * i] = tr[i].x;
+        trace[3 * i + 1] = tr[i].y;
+        trace[3 * i + 2] = tr[i].scale;
+      }
+    }
+    return 0;
+  } catch (std::exception& e) {
+    g_error = e.what();
+    return 1;
+  }
+}
+
+}  // extern "C"

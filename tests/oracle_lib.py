@@ -1,0 +1,238 @@
+"""ctypes bindings of the CPU restatement (oracle/build/liboracle.so).
+
+TEST INFRASTRUCTURE: imported only by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg. Never by the product package.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "build", "liboracle.so")
+REF_SO = os.path.join(ROOT, "oracle", "_ref", "libref_simple_clean.so")
+
+f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+u8p = C.c_void_p
+
+
+class SetDesc(C.Structure):
+    _fields_ = [("width", C.c_uint64), ("height", C.c_uint64),
+                ("n_channels", C.c_uint64), ("n_pol", C.c_uint64),
+                ("weights", C.c_void_p), ("pol_factor", C.c_float),
+                ("squared_joins", C.c_int32)]
+
+
+class AlgoSettings(C.Structure):
+    _fields_ = [("threshold", C.c_double), ("major_iteration_threshold", C.c_double),
+                ("minor_loop_gain", C.c_double), ("major_loop_gain", C.c_double),
+                ("border_ratio", C.c_double), ("divergence_limit", C.c_double),
+                ("max_iterations", C.c_uint64),
+                ("allow_negative", C.c_int32), ("stop_on_negative", C.c_int32),
+                ("use_sub_minor", C.c_int32), ("fast_sub_minor_loop", C.c_int32),
+                ("sub_minor_loop_gain", C.c_double), ("scale_bias", C.c_double),
+                ("max_scales", C.c_uint64), ("convolution_padding", C.c_double),
+                ("shape", C.c_int32), ("pad0", C.c_int32),
+                ("beam_size_in_pixels", C.c_double),
+                ("scale_list", C.c_void_p), ("n_scale_list", C.c_uint64),
+                ("clean_mask", C.c_void_p)]
+
+
+class Result(C.Structure):
+    _fields_ = [("has_starting_peak", C.c_int32), ("starting_peak", C.c_float),
+                ("final_peak", C.c_float), ("another_iteration_required", C.c_int32),
+                ("is_diverging", C.c_int32), ("pad0", C.c_int32),
+                ("iteration_number", C.c_uint64), ("n_trace", C.c_uint64)]
+
+
+def algo_settings(**kw):
+    """Defaults of DeconvolutionAlgorithm (cpp/algorithms/deconvolution_algorithm.h:187-199)
+    and Settings::Multiscale (cpp/settings.h:465-524)."""
+    s = AlgoSettings()
+    d = dict(threshold=0.0, major_iteration_threshold=0.0, minor_loop_gain=0.1,
+             major_loop_gain=1.0, border_ratio=0.05, divergence_limit=4.0,
+             max_iterations=500, allow_negative=1, stop_on_negative=0,
+             use_sub_minor=1, fast_sub_minor_loop=1, sub_minor_loop_gain=0.2,
+             scale_bias=0.6, max_scales=0, convolution_padding=1.1, shape=0,
+             beam_size_in_pixels=1.0)
+    d.update(kw)
+    s._keep = []
+    for k, v in d.items():
+        if k == "clean_mask":
+            continue
+        setattr(s, k, v)
+    mask = kw.get("clean_mask")
+    if mask is not None:
+        m = np.ascontiguousarray(mask, dtype=np.uint8)
+        s._keep.append(m)
+        s.clean_mask = m.ctypes.data
+    return s
+
+
+class Oracle:
+    def __init__(self, path=ORACLE_SO):
+        if not os.path.exists(path):
+            raise RuntimeError(f"oracle not built: {path} (run __graft_entry__.build())")
+        L = self.lib = C.CDLL(path)
+        L.orc_set_threads.argtypes = [C.c_uint64]
+        L.orc_find_peak.argtypes = [f32p, C.c_uint64, C.c_uint64, C.c_int, C.c_uint64,
+                                    C.c_uint64, C.c_uint64, C.c_uint64, u8p, C.c_int,
+                                    C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                    C.POINTER(C.c_float)]
+        L.orc_find_peak.restype = C.c_int
+        L.orc_partial_subtract.argtypes = [f32p, f32p, C.c_uint64, C.c_uint64, C.c_uint64,
+                                           C.c_uint64, C.c_float, C.c_uint64, C.c_uint64]
+        L.orc_subtract.argtypes = [f32p, f32p, C.c_uint64, C.c_uint64, C.c_uint64,
+                                   C.c_uint64, C.c_float]
+        L.orc_good_fft_size.argtypes = [C.c_uint64]
+        L.orc_good_fft_size.restype = C.c_uint64
+        L.orc_convolution_size.argtypes = [C.c_double, C.c_uint64, C.c_double]
+        L.orc_convolution_size.restype = C.c_uint64
+        L.orc_convolve.argtypes = [f32p, f32p, C.c_uint64, C.c_uint64]
+        L.orc_shape_function.argtypes = [C.c_float, C.c_uint64, C.c_int, C.c_void_p]
+        L.orc_shape_function.restype = C.c_uint64
+        L.orc_kernel_peak.argtypes = [C.c_double, C.c_uint64, C.c_int]
+        L.orc_kernel_peak.restype = C.c_float
+        L.orc_ms_transform.argtypes = [f32p, C.c_uint64, C.c_uint64, C.c_uint64,
+                                       C.c_float, C.c_int]
+        L.orc_add_shape_component.argtypes = [f32p, C.c_uint64, C.c_uint64, C.c_float,
+                                              C.c_uint64, C.c_uint64, C.c_float, C.c_int]
+        L.orc_integrate.argtypes = [C.POINTER(SetDesc), f32p, f32p, C.c_int]
+        L.orc_algo_create.argtypes = [C.c_int, C.POINTER(AlgoSettings)]
+        L.orc_algo_create.restype = C.c_void_p
+        L.orc_algo_destroy.argtypes = [C.c_void_p]
+        L.orc_algo_update.argtypes = [C.c_void_p, C.POINTER(AlgoSettings)]
+        L.orc_algo_execute.argtypes = [C.c_void_p, C.POINTER(SetDesc), f32p, f32p, f32p,
+                                       C.POINTER(Result), C.c_void_p, C.c_uint64]
+        L.orc_algo_execute.restype = C.c_int
+        L.orc_last_error.restype = C.c_char_p
+
+    def set_threads(self, n):
+        self.lib.orc_set_threads(n)
+
+    def find_peak(self, img, allow_negative=True, start_y=0, end_y=None, hb=0, vb=0,
+                  mask=None, simple=False):
+        img = np.ascontiguousarray(img, dtype=np.float32)
+        h, w = img.shape
+        end_y = h if end_y is None else end_y
+        x, y, v = C.c_uint64(), C.c_uint64(), C.c_float()
+        m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        has = self.lib.orc_find_peak(img, w, h, int(allow_negative), start_y, end_y, hb, vb,
+                                     None if m is None else m.ctypes.data, int(simple),
+                                     C.byref(x), C.byref(y), C.byref(v))
+        return bool(has), int(x.value), int(y.value), float(v.value)
+
+    def subtract(self, img, psf, x, y, factor):
+        h, w = img.shape
+        self.lib.orc_subtract(img, psf, w, h, x, y, factor)
+
+    def partial_subtract(self, img, psf, x, y, factor, start_y, end_y):
+        h, w = img.shape
+        self.lib.orc_partial_subtract(img, psf, w, h, x, y, factor, start_y, end_y)
+
+    def good_fft_size(self, n):
+        return self.lib.orc_good_fft_size(n)
+
+    def convolution_size(self, scale, n, padding):
+        return self.lib.orc_convolution_size(scale, n, padding)
+
+    def convolve(self, img, kernel):
+        h, w = img.shape
+        self.lib.orc_convolve(img, np.ascontiguousarray(kernel, np.float32), w, h)
+
+    def shape_function(self, scale, max_n, shape=0):
+        n = self.lib.orc_shape_function(scale, max_n, shape, None)
+        out = np.zeros((n, n), np.float32)
+        self.lib.orc_shape_function(scale, max_n, shape, out.ctypes.data)
+        return out
+
+    def kernel_peak(self, scale, max_n, shape=0):
+        return self.lib.orc_kernel_peak(scale, max_n, shape)
+
+    def ms_transform(self, imgs, scale, shape=0):
+        imgs = np.ascontiguousarray(imgs, np.float32)
+        n = 1 if imgs.ndim == 2 else imgs.shape[0]
+        h, w = imgs.shape[-2:]
+        self.lib.orc_ms_transform(imgs, n, w, h, scale, shape)
+        return imgs
+
+    def add_shape_component(self, img, scale, x, y, gain, shape=0):
+        h, w = img.shape
+        self.lib.orc_add_shape_component(img, w, h, scale, x, y, gain, shape)
+
+    @staticmethod
+    def set_desc(width, height, n_channels=1, n_pol=1, weights=None, pol_factor=1.0,
+                 squared_joins=False):
+        d = SetDesc()
+        w = np.ones(n_channels, np.float32) if weights is None else np.asarray(weights, np.float32)
+        d._w = np.ascontiguousarray(w)
+        d.width, d.height, d.n_channels, d.n_pol = width, height, n_channels, n_pol
+        d.weights = d._w.ctypes.data
+        d.pol_factor = pol_factor
+        d.squared_joins = int(squared_joins)
+        return d
+
+    def integrate(self, images, weights=None, n_pol=1, pol_factor=1.0, square=False):
+        images = np.ascontiguousarray(images, np.float32)
+        n, h, w = images.shape
+        d = self.set_desc(w, h, n // n_pol, n_pol, weights, pol_factor)
+        out = np.zeros((h, w), np.float32)
+        self.lib.orc_integrate(C.byref(d), images, out, int(square))
+        return out
+
+
+class OracleAlgorithm:
+    """A persistent DeconvolutionAlgorithm (GenericClean=0, MultiScale=1)."""
+
+    def __init__(self, oracle, kind, **settings):
+        self.o = oracle
+        self.settings = algo_settings(**settings)
+        self.h = oracle.lib.orc_algo_create(kind, C.byref(self.settings))
+
+    def update(self, **settings):
+        self.settings = algo_settings(**settings)
+        self.o.lib.orc_algo_update(self.h, C.byref(self.settings))
+
+    def execute(self, residual, model, psfs, weights=None, trace_cap=1 << 22):
+        """residual/model: (n_img, h, w) float32 updated in place; psfs (n_ch, h, w)."""
+        n, h, w = residual.shape
+        d = Oracle.set_desc(w, h, psfs.shape[0], n // psfs.shape[0], weights)
+        r = Result()
+        trace = np.zeros((trace_cap, 3), np.uint32)
+        rc = self.o.lib.orc_algo_execute(self.h, C.byref(d), residual, model,
+                                         np.ascontiguousarray(psfs, np.float32), C.byref(r),
+                                         trace.ctypes.data, trace_cap)
+        if rc != 0:
+            raise RuntimeError(self.o.lib.orc_last_error().decode())
+        return r, trace[: min(r.n_trace, trace_cap)].copy()
+
+    def __del__(self):
+        try:
+            self.o.lib.orc_algo_destroy(self.h)
+        except Exception:
+            pass
+
+
+_ORACLE = None
+
+
+def get_oracle():
+    global _ORACLE
+    if _ORACLE is None:
+        _ORACLE = Oracle()
+    return _ORACLE
+
+
+def get_ref():
+    """The reference's own simple_clean.cc / fft_size_calculations.h, compiled
+    from /root/reference by oracle/Makefile (None if it was not built)."""
+    if not os.path.exists(REF_SO):
+        return None
+    L = C.CDLL(REF_SO)
+    L.ref_partial_subtract.argtypes = [f32p, f32p, C.c_uint64, C.c_uint64, C.c_uint64,
+                                       C.c_uint64, C.c_float, C.c_uint64, C.c_uint64]
+    L.ref_good_fft_size.argtypes = [C.c_uint64]
+    L.ref_good_fft_size.restype = C.c_uint64
+    L.ref_convolution_size.argtypes = [C.c_double, C.c_uint64, C.c_double]
+    L.ref_convolution_size.restype = C.c_uint64
+    return L
