@@ -1,0 +1,299 @@
+/*
+ * rdl_hip.h — C-ABI of the MI355X-native Radler CLEAN engine (librdl_hip.so).
+ *
+ * Plain pointers and sizes only: no C++ or torch types cross this boundary.
+ * Device pointers ("d_" prefix) are addresses returned by rdl_malloc (or any
+ * hipMalloc'd memory on the session's device). Every call is ordered on the
+ * session's HIP stream; calls that return values to the host (peaks, loop
+ * results) synchronise that stream. All functions return RDL_OK (0) or an
+ * error code; rdl_last_error() gives the thread's last message. The host C++
+ * library (libradler_amd) wraps these calls and rethrows std::runtime_error
+ * where the reference throws.
+ *
+ * Each entry point cites the reference interface it replaces
+ * (paths relative to ska-sdp-func-radler/, snapshot 2025-04-10).
+ */
+#ifndef RDL_HIP_H_
+#define RDL_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RDL_OK 0
+#define RDL_ERR_ARG 1
+#define RDL_ERR_HIP 2
+#define RDL_ERR_FFT 3
+#define RDL_ERR_TIMEOUT 4
+#define RDL_ERR_UNSUPPORTED 5
+
+/* Maximum images in one ImageSet handled by the fused kernels
+ * (channels x polarizations). */
+#define RDL_MAX_IMAGES 64
+
+typedef struct rdl_session rdl_session;
+typedef struct rdl_fft rdl_fft;
+typedef struct rdl_subminor rdl_subminor;
+
+/* ---------------------------------------------------------------- runtime */
+const char* rdl_last_error(void);
+const char* rdl_version(void);
+int rdl_device_count(int* count);
+int rdl_session_create(int device, rdl_session** out);
+int rdl_session_destroy(rdl_session* s);
+int rdl_session_sync(rdl_session* s);
+/* hipStream_t of the session, for callers that record events on it. */
+void* rdl_session_stream(rdl_session* s);
+
+int rdl_malloc(rdl_session* s, size_t bytes, void** d_out);
+int rdl_free(rdl_session* s, void* d_ptr);
+int rdl_memcpy_h2d(rdl_session* s, void* d_dst, const void* h_src, size_t bytes);
+int rdl_memcpy_d2h(rdl_session* s, void* h_dst, const void* d_src, size_t bytes);
+int rdl_memcpy_d2d(rdl_session* s, void* d_dst, const void* d_src, size_t bytes);
+int rdl_memset_zero(rdl_session* s, void* d_dst, size_t bytes);
+
+/* Per-kernel device timing (HIP events around every launch of a kernel
+ * family on the session stream). Used by bench.py's roofline. */
+int rdl_timing_enable(rdl_session* s, int enable);
+/* Returns accumulated milliseconds and launch count for a kernel family name
+ * ("find_peak", "subminor_loop", "fft", "spectrum_multiply", ...). */
+int rdl_timing_get(rdl_session* s, const char* family, double* ms,
+                   uint64_t* launches, double* bytes);
+int rdl_timing_reset(rdl_session* s);
+
+/* ------------------------------------------------------------ peak finder */
+typedef struct {
+  float value;     /* signed image value at (x, y) */
+  uint32_t x, y;
+  int32_t found;   /* 0 = no qualifying pixel (Simple / FindWithMask) */
+} rdl_peak;
+
+/* Replaces math::peak_finder::Find / Avx<bool> / Simple / FindWithMask
+ * (cpp/math/peak_finder.h:80-127, peak_finder.cc:19-56, 97-131, 199-253).
+ * Box x in [h_border, w-h_border), y in [max(start_y,v_border),
+ * min(end_y,h-v_border)); strict '>' from FLT_MIN, first row-major index on
+ * ties, NaN never selected, value = signed pixel. d_mask (uint8, may be NULL)
+ * selects FindWithMask. avx_semantics=1 reproduces the x86 default Avx<>
+ * path: with no qualifying pixel it returns (0,0) and image[0] as found. */
+int rdl_find_peak(rdl_session* s, const float* d_image, uint32_t width,
+                  uint32_t height, uint32_t start_y, uint32_t end_y,
+                  uint32_t h_border, uint32_t v_border, int allow_negative,
+                  const uint8_t* d_mask, int avx_semantics, rdl_peak* out);
+
+/* Sum of squares in double (ThreadedDeconvolutionTools::RMS,
+ * cpp/algorithms/threaded_deconvolution_tools.h:40-44; logging only). */
+int rdl_rms(rdl_session* s, const float* d_image, size_t n, float* out);
+
+/* --------------------------------------------------------- PSF subtraction */
+/* Replaces ThreadedDeconvolutionTools::SubtractImage ->
+ * simple_clean::PartialSubtractImage (threaded_deconvolution_tools.cc:18-28,
+ * simple_clean.cc:96-131): image -= psf(shifted to x,y) * factor over the
+ * reference's window, one fused multiply-add per pixel. */
+int rdl_subtract_psf(rdl_session* s, float* d_image, const float* d_psf,
+                     uint32_t width, uint32_t height, uint32_t x, uint32_t y,
+                     float factor);
+
+/* ------------------------------------------------------ ImageSet integration */
+#define RDL_INTEGRATE_LINEAR 0        /* GetLinearIntegratedWithNormalChannels */
+#define RDL_INTEGRATE_SQUARE 1        /* GetSquareIntegratedWithNormalChannels */
+#define RDL_INTEGRATE_SQUARED_JOINS 2 /* GetSquareIntegratedWithSquaredChannels */
+typedef struct {
+  uint32_t n_images;       /* images in the set, index = channel*n_pol + pol */
+  uint32_t n_pol;
+  uint32_t n_channels;
+  uint32_t mode;           /* RDL_INTEGRATE_* */
+  uint32_t copy_fast_path; /* image_set.cc:425-430 / :289-301 (1 image) */
+  float weights[RDL_MAX_IMAGES]; /* channel weight of each image; 0 skips */
+  /* LINEAR: float(pol_factor/sum w); SQUARE with 1 channel: sqrtf(pol_factor);
+   * SQUARE with >1 channel: float(sqrtf(pol_factor)/sum w);
+   * SQUARED_JOINS: float(sqrt(pol_factor/sum w)) (0 when sum w == 0). */
+  float factor;
+} rdl_integration;
+
+/* Replaces ImageSet::GetLinearIntegrated / GetSquareIntegrated
+ * (cpp/image_set.cc:309-462): images are n_images consecutive planes of
+ * `n` floats each. Summation order and FMA placement follow the reference. */
+int rdl_integrate(rdl_session* s, const rdl_integration* integ,
+                  const float* d_images, size_t n, float* d_dest);
+
+/* dest = a*alpha (assign=1) or dest = fma(a, alpha, dest) (assign=0);
+ * aocommon Image::AddWithFactor / operator*= used by ImageSet::LoadAndAverage
+ * and GetIntegratedPsf (cpp/image_set.cc:105-140, 499-530). */
+int rdl_axpy(rdl_session* s, float* d_dest, const float* d_a, size_t n,
+             float alpha, int assign);
+int rdl_scale(rdl_session* s, float* d_dest, size_t n, float alpha);
+/* dest += a (model accumulation, multiscale_algorithm.cc:457-460). */
+int rdl_add(rdl_session* s, float* d_dest, const float* d_a, size_t n);
+
+/* Exact median of values (or of |values - center| when use_center) by radix
+ * select on the float order; aocommon Image::MedianAndStdDevFromMAD, used by
+ * Radler::Perform (cpp/radler.cc:162-166). */
+int rdl_median(rdl_session* s, const float* d_values, size_t n, int use_center,
+               float center, float* out);
+
+/* ---------------------------------------------------------------- Högbom */
+typedef struct {
+  uint32_t width, height;
+  uint32_t n_images;
+  uint32_t n_pol;          /* psf index of image i = i / n_pol */
+  rdl_integration integ;   /* square integration used between iterations */
+  float gain;              /* minor loop gain */
+  float threshold;         /* first threshold (generic_clean.cc:99-112) */
+  float initial_max;       /* |peak| at start, for the divergence test */
+  float divergence_limit;
+  uint64_t iteration_start, max_iterations;
+  int32_t allow_negative, stop_on_negative;
+  uint32_t h_border, v_border;
+  const uint8_t* d_mask;   /* may be NULL */
+  /* starting peak, from a prior rdl_find_peak on the integrated image */
+  uint32_t start_x, start_y;
+  float start_value;
+  int32_t start_found;
+} rdl_hogbom_params;
+
+typedef struct {
+  uint64_t iteration;      /* IterationNumber() after the loop */
+  float peak;              /* final signed integrated peak */
+  uint32_t x, y;
+  int32_t found;
+  int32_t diverging;
+} rdl_hogbom_result;
+
+/* Replaces the Högbom branch of GenericClean::ExecuteMajorIteration
+ * (cpp/algorithms/generic_clean.cc:163-207): per iteration gather N_img peak
+ * values, model += gain*v, subtract PSF_i, square-integrate, find peak,
+ * divergence test. The loop runs device-resident; h_trace (may be NULL)
+ * receives x,y per component (2 x uint32 each, up to trace_cap). */
+int rdl_hogbom_run(rdl_session* s, float* d_residuals, float* d_models,
+                   const float* d_psfs, const rdl_hogbom_params* p,
+                   rdl_hogbom_result* out, uint32_t* h_trace,
+                   uint64_t trace_cap);
+
+/* ------------------------------------------------------- sub-minor loop */
+typedef struct {
+  uint32_t width, height;  /* image size (psf size equals image size) */
+  uint32_t n_images, n_pol;
+  rdl_integration integ;   /* linear integration (subminor_loop.cc:17) */
+  uint32_t h_border, v_border;
+  int32_t allow_negative, stop_on_negative;
+  float threshold;         /* SubMinorLoop::_threshold */
+  float gain;
+  float divergence_limit;
+  uint64_t iteration_start, max_iterations;
+  const uint8_t* d_mask;   /* may be NULL */
+} rdl_subminor_params;
+
+typedef struct {
+  uint64_t n_selected;
+  uint64_t iteration;      /* CurrentIteration() after Run() */
+  int32_t has_peak;        /* OptionalNumber set */
+  float peak;              /* signed integrated value */
+  int32_t diverging;
+  float flux_cleaned;
+} rdl_subminor_result;
+
+int rdl_subminor_create(rdl_session* s, rdl_subminor** out);
+int rdl_subminor_destroy(rdl_subminor* h);
+
+/* Replaces SubMinorLoop::Run (cpp/algorithms/subminor_loop.cc:38-117) with
+ * findPeakPositions/MakeSets (:119-184) and GetMaxComponent (:13-36):
+ * stream-compaction of |integrated| >= threshold in the border box (and
+ * mask), then a persistent device loop over the selected set.
+ * d_residuals: n_images planes (the convolved residual set);
+ * d_psfs: n_images/n_pol planes (twice convolved PSFs).
+ * h_trace (may be NULL) receives x,y per component. */
+int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
+                     const float* d_psfs, const rdl_subminor_params* p,
+                     rdl_subminor_result* out, uint32_t* h_trace,
+                     uint64_t trace_cap);
+
+/* SubMinorLoop::GetFullIndividualModel (subminor_loop.cc:186-193), fused
+ * with the caller's use: mode 0 writes the model of image `image_index` into
+ * a zeroed dest (dest_w x dest_h, placed at offset ox,oy — Image::Untrim);
+ * mode 1 adds it (model += scratch, generic_clean.cc:145-148). */
+int rdl_subminor_model(rdl_subminor* h, uint32_t image_index, float* d_dest,
+                       uint32_t dest_w, uint32_t dest_h, uint32_t ox,
+                       uint32_t oy, int mode);
+/* Selected positions (packed y<<16|x) and per-image model values of the last
+ * run, copied to host (UpdateComponentList / UpdateAutoMask inputs). */
+int rdl_subminor_get(rdl_subminor* h, uint32_t* h_positions, float* h_models,
+                     uint64_t capacity);
+
+/* ---------------------------------------------------- FFT convolution */
+/* Real 2-D transform pair at width x height (rocFFT, single precision).
+ * Spectra are (width/2+1) x height complex float. */
+int rdl_fft_create(rdl_session* s, uint32_t width, uint32_t height,
+                   rdl_fft** out);
+int rdl_fft_destroy(rdl_fft* f);
+size_t rdl_fft_spectrum_bytes(const rdl_fft* f);
+int rdl_fft_forward(rdl_fft* f, const float* d_in, void* d_spectrum);
+/* Unnormalised inverse; d_spectrum is destroyed. */
+int rdl_fft_inverse(rdl_fft* f, void* d_spectrum, float* d_out);
+/* dst = a * b * scale, complex, n_complex elements. */
+int rdl_spectrum_multiply(rdl_session* s, void* d_dst, const void* d_a,
+                          const void* d_b, size_t n_complex, float scale);
+/* Circular convolution of d_image (in place) with a kernel spectrum:
+ * schaapcommon::math::Convolve contract (multiscale_transforms.cc:16-20,
+ * subminor_loop.cc:210-211); normalised. d_work: spectrum-sized scratch. */
+int rdl_fft_convolve(rdl_fft* f, float* d_image, const void* d_kernel_spectrum,
+                     void* d_work);
+
+/* schaapcommon::math::PrepareSmallConvolutionKernel: zero d_dest (w x h) and
+ * wrap an n x n host kernel with its centre at the origin. */
+int rdl_prepare_small_kernel(rdl_session* s, float* d_dest, uint32_t width,
+                             uint32_t height, const float* h_kernel,
+                             uint32_t n);
+/* Image::Untrim + schaapcommon::math::PrepareConvolutionKernel fused
+ * (subminor_loop.cc:199-202): centre a w x h image in a zeroed pw x ph
+ * plane, then quadrant-shift so its (pw/2, ph/2) lands at the origin. */
+int rdl_prepare_psf_kernel(rdl_session* s, float* d_dest, uint32_t pw,
+                           uint32_t ph, const float* d_psf, uint32_t width,
+                           uint32_t height);
+/* Image::Trim + `residual -= trimmed` (subminor_loop.cc:214-217). */
+int rdl_trim_subtract(rdl_session* s, float* d_residual, uint32_t width,
+                      uint32_t height, const float* d_padded, uint32_t pw,
+                      uint32_t ph);
+/* Image::Untrim / Trim as plain copies (ParallelDeconvolution PSF resize). */
+int rdl_untrim(rdl_session* s, float* d_dest, uint32_t pw, uint32_t ph,
+               const float* d_src, uint32_t width, uint32_t height);
+int rdl_trim(rdl_session* s, float* d_dest, uint32_t width, uint32_t height,
+             const float* d_src, uint32_t pw, uint32_t ph);
+
+/* multiscale::MultiScaleTransforms::AddShapeComponent
+ * (multiscale_transforms.h:62-89): image += kernel(n x n host) * gain at x,y. */
+int rdl_add_shape_component(rdl_session* s, float* d_image, uint32_t width,
+                            uint32_t height, const float* h_kernel, uint32_t n,
+                            uint32_t x, uint32_t y, float gain);
+
+/* -------------------------------------------------- IUWT (à-trous) */
+/* IuwtDecomposition::DecomposeMt / Recompose
+ * (cpp/algorithms/iuwt/iuwt_decomposition.cc:9-237, .h:121-261).
+ * d_coeffs: n_scales+1 planes (detail scales then the residual approx).
+ * d_scratch: 2 planes. */
+int rdl_iuwt_decompose(rdl_session* s, const float* d_input, uint32_t width,
+                       uint32_t height, uint32_t n_scales, float* d_coeffs,
+                       float* d_scratch, int include_residual);
+int rdl_iuwt_recompose(rdl_session* s, const float* d_coeffs, uint32_t width,
+                       uint32_t height, uint32_t n_scales, float* d_out,
+                       float* d_scratch, int include_residual);
+
+/* -------------------------------------------- multi-GPU (RCCL over xGMI) */
+/* Size of an RCCL unique id blob; rank 0 creates it and the host side
+ * distributes it (torch.distributed / MPI). */
+int rdl_comm_id_size(void);
+int rdl_comm_get_unique_id(void* h_id);
+int rdl_comm_init(rdl_session* s, int n_ranks, int rank, const void* h_id);
+int rdl_comm_destroy(rdl_session* s);
+/* Signed max of one float over all ranks (ParallelDeconvolution start peak,
+ * cpp/algorithms/parallel_deconvolution.cc:592-603). */
+int rdl_comm_allreduce_max(rdl_session* s, float* value);
+int rdl_comm_allreduce_sum_u64(rdl_session* s, uint64_t* value);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RDL_HIP_H_ */

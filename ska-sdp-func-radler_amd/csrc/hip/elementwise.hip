@@ -1,0 +1,146 @@
+// ImageSet integration and elementwise helpers (cpp/image_set.cc,
+// aocommon Image arithmetic as used by the reference), plus the shape-kernel
+// stamp used by the non-fast multiscale loop. All HBM-streaming, float4 wide
+// where the plane size allows.
+#include "rdl_internal.h"
+
+namespace rdl {
+
+__global__ __launch_bounds__(256) void IntegrateKernel(rdl_integration g,
+                                                       const float* images,
+                                                       size_t n, float* dest) {
+  for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n;
+       i += size_t(gridDim.x) * blockDim.x) {
+    dest[i] = IntegratePixel(g, [&](uint32_t k) { return images[k * n + i]; });
+  }
+}
+
+__global__ __launch_bounds__(256) void AxpyKernel(float* dest, const float* a,
+                                                  size_t n, float alpha,
+                                                  int assign) {
+  for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n;
+       i += size_t(gridDim.x) * blockDim.x) {
+    dest[i] = assign ? a[i] * alpha : __builtin_fmaf(a[i], alpha, dest[i]);
+  }
+}
+
+__global__ __launch_bounds__(256) void ScaleKernel(float* dest, size_t n,
+                                                   float alpha) {
+  for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n;
+       i += size_t(gridDim.x) * blockDim.x)
+    dest[i] *= alpha;
+}
+
+__global__ __launch_bounds__(256) void AddKernel(float* dest, const float* a,
+                                                 size_t n) {
+  const size_t n4 = n / 4;
+  float4* d4 = reinterpret_cast<float4*>(dest);
+  const float4* a4 = reinterpret_cast<const float4*>(a);
+  for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n4;
+       i += size_t(gridDim.x) * blockDim.x) {
+    float4 x = d4[i];
+    const float4 y = a4[i];
+    x.x += y.x;
+    x.y += y.y;
+    x.z += y.z;
+    x.w += y.w;
+    d4[i] = x;
+  }
+  for (size_t i = n4 * 4 + blockIdx.x * size_t(blockDim.x) + threadIdx.x;
+       i < n; i += size_t(gridDim.x) * blockDim.x)
+    dest[i] += a[i];
+}
+
+// multiscale_transforms.h:62-89: image[yi][xi] += kernel * gain over the
+// clipped n x n window centred at (x, y); contracted to FMA by the reference.
+__global__ void AddShapeKernel(float* image, uint32_t width, const float* k,
+                               uint32_t n, uint32_t x, uint32_t y,
+                               uint32_t left, uint32_t top, uint32_t right,
+                               uint32_t bottom, float gain) {
+  const uint32_t xi = left + blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t yi = top + blockIdx.y;
+  if (xi >= right || yi >= bottom) return;
+  const float kv = k[(yi + n / 2 - y) * n + xi + n / 2 - x];
+  float& px = image[size_t(yi) * width + xi];
+  px = __builtin_fmaf(kv, gain, px);
+}
+
+inline unsigned GridFor(size_t n) {
+  return unsigned(std::min<size_t>(8192, std::max<size_t>(1, DivUp(n, 256))));
+}
+
+}  // namespace rdl
+
+extern "C" {
+
+int rdl_integrate(rdl_session* s, const rdl_integration* integ,
+                  const float* d_images, size_t n, float* d_dest) {
+  RDL_ARG_CHECK(s && integ && d_images && d_dest, "NULL argument");
+  RDL_ARG_CHECK(integ->n_images >= 1 && integ->n_images <= RDL_MAX_IMAGES,
+                "n_images out of range");
+  if (n == 0) return RDL_OK;
+  rdl::ScopedTiming t(s, "integrate", double(n) * 4.0 * (integ->n_images + 1));
+  rdl::IntegrateKernel<<<rdl::GridFor(n), 256, 0, s->stream>>>(*integ, d_images,
+                                                                n, d_dest);
+  RDL_HIP_CHECK(hipGetLastError());
+  return RDL_OK;
+}
+
+int rdl_axpy(rdl_session* s, float* d_dest, const float* d_a, size_t n,
+             float alpha, int assign) {
+  RDL_ARG_CHECK(s && d_dest && d_a, "NULL argument");
+  if (n == 0) return RDL_OK;
+  rdl::ScopedTiming t(s, "axpy", double(n) * (assign ? 8.0 : 12.0));
+  rdl::AxpyKernel<<<rdl::GridFor(n), 256, 0, s->stream>>>(d_dest, d_a, n, alpha,
+                                                           assign);
+  RDL_HIP_CHECK(hipGetLastError());
+  return RDL_OK;
+}
+
+int rdl_scale(rdl_session* s, float* d_dest, size_t n, float alpha) {
+  RDL_ARG_CHECK(s && d_dest, "NULL argument");
+  if (n == 0) return RDL_OK;
+  rdl::ScaleKernel<<<rdl::GridFor(n), 256, 0, s->stream>>>(d_dest, n, alpha);
+  RDL_HIP_CHECK(hipGetLastError());
+  return RDL_OK;
+}
+
+int rdl_add(rdl_session* s, float* d_dest, const float* d_a, size_t n) {
+  RDL_ARG_CHECK(s && d_dest && d_a, "NULL argument");
+  RDL_ARG_CHECK(reinterpret_cast<uintptr_t>(d_dest) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(d_a) % 16 == 0,
+                "rdl_add needs 16-byte aligned planes");
+  if (n == 0) return RDL_OK;
+  rdl::ScopedTiming t(s, "add", double(n) * 12.0);
+  rdl::AddKernel<<<rdl::GridFor(n / 4 + 1), 256, 0, s->stream>>>(d_dest, d_a,
+                                                                  n);
+  RDL_HIP_CHECK(hipGetLastError());
+  return RDL_OK;
+}
+
+int rdl_add_shape_component(rdl_session* s, float* d_image, uint32_t width,
+                            uint32_t height, const float* h_kernel, uint32_t n,
+                            uint32_t x, uint32_t y, float gain) {
+  RDL_ARG_CHECK(s && d_image && h_kernel && n > 0, "bad argument");
+  RDL_ARG_CHECK(x < width && y < height, "component outside the image");
+  const size_t kbytes = size_t(n) * n * sizeof(float);
+  RDL_ARG_CHECK(kbytes <= (1 << 16), "shape kernel larger than 64 KiB scratch");
+  // d_small holds the kernel for the duration of the launch (stream ordered)
+  RDL_HIP_CHECK(hipMemcpyAsync(s->d_small, h_kernel, kbytes,
+                               hipMemcpyHostToDevice, s->stream));
+  const uint32_t left = x > n / 2 ? x - n / 2 : 0;
+  const uint32_t top = y > n / 2 ? y - n / 2 : 0;
+  const uint32_t right = std::min(x + (n + 1) / 2, width);
+  const uint32_t bottom = std::min(y + (n + 1) / 2, height);
+  if (right > left && bottom > top) {
+    dim3 grid(rdl::DivUp(right - left, 64), bottom - top);
+    rdl::AddShapeKernel<<<grid, 64, 0, s->stream>>>(
+        d_image, width, static_cast<const float*>(s->d_small), n, x, y, left,
+        top, right, bottom, gain);
+    RDL_HIP_CHECK(hipGetLastError());
+  }
+  RDL_HIP_CHECK(hipStreamSynchronize(s->stream));
+  return RDL_OK;
+}
+
+}  // extern "C"

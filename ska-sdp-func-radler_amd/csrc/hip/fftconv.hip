@@ -1,0 +1,308 @@
+// FFT convolution (rocFFT) and the kernel-preparation passes that replace
+// schaapcommon::math::{PrepareSmallConvolutionKernel, PrepareConvolutionKernel,
+// Convolve} and aocommon Image::{Untrim, Trim} (call sites:
+// cpp/algorithms/multiscale/multiscale_transforms.cc:9-21,
+// cpp/algorithms/subminor_loop.cc:195-218).
+//
+// rocFFT is used only for the transforms themselves (real 2-D, single
+// precision, not-in-place). The pointwise spectrum product, the kernel
+// placement and the trim/subtract epilogue are hand-written streaming
+// kernels; callers cache kernel spectra so one convolution costs one forward
+// transform, one multiply pass and one inverse transform.
+#include <rocfft/rocfft.h>
+
+#include "rdl_internal.h"
+
+namespace {
+std::once_flag g_rocfft_once;
+}
+
+struct rdl_fft {
+  rdl_session* s = nullptr;
+  uint32_t width = 0, height = 0;
+  rocfft_plan fwd = nullptr, inv = nullptr;
+  rocfft_execution_info info_fwd = nullptr, info_inv = nullptr;
+  void* work = nullptr;
+  size_t work_bytes = 0;
+};
+
+namespace rdl {
+
+#define RDL_FFT_CHECK(expr)                                         \
+  do {                                                              \
+    rocfft_status _st = (expr);                                     \
+    if (_st != rocfft_status_success) {                             \
+      ::rdl::SetError(std::string(#expr) + " failed: rocfft status " + \
+                      std::to_string(int(_st)));                    \
+      return RDL_ERR_FFT;                                           \
+    }                                                               \
+  } while (0)
+
+__global__ __launch_bounds__(256) void SpectrumMultiply(float2* dst,
+                                                        const float2* a,
+                                                        const float2* b,
+                                                        size_t n, float scale) {
+  for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n;
+       i += size_t(gridDim.x) * blockDim.x) {
+    const float2 x = a[i], y = b[i];
+    float2 r;
+    r.x = (x.x * y.x - x.y * y.y) * scale;
+    r.y = (x.x * y.y + x.y * y.x) * scale;
+    dst[i] = r;
+  }
+}
+
+// Zero + wrap an n x n kernel (centre n/2) so its centre sits at the origin.
+__global__ __launch_bounds__(256) void PlaceSmallKernel(float* dest,
+                                                        uint32_t width,
+                                                        uint32_t height,
+                                                        const float* k,
+                                                        uint32_t n) {
+  const size_t total = size_t(n) * n;
+  for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < total;
+       i += size_t(gridDim.x) * blockDim.x) {
+    const uint32_t kx = i % n, ky = i / n;
+    int64_t dx = int64_t(kx) - int64_t(n / 2);
+    int64_t dy = int64_t(ky) - int64_t(n / 2);
+    if (dx < 0) dx += width;
+    if (dy < 0) dy += height;
+    dest[size_t(dy) * width + dx] = k[i];
+  }
+}
+
+// dest(x, y) of the pw x ph plane = untrimmed(sx, sy) with
+// sx = (x + pw/2) % pw, sy = (y + ph/2) % ph, where untrimmed is the w x h
+// image centred at offset ((pw-w)/2, (ph-h)/2) in a zero plane.
+__global__ __launch_bounds__(256) void PreparePsfKernel(float* dest,
+                                                        uint32_t pw,
+                                                        uint32_t ph,
+                                                        const float* psf,
+                                                        uint32_t w, uint32_t h) {
+  const uint32_t ox = (pw - w) / 2, oy = (ph - h) / 2;
+  const size_t total = size_t(pw) * ph;
+  for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < total;
+       i += size_t(gridDim.x) * blockDim.x) {
+    const uint32_t x = i % pw, y = i / pw;
+    const uint32_t sx = (x + pw / 2) % pw, sy = (y + ph / 2) % ph;
+    float v = 0.0f;
+    if (sx >= ox && sx < ox + w && sy >= oy && sy < oy + h)
+      v = psf[size_t(sy - oy) * w + (sx - ox)];
+    dest[i] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void TrimSubtract(float* residual,
+                                                    uint32_t w, uint32_t h,
+                                                    const float* padded,
+                                                    uint32_t pw, uint32_t ph) {
+  const uint32_t ox = (pw - w) / 2, oy = (ph - h) / 2;
+  const size_t total = size_t(w) * h;
+  for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < total;
+       i += size_t(gridDim.x) * blockDim.x) {
+    const uint32_t x = i % w, y = i / w;
+    residual[i] -= padded[size_t(y + oy) * pw + x + ox];
+  }
+}
+
+__global__ __launch_bounds__(256) void UntrimKernel(float* dest, uint32_t pw,
+                                                    uint32_t ph,
+                                                    const float* src,
+                                                    uint32_t w, uint32_t h) {
+  const uint32_t ox = (pw - w) / 2, oy = (ph - h) / 2;
+  const size_t total = size_t(pw) * ph;
+  for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < total;
+       i += size_t(gridDim.x) * blockDim.x) {
+    const uint32_t x = i % pw, y = i / pw;
+    float v = 0.0f;
+    if (x >= ox && x < ox + w && y >= oy && y < oy + h)
+      v = src[size_t(y - oy) * w + (x - ox)];
+    dest[i] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void TrimKernel(float* dest, uint32_t w,
+                                                  uint32_t h, const float* src,
+                                                  uint32_t pw, uint32_t ph) {
+  const uint32_t ox = (pw - w) / 2, oy = (ph - h) / 2;
+  const size_t total = size_t(w) * h;
+  for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < total;
+       i += size_t(gridDim.x) * blockDim.x) {
+    const uint32_t x = i % w, y = i / w;
+    dest[i] = src[size_t(y + oy) * pw + x + ox];
+  }
+}
+
+inline unsigned Grid(size_t n) {
+  return unsigned(std::min<size_t>(16384, std::max<size_t>(1, DivUp(n, 256))));
+}
+
+}  // namespace rdl
+
+extern "C" {
+
+int rdl_fft_create(rdl_session* s, uint32_t width, uint32_t height,
+                   rdl_fft** out) {
+  RDL_ARG_CHECK(s && out, "NULL argument");
+  RDL_ARG_CHECK(width >= 2 && height >= 1, "bad FFT size");
+  std::call_once(g_rocfft_once, [] { rocfft_setup(); });
+  RDL_HIP_CHECK(hipSetDevice(s->device));
+  auto f = std::make_unique<rdl_fft>();
+  f->s = s;
+  f->width = width;
+  f->height = height;
+  size_t lengths[2] = {width, height};  // fastest dimension first
+  RDL_FFT_CHECK(rocfft_plan_create(&f->fwd, rocfft_placement_notinplace,
+                                   rocfft_transform_type_real_forward,
+                                   rocfft_precision_single, 2, lengths, 1,
+                                   nullptr));
+  RDL_FFT_CHECK(rocfft_plan_create(&f->inv, rocfft_placement_notinplace,
+                                   rocfft_transform_type_real_inverse,
+                                   rocfft_precision_single, 2, lengths, 1,
+                                   nullptr));
+  size_t w1 = 0, w2 = 0;
+  RDL_FFT_CHECK(rocfft_plan_get_work_buffer_size(f->fwd, &w1));
+  RDL_FFT_CHECK(rocfft_plan_get_work_buffer_size(f->inv, &w2));
+  f->work_bytes = std::max(w1, w2);
+  if (f->work_bytes) RDL_HIP_CHECK(hipMalloc(&f->work, f->work_bytes));
+  RDL_FFT_CHECK(rocfft_execution_info_create(&f->info_fwd));
+  RDL_FFT_CHECK(rocfft_execution_info_create(&f->info_inv));
+  RDL_FFT_CHECK(rocfft_execution_info_set_stream(f->info_fwd, s->stream));
+  RDL_FFT_CHECK(rocfft_execution_info_set_stream(f->info_inv, s->stream));
+  if (f->work_bytes) {
+    RDL_FFT_CHECK(
+        rocfft_execution_info_set_work_buffer(f->info_fwd, f->work, f->work_bytes));
+    RDL_FFT_CHECK(
+        rocfft_execution_info_set_work_buffer(f->info_inv, f->work, f->work_bytes));
+  }
+  *out = f.release();
+  return RDL_OK;
+}
+
+int rdl_fft_destroy(rdl_fft* f) {
+  if (!f) return RDL_OK;
+  (void)hipStreamSynchronize(f->s->stream);
+  if (f->fwd) rocfft_plan_destroy(f->fwd);
+  if (f->inv) rocfft_plan_destroy(f->inv);
+  if (f->info_fwd) rocfft_execution_info_destroy(f->info_fwd);
+  if (f->info_inv) rocfft_execution_info_destroy(f->info_inv);
+  if (f->work) (void)hipFree(f->work);
+  delete f;
+  return RDL_OK;
+}
+
+size_t rdl_fft_spectrum_bytes(const rdl_fft* f) {
+  return f ? size_t(f->width / 2 + 1) * f->height * 2 * sizeof(float) : 0;
+}
+
+int rdl_fft_forward(rdl_fft* f, const float* d_in, void* d_spectrum) {
+  RDL_ARG_CHECK(f && d_in && d_spectrum, "NULL argument");
+  const double bytes = double(f->width) * f->height * 4.0 +
+                       double(rdl_fft_spectrum_bytes(f));
+  rdl::ScopedTiming t(f->s, "fft", bytes);
+  void* in[1] = {const_cast<float*>(d_in)};
+  void* out[1] = {d_spectrum};
+  RDL_FFT_CHECK(rocfft_execute(f->fwd, in, out, f->info_fwd));
+  return RDL_OK;
+}
+
+int rdl_fft_inverse(rdl_fft* f, void* d_spectrum, float* d_out) {
+  RDL_ARG_CHECK(f && d_out && d_spectrum, "NULL argument");
+  const double bytes = double(f->width) * f->height * 4.0 +
+                       double(rdl_fft_spectrum_bytes(f));
+  rdl::ScopedTiming t(f->s, "fft", bytes);
+  void* in[1] = {d_spectrum};
+  void* out[1] = {d_out};
+  RDL_FFT_CHECK(rocfft_execute(f->inv, in, out, f->info_inv));
+  return RDL_OK;
+}
+
+int rdl_spectrum_multiply(rdl_session* s, void* d_dst, const void* d_a,
+                          const void* d_b, size_t n_complex, float scale) {
+  RDL_ARG_CHECK(s && d_dst && d_a && d_b, "NULL argument");
+  if (n_complex == 0) return RDL_OK;
+  rdl::ScopedTiming t(s, "spectrum_multiply", double(n_complex) * 24.0);
+  rdl::SpectrumMultiply<<<rdl::Grid(n_complex), 256, 0, s->stream>>>(
+      static_cast<float2*>(d_dst), static_cast<const float2*>(d_a),
+      static_cast<const float2*>(d_b), n_complex, scale);
+  RDL_HIP_CHECK(hipGetLastError());
+  return RDL_OK;
+}
+
+int rdl_fft_convolve(rdl_fft* f, float* d_image, const void* d_kernel_spectrum,
+                     void* d_work) {
+  RDL_ARG_CHECK(f && d_image && d_kernel_spectrum && d_work, "NULL argument");
+  RDL_TRY(rdl_fft_forward(f, d_image, d_work));
+  const size_t nc = size_t(f->width / 2 + 1) * f->height;
+  RDL_TRY(rdl_spectrum_multiply(f->s, d_work, d_work, d_kernel_spectrum, nc,
+                                1.0f / float(double(f->width) * f->height)));
+  RDL_TRY(rdl_fft_inverse(f, d_work, d_image));
+  return RDL_OK;
+}
+
+int rdl_prepare_small_kernel(rdl_session* s, float* d_dest, uint32_t width,
+                             uint32_t height, const float* h_kernel,
+                             uint32_t n) {
+  RDL_ARG_CHECK(s && d_dest && h_kernel, "NULL argument");
+  if (n > width || n > height) {
+    rdl::SetError("Kernel size is larger than the image size");
+    return RDL_ERR_ARG;
+  }
+  const size_t kbytes = size_t(n) * n * sizeof(float);
+  float* d_k = nullptr;
+  RDL_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&d_k), kbytes, s->stream));
+  RDL_HIP_CHECK(hipMemcpyAsync(d_k, h_kernel, kbytes, hipMemcpyHostToDevice,
+                               s->stream));
+  RDL_HIP_CHECK(hipMemsetAsync(d_dest, 0, size_t(width) * height * sizeof(float),
+                               s->stream));
+  rdl::PlaceSmallKernel<<<rdl::Grid(size_t(n) * n), 256, 0, s->stream>>>(
+      d_dest, width, height, d_k, n);
+  RDL_HIP_CHECK(hipGetLastError());
+  RDL_HIP_CHECK(hipFreeAsync(d_k, s->stream));
+  RDL_HIP_CHECK(hipStreamSynchronize(s->stream));
+  return RDL_OK;
+}
+
+int rdl_prepare_psf_kernel(rdl_session* s, float* d_dest, uint32_t pw,
+                           uint32_t ph, const float* d_psf, uint32_t width,
+                           uint32_t height) {
+  RDL_ARG_CHECK(s && d_dest && d_psf, "NULL argument");
+  RDL_ARG_CHECK(pw >= width && ph >= height, "padded size smaller than image");
+  rdl::PreparePsfKernel<<<rdl::Grid(size_t(pw) * ph), 256, 0, s->stream>>>(
+      d_dest, pw, ph, d_psf, width, height);
+  RDL_HIP_CHECK(hipGetLastError());
+  return RDL_OK;
+}
+
+int rdl_trim_subtract(rdl_session* s, float* d_residual, uint32_t width,
+                      uint32_t height, const float* d_padded, uint32_t pw,
+                      uint32_t ph) {
+  RDL_ARG_CHECK(s && d_residual && d_padded, "NULL argument");
+  RDL_ARG_CHECK(pw >= width && ph >= height, "padded size smaller than image");
+  rdl::ScopedTiming t(s, "trim_subtract", double(width) * height * 12.0);
+  rdl::TrimSubtract<<<rdl::Grid(size_t(width) * height), 256, 0, s->stream>>>(
+      d_residual, width, height, d_padded, pw, ph);
+  RDL_HIP_CHECK(hipGetLastError());
+  return RDL_OK;
+}
+
+int rdl_untrim(rdl_session* s, float* d_dest, uint32_t pw, uint32_t ph,
+               const float* d_src, uint32_t width, uint32_t height) {
+  RDL_ARG_CHECK(s && d_dest && d_src, "NULL argument");
+  RDL_ARG_CHECK(pw >= width && ph >= height, "padded size smaller than image");
+  rdl::UntrimKernel<<<rdl::Grid(size_t(pw) * ph), 256, 0, s->stream>>>(
+      d_dest, pw, ph, d_src, width, height);
+  RDL_HIP_CHECK(hipGetLastError());
+  return RDL_OK;
+}
+
+int rdl_trim(rdl_session* s, float* d_dest, uint32_t width, uint32_t height,
+             const float* d_src, uint32_t pw, uint32_t ph) {
+  RDL_ARG_CHECK(s && d_dest && d_src, "NULL argument");
+  RDL_ARG_CHECK(pw >= width && ph >= height, "padded size smaller than image");
+  rdl::TrimKernel<<<rdl::Grid(size_t(width) * height), 256, 0, s->stream>>>(
+      d_dest, width, height, d_src, pw, ph);
+  RDL_HIP_CHECK(hipGetLastError());
+  return RDL_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,227 @@
+// Peak finding (argmax) and RMS: replaces math::peak_finder
+// (cpp/math/peak_finder.cc) and ThreadedDeconvolutionTools::RMS.
+//
+// One streaming pass over the border box (4 B/px, +1 B/px with a mask):
+// rows are dealt to 256-thread workgroups, each lane reads float4 (16 B)
+// so a wave moves 1 KiB per load; the per-lane (value,index) max is packed in
+// a 64-bit key (rdl::PeakKey) so the reduction is a plain integer max that
+// reproduces the reference's "strict '>' from FLT_MIN, first index wins".
+// A single-workgroup second stage reduces the per-block keys.
+#include <cfloat>
+
+#include "rdl_internal.h"
+
+namespace rdl {
+
+struct BoxArgs {
+  const float* image;
+  const uint8_t* mask;
+  uint32_t width, height;
+  uint32_t xs, xe, ys, ye;
+  uint32_t rows_per_block;
+  int allow_negative;
+};
+
+template <bool kVec>
+__global__ __launch_bounds__(256) void FindPeakPartial(BoxArgs a,
+                                                       uint64_t* partials) {
+  __shared__ uint64_t lds[16];
+  uint64_t best = 0;
+  const uint32_t y0 = a.ys + blockIdx.x * a.rows_per_block;
+  const uint32_t y1 = min(a.ye, y0 + a.rows_per_block);
+  for (uint32_t y = y0; y < y1; ++y) {
+    const float* row = a.image + size_t(y) * a.width;
+    const uint8_t* mrow = a.mask ? a.mask + size_t(y) * a.width : nullptr;
+    if constexpr (kVec) {
+      const uint32_t q0 = a.xs >> 2, q1 = (a.xe + 3) >> 2;
+      for (uint32_t q = q0 + threadIdx.x; q < q1; q += blockDim.x) {
+        const float4 v = reinterpret_cast<const float4*>(row)[q];
+        uint32_t m4 = 0x01010101u;
+        if (mrow) m4 = reinterpret_cast<const uint32_t*>(mrow)[q];
+        const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t x = q * 4 + j;
+          if (x >= a.xs && x < a.xe && ((m4 >> (8 * j)) & 0xffu)) {
+            const uint64_t k =
+                PeakKey(vv[j], a.allow_negative, y * a.width + x);
+            best = k > best ? k : best;
+          }
+        }
+      }
+    } else {
+      for (uint32_t x = a.xs + threadIdx.x; x < a.xe; x += blockDim.x) {
+        if (mrow && !mrow[x]) continue;
+        const uint64_t k = PeakKey(row[x], a.allow_negative, y * a.width + x);
+        best = k > best ? k : best;
+      }
+    }
+  }
+  best = BlockMaxU64(best, lds);
+  if (threadIdx.x == 0) partials[blockIdx.x] = best;
+}
+
+struct PeakOut {
+  uint64_t key;
+  float value;
+  uint32_t x, y;
+  int32_t found;
+};
+
+__global__ __launch_bounds__(1024) void FindPeakFinal(
+    const uint64_t* partials, uint32_t n, const float* image, uint32_t width,
+    uint32_t height, int avx_semantics, int has_mask, PeakOut* out) {
+  __shared__ uint64_t lds[16];
+  uint64_t best = 0;
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
+    best = partials[i] > best ? partials[i] : best;
+  best = BlockMaxU64(best, lds);
+  if (threadIdx.x == 0) {
+    PeakOut o;
+    o.key = best;
+    if (best != 0) {
+      const uint32_t idx = 0xffffffffu - uint32_t(best & 0xffffffffu);
+      o.x = idx % width;
+      o.y = idx / width;
+      o.value = image[idx];
+      o.found = 1;
+    } else if (avx_semantics && !has_mask) {
+      // peak_finder.cc:202,250-252: peakIndex starts at 0
+      o.x = 0;
+      o.y = 0;
+      o.value = image[0];
+      o.found = 1;
+    } else {
+      o.x = width;
+      o.y = height;
+      o.value = 0.0f;
+      o.found = 0;
+    }
+    *out = o;
+  }
+}
+
+__global__ __launch_bounds__(256) void SumSquaresPartial(const float* v,
+                                                         size_t n,
+                                                         double* partials) {
+  __shared__ double lds[16];
+  double acc = 0.0;
+  for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n;
+       i += size_t(gridDim.x) * blockDim.x) {
+    const double x = v[i];
+    acc += x * x;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+    for (unsigned w = 0; w < blockDim.x / 64; ++w) s += lds[w];
+    partials[blockIdx.x] = s;
+  }
+}
+
+__global__ void SumSquaresFinal(const double* partials, uint32_t n, size_t count,
+                                float* out) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    double s = 0.0;
+    for (uint32_t i = 0; i < n; ++i) s += partials[i];
+    *out = float(std::sqrt(s / double(count)));
+  }
+}
+
+int LaunchFindPeak(rdl_session* s, const float* d_image, uint32_t width,
+                   uint32_t height, uint32_t start_y, uint32_t end_y,
+                   uint32_t h_border, uint32_t v_border, int allow_negative,
+                   const uint8_t* d_mask, int avx_semantics, void* d_out) {
+  BoxArgs a;
+  a.image = d_image;
+  a.mask = d_mask;
+  a.width = width;
+  a.height = height;
+  // peak_finder.cc:27-32 (unsigned wrap-around as in the reference)
+  a.xs = h_border;
+  a.xe = width - h_border;
+  a.ys = start_y > v_border ? start_y : v_border;
+  a.ye = end_y < height - v_border ? end_y : height - v_border;
+  if (a.xe < a.xs) a.xe = a.xs;
+  if (a.ye < a.ys) a.ye = a.ys;
+  if (a.xe > width) a.xe = width;
+  if (a.ye > height) a.ye = height;
+  a.allow_negative = allow_negative;
+  const uint32_t rows = a.ye - a.ys;
+  const uint32_t target_blocks = 2048;
+  a.rows_per_block = rows == 0 ? 1 : (rows + target_blocks - 1) / target_blocks;
+  const uint32_t blocks =
+      rows == 0 ? 1 : (rows + a.rows_per_block - 1) / a.rows_per_block;
+  RDL_TRY(s->EnsureScratch(s->partials, size_t(blocks) * sizeof(uint64_t)));
+  uint64_t* partials = static_cast<uint64_t*>(s->partials.ptr);
+  const bool vec = (width % 4 == 0) &&
+                   (reinterpret_cast<uintptr_t>(d_image) % 16 == 0) &&
+                   (!d_mask || reinterpret_cast<uintptr_t>(d_mask) % 4 == 0);
+  const double bytes = double(rows) * (a.xe - a.xs) * (d_mask ? 5.0 : 4.0);
+  {
+    ScopedTiming t(s, "find_peak", bytes);
+    if (rows == 0) {
+      RDL_HIP_CHECK(hipMemsetAsync(partials, 0, sizeof(uint64_t), s->stream));
+    } else if (vec) {
+      FindPeakPartial<true><<<blocks, 256, 0, s->stream>>>(a, partials);
+    } else {
+      FindPeakPartial<false><<<blocks, 256, 0, s->stream>>>(a, partials);
+    }
+    FindPeakFinal<<<1, 1024, 0, s->stream>>>(
+        partials, blocks, d_image, width, height, avx_semantics,
+        d_mask != nullptr, static_cast<PeakOut*>(d_out));
+  }
+  RDL_HIP_CHECK(hipGetLastError());
+  return RDL_OK;
+}
+
+}  // namespace rdl
+
+extern "C" {
+
+int rdl_find_peak(rdl_session* s, const float* d_image, uint32_t width,
+                  uint32_t height, uint32_t start_y, uint32_t end_y,
+                  uint32_t h_border, uint32_t v_border, int allow_negative,
+                  const uint8_t* d_mask, int avx_semantics, rdl_peak* out) {
+  RDL_ARG_CHECK(s && d_image && out, "NULL argument");
+  RDL_ARG_CHECK(width > 0 && height > 0, "empty image");
+  RDL_ARG_CHECK(uint64_t(width) * height < 0xffffffffull,
+                "image too large for 32-bit pixel index");
+  RDL_TRY(rdl::LaunchFindPeak(s, d_image, width, height, start_y, end_y,
+                              h_border, v_border, allow_negative, d_mask,
+                              avx_semantics, s->d_small));
+  rdl::PeakOut o;
+  RDL_HIP_CHECK(hipMemcpyAsync(&o, s->d_small, sizeof(o),
+                               hipMemcpyDeviceToHost, s->stream));
+  RDL_HIP_CHECK(hipStreamSynchronize(s->stream));
+  out->value = o.value;
+  out->x = o.x;
+  out->y = o.y;
+  out->found = o.found;
+  return RDL_OK;
+}
+
+int rdl_rms(rdl_session* s, const float* d_image, size_t n, float* out) {
+  RDL_ARG_CHECK(s && d_image && out, "NULL argument");
+  RDL_ARG_CHECK(n > 0, "empty image");
+  const uint32_t blocks = std::min<size_t>(1024, rdl::DivUp(n, 256));
+  RDL_TRY(s->EnsureScratch(s->partials, blocks * sizeof(double)));
+  double* partials = static_cast<double*>(s->partials.ptr);
+  float* d_out = static_cast<float*>(s->d_small);
+  {
+    rdl::ScopedTiming t(s, "rms", double(n) * 4.0);
+    rdl::SumSquaresPartial<<<blocks, 256, 0, s->stream>>>(d_image, n,
+                                                           partials);
+    rdl::SumSquaresFinal<<<1, 64, 0, s->stream>>>(partials, blocks, n, d_out);
+  }
+  RDL_HIP_CHECK(hipGetLastError());
+  RDL_HIP_CHECK(
+      hipMemcpyAsync(out, d_out, sizeof(float), hipMemcpyDeviceToHost, s->stream));
+  RDL_HIP_CHECK(hipStreamSynchronize(s->stream));
+  return RDL_OK;
+}
+
+}  // extern "C"

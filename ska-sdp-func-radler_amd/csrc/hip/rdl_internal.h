@@ -1,0 +1,200 @@
+// Internal declarations of librdl_hip.so (HIP for gfx950 / MI355X).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "rdl_hip.h"
+
+namespace rdl {
+
+void SetError(const std::string& msg);
+
+#define RDL_HIP_CHECK(expr)                                               \
+  do {                                                                    \
+    hipError_t _e = (expr);                                               \
+    if (_e != hipSuccess) {                                               \
+      ::rdl::SetError(std::string(#expr) + ": " + hipGetErrorString(_e)); \
+      return RDL_ERR_HIP;                                                 \
+    }                                                                     \
+  } while (0)
+
+#define RDL_ARG_CHECK(cond, msg)      \
+  do {                                \
+    if (!(cond)) {                    \
+      ::rdl::SetError(msg);           \
+      return RDL_ERR_ARG;             \
+    }                                 \
+  } while (0)
+
+#define RDL_TRY(expr)         \
+  do {                        \
+    int _rc = (expr);         \
+    if (_rc != RDL_OK) return _rc; \
+  } while (0)
+
+// Kernel-family timing with HIP events on the session stream (bench.py's
+// roofline reads it; off by default).
+struct TimingEntry {
+  double ms = 0.0;
+  uint64_t launches = 0;
+  double bytes = 0.0;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+};
+
+// A reusable device scratch buffer that only grows.
+struct Scratch {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+};
+
+}  // namespace rdl
+
+struct rdl_session {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int n_cus = 256;
+  bool timing = false;
+  std::map<std::string, rdl::TimingEntry> timings;
+  std::vector<hipEvent_t> event_pool;
+  // small device/host scratch used by reductions
+  void* d_small = nullptr;       // 64 KiB device
+  void* h_small = nullptr;       // 64 KiB pinned host
+  rdl::Scratch partials;         // per-block partial keys
+  rdl::Scratch radix;            // radix-select histograms
+  void* comm = nullptr;          // ncclComm_t when initialised
+
+  hipEvent_t GetEvent();
+  void BeginTiming(const char* family, hipEvent_t* start);
+  void EndTiming(const char* family, hipEvent_t start, double bytes);
+  int CollectTimings();
+  int EnsureScratch(rdl::Scratch& s, size_t bytes);
+};
+
+namespace rdl {
+// RAII-less helper used by launchers: records start/end events when timing.
+struct ScopedTiming {
+  rdl_session* s;
+  const char* family;
+  double bytes;
+  hipEvent_t start = nullptr;
+  ScopedTiming(rdl_session* s_, const char* f, double b)
+      : s(s_), family(f), bytes(b) {
+    if (s->timing) s->BeginTiming(family, &start);
+  }
+  ~ScopedTiming() {
+    if (s->timing && start) s->EndTiming(family, start, bytes);
+  }
+};
+
+// Integration of one pixel across the image set, bit-for-bit the reference's
+// ImageSet::Get{Linear,Square}Integrated* (cpp/image_set.cc:309-462).
+// `get(i)` returns image i's value at this pixel.
+template <typename Get>
+__device__ __forceinline__ float IntegratePixel(const rdl_integration& g,
+                                                Get get) {
+  if (g.copy_fast_path) return get(0);
+  if (g.mode == RDL_INTEGRATE_LINEAR) {
+    float acc = 0.0f;
+    bool first = true;
+    for (uint32_t i = 0; i < g.n_images; ++i) {
+      const float w = g.weights[i];
+      if (w != 0.0f) {
+        const float v = get(i);
+        acc = first ? v * w : __builtin_fmaf(v, w, acc);
+        first = false;
+      }
+    }
+    return first ? 0.0f : acc * g.factor;
+  }
+  if (g.mode == RDL_INTEGRATE_SQUARE) {
+    if (g.n_channels == 1) {
+      float acc = get(0) * get(0);
+      for (uint32_t p = 1; p < g.n_pol; ++p) {
+        const float v = get(p);
+        acc = __builtin_fmaf(v, v, acc);
+      }
+      return __builtin_sqrtf(acc) * g.factor;
+    }
+    float dest = 0.0f;
+    for (uint32_t ch = 0; ch < g.n_channels; ++ch) {
+      const float w = g.weights[ch * g.n_pol];
+      float scratch = 0.0f;
+      if (w != 0.0f) {
+        if (g.n_pol == 1) {
+          scratch = get(ch);
+        } else {
+          const float v0 = get(ch * g.n_pol);
+          float acc = v0 * v0;
+          for (uint32_t p = 1; p < g.n_pol; ++p) {
+            const float v = get(ch * g.n_pol + p);
+            acc = __builtin_fmaf(v, v, acc);
+          }
+          scratch = __builtin_sqrtf(acc);
+        }
+      }
+      dest = ch == 0 ? scratch * w : __builtin_fmaf(scratch, w, dest);
+    }
+    return dest * g.factor;
+  }
+  // RDL_INTEGRATE_SQUARED_JOINS (aocommon op order unpinned)
+  float acc = 0.0f;
+  bool first = true;
+  for (uint32_t i = 0; i < g.n_images; ++i) {
+    const float w = g.weights[i];
+    if (w != 0.0f) {
+      const float v = get(i);
+      acc = first ? v * v * w : __builtin_fmaf(v * v, w, acc);
+      first = false;
+    }
+  }
+  return first ? 0.0f : __builtin_sqrtf(acc) * g.factor;
+}
+
+// Orderable 64-bit argmax key: larger key = larger value, ties -> smaller
+// index. Values that do not qualify (<= FLT_MIN, NaN, sign filtered) get 0.
+__device__ __forceinline__ uint64_t PeakKey(float v, bool allow_negative,
+                                            uint32_t index) {
+  uint32_t u = __float_as_uint(v);
+  if (allow_negative) u &= 0x7fffffffu;
+  // qualify: FLT_MIN < value <= +inf (sign bit set -> fails the <= test)
+  const bool q = (u > 0x00800000u) && (u <= 0x7f800000u);
+  return q ? ((uint64_t(u) << 32) | uint64_t(0xffffffffu - index)) : 0ull;
+}
+
+__device__ __forceinline__ uint64_t WaveMaxU64(uint64_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint64_t o = __shfl_xor(v, off, 64);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
+// Block-wide max of a uint64 (blockDim multiple of 64, <= 1024).
+__device__ __forceinline__ uint64_t BlockMaxU64(uint64_t v, uint64_t* lds) {
+  v = WaveMaxU64(v);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n_waves = blockDim.x >> 6;
+  __syncthreads();
+  if (lane == 0) lds[wave] = v;
+  __syncthreads();
+  if (wave == 0) {
+    uint64_t w = lane < n_waves ? lds[lane] : 0ull;
+    w = WaveMaxU64(w);
+    if (lane == 0) lds[0] = w;
+  }
+  __syncthreads();
+  const uint64_t r = lds[0];
+  return r;
+}
+
+inline unsigned DivUp(size_t a, size_t b) { return unsigned((a + b - 1) / b); }
+
+}  // namespace rdl

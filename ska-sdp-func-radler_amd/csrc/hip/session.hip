@@ -1,0 +1,209 @@
+// Session / runtime part of the C-ABI (rdl_hip.h "runtime" section).
+#include <cstring>
+
+#include "rdl_internal.h"
+
+namespace rdl {
+namespace {
+thread_local std::string g_last_error;
+}
+void SetError(const std::string& msg) { g_last_error = msg; }
+}  // namespace rdl
+
+hipEvent_t rdl_session::GetEvent() {
+  if (!event_pool.empty()) {
+    hipEvent_t e = event_pool.back();
+    event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+void rdl_session::BeginTiming(const char* family, hipEvent_t* start) {
+  (void)family;
+  *start = GetEvent();
+  (void)hipEventRecord(*start, stream);
+}
+
+void rdl_session::EndTiming(const char* family, hipEvent_t start,
+                            double bytes) {
+  hipEvent_t end = GetEvent();
+  (void)hipEventRecord(end, stream);
+  rdl::TimingEntry& t = timings[family];
+  t.pending.emplace_back(start, end);
+  t.launches += 1;
+  t.bytes += bytes;
+}
+
+int rdl_session::CollectTimings() {
+  for (auto& [name, t] : timings) {
+    for (auto& [a, b] : t.pending) {
+      RDL_HIP_CHECK(hipEventSynchronize(b));
+      float ms = 0.0f;
+      RDL_HIP_CHECK(hipEventElapsedTime(&ms, a, b));
+      t.ms += ms;
+      event_pool.push_back(a);
+      event_pool.push_back(b);
+    }
+    t.pending.clear();
+  }
+  return RDL_OK;
+}
+
+int rdl_session::EnsureScratch(rdl::Scratch& s, size_t bytes) {
+  if (s.bytes >= bytes) return RDL_OK;
+  if (s.ptr) {
+    RDL_HIP_CHECK(hipStreamSynchronize(stream));
+    RDL_HIP_CHECK(hipFree(s.ptr));
+    s.ptr = nullptr;
+    s.bytes = 0;
+  }
+  RDL_HIP_CHECK(hipMalloc(&s.ptr, bytes));
+  s.bytes = bytes;
+  return RDL_OK;
+}
+
+extern "C" {
+
+const char* rdl_last_error(void) { return rdl::g_last_error.c_str(); }
+
+const char* rdl_version(void) { return "rdl_hip 0.1.0 (gfx950)"; }
+
+int rdl_device_count(int* count) {
+  RDL_ARG_CHECK(count, "count is NULL");
+  RDL_HIP_CHECK(hipGetDeviceCount(count));
+  return RDL_OK;
+}
+
+int rdl_session_create(int device, rdl_session** out) {
+  RDL_ARG_CHECK(out, "out is NULL");
+  int n = 0;
+  RDL_HIP_CHECK(hipGetDeviceCount(&n));
+  RDL_ARG_CHECK(device >= 0 && device < n, "invalid device index");
+  RDL_HIP_CHECK(hipSetDevice(device));
+  auto s = std::make_unique<rdl_session>();
+  s->device = device;
+  RDL_HIP_CHECK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+  hipDeviceProp_t prop;
+  RDL_HIP_CHECK(hipGetDeviceProperties(&prop, device));
+  s->n_cus = prop.multiProcessorCount;
+  RDL_HIP_CHECK(hipMalloc(&s->d_small, 1 << 16));
+  RDL_HIP_CHECK(hipHostMalloc(&s->h_small, 1 << 16, hipHostMallocDefault));
+  *out = s.release();
+  return RDL_OK;
+}
+
+int rdl_session_destroy(rdl_session* s) {
+  if (!s) return RDL_OK;
+  (void)hipSetDevice(s->device);
+  (void)hipStreamSynchronize(s->stream);
+  for (auto& [name, t] : s->timings)
+    for (auto& [a, b] : t.pending) {
+      (void)hipEventDestroy(a);
+      (void)hipEventDestroy(b);
+    }
+  for (hipEvent_t e : s->event_pool) (void)hipEventDestroy(e);
+  if (s->partials.ptr) (void)hipFree(s->partials.ptr);
+  if (s->radix.ptr) (void)hipFree(s->radix.ptr);
+  if (s->d_small) (void)hipFree(s->d_small);
+  if (s->h_small) (void)hipHostFree(s->h_small);
+  if (s->comm) rdl_comm_destroy(s);
+  (void)hipStreamDestroy(s->stream);
+  delete s;
+  return RDL_OK;
+}
+
+int rdl_session_sync(rdl_session* s) {
+  RDL_ARG_CHECK(s, "session is NULL");
+  RDL_HIP_CHECK(hipStreamSynchronize(s->stream));
+  return RDL_OK;
+}
+
+void* rdl_session_stream(rdl_session* s) { return s ? s->stream : nullptr; }
+
+int rdl_malloc(rdl_session* s, size_t bytes, void** d_out) {
+  RDL_ARG_CHECK(s && d_out, "NULL argument");
+  RDL_HIP_CHECK(hipSetDevice(s->device));
+  *d_out = nullptr;
+  if (bytes == 0) return RDL_OK;
+  RDL_HIP_CHECK(hipMalloc(d_out, bytes));
+  return RDL_OK;
+}
+
+int rdl_free(rdl_session* s, void* d_ptr) {
+  RDL_ARG_CHECK(s, "NULL session");
+  if (!d_ptr) return RDL_OK;
+  RDL_HIP_CHECK(hipStreamSynchronize(s->stream));
+  RDL_HIP_CHECK(hipFree(d_ptr));
+  return RDL_OK;
+}
+
+int rdl_memcpy_h2d(rdl_session* s, void* d_dst, const void* h_src,
+                   size_t bytes) {
+  RDL_ARG_CHECK(s, "NULL session");
+  if (bytes == 0) return RDL_OK;
+  RDL_HIP_CHECK(
+      hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, s->stream));
+  RDL_HIP_CHECK(hipStreamSynchronize(s->stream));
+  return RDL_OK;
+}
+
+int rdl_memcpy_d2h(rdl_session* s, void* h_dst, const void* d_src,
+                   size_t bytes) {
+  RDL_ARG_CHECK(s, "NULL session");
+  if (bytes == 0) return RDL_OK;
+  RDL_HIP_CHECK(
+      hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, s->stream));
+  RDL_HIP_CHECK(hipStreamSynchronize(s->stream));
+  return RDL_OK;
+}
+
+int rdl_memcpy_d2d(rdl_session* s, void* d_dst, const void* d_src,
+                   size_t bytes) {
+  RDL_ARG_CHECK(s, "NULL session");
+  if (bytes == 0) return RDL_OK;
+  RDL_HIP_CHECK(hipMemcpyAsync(d_dst, d_src, bytes, hipMemcpyDeviceToDevice,
+                               s->stream));
+  return RDL_OK;
+}
+
+int rdl_memset_zero(rdl_session* s, void* d_dst, size_t bytes) {
+  RDL_ARG_CHECK(s, "NULL session");
+  if (bytes == 0) return RDL_OK;
+  RDL_HIP_CHECK(hipMemsetAsync(d_dst, 0, bytes, s->stream));
+  return RDL_OK;
+}
+
+int rdl_timing_enable(rdl_session* s, int enable) {
+  RDL_ARG_CHECK(s, "NULL session");
+  s->timing = enable != 0;
+  return RDL_OK;
+}
+
+int rdl_timing_get(rdl_session* s, const char* family, double* ms,
+                   uint64_t* launches, double* bytes) {
+  RDL_ARG_CHECK(s && family, "NULL argument");
+  RDL_TRY(s->CollectTimings());
+  auto it = s->timings.find(family);
+  if (it == s->timings.end()) {
+    if (ms) *ms = 0.0;
+    if (launches) *launches = 0;
+    if (bytes) *bytes = 0.0;
+    return RDL_OK;
+  }
+  if (ms) *ms = it->second.ms;
+  if (launches) *launches = it->second.launches;
+  if (bytes) *bytes = it->second.bytes;
+  return RDL_OK;
+}
+
+int rdl_timing_reset(rdl_session* s) {
+  RDL_ARG_CHECK(s, "NULL session");
+  RDL_TRY(s->CollectTimings());
+  s->timings.clear();
+  return RDL_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,726 @@
+// The sub-minor (Clark-style) loop: replaces SubMinorLoop::Run with
+// findPeakPositions / MakeSets / GetMaxComponent
+// (cpp/algorithms/subminor_loop.cc:13-184).
+//
+// Selection: three streaming passes over the border box (count, scan,
+// scatter) compact the pixels whose integrated value passes the threshold
+// into a row-major list (packed y<<16|x) and gather their N_img residual
+// values — the same order the reference's nested x/y loops produce.
+//
+// Loop: one persistent launch. The selected set is partitioned over G
+// workgroups (one per CU); each keeps its pixels' positions, residual and
+// model values in LDS (global scratch when the set outgrows G x 160 KiB).
+// Per iteration every workgroup subtracts the current component's shifted
+// twice-convolved PSF from its pixels (one FMA per pixel and image, PSF
+// gathered from HBM/L2), re-integrates and reduces its argmax; with G > 1 the
+// winners are exchanged through write-through (sc1) records and a monotonic
+// arrival counter, so all workgroups take the same next component. The
+// per-iteration argmax key orders the signed (or absolute) integrated value
+// with the first index winning ties, which is GetMaxComponent's
+// "start at scratch[0], strict '>'" scan.
+#include <cmath>
+
+#include "rdl_internal.h"
+
+struct rdl_subminor {
+  rdl_session* s = nullptr;
+  void* counts = nullptr;  // per-chunk counts / offsets
+  size_t counts_bytes = 0;
+  void* sel = nullptr;     // positions + R + M for the selected set
+  size_t sel_bytes = 0;
+  void* sync = nullptr;    // records + counter + result + trace
+  size_t sync_bytes = 0;
+  uint64_t n_selected = 0;
+  uint32_t n_images = 0;
+  uint32_t width = 0, height = 0;
+  uint32_t* d_pos = nullptr;
+  float* d_r = nullptr;
+  float* d_m = nullptr;
+};
+
+namespace rdl {
+
+constexpr uint32_t kChunk = 2048;  // box pixels per selection workgroup
+constexpr uint32_t kSelThreads = 256;
+constexpr uint32_t kLoopThreads = 512;
+
+struct SelArgs {
+  const float* residuals;
+  const uint8_t* mask;
+  uint32_t width, height, n;  // n = width*height
+  uint32_t xs, xe, ys, ye, bw;
+  uint64_t box_pixels;
+  rdl_integration integ;
+  float threshold;
+  int32_t allow_negative;
+};
+
+__device__ __forceinline__ bool Selected(const SelArgs& a, uint64_t b,
+                                         uint32_t& idx) {
+  if (b >= a.box_pixels) return false;
+  const uint32_t x = a.xs + uint32_t(b % a.bw);
+  const uint32_t y = a.ys + uint32_t(b / a.bw);
+  idx = y * a.width + x;
+  if (a.mask && !a.mask[idx]) return false;
+  const float v = IntegratePixel(
+      a.integ, [&](uint32_t k) { return a.residuals[size_t(k) * a.n + idx]; });
+  const float value = a.allow_negative ? fabsf(v) : v;
+  return value >= a.threshold;
+}
+
+__global__ __launch_bounds__(kSelThreads) void SelCount(SelArgs a,
+                                                        uint32_t* counts) {
+  __shared__ uint32_t lds[kSelThreads / 64];
+  uint32_t c = 0;
+  const uint64_t base = uint64_t(blockIdx.x) * kChunk;
+  for (uint32_t j = threadIdx.x; j < kChunk; j += kSelThreads) {
+    uint32_t idx;
+    c += Selected(a, base + j, idx) ? 1u : 0u;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+  if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (uint32_t w = 0; w < kSelThreads / 64; ++w) t += lds[w];
+    counts[blockIdx.x] = t;
+  }
+}
+
+// Exclusive scan of the chunk counts in one workgroup; writes the total.
+__global__ __launch_bounds__(1024) void SelScan(uint32_t* counts, uint32_t n,
+                                                uint64_t* total) {
+  __shared__ uint64_t lds[1024];
+  __shared__ uint64_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t base = 0; base < n; base += 1024) {
+    const uint32_t i = base + threadIdx.x;
+    const uint64_t v = i < n ? counts[i] : 0;
+    lds[threadIdx.x] = v;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {
+      const uint64_t t = threadIdx.x >= off ? lds[threadIdx.x - off] : 0;
+      __syncthreads();
+      lds[threadIdx.x] += t;
+      __syncthreads();
+    }
+    const uint64_t incl = lds[threadIdx.x];
+    if (i < n) counts[i] = uint32_t(carry + incl - v);
+    __syncthreads();
+    if (threadIdx.x == 1023) carry += incl;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *total = carry;
+}
+
+__global__ __launch_bounds__(kSelThreads) void SelScatter(
+    SelArgs a, const uint32_t* offsets, uint32_t n_img, uint64_t n_sel,
+    uint32_t* pos, float* r) {
+  __shared__ uint32_t wave_tot[kSelThreads / 64];
+  const uint64_t base = uint64_t(blockIdx.x) * kChunk;
+  uint32_t running = offsets[blockIdx.x];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (uint32_t j0 = 0; j0 < kChunk; j0 += kSelThreads) {
+    uint32_t idx = 0;
+    const bool sel = Selected(a, base + j0 + threadIdx.x, idx);
+    const uint64_t ballot = __ballot(sel);
+    const uint32_t before = __popcll(ballot & ((1ull << lane) - 1ull));
+    if (lane == 0) wave_tot[wave] = __popcll(ballot);
+    __syncthreads();
+    uint32_t woff = 0;
+    for (int w = 0; w < wave; ++w) woff += wave_tot[w];
+    uint32_t step = 0;
+    for (uint32_t w = 0; w < kSelThreads / 64; ++w) step += wave_tot[w];
+    if (sel) {
+      const uint64_t o = running + woff + before;
+      const uint32_t x = idx % a.width, y = idx / a.width;
+      pos[o] = (y << 16) | x;
+      for (uint32_t k = 0; k < n_img; ++k)
+        r[size_t(k) * n_sel + o] = a.residuals[size_t(k) * a.n + idx];
+    }
+    running += step;
+    __syncthreads();
+  }
+}
+
+// ----------------------------------------------------------------- loop
+struct LoopArgs {
+  const uint32_t* pos;    // n_sel
+  float* r;               // [n_img][n_sel] (in: gathered residuals)
+  float* m;               // [n_img][n_sel] (out: model values)
+  const float* psfs;      // twice-convolved PSFs, W*H planes
+  uint32_t* records;      // [2][G][rec_words] (G > 1)
+  uint32_t* counter;      // arrival counter (G > 1), zeroed per launch
+  uint32_t* result;       // LoopResult
+  uint32_t* trace;        // 2 x u32 per component
+  uint64_t trace_cap;
+  uint64_t n_sel;
+  uint32_t per_block;
+  uint32_t n_blocks;
+  uint32_t rec_words;
+  uint32_t width, height, n_img, n_pol;
+  rdl_integration integ;
+  float threshold, gain, divergence_limit;
+  uint64_t iteration_start, max_iterations;
+  int32_t allow_negative, stop_on_negative;
+  int32_t use_lds;
+};
+
+struct LoopResult {
+  uint64_t iteration;
+  float peak;
+  int32_t diverging;
+  float flux;
+  uint32_t error;
+};
+
+__device__ __forceinline__ uint64_t MaxKey(float integ, bool allow_negative,
+                                           uint64_t p) {
+  const float v = allow_negative ? fabsf(integ) : integ;
+  if (v != v) return 0ull;  // NaN never wins (unless everything is NaN)
+  uint32_t u = __float_as_uint(v);
+  u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  return (uint64_t(u) << 32) | uint64_t(0xffffffffu - uint32_t(p));
+}
+
+__device__ __forceinline__ void StoreSc1(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t LoadSc1(uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Winner record layout (u32 words): key lo, key hi, integ (f32), pos, r[n_img]
+template <int NI>
+__global__ __launch_bounds__(kLoopThreads) void SubminorLoop(LoopArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  __shared__ uint64_t red[kLoopThreads / 64];
+  __shared__ uint32_t win[4 + RDL_MAX_IMAGES];
+  __shared__ uint32_t flags[2];
+
+  const uint32_t tid = threadIdx.x;
+  const uint64_t base = uint64_t(blockIdx.x) * a.per_block;
+  const uint32_t cnt =
+      base >= a.n_sel ? 0u : uint32_t(min<uint64_t>(a.per_block, a.n_sel - base));
+  const uint32_t n_img = a.n_img;
+
+  uint32_t* pos;
+  float* R;
+  float* M;
+  size_t stride;  // between images
+  if (a.use_lds) {
+    pos = smem;
+    R = reinterpret_cast<float*>(smem + a.per_block);
+    M = R + size_t(n_img) * a.per_block;
+    stride = a.per_block;
+    for (uint32_t j = tid; j < cnt; j += kLoopThreads) {
+      pos[j] = a.pos[base + j];
+      for (uint32_t k = 0; k < n_img; ++k) {
+        R[k * stride + j] = a.r[size_t(k) * a.n_sel + base + j];
+        M[k * stride + j] = 0.0f;
+      }
+    }
+  } else {
+    pos = const_cast<uint32_t*>(a.pos) + base;
+    R = a.r + base;
+    M = a.m + base;
+    stride = a.n_sel;
+    for (uint32_t j = tid; j < cnt; j += kLoopThreads)
+      for (uint32_t k = 0; k < n_img; ++k) M[k * stride + j] = 0.0f;
+  }
+  __syncthreads();
+
+  const int W = int(a.width), H = int(a.height);
+  const size_t plane = size_t(a.width) * a.height;
+  float c[NI];
+#pragma unroll
+  for (int k = 0; k < NI; ++k) c[k] = 0.0f;
+  int cx = 0, cy = 0;
+  bool have_component = false;
+  float start_abs = 0.0f;
+  bool diverging = false;
+  float flux = 0.0f;
+  uint64_t iteration = a.iteration_start;
+  uint32_t gen = 0;
+  float m = 0.0f;
+  uint64_t winner_p = 0;
+
+  while (true) {
+    // ---- subtract the current component, integrate, local argmax
+    uint64_t best = 0;
+    for (uint32_t j = tid; j < cnt; j += kLoopThreads) {
+      const uint32_t pk = pos[j];
+      const int px = int(pk & 0xffffu), py = int(pk >> 16);
+      float v[NI];
+      if (have_component) {
+        const int dx = px - cx + W / 2, dy = py - cy + H / 2;
+        const bool in = dx >= 0 && dx < W && dy >= 0 && dy < H;
+        const size_t off = size_t(dy) * a.width + size_t(dx);
+#pragma unroll
+        for (int k = 0; k < NI; ++k) {
+          if (k < int(n_img)) {
+            float rv = R[k * stride + j];
+            if (in) {
+              const float pv = a.psfs[size_t(k / int(a.n_pol)) * plane + off];
+              rv = __builtin_fmaf(-pv, c[k], rv);
+              R[k * stride + j] = rv;
+            }
+            v[k] = rv;
+          } else {
+            v[k] = 0.0f;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < NI; ++k)
+          v[k] = k < int(n_img) ? R[k * stride + j] : 0.0f;
+      }
+      const float integ = IntegratePixel(a.integ, [&](uint32_t kk) {
+        float r = v[0];
+#pragma unroll
+        for (int q = 1; q < NI; ++q) r = (uint32_t(q) == kk) ? v[q] : r;
+        return r;
+      });
+      uint64_t key = MaxKey(integ, a.allow_negative, base + j);
+      if (base + j == 0 && integ != integ) key = ~0ull;  // scratch[0] is NaN
+      best = key > best ? key : best;
+    }
+    // block reduce
+    {
+      uint64_t w = WaveMaxU64(best);
+      if ((tid & 63) == 0) red[tid >> 6] = w;
+      __syncthreads();
+      if (tid < 64) {
+        uint64_t x = tid < kLoopThreads / 64 ? red[tid] : 0ull;
+        x = WaveMaxU64(x);
+        if (tid == 0) red[0] = x;
+      }
+      __syncthreads();
+    }
+    const uint64_t block_best = red[0];
+    // owner of the block winner fills the local record
+    if (cnt > 0) {
+      const uint64_t lp = block_best == 0 ? 0ull
+                          : block_best == ~0ull ? 0ull
+                          : uint64_t(0xffffffffu - uint32_t(block_best));
+      const uint64_t j = lp - base;
+      if (lp >= base && j < cnt && (j % kLoopThreads) == tid) {
+        win[0] = uint32_t(block_best);
+        win[1] = uint32_t(block_best >> 32);
+        float vv[NI];
+#pragma unroll
+        for (int k = 0; k < NI; ++k)
+          vv[k] = k < int(n_img) ? R[k * stride + j] : 0.0f;
+        const float integ = IntegratePixel(a.integ, [&](uint32_t kk) {
+          float r = vv[0];
+#pragma unroll
+          for (int q = 1; q < NI; ++q) r = (uint32_t(q) == kk) ? vv[q] : r;
+          return r;
+        });
+        win[2] = __float_as_uint(integ);
+        win[3] = pos[j];
+        for (uint32_t k = 0; k < n_img; ++k) win[4 + k] = __float_as_uint(vv[k]);
+      }
+    } else if (tid == 0) {
+      win[0] = 0;
+      win[1] = 0;
+    }
+    __syncthreads();
+
+    if (a.n_blocks > 1) {
+      // ---- exchange records: write-through stores, arrival counter
+      uint32_t* rec_base = a.records + size_t(gen & 1) * a.n_blocks * a.rec_words;
+      if (tid == 0) {
+        uint32_t* rec = rec_base + size_t(blockIdx.x) * a.rec_words;
+        for (uint32_t w = 0; w < 4 + n_img; ++w) StoreSc1(rec + w, win[w]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t target = (gen + 1) * a.n_blocks;
+        uint64_t spins = 0;
+        flags[0] = 0;
+        while (LoadSc1(a.counter) < target) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > (1ull << 28)) {  // ~minutes: a lost workgroup
+            flags[0] = 1;
+            break;
+          }
+        }
+      }
+      __syncthreads();
+      if (flags[0]) {
+        if (tid == 0) StoreSc1(&a.result[8], 1u);
+        return;
+      }
+      // wave 0 reduces the G keys
+      if (tid < 64) {
+        uint64_t bk = 0;
+        uint32_t bb = 0;
+        for (uint32_t b = tid; b < a.n_blocks; b += 64) {
+          uint32_t* rec = rec_base + size_t(b) * a.rec_words;
+          const uint64_t k =
+              uint64_t(LoadSc1(rec)) | (uint64_t(LoadSc1(rec + 1)) << 32);
+          if (k > bk) {
+            bk = k;
+            bb = b;
+          }
+        }
+        // wave argmax over (key, block)
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+          const uint64_t ok = __shfl_xor(bk, off, 64);
+          const uint32_t ob = __shfl_xor(bb, off, 64);
+          if (ok > bk || (ok == bk && ob < bb)) {
+            bk = ok;
+            bb = ob;
+          }
+        }
+        if (tid == 0) flags[1] = bb;
+      }
+      __syncthreads();
+      if (tid < 4 + n_img) {
+        uint32_t* rec = rec_base + size_t(flags[1]) * a.rec_words;
+        win[tid] = LoadSc1(rec + tid);
+      }
+      __syncthreads();
+      ++gen;
+    }
+
+    // ---- the global winner is in win[]; identical decisions everywhere
+    const uint64_t gkey = uint64_t(win[0]) | (uint64_t(win[1]) << 32);
+    winner_p = (gkey == 0 || gkey == ~0ull)
+                   ? 0ull
+                   : uint64_t(0xffffffffu - uint32_t(gkey));
+    m = __uint_as_float(win[2]);
+    if (!have_component) {
+      start_abs = fabsf(m);  // subminor_loop.cc:59
+    } else {
+      if (a.divergence_limit != 0.0f)
+        diverging = fabsf(m) > start_abs * a.divergence_limit;
+      ++iteration;
+    }
+    // loop condition (subminor_loop.cc:61-63)
+    const bool go = fabsf(m) > a.threshold && iteration < a.max_iterations &&
+                    (!a.stop_on_negative || m >= 0.0f) && !diverging;
+    if (!go) break;
+    // next component (subminor_loop.cc:64-89)
+#pragma unroll
+    for (int k = 0; k < NI; ++k)
+      c[k] = k < int(n_img) ? __uint_as_float(win[4 + k]) * a.gain : 0.0f;
+    flux += m * a.gain;
+    cx = int(win[3] & 0xffffu);
+    cy = int(win[3] >> 16);
+    {
+      const uint64_t j = winner_p - base;
+      if (winner_p >= base && j < cnt && (j % kLoopThreads) == tid) {
+#pragma unroll
+        for (int k = 0; k < NI; ++k)
+          if (k < int(n_img)) M[k * stride + j] += c[k];
+      }
+    }
+    if (blockIdx.x == 0 && tid == 0 && a.trace) {
+      const uint64_t t = iteration - a.iteration_start;
+      if (t < a.trace_cap) {
+        a.trace[2 * t] = uint32_t(cx);
+        a.trace[2 * t + 1] = uint32_t(cy);
+      }
+    }
+    have_component = true;
+    __syncthreads();
+  }
+
+  // write back model values (LDS variant)
+  if (a.use_lds) {
+    for (uint32_t j = tid; j < cnt; j += kLoopThreads)
+      for (uint32_t k = 0; k < n_img; ++k)
+        a.m[size_t(k) * a.n_sel + base + j] = M[k * stride + j];
+  }
+  if (blockIdx.x == 0 && tid == 0) {
+    LoopResult* r = reinterpret_cast<LoopResult*>(a.result);
+    r->iteration = iteration;
+    r->peak = m;
+    r->diverging = diverging ? 1 : 0;
+    r->flux = flux;
+  }
+}
+
+__global__ __launch_bounds__(256) void ScatterModel(const uint32_t* pos,
+                                                    const float* m,
+                                                    uint64_t n_sel,
+                                                    float* dest, uint32_t dw,
+                                                    uint32_t ox, uint32_t oy,
+                                                    int add) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n_sel;
+       i += uint64_t(gridDim.x) * blockDim.x) {
+    const uint32_t pk = pos[i];
+    const size_t d = size_t((pk >> 16) + oy) * dw + (pk & 0xffffu) + ox;
+    if (add)
+      dest[d] += m[i];
+    else
+      dest[d] = m[i];
+  }
+}
+
+int Grow(void** p, size_t* have, size_t need, hipStream_t stream) {
+  if (*have >= need) return RDL_OK;
+  if (*p) {
+    RDL_HIP_CHECK(hipStreamSynchronize(stream));
+    RDL_HIP_CHECK(hipFree(*p));
+    *p = nullptr;
+    *have = 0;
+  }
+  RDL_HIP_CHECK(hipMalloc(p, need));
+  *have = need;
+  return RDL_OK;
+}
+
+template <int NI>
+int LaunchLoop(const LoopArgs& a, size_t lds_bytes, hipStream_t stream) {
+  auto kernel = SubminorLoop<NI>;
+  if (lds_bytes > 0)
+    RDL_HIP_CHECK(hipFuncSetAttribute(
+        reinterpret_cast<const void*>(kernel),
+        hipFuncAttributeMaxDynamicSharedMemorySize, int(lds_bytes)));
+  if (a.n_blocks > 1) {
+    void* args[] = {const_cast<LoopArgs*>(&a)};
+    RDL_HIP_CHECK(hipLaunchCooperativeKernel(
+        reinterpret_cast<const void*>(kernel), dim3(a.n_blocks),
+        dim3(kLoopThreads), args, unsigned(lds_bytes), stream));
+  } else {
+    kernel<<<1, kLoopThreads, lds_bytes, stream>>>(a);
+    RDL_HIP_CHECK(hipGetLastError());
+  }
+  return RDL_OK;
+}
+
+}  // namespace rdl
+
+extern "C" {
+
+int rdl_subminor_create(rdl_session* s, rdl_subminor** out) {
+  RDL_ARG_CHECK(s && out, "NULL argument");
+  auto h = new rdl_subminor();
+  h->s = s;
+  *out = h;
+  return RDL_OK;
+}
+
+int rdl_subminor_destroy(rdl_subminor* h) {
+  if (!h) return RDL_OK;
+  (void)hipStreamSynchronize(h->s->stream);
+  if (h->counts) (void)hipFree(h->counts);
+  if (h->sel) (void)hipFree(h->sel);
+  if (h->sync) (void)hipFree(h->sync);
+  delete h;
+  return RDL_OK;
+}
+
+int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
+                     const float* d_psfs, const rdl_subminor_params* p,
+                     rdl_subminor_result* out, uint32_t* h_trace,
+                     uint64_t trace_cap) {
+  RDL_ARG_CHECK(h && d_residuals && d_psfs && p && out, "NULL argument");
+  RDL_ARG_CHECK(p->n_images >= 1 && p->n_images <= RDL_MAX_IMAGES,
+                "n_images out of range");
+  RDL_ARG_CHECK(p->n_pol >= 1 && p->n_images % p->n_pol == 0, "bad n_pol");
+  RDL_ARG_CHECK(p->width > 0 && p->height > 0 && p->width <= 65535 &&
+                    p->height <= 65535,
+                "image size out of range (1..65535)");
+  rdl_session* s = h->s;
+  hipStream_t st = s->stream;
+  h->width = p->width;
+  h->height = p->height;
+  h->n_images = p->n_images;
+
+  // ---------------- selection (subminor_loop.cc:143-184)
+  rdl::SelArgs sa{};
+  sa.residuals = d_residuals;
+  sa.mask = p->d_mask;
+  sa.width = p->width;
+  sa.height = p->height;
+  sa.n = p->width * p->height;
+  sa.xs = p->h_border;
+  sa.xe = std::max<int64_t>(sa.xs, int64_t(p->width) - int64_t(p->h_border));
+  sa.ys = p->v_border;
+  sa.ye = std::max<int64_t>(sa.ys, int64_t(p->height) - int64_t(p->v_border));
+  sa.xe = std::min(sa.xe, p->width);
+  sa.ye = std::min(sa.ye, p->height);
+  sa.xs = std::min(sa.xs, sa.xe);
+  sa.ys = std::min(sa.ys, sa.ye);
+  sa.bw = std::max<uint32_t>(1, sa.xe - sa.xs);
+  sa.box_pixels = uint64_t(sa.xe - sa.xs) * (sa.ye - sa.ys);
+  sa.integ = p->integ;
+  sa.threshold = p->threshold;
+  sa.allow_negative = p->allow_negative;
+  const uint32_t n_chunks =
+      std::max<uint32_t>(1, rdl::DivUp(sa.box_pixels, rdl::kChunk));
+  RDL_TRY(rdl::Grow(&h->counts, &h->counts_bytes,
+                    size_t(n_chunks) * sizeof(uint32_t) + 64, st));
+  uint32_t* counts = static_cast<uint32_t*>(h->counts);
+  uint64_t* d_total = reinterpret_cast<uint64_t*>(s->d_small);
+  const double sel_bytes = double(sa.box_pixels) * 4.0 * p->n_images;
+  {
+    rdl::ScopedTiming t(s, "subminor_select", 2.0 * sel_bytes);
+    rdl::SelCount<<<n_chunks, rdl::kSelThreads, 0, st>>>(sa, counts);
+    rdl::SelScan<<<1, 1024, 0, st>>>(counts, n_chunks, d_total);
+  }
+  RDL_HIP_CHECK(hipGetLastError());
+  uint64_t n_sel = 0;
+  RDL_HIP_CHECK(hipMemcpyAsync(&n_sel, d_total, sizeof(n_sel),
+                               hipMemcpyDeviceToHost, st));
+  RDL_HIP_CHECK(hipStreamSynchronize(st));
+  h->n_selected = n_sel;
+  out->n_selected = n_sel;
+  out->iteration = p->iteration_start;
+  out->diverging = 0;
+  out->flux_cleaned = 0.0f;
+  if (n_sel == 0) {  // subminor_loop.cc:52-54
+    out->has_peak = 0;
+    out->peak = 0.0f;
+    return RDL_OK;
+  }
+  const uint32_t ni = p->n_images;
+  const size_t sel_need = n_sel * sizeof(uint32_t) + 2 * n_sel * ni * sizeof(float) + 256;
+  RDL_TRY(rdl::Grow(&h->sel, &h->sel_bytes, sel_need, st));
+  h->d_pos = static_cast<uint32_t*>(h->sel);
+  h->d_r = reinterpret_cast<float*>(
+      static_cast<char*>(h->sel) + (n_sel * sizeof(uint32_t) + 15) / 16 * 16);
+  h->d_m = h->d_r + n_sel * ni;
+  {
+    rdl::ScopedTiming t(s, "subminor_select", sel_bytes + 8.0 * n_sel * ni);
+    rdl::SelScatter<<<n_chunks, rdl::kSelThreads, 0, st>>>(
+        sa, counts, ni, n_sel, h->d_pos, h->d_r);
+  }
+  RDL_HIP_CHECK(hipGetLastError());
+
+  // ---------------- partition and loop
+  const size_t bytes_per_px = 4 + 8 * size_t(ni);
+  const size_t lds_cap = 150 * 1024;
+  const uint32_t max_blocks = std::max(1, std::min(s->n_cus, 256));
+  uint32_t g;
+  if (n_sel <= 4096)
+    g = 1;
+  else
+    g = std::min<uint64_t>(max_blocks, (n_sel + 4095) / 4096);
+  uint64_t per = (n_sel + g - 1) / g;
+  bool use_lds = per * bytes_per_px <= lds_cap;
+  if (!use_lds) {
+    g = max_blocks;
+    per = (n_sel + g - 1) / g;
+    use_lds = per * bytes_per_px <= lds_cap;
+  }
+  const size_t lds_bytes = use_lds ? per * bytes_per_px : 0;
+  rdl::LoopArgs la{};
+  la.pos = h->d_pos;
+  la.r = h->d_r;
+  la.m = h->d_m;
+  la.psfs = d_psfs;
+  la.n_sel = n_sel;
+  la.per_block = uint32_t(per);
+  la.n_blocks = g;
+  la.rec_words = (4 + ni + 3) / 4 * 4;
+  la.width = p->width;
+  la.height = p->height;
+  la.n_img = ni;
+  la.n_pol = p->n_pol;
+  la.integ = p->integ;
+  la.threshold = p->threshold;
+  la.gain = p->gain;
+  la.divergence_limit = p->divergence_limit;
+  la.iteration_start = p->iteration_start;
+  la.max_iterations = p->max_iterations;
+  la.allow_negative = p->allow_negative;
+  la.stop_on_negative = p->stop_on_negative;
+  la.use_lds = use_lds ? 1 : 0;
+  const uint64_t n_trace = (h_trace && trace_cap) ? trace_cap : 0;
+  const size_t rec_bytes = size_t(2) * g * la.rec_words * sizeof(uint32_t);
+  const size_t sync_need = 256 + 256 + rec_bytes + n_trace * 8;
+  RDL_TRY(rdl::Grow(&h->sync, &h->sync_bytes, sync_need, st));
+  char* sb = static_cast<char*>(h->sync);
+  la.counter = reinterpret_cast<uint32_t*>(sb);
+  la.result = reinterpret_cast<uint32_t*>(sb + 256);
+  la.records = reinterpret_cast<uint32_t*>(sb + 512);
+  la.trace = n_trace ? reinterpret_cast<uint32_t*>(sb + 512 + rec_bytes) : nullptr;
+  la.trace_cap = n_trace;
+  RDL_HIP_CHECK(hipMemsetAsync(sb, 0, 512, st));
+  {
+    rdl::ScopedTiming t(s, "subminor_loop", 0.0);
+    if (ni == 1)
+      RDL_TRY(rdl::LaunchLoop<1>(la, lds_bytes, st));
+    else if (ni <= 2)
+      RDL_TRY(rdl::LaunchLoop<2>(la, lds_bytes, st));
+    else if (ni <= 4)
+      RDL_TRY(rdl::LaunchLoop<4>(la, lds_bytes, st));
+    else if (ni <= 8)
+      RDL_TRY(rdl::LaunchLoop<8>(la, lds_bytes, st));
+    else if (ni <= 16)
+      RDL_TRY(rdl::LaunchLoop<16>(la, lds_bytes, st));
+    else
+      RDL_TRY(rdl::LaunchLoop<RDL_MAX_IMAGES>(la, lds_bytes, st));
+  }
+  rdl::LoopResult res{};
+  uint32_t err = 0;
+  RDL_HIP_CHECK(hipMemcpyAsync(&res, la.result, sizeof(res),
+                               hipMemcpyDeviceToHost, st));
+  RDL_HIP_CHECK(hipMemcpyAsync(&err, la.result + 8, sizeof(err),
+                               hipMemcpyDeviceToHost, st));
+  RDL_HIP_CHECK(hipStreamSynchronize(st));
+  if (err) {
+    rdl::SetError("sub-minor loop: grid exchange timed out");
+    return RDL_ERR_TIMEOUT;
+  }
+  out->iteration = res.iteration;
+  out->has_peak = 1;
+  out->peak = res.peak;
+  out->diverging = res.diverging;
+  out->flux_cleaned = res.flux;
+  if (n_trace) {
+    const uint64_t n = std::min<uint64_t>(res.iteration - p->iteration_start, n_trace);
+    RDL_HIP_CHECK(hipMemcpyAsync(h_trace, la.trace, n * 8,
+                                 hipMemcpyDeviceToHost, st));
+    RDL_HIP_CHECK(hipStreamSynchronize(st));
+  }
+  return RDL_OK;
+}
+
+int rdl_subminor_model(rdl_subminor* h, uint32_t image_index, float* d_dest,
+                       uint32_t dest_w, uint32_t dest_h, uint32_t ox,
+                       uint32_t oy, int mode) {
+  RDL_ARG_CHECK(h && d_dest, "NULL argument");
+  RDL_ARG_CHECK(image_index < h->n_images || h->n_selected == 0,
+                "image index out of range");
+  RDL_ARG_CHECK(dest_w >= h->width + ox && dest_h >= h->height + oy,
+                "destination too small");
+  rdl_session* s = h->s;
+  if (mode == 0)
+    RDL_HIP_CHECK(hipMemsetAsync(d_dest, 0, size_t(dest_w) * dest_h * sizeof(float),
+                                 s->stream));
+  if (h->n_selected == 0) return RDL_OK;
+  const unsigned grid = std::min<uint64_t>(4096, rdl::DivUp(h->n_selected, 256));
+  rdl::ScatterModel<<<grid, 256, 0, s->stream>>>(
+      h->d_pos, h->d_m + size_t(image_index) * h->n_selected, h->n_selected,
+      d_dest, dest_w, ox, oy, mode == 1);
+  RDL_HIP_CHECK(hipGetLastError());
+  return RDL_OK;
+}
+
+int rdl_subminor_get(rdl_subminor* h, uint32_t* h_positions, float* h_models,
+                     uint64_t capacity) {
+  RDL_ARG_CHECK(h, "NULL argument");
+  const uint64_t n = std::min(capacity, h->n_selected);
+  if (n == 0) return RDL_OK;
+  if (h_positions)
+    RDL_HIP_CHECK(hipMemcpyAsync(h_positions, h->d_pos, n * sizeof(uint32_t),
+                                 hipMemcpyDeviceToHost, h->s->stream));
+  if (h_models)
+    for (uint32_t k = 0; k < h->n_images; ++k)
+      RDL_HIP_CHECK(hipMemcpyAsync(h_models + k * n, h->d_m + k * h->n_selected,
+                                   n * sizeof(float), hipMemcpyDeviceToHost,
+                                   h->s->stream));
+  RDL_HIP_CHECK(hipStreamSynchronize(h->s->stream));
+  return RDL_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,295 @@
+"""GPU parity of the C-ABI kernels against the CPU restatement (oracle/).
+
+Bit-exact for peak positions/values, PSF subtraction, integration, the
+Högbom loop and the sub-minor loop's component trace and model values; FFT
+convolutions within a float tolerance (rocFFT vs the oracle's float64 FFT):
+|err| <= 2e-6 * max|x| per convolution (tolerance written in each test).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from oracle_lib import OracleAlgorithm, get_oracle
+from rdl_lib import (HogbomParams, HogbomResult, Session, SubminorParams, SubminorResult,
+                     integration)
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def sess():
+    s = Session(0)
+    yield s
+    s.close()
+
+
+@pytest.fixture(scope="module")
+def orc():
+    return get_oracle()
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+# ------------------------------------------------------------------ peak
+PEAK_CASES = [
+    (64, 64, 0, 0), (63, 65, 3, 2), (1024, 1024, 51, 51), (4096, 17, 0, 1),
+    (17, 4096, 2, 100), (2, 18, 0, 0), (1000, 999, 0, 0),
+]
+
+
+@pytest.mark.parametrize("w,h,hb,vb", PEAK_CASES)
+@pytest.mark.parametrize("allow_negative", [True, False])
+def test_find_peak_random(sess, orc, w, h, hb, vb, allow_negative):
+    rng = np.random.default_rng(w * 7 + h)
+    img = rng.standard_normal((h, w)).astype(np.float32)
+    d = sess.array(img)
+    for start_y, end_y in ((0, h), (h // 3, h - h // 4)):
+        g = sess.find_peak(d, w, h, allow_negative, start_y, end_y, hb, vb)
+        o = orc.find_peak(img, allow_negative, start_y, end_y, hb, vb)
+        assert g[:3] == o[:3] and bits(g[3]) == bits(o[3])
+    d.free()
+
+
+def test_find_peak_ties_nan_mask(sess, orc):
+    rng = np.random.default_rng(1)
+    w, h = 300, 200
+    img = rng.integers(-3, 4, (h, w)).astype(np.float32)   # many exact ties
+    img[5, 7] = np.nan
+    d = sess.array(img)
+    mask = (rng.random((h, w)) < 0.3)
+    dm = sess.array(mask.astype(np.uint8))
+    for an in (True, False):
+        assert sess.find_peak(d, w, h, an)[:3] == orc.find_peak(img, an)[:3]
+        g = sess.find_peak(d, w, h, an, dmask=dm)
+        o = orc.find_peak(img, an, mask=mask)
+        assert g[:3] == o[:3]
+    # nothing qualifies: Avx returns (0,0)/image[0]; mask/simple return none
+    z = np.zeros((h, w), np.float32)
+    z[0, 0] = -1e-39   # denormal, <= FLT_MIN: never a peak
+    dz = sess.array(z)
+    assert sess.find_peak(dz, w, h)[:3] == (True, 0, 0)
+    assert sess.find_peak(dz, w, h, avx=False)[0] is False
+    assert sess.find_peak(dz, w, h, dmask=dm)[0] is False
+    # box degenerates when the border swallows the image
+    assert sess.find_peak(d, w, h, True, 0, h, 200, 0)[:3] == orc.find_peak(img, True, 0, h, 200, 0)[:3]
+    for x in (d, dm, dz):
+        x.free()
+
+
+# ------------------------------------------------------------------ subtract
+@pytest.mark.parametrize("w,h", [(64, 64), (63, 65), (257, 130)])
+def test_subtract_bit_exact(sess, orc, w, h):
+    rng = np.random.default_rng(5)
+    img = rng.standard_normal((h, w)).astype(np.float32)
+    psf = rng.standard_normal((h, w)).astype(np.float32)
+    d, dp = sess.array(img), sess.array(psf)
+    ref = img.copy()
+    for x, y in [(0, 0), (w - 1, h - 1), (w // 2, h // 2), (3, h - 2), (w - 5, 1)]:
+        f = np.float32(rng.standard_normal())
+        sess.rdl.rdl_subtract_psf(sess.h, d.vp, dp.vp, w, h, x, y, C.c_float(f))
+        orc.subtract(ref, psf, x, y, f)
+    assert np.array_equal(bits(d.get()), bits(ref))
+    d.free()
+    dp.free()
+
+
+# ------------------------------------------------------------------ integrate
+@pytest.mark.parametrize("n_ch,n_pol,weights,mode", [
+    (1, 1, None, 0), (3, 1, [0.5, 0.0, 4.2], 0), (4, 1, [1, 2, 3, 4], 1),
+    (2, 2, [0.7, 1.3], 0), (1, 4, None, 1), (3, 2, [1.0, 0.0, 2.0], 1)])
+def test_integrate_bit_exact(sess, orc, n_ch, n_pol, weights, mode):
+    rng = np.random.default_rng(9)
+    n, h, w = n_ch * n_pol, 37, 53
+    imgs = rng.standard_normal((n, h, w)).astype(np.float32)
+    if weights is not None and 0.0 in weights:
+        imgs[weights.index(0.0) * n_pol] = np.nan  # zero-weight channel may be NaN
+    pf = 0.5 if n_pol == 2 else 1.0
+    g = integration(n_ch, n_pol, weights, pf, mode)
+    di, dd = sess.array(imgs), sess.array(shape=(h, w))
+    sess.rdl.rdl_integrate(sess.h, C.byref(g), di.vp, C.c_size_t(h * w), dd.vp)
+    expect = orc.integrate(imgs, weights, n_pol, pf, square=(mode == 1))
+    assert np.array_equal(bits(dd.get()), bits(expect))
+    di.free()
+    dd.free()
+
+
+# ------------------------------------------------------------------ FFT
+def fft_convolve(sess, img, kernel):
+    h, w = img.shape
+    f = C.c_void_p()
+    sess.rdl.rdl_fft_create(sess.h, w, h, C.byref(f))
+    nb = sess.rdl.lib.rdl_fft_spectrum_bytes(f)
+    di, dk = sess.array(img), sess.array(kernel)
+    spec_k = sess.array(shape=(nb // 4,))
+    work = sess.array(shape=(nb // 4,))
+    sess.rdl.rdl_fft_forward(f, dk.vp, spec_k.vp)
+    sess.rdl.rdl_fft_convolve(f, di.vp, spec_k.vp, work.vp)
+    out = di.get()
+    for x in (di, dk, spec_k, work):
+        x.free()
+    sess.rdl.rdl_fft_destroy(f)
+    return out
+
+
+@pytest.mark.parametrize("w,h", [(64, 64), (1128, 96), (94, 47), (512, 512)])
+def test_fft_convolve(sess, orc, w, h):
+    rng = np.random.default_rng(11)
+    img = rng.standard_normal((h, w)).astype(np.float32)
+    ker = rng.standard_normal((h, w)).astype(np.float32)
+    g = fft_convolve(sess, img, ker)
+    o = img.copy()
+    orc.convolve(o, ker)
+    tol = 2e-6 * np.abs(o).max() * np.sqrt(np.log2(w * h))
+    assert np.abs(g - o).max() <= tol
+
+
+def test_prepare_kernels(sess, orc):
+    w, h, pw, ph = 40, 30, 48, 36
+    rng = np.random.default_rng(2)
+    psf = rng.standard_normal((h, w)).astype(np.float32)
+    dp, dk = sess.array(psf), sess.array(shape=(ph, pw))
+    sess.rdl.rdl_prepare_psf_kernel(sess.h, dk.vp, pw, ph, dp.vp, w, h)
+    unt = np.zeros((ph, pw), np.float32)
+    unt[(ph - h) // 2:(ph - h) // 2 + h, (pw - w) // 2:(pw - w) // 2 + w] = psf
+    expect = np.roll(unt, (-(ph // 2), -(pw // 2)), axis=(0, 1))
+    assert np.array_equal(dk.get(), expect)
+    k = orc.shape_function(8.0, 64, 0)
+    n = k.shape[0]
+    sess.rdl.rdl_prepare_small_kernel(sess.h, dk.vp, pw, ph, k.ctypes.data_as(C.c_void_p), n)
+    full = np.zeros((ph, pw), np.float32)
+    full[:n, :n] = k
+    assert np.array_equal(dk.get(), np.roll(full, (-(n // 2), -(n // 2)), axis=(0, 1)))
+    dp.free()
+    dk.free()
+
+
+def test_median(sess):
+    rng = np.random.default_rng(4)
+    for n in (1, 2, 1001, 4096):
+        v = rng.standard_normal(n).astype(np.float32)
+        d = sess.array(v)
+        out = C.c_float()
+        sess.rdl.rdl_median(sess.h, d.vp, C.c_size_t(n), 0, C.c_float(0), C.byref(out))
+        s = np.sort(v)
+        med = s[n // 2] if n % 2 else np.float32(0.5) * (s[n // 2 - 1] + s[n // 2])
+        assert out.value == med
+        d.free()
+
+
+# ------------------------------------------------------------------ loops
+def synthetic(w, h, n_src, seed, psf_fwhm=3.0):
+    """Small deterministic sky ⊛ analytic PSF (peak exactly 1.0 at (w/2, h/2))."""
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:h, 0:w]
+    s = psf_fwhm / 2.355
+    r2 = ((xx - w // 2) ** 2 + (yy - h // 2) ** 2)
+    psf = np.exp(-r2 / (2 * s * s)) + 0.05 * np.cos(2 * np.pi * np.sqrt(r2) / 9.0) * np.exp(-np.sqrt(r2) / 20.0)
+    psf = (psf / psf[h // 2, w // 2]).astype(np.float32)
+    sky = np.zeros((h, w))
+    xs = rng.integers(8, w - 8, n_src)
+    ys = rng.integers(8, h - 8, n_src)
+    fl = np.exp(rng.uniform(np.log(0.01), np.log(1.0), n_src))
+    for x, y, f in zip(xs, ys, fl):
+        sky[y, x] += f
+    P = np.fft.fft2(np.fft.ifftshift(psf.astype(np.float64)))
+    dirty = np.real(np.fft.ifft2(np.fft.fft2(sky) * P))
+    dirty += 1e-3 * rng.standard_normal((h, w))
+    return psf, dirty.astype(np.float32)
+
+
+def test_hogbom_bit_exact(sess, orc):
+    w = h = 256
+    psf, dirty = synthetic(w, h, 40, 3)
+    niter, gain = 400, 0.1
+    # oracle
+    res_o, mod_o = dirty[None].copy(), np.zeros((1, h, w), np.float32)
+    alg = OracleAlgorithm(orc, 0, threshold=0.0, max_iterations=niter, border_ratio=0.0,
+                          use_sub_minor=0)
+    r, trace_o = alg.execute(res_o, mod_o, psf[None])
+    # GPU: initial FindPeak on the (linear) integrated image, then the loop
+    dres, dmod, dpsf = sess.array(dirty), sess.array(shape=(h, w)), sess.array(psf)
+    found, x, y, v = sess.find_peak(dres, w, h)
+    p = HogbomParams()
+    p.width, p.height, p.n_images, p.n_pol = w, h, 1, 1
+    p.integ = integration(1, 1, mode=1)
+    p.gain, p.threshold, p.initial_max = gain, 0.0, abs(v)
+    p.divergence_limit = 4.0
+    p.iteration_start, p.max_iterations = 0, niter
+    p.allow_negative, p.stop_on_negative = 1, 0
+    p.start_x, p.start_y, p.start_value, p.start_found = x, y, v, int(found)
+    res = HogbomResult()
+    trace = np.zeros((niter, 2), np.uint32)
+    sess.rdl.rdl_hogbom_run(sess.h, dres.vp, dmod.vp, dpsf.vp, C.byref(p), C.byref(res),
+                            trace.ctypes.data_as(C.c_void_p), C.c_uint64(niter))
+    assert res.iteration == r.iteration_number == niter
+    assert np.array_equal(trace, trace_o[:, :2])
+    assert np.array_equal(bits(dres.get()), bits(res_o[0]))
+    assert np.array_equal(bits(dmod.get()), bits(mod_o[0]))
+    assert bits(res.peak) == bits(r.final_peak)
+    for a in (dres, dmod, dpsf):
+        a.free()
+
+
+@pytest.mark.parametrize("w,n_src,threshold_frac,mgain,max_iter", [
+    (128, 10, 0.0, 0.8, 300),       # small set: one workgroup
+    (512, 200, 0.002, 1.0, 2000),   # noise-level selection: multi-workgroup exchange
+])
+def test_subminor_loop_bit_exact(sess, orc, w, n_src, threshold_frac, mgain, max_iter):
+    """GenericClean's Clark path: the sub-minor loop's component trace and
+    model values are bit-exact; the residual after CorrectResidualDirty is
+    FFT-based (rocFFT vs float64), |err| <= 5e-6 * max|dirty|."""
+    h = w
+    psf, dirty = synthetic(w, h, n_src, 7)
+    res_o, mod_o = dirty[None].copy(), np.zeros((1, h, w), np.float32)
+    pk = float(np.abs(dirty).max())
+    thr = threshold_frac * pk
+    alg = OracleAlgorithm(orc, 0, threshold=thr, max_iterations=max_iter, border_ratio=0.0,
+                          use_sub_minor=1, major_loop_gain=mgain)
+    r, trace_o = alg.execute(res_o, mod_o, psf[None])
+    # GPU, as GenericClean::ExecuteMajorIteration with sub-minor optimisation
+    dres, dpsf = sess.array(dirty), sess.array(psf)
+    found, x, y, v = sess.find_peak(dres, w, h)
+    # generic_clean.cc:99-112 in float arithmetic
+    first = max(np.float32(thr),
+                np.float32(abs(v)) * (np.float32(1.0) - np.float32(mgain)))
+    sm = C.c_void_p()
+    sess.rdl.rdl_subminor_create(sess.h, C.byref(sm))
+    p = SubminorParams()
+    p.width, p.height, p.n_images, p.n_pol = w, h, 1, 1
+    p.integ = integration(1, 1, mode=0)
+    p.allow_negative, p.stop_on_negative = 1, 0
+    p.threshold, p.gain, p.divergence_limit = np.float32(first), 0.1, 4.0
+    p.iteration_start, p.max_iterations = 0, max_iter
+    out = SubminorResult()
+    trace = np.zeros((max_iter, 2), np.uint32)
+    sess.rdl.rdl_subminor_run(sm, dres.vp, dpsf.vp, C.byref(p), C.byref(out),
+                              trace.ctypes.data_as(C.c_void_p), C.c_uint64(max_iter))
+    n_it = out.iteration
+    assert n_it == r.iteration_number
+    assert np.array_equal(trace[:n_it], trace_o[:n_it, :2])
+    # model via the scatter path; CorrectResidualDirty on the padded grid
+    dmod = sess.array(shape=(h, w))
+    sess.rdl.rdl_subminor_model(sm, 0, dmod.vp, w, h, 0, 0, 1)
+    assert np.array_equal(bits(dmod.get()), bits(mod_o[0]))
+    pw = ph = int(np.ceil(np.float32(1.1) * np.float32(w)))
+    pw += pw % 2
+    ph = pw
+    f = C.c_void_p()
+    sess.rdl.rdl_fft_create(sess.h, pw, ph, C.byref(f))
+    nb = sess.rdl.lib.rdl_fft_spectrum_bytes(f)
+    kern, spec_k = sess.array(shape=(ph, pw)), sess.array(shape=(nb // 4,))
+    padded, work = sess.array(shape=(ph, pw)), sess.array(shape=(nb // 4,))
+    sess.rdl.rdl_prepare_psf_kernel(sess.h, kern.vp, pw, ph, dpsf.vp, w, h)
+    sess.rdl.rdl_fft_forward(f, kern.vp, spec_k.vp)
+    sess.rdl.rdl_subminor_model(sm, 0, padded.vp, pw, ph, (pw - w) // 2, (ph - h) // 2, 0)
+    sess.rdl.rdl_fft_convolve(f, padded.vp, spec_k.vp, work.vp)
+    sess.rdl.rdl_trim_subtract(sess.h, dres.vp, w, h, padded.vp, pw, ph)
+    g = dres.get()
+    assert np.abs(g - res_o[0]).max() <= 5e-6 * np.abs(dirty).max()
+    sess.rdl.rdl_fft_destroy(f)
+    sess.rdl.rdl_subminor_destroy(sm)
+    for a in (dres, dpsf, dmod, kern, spec_k, padded, work):
+        a.free()
