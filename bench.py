@@ -1,0 +1,250 @@
+#!/usr/bin/env python3
+"""Benchmark: CLEAN components/sec and wall-clock-to-threshold of Radler's
+multiscale CLEAN on an 8192^2 synthetic sky (BASELINE.json metric), on the
+MI355X-native engine.
+
+One step = one major iteration to threshold (Radler::Perform's hot path,
+ParallelDeconvolution -> MultiScaleAlgorithm) on the device-resident image set,
+restored to the same dirty image before every step (a 256 MiB device copy,
+inside the timed region). Inputs are resident in HBM when timing starts.
+
+Multi-GPU (weak scaling): one process per GPU (torch.distributed, RCCL); each
+rank deconvolves its own 8192^2 field of the mosaic (independent subimages, as
+ParallelDeconvolution does with one subimage per GPU); barrier + sync bracket
+the timed region and the slowest rank's time is used. value = components of
+all ranks / that time.
+
+Also reported: `roofline` of the dominant kernel family (HIP-event device
+time, algorithmic bytes per SURVEY.md §8(d)) and `cpu_baseline` = the oracle
+(C++ restatement, std::thread) on a bounded sample of the same workload.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "ska-sdp-func-radler_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PIXEL_SCALE = 1.0 / 3600.0 * np.pi / 180.0  # 1 arcsec
+BEAM_PX = 4.0
+NOISE = 1e-4
+SEED = 20251015
+
+
+def make_problem(size, seed, n_points, n_blobs, fwhm=4.0):
+    from synthetic import make_dirty, make_psf, make_sky
+    psf = make_psf(size, size, fwhm=fwhm)
+    sky = make_sky(size, size, n_points, n_blobs, seed, flux_range=(1e-3, 1.0),
+                   blob_sigma=(2.0, 40.0))
+    dirty = make_dirty(psf, sky, NOISE, seed)
+    return psf, dirty
+
+
+def settings_for(rd, size, max_iter, max_scales, threshold):
+    s = rd.Settings()
+    s.algorithm_type = rd.AlgorithmType.multiscale
+    s.trimmed_image_width = s.trimmed_image_height = size
+    s.pixel_scale.x = s.pixel_scale.y = PIXEL_SCALE
+    s.minor_iteration_count = max_iter
+    s.absolute_threshold = threshold
+    s.minor_loop_gain = 0.1
+    s.major_loop_gain = 1.0
+    s.allow_negative_components = True
+    s.border_ratio = 0.0
+    s.multiscale.max_scales = max_scales
+    return s
+
+
+# algorithmic bytes per launch are accumulated by the C-ABI per family
+FAMILIES = ["fft", "spectrum_multiply", "find_peak", "subminor_loop", "subminor_select",
+            "trim_subtract", "add", "integrate", "rms", "axpy", "radix_select"]
+
+
+class Timing:
+    def __init__(self, session_handle):
+        self.lib = C.CDLL(os.path.join(ROOT, "ska-sdp-func-radler_amd", "lib", "librdl_hip.so"))
+        self.h = C.c_void_p(session_handle)
+        self.lib.rdl_timing_get.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.c_double),
+                                            C.POINTER(C.c_uint64), C.POINTER(C.c_double)]
+
+    def enable(self, on):
+        self.lib.rdl_timing_enable(self.h, int(on))
+
+    def reset(self):
+        self.lib.rdl_timing_reset(self.h)
+
+    def get(self):
+        out = {}
+        for fam in FAMILIES:
+            ms, n, b = C.c_double(), C.c_uint64(), C.c_double()
+            self.lib.rdl_timing_get(self.h, fam.encode(), C.byref(ms), C.byref(n), C.byref(b))
+            if n.value:
+                out[fam] = {"ms": ms.value, "launches": n.value, "bytes": b.value}
+        return out
+
+
+def cpu_baseline(size, n_points, n_blobs, max_scales, threshold, sample_components, threads):
+    """The oracle (tests/oracle_lib -> oracle/build/liboracle.so) on the first
+    `sample_components` components of the same workload."""
+    from oracle_lib import OracleAlgorithm, get_oracle
+    orc = get_oracle()
+    orc.set_threads(threads)
+    psf, dirty = make_problem(size, SEED, n_points, n_blobs)
+    res, mod = dirty[None].copy(), np.zeros_like(dirty)[None]
+    alg = OracleAlgorithm(orc, 1, threshold=threshold, max_iterations=sample_components,
+                          border_ratio=0.0, max_scales=max_scales, beam_size_in_pixels=BEAM_PX,
+                          minor_loop_gain=0.1, major_loop_gain=1.0)
+    t0 = time.perf_counter()
+    r, _ = alg.execute(res, mod, psf[None], trace_cap=1)
+    dt = time.perf_counter() - t0
+    return {"value": r.iteration_number / dt, "unit": "components/s", "cores": threads,
+            "kind": "port",
+            "sample": (f"oracle MultiScale (C++ restatement, float64 FFT) on the same "
+                       f"{size}x{size} {max_scales}-scale sky, first {r.iteration_number} "
+                       f"components incl. PSF/scale setup, {dt:.1f} s")}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--size", type=int, default=8192)
+    ap.add_argument("--scales", type=int, default=6)
+    ap.add_argument("--points", type=int, default=2000)
+    ap.add_argument("--blobs", type=int, default=200)
+    ap.add_argument("--max-iter", type=int, default=1000000)
+    ap.add_argument("--sigma", type=float, default=5.0)
+    ap.add_argument("--cpu-sample", type=int, default=200,
+                    help="components in the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--breakdown", action="store_true", help="per-kernel times to stderr")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local_rank)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        dist = tdist
+    os.environ.setdefault("RADLER_DEVICE", str(local_rank))
+
+    import radler as rd
+
+    threshold = args.sigma * NOISE
+    psf, dirty = make_problem(args.size, SEED + rank, args.points, args.blobs)
+    s = settings_for(rd, args.size, args.max_iter, args.scales, threshold)
+    run = rd.gpu.DeviceRun(s, psf, dirty, [], BEAM_PX * PIXEL_SCALE)
+    timing = Timing(run.session_handle())
+
+    for _ in range(args.warmup):
+        run.restore()
+        run.execute()
+    run.sync()
+
+    def barrier():
+        if dist is not None:
+            import torch
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    timing.reset()
+    timing.enable(True)
+    barrier()
+    run.sync()
+    t0 = time.perf_counter()
+    comps, results = 0, []
+    for _ in range(args.steps):
+        run.restore()
+        r = run.execute()
+        comps += r["iterations"]
+        results.append(r)
+    run.sync()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    timing.enable(False)
+    fams = timing.get()
+
+    total_comps, max_elapsed = comps, elapsed
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        c = torch.tensor([comps], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        max_elapsed, total_comps = float(t.item()), int(c.item())
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    ms_per_step = 1e3 * max_elapsed / args.steps
+    device_ms = sum(v["ms"] for v in fams.values())
+    # dominant kernel family by device time
+    dom_name, dom = max(fams.items(), key=lambda kv: kv[1]["ms"]) if fams else (None, None)
+    roofline = None
+    if dom is not None and dom["ms"] > 0:
+        avg_ms = dom["ms"] / dom["launches"]
+        bytes_per_launch = dom["bytes"] / dom["launches"]
+        achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+        roofline = {"bound": "hbm", "kernel": dom_name, "achieved": round(achieved, 1),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                    "avg_launch_us": round(avg_ms * 1e3, 2),
+                    "bytes_per_launch": bytes_per_launch,
+                    "share_of_device_time": round(dom["ms"] / device_ms, 3) if device_ms else None}
+    if args.breakdown:
+        for k, v in sorted(fams.items(), key=lambda kv: -kv[1]["ms"]):
+            gbs = v["bytes"] / (v["ms"] * 1e-3) / 1e9 if v["ms"] else 0.0
+            print(f"[breakdown] {k:18s} {v['ms']:10.2f} ms {v['launches']:8d} launches "
+                  f"{gbs:8.1f} GB/s", file=sys.stderr)
+        print(f"[breakdown] device {device_ms:.1f} ms of {1e3 * elapsed:.1f} ms wall; "
+              f"results {results}", file=sys.stderr)
+
+    cpu = None
+    if args.cpu_sample > 0 and world == 1:
+        cpu = cpu_baseline(args.size, args.points, args.blobs, args.scales, threshold,
+                           args.cpu_sample, args.cpu_threads)
+
+    line = {
+        "metric": "CLEAN components/sec (multiscale, to 5-sigma threshold)",
+        "value": round(total_comps / max_elapsed, 2),
+        "unit": "components/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 2),
+        "wall_clock_to_threshold_s": round(max_elapsed / args.steps, 4),
+        "components_per_step": total_comps // (args.steps * world),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded sky: points + Gaussian blobs, analytic PSF, noise)",
+        "config": {"workload": f"multiscale-{args.size}x{args.size}-{args.scales}scales",
+                   "image": [args.size, args.size], "scales": args.scales,
+                   "points": args.points, "blobs": args.blobs, "noise": NOISE,
+                   "threshold": threshold, "minor_loop_gain": 0.1, "major_loop_gain": 1.0,
+                   "fields_per_gpu": 1, "parallelism": f"fields{world}"},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -106,6 +106,7 @@ typedef struct {
   uint32_t n_channels;
   uint32_t mode;           /* RDL_INTEGRATE_* */
   uint32_t copy_fast_path; /* image_set.cc:425-430 / :289-301 (1 image) */
+  uint32_t pol_mask;       /* bit p: polarization p is joined (linked) */
   float weights[RDL_MAX_IMAGES]; /* channel weight of each image; 0 skips */
   /* LINEAR: float(pol_factor/sum w); SQUARE with 1 channel: sqrtf(pol_factor);
    * SQUARE with >1 channel: float(sqrtf(pol_factor)/sum w);
@@ -125,6 +126,11 @@ int rdl_integrate(rdl_session* s, const rdl_integration* integ,
 int rdl_axpy(rdl_session* s, float* d_dest, const float* d_a, size_t n,
              float alpha, int assign);
 int rdl_scale(rdl_session* s, float* d_dest, size_t n, float alpha);
+/* Double-precision accumulation of ImageSet::LoadAndAveragePsfs
+ * (cpp/image_set.cc:167-186): mode 0: dest = float(fma(double(a), alpha,
+ * double(dest))); mode 1: dest = float(double(dest) * alpha) (d_a unused). */
+int rdl_axpy_f64(rdl_session* s, float* d_dest, const float* d_a, size_t n,
+                 double alpha, int mode);
 /* dest += a (model accumulation, multiscale_algorithm.cc:457-460). */
 int rdl_add(rdl_session* s, float* d_dest, const float* d_a, size_t n);
 
@@ -217,6 +223,11 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
 int rdl_subminor_model(rdl_subminor* h, uint32_t image_index, float* d_dest,
                        uint32_t dest_w, uint32_t dest_h, uint32_t ox,
                        uint32_t oy, int mode);
+/* As mode 0 of rdl_subminor_model, into a zeroed float64 plane (input of the
+ * double-precision residual correction, rdl_fft64_convolve). */
+int rdl_subminor_model_f64(rdl_subminor* h, uint32_t image_index,
+                           double* d_dest, uint32_t dest_w, uint32_t dest_h,
+                           uint32_t ox, uint32_t oy);
 /* Selected positions (packed y<<16|x) and per-image model values of the last
  * run, copied to host (UpdateComponentList / UpdateAutoMask inputs). */
 int rdl_subminor_get(rdl_subminor* h, uint32_t* h_positions, float* h_models,
@@ -227,11 +238,23 @@ int rdl_subminor_get(rdl_subminor* h, uint32_t* h_positions, float* h_models,
  * Spectra are (width/2+1) x height complex float. */
 int rdl_fft_create(rdl_session* s, uint32_t width, uint32_t height,
                    rdl_fft** out);
+/* Same pair in double precision: spectra are (width/2+1) x height complex
+ * double. Used for SubMinorLoop::CorrectResidualDirty (subminor_loop.cc:
+ * 195-218), whose result feeds every later peak search: the float64 pass
+ * keeps the corrected residual within float rounding of the exact
+ * convolution (see DESIGN.md "Residual correction precision"). */
+int rdl_fft_create_f64(rdl_session* s, uint32_t width, uint32_t height,
+                       rdl_fft** out);
 int rdl_fft_destroy(rdl_fft* f);
 size_t rdl_fft_spectrum_bytes(const rdl_fft* f);
 int rdl_fft_forward(rdl_fft* f, const float* d_in, void* d_spectrum);
 /* Unnormalised inverse; d_spectrum is destroyed. */
 int rdl_fft_inverse(rdl_fft* f, void* d_spectrum, float* d_out);
+int rdl_fft64_forward(rdl_fft* f, const double* d_in, void* d_spectrum);
+int rdl_fft64_inverse(rdl_fft* f, void* d_spectrum, double* d_out);
+/* In-place circular convolution in double precision (see rdl_fft_convolve). */
+int rdl_fft64_convolve(rdl_fft* f, double* d_image, const void* d_kernel_spectrum,
+                       void* d_work);
 /* dst = a * b * scale, complex, n_complex elements. */
 int rdl_spectrum_multiply(rdl_session* s, void* d_dst, const void* d_a,
                           const void* d_b, size_t n_complex, float scale);
@@ -252,6 +275,14 @@ int rdl_prepare_small_kernel(rdl_session* s, float* d_dest, uint32_t width,
 int rdl_prepare_psf_kernel(rdl_session* s, float* d_dest, uint32_t pw,
                            uint32_t ph, const float* d_psf, uint32_t width,
                            uint32_t height);
+/* rdl_prepare_psf_kernel into a float64 plane. */
+int rdl_prepare_psf_kernel_f64(rdl_session* s, double* d_dest, uint32_t pw,
+                               uint32_t ph, const float* d_psf, uint32_t width,
+                               uint32_t height);
+/* Image::Trim into float + `residual -= trimmed` from a float64 plane. */
+int rdl_trim_subtract_f64(rdl_session* s, float* d_residual, uint32_t width,
+                          uint32_t height, const double* d_padded, uint32_t pw,
+                          uint32_t ph);
 /* Image::Trim + `residual -= trimmed` (subminor_loop.cc:214-217). */
 int rdl_trim_subtract(rdl_session* s, float* d_residual, uint32_t width,
                       uint32_t height, const float* d_padded, uint32_t pw,

@@ -4,6 +4,8 @@
 
 #include <algorithm>
 #include <cassert>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 
@@ -1030,6 +1032,14 @@ Result MultiScale::Execute(ImageSet& data, ImageSet& model,
     }
     ActivateScales(scale_with_peak);
     FindActiveScaleConvolvedMaxima(data, integrated.data(), false);
+    if (std::getenv("ORACLE_DEBUG")) {
+      std::fprintf(stderr, "[ms] it=%zu", iteration_number);
+      for (const ScaleInfo& e : scales_)
+        std::fprintf(stderr, " | s=%g a=%d v=%.9g x=%zu y=%zu", e.scale,
+                     int(e.is_active), e.max_unnormalized_image_value * e.bias_factor,
+                     e.max_image_value_x, e.max_image_value_y);
+      std::fprintf(stderr, "\n");
+    }
     if (!SelectMaximumScale(scales_, scale_with_peak)) {
       result.another_iteration_required = false;
       return result;

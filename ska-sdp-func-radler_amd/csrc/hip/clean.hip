@@ -265,9 +265,8 @@ int rdl_hogbom_run(rdl_session* s, float* d_residuals, float* d_models,
   const size_t state_bytes = (sizeof(rdl::HogbomState) + 255) / 256 * 256;
   const size_t part_bytes = size_t(a.n_blocks) * sizeof(uint64_t);
   const size_t trace_bytes = n_trace * 2 * sizeof(uint32_t);
-  void* buf = nullptr;
-  RDL_HIP_CHECK(hipMallocAsync(&buf, state_bytes + part_bytes + trace_bytes,
-                               s->stream));
+  RDL_TRY(s->EnsureScratch(s->loop_state, state_bytes + part_bytes + trace_bytes));
+  void* buf = s->loop_state.ptr;
   a.state = static_cast<rdl::HogbomState*>(buf);
   a.partials = reinterpret_cast<uint64_t*>(static_cast<char*>(buf) + state_bytes);
   a.trace = n_trace ? reinterpret_cast<uint32_t*>(static_cast<char*>(buf) +
@@ -321,7 +320,6 @@ int rdl_hogbom_run(rdl_session* s, float* d_residuals, float* d_models,
     RDL_HIP_CHECK(hipMemcpyAsync(h_trace, a.trace, n * 2 * sizeof(uint32_t),
                                  hipMemcpyDeviceToHost, s->stream));
   }
-  RDL_HIP_CHECK(hipFreeAsync(buf, s->stream));
   RDL_HIP_CHECK(hipStreamSynchronize(s->stream));
   out->iteration = st.iteration;
   out->found = st.found;

@@ -20,7 +20,19 @@ __global__ __launch_bounds__(256) void AxpyKernel(float* dest, const float* a,
                                                   int assign) {
   for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n;
        i += size_t(gridDim.x) * blockDim.x) {
-    dest[i] = assign ? a[i] * alpha : __builtin_fmaf(a[i], alpha, dest[i]);
+    dest[i] = assign == 1   ? a[i] * alpha
+              : assign == 2 ? dest[i] + a[i]
+                            : __builtin_fmaf(a[i], alpha, dest[i]);
+  }
+}
+
+__global__ __launch_bounds__(256) void AxpyF64Kernel(float* dest,
+                                                     const float* a, size_t n,
+                                                     double alpha, int mode) {
+  for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n;
+       i += size_t(gridDim.x) * blockDim.x) {
+    dest[i] = mode == 0 ? float(__builtin_fma(double(a[i]), alpha, double(dest[i])))
+                        : float(double(dest[i]) * alpha);
   }
 }
 
@@ -97,6 +109,16 @@ int rdl_axpy(rdl_session* s, float* d_dest, const float* d_a, size_t n,
   return RDL_OK;
 }
 
+int rdl_axpy_f64(rdl_session* s, float* d_dest, const float* d_a, size_t n,
+                 double alpha, int mode) {
+  RDL_ARG_CHECK(s && d_dest && (d_a || mode == 1), "NULL argument");
+  if (n == 0) return RDL_OK;
+  rdl::AxpyF64Kernel<<<rdl::GridFor(n), 256, 0, s->stream>>>(d_dest, d_a, n,
+                                                              alpha, mode);
+  RDL_HIP_CHECK(hipGetLastError());
+  return RDL_OK;
+}
+
 int rdl_scale(rdl_session* s, float* d_dest, size_t n, float alpha) {
   RDL_ARG_CHECK(s && d_dest, "NULL argument");
   if (n == 0) return RDL_OK;
@@ -107,13 +129,15 @@ int rdl_scale(rdl_session* s, float* d_dest, size_t n, float alpha) {
 
 int rdl_add(rdl_session* s, float* d_dest, const float* d_a, size_t n) {
   RDL_ARG_CHECK(s && d_dest && d_a, "NULL argument");
-  RDL_ARG_CHECK(reinterpret_cast<uintptr_t>(d_dest) % 16 == 0 &&
-                    reinterpret_cast<uintptr_t>(d_a) % 16 == 0,
-                "rdl_add needs 16-byte aligned planes");
   if (n == 0) return RDL_OK;
   rdl::ScopedTiming t(s, "add", double(n) * 12.0);
-  rdl::AddKernel<<<rdl::GridFor(n / 4 + 1), 256, 0, s->stream>>>(d_dest, d_a,
-                                                                  n);
+  if (reinterpret_cast<uintptr_t>(d_dest) % 16 == 0 &&
+      reinterpret_cast<uintptr_t>(d_a) % 16 == 0)
+    rdl::AddKernel<<<rdl::GridFor(n / 4 + 1), 256, 0, s->stream>>>(d_dest, d_a,
+                                                                    n);
+  else
+    rdl::AxpyKernel<<<rdl::GridFor(n), 256, 0, s->stream>>>(d_dest, d_a, n,
+                                                             1.0f, 2);
   RDL_HIP_CHECK(hipGetLastError());
   return RDL_OK;
 }
@@ -124,10 +148,10 @@ int rdl_add_shape_component(rdl_session* s, float* d_image, uint32_t width,
   RDL_ARG_CHECK(s && d_image && h_kernel && n > 0, "bad argument");
   RDL_ARG_CHECK(x < width && y < height, "component outside the image");
   const size_t kbytes = size_t(n) * n * sizeof(float);
-  RDL_ARG_CHECK(kbytes <= (1 << 16), "shape kernel larger than 64 KiB scratch");
-  // d_small holds the kernel for the duration of the launch (stream ordered)
-  RDL_HIP_CHECK(hipMemcpyAsync(s->d_small, h_kernel, kbytes,
-                               hipMemcpyHostToDevice, s->stream));
+  RDL_TRY(s->EnsureScratch(s->kernel, kbytes));
+  float* d_k = static_cast<float*>(s->kernel.ptr);
+  RDL_HIP_CHECK(hipMemcpyAsync(d_k, h_kernel, kbytes, hipMemcpyHostToDevice,
+                               s->stream));
   const uint32_t left = x > n / 2 ? x - n / 2 : 0;
   const uint32_t top = y > n / 2 ? y - n / 2 : 0;
   const uint32_t right = std::min(x + (n + 1) / 2, width);
@@ -135,8 +159,7 @@ int rdl_add_shape_component(rdl_session* s, float* d_image, uint32_t width,
   if (right > left && bottom > top) {
     dim3 grid(rdl::DivUp(right - left, 64), bottom - top);
     rdl::AddShapeKernel<<<grid, 64, 0, s->stream>>>(
-        d_image, width, static_cast<const float*>(s->d_small), n, x, y, left,
-        top, right, bottom, gain);
+        d_image, width, d_k, n, x, y, left, top, right, bottom, gain);
     RDL_HIP_CHECK(hipGetLastError());
   }
   RDL_HIP_CHECK(hipStreamSynchronize(s->stream));

@@ -20,6 +20,7 @@ std::once_flag g_rocfft_once;
 struct rdl_fft {
   rdl_session* s = nullptr;
   uint32_t width = 0, height = 0;
+  bool f64 = false;
   rocfft_plan fwd = nullptr, inv = nullptr;
   rocfft_execution_info info_fwd = nullptr, info_inv = nullptr;
   void* work = nullptr;
@@ -46,6 +47,21 @@ __global__ __launch_bounds__(256) void SpectrumMultiply(float2* dst,
        i += size_t(gridDim.x) * blockDim.x) {
     const float2 x = a[i], y = b[i];
     float2 r;
+    r.x = (x.x * y.x - x.y * y.y) * scale;
+    r.y = (x.x * y.y + x.y * y.x) * scale;
+    dst[i] = r;
+  }
+}
+
+__global__ __launch_bounds__(256) void SpectrumMultiplyF64(double2* dst,
+                                                           const double2* a,
+                                                           const double2* b,
+                                                           size_t n,
+                                                           double scale) {
+  for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n;
+       i += size_t(gridDim.x) * blockDim.x) {
+    const double2 x = a[i], y = b[i];
+    double2 r;
     r.x = (x.x * y.x - x.y * y.y) * scale;
     r.y = (x.x * y.y + x.y * y.x) * scale;
     dst[i] = r;
@@ -88,6 +104,40 @@ __global__ __launch_bounds__(256) void PreparePsfKernel(float* dest,
     if (sx >= ox && sx < ox + w && sy >= oy && sy < oy + h)
       v = psf[size_t(sy - oy) * w + (sx - ox)];
     dest[i] = v;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void PreparePsfKernelT(T* dest, uint32_t pw,
+                                                         uint32_t ph,
+                                                         const float* psf,
+                                                         uint32_t w, uint32_t h) {
+  const uint32_t ox = (pw - w) / 2, oy = (ph - h) / 2;
+  const size_t total = size_t(pw) * ph;
+  for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < total;
+       i += size_t(gridDim.x) * blockDim.x) {
+    const uint32_t x = i % pw, y = i / pw;
+    const uint32_t sx = (x + pw / 2) % pw, sy = (y + ph / 2) % ph;
+    T v = T(0);
+    if (sx >= ox && sx < ox + w && sy >= oy && sy < oy + h)
+      v = T(psf[size_t(sy - oy) * w + (sx - ox)]);
+    dest[i] = v;
+  }
+}
+
+// residual -= float(trimmed convolution): the reference trims into a float
+// scratch image before subtracting (subminor_loop.cc:214-217).
+__global__ __launch_bounds__(256) void TrimSubtractF64(float* residual,
+                                                       uint32_t w, uint32_t h,
+                                                       const double* padded,
+                                                       uint32_t pw,
+                                                       uint32_t ph) {
+  const uint32_t ox = (pw - w) / 2, oy = (ph - h) / 2;
+  const size_t total = size_t(w) * h;
+  for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < total;
+       i += size_t(gridDim.x) * blockDim.x) {
+    const uint32_t x = i % w, y = i / w;
+    residual[i] -= float(padded[size_t(y + oy) * pw + x + ox]);
   }
 }
 
@@ -138,10 +188,8 @@ inline unsigned Grid(size_t n) {
 
 }  // namespace rdl
 
-extern "C" {
-
-int rdl_fft_create(rdl_session* s, uint32_t width, uint32_t height,
-                   rdl_fft** out) {
+static int CreateFft(rdl_session* s, uint32_t width, uint32_t height, bool f64,
+                     rdl_fft** out) {
   RDL_ARG_CHECK(s && out, "NULL argument");
   RDL_ARG_CHECK(width >= 2 && height >= 1, "bad FFT size");
   std::call_once(g_rocfft_once, [] { rocfft_setup(); });
@@ -150,15 +198,16 @@ int rdl_fft_create(rdl_session* s, uint32_t width, uint32_t height,
   f->s = s;
   f->width = width;
   f->height = height;
+  f->f64 = f64;
+  const rocfft_precision prec =
+      f64 ? rocfft_precision_double : rocfft_precision_single;
   size_t lengths[2] = {width, height};  // fastest dimension first
   RDL_FFT_CHECK(rocfft_plan_create(&f->fwd, rocfft_placement_notinplace,
-                                   rocfft_transform_type_real_forward,
-                                   rocfft_precision_single, 2, lengths, 1,
-                                   nullptr));
+                                   rocfft_transform_type_real_forward, prec, 2,
+                                   lengths, 1, nullptr));
   RDL_FFT_CHECK(rocfft_plan_create(&f->inv, rocfft_placement_notinplace,
-                                   rocfft_transform_type_real_inverse,
-                                   rocfft_precision_single, 2, lengths, 1,
-                                   nullptr));
+                                   rocfft_transform_type_real_inverse, prec, 2,
+                                   lengths, 1, nullptr));
   size_t w1 = 0, w2 = 0;
   RDL_FFT_CHECK(rocfft_plan_get_work_buffer_size(f->fwd, &w1));
   RDL_FFT_CHECK(rocfft_plan_get_work_buffer_size(f->inv, &w2));
@@ -178,6 +227,29 @@ int rdl_fft_create(rdl_session* s, uint32_t width, uint32_t height,
   return RDL_OK;
 }
 
+static int Execute(rdl_fft* f, bool forward, void* in, void* out) {
+  const double real_bytes = double(f->width) * f->height * (f->f64 ? 8.0 : 4.0);
+  rdl::ScopedTiming t(f->s, f->f64 ? "fft64" : "fft",
+                      real_bytes + double(rdl_fft_spectrum_bytes(f)));
+  void* ins[1] = {in};
+  void* outs[1] = {out};
+  RDL_FFT_CHECK(rocfft_execute(forward ? f->fwd : f->inv, ins, outs,
+                               forward ? f->info_fwd : f->info_inv));
+  return RDL_OK;
+}
+
+extern "C" {
+
+int rdl_fft_create(rdl_session* s, uint32_t width, uint32_t height,
+                   rdl_fft** out) {
+  return CreateFft(s, width, height, false, out);
+}
+
+int rdl_fft_create_f64(rdl_session* s, uint32_t width, uint32_t height,
+                       rdl_fft** out) {
+  return CreateFft(s, width, height, true, out);
+}
+
 int rdl_fft_destroy(rdl_fft* f) {
   if (!f) return RDL_OK;
   (void)hipStreamSynchronize(f->s->stream);
@@ -191,28 +263,49 @@ int rdl_fft_destroy(rdl_fft* f) {
 }
 
 size_t rdl_fft_spectrum_bytes(const rdl_fft* f) {
-  return f ? size_t(f->width / 2 + 1) * f->height * 2 * sizeof(float) : 0;
+  return f ? size_t(f->width / 2 + 1) * f->height * 2 *
+                 (f->f64 ? sizeof(double) : sizeof(float))
+           : 0;
 }
 
 int rdl_fft_forward(rdl_fft* f, const float* d_in, void* d_spectrum) {
   RDL_ARG_CHECK(f && d_in && d_spectrum, "NULL argument");
-  const double bytes = double(f->width) * f->height * 4.0 +
-                       double(rdl_fft_spectrum_bytes(f));
-  rdl::ScopedTiming t(f->s, "fft", bytes);
-  void* in[1] = {const_cast<float*>(d_in)};
-  void* out[1] = {d_spectrum};
-  RDL_FFT_CHECK(rocfft_execute(f->fwd, in, out, f->info_fwd));
-  return RDL_OK;
+  RDL_ARG_CHECK(!f->f64, "double-precision plan: use rdl_fft64_*");
+  return Execute(f, true, const_cast<float*>(d_in), d_spectrum);
 }
 
 int rdl_fft_inverse(rdl_fft* f, void* d_spectrum, float* d_out) {
   RDL_ARG_CHECK(f && d_out && d_spectrum, "NULL argument");
-  const double bytes = double(f->width) * f->height * 4.0 +
-                       double(rdl_fft_spectrum_bytes(f));
-  rdl::ScopedTiming t(f->s, "fft", bytes);
-  void* in[1] = {d_spectrum};
-  void* out[1] = {d_out};
-  RDL_FFT_CHECK(rocfft_execute(f->inv, in, out, f->info_inv));
+  RDL_ARG_CHECK(!f->f64, "double-precision plan: use rdl_fft64_*");
+  return Execute(f, false, d_spectrum, d_out);
+}
+
+int rdl_fft64_forward(rdl_fft* f, const double* d_in, void* d_spectrum) {
+  RDL_ARG_CHECK(f && d_in && d_spectrum, "NULL argument");
+  RDL_ARG_CHECK(f->f64, "single-precision plan: use rdl_fft_*");
+  return Execute(f, true, const_cast<double*>(d_in), d_spectrum);
+}
+
+int rdl_fft64_inverse(rdl_fft* f, void* d_spectrum, double* d_out) {
+  RDL_ARG_CHECK(f && d_out && d_spectrum, "NULL argument");
+  RDL_ARG_CHECK(f->f64, "single-precision plan: use rdl_fft_*");
+  return Execute(f, false, d_spectrum, d_out);
+}
+
+int rdl_fft64_convolve(rdl_fft* f, double* d_image, const void* d_kernel_spectrum,
+                       void* d_work) {
+  RDL_ARG_CHECK(f && d_image && d_kernel_spectrum && d_work, "NULL argument");
+  RDL_TRY(rdl_fft64_forward(f, d_image, d_work));
+  const size_t nc = size_t(f->width / 2 + 1) * f->height;
+  {
+    rdl::ScopedTiming t(f->s, "spectrum_multiply64", double(nc) * 48.0);
+    rdl::SpectrumMultiplyF64<<<rdl::Grid(nc), 256, 0, f->s->stream>>>(
+        static_cast<double2*>(d_work), static_cast<const double2*>(d_work),
+        static_cast<const double2*>(d_kernel_spectrum), nc,
+        1.0 / (double(f->width) * f->height));
+    RDL_HIP_CHECK(hipGetLastError());
+  }
+  RDL_TRY(rdl_fft64_inverse(f, d_work, d_image));
   return RDL_OK;
 }
 
@@ -231,6 +324,7 @@ int rdl_spectrum_multiply(rdl_session* s, void* d_dst, const void* d_a,
 int rdl_fft_convolve(rdl_fft* f, float* d_image, const void* d_kernel_spectrum,
                      void* d_work) {
   RDL_ARG_CHECK(f && d_image && d_kernel_spectrum && d_work, "NULL argument");
+  RDL_ARG_CHECK(!f->f64, "double-precision plan: use rdl_fft64_convolve");
   RDL_TRY(rdl_fft_forward(f, d_image, d_work));
   const size_t nc = size_t(f->width / 2 + 1) * f->height;
   RDL_TRY(rdl_spectrum_multiply(f->s, d_work, d_work, d_kernel_spectrum, nc,
@@ -247,9 +341,11 @@ int rdl_prepare_small_kernel(rdl_session* s, float* d_dest, uint32_t width,
     rdl::SetError("Kernel size is larger than the image size");
     return RDL_ERR_ARG;
   }
+  // H2D into hipMalloc'd session scratch (a pageable copy into hipMallocAsync
+  // memory was observed to land incompletely above ~4 KiB on ROCm 7.2)
   const size_t kbytes = size_t(n) * n * sizeof(float);
-  float* d_k = nullptr;
-  RDL_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&d_k), kbytes, s->stream));
+  RDL_TRY(s->EnsureScratch(s->kernel, kbytes));
+  float* d_k = static_cast<float*>(s->kernel.ptr);
   RDL_HIP_CHECK(hipMemcpyAsync(d_k, h_kernel, kbytes, hipMemcpyHostToDevice,
                                s->stream));
   RDL_HIP_CHECK(hipMemsetAsync(d_dest, 0, size_t(width) * height * sizeof(float),
@@ -257,7 +353,6 @@ int rdl_prepare_small_kernel(rdl_session* s, float* d_dest, uint32_t width,
   rdl::PlaceSmallKernel<<<rdl::Grid(size_t(n) * n), 256, 0, s->stream>>>(
       d_dest, width, height, d_k, n);
   RDL_HIP_CHECK(hipGetLastError());
-  RDL_HIP_CHECK(hipFreeAsync(d_k, s->stream));
   RDL_HIP_CHECK(hipStreamSynchronize(s->stream));
   return RDL_OK;
 }
@@ -269,6 +364,30 @@ int rdl_prepare_psf_kernel(rdl_session* s, float* d_dest, uint32_t pw,
   RDL_ARG_CHECK(pw >= width && ph >= height, "padded size smaller than image");
   rdl::PreparePsfKernel<<<rdl::Grid(size_t(pw) * ph), 256, 0, s->stream>>>(
       d_dest, pw, ph, d_psf, width, height);
+  RDL_HIP_CHECK(hipGetLastError());
+  return RDL_OK;
+}
+
+int rdl_prepare_psf_kernel_f64(rdl_session* s, double* d_dest, uint32_t pw,
+                               uint32_t ph, const float* d_psf, uint32_t width,
+                               uint32_t height) {
+  RDL_ARG_CHECK(s && d_dest && d_psf, "NULL argument");
+  RDL_ARG_CHECK(pw >= width && ph >= height, "padded size smaller than image");
+  rdl::PreparePsfKernelT<double>
+      <<<rdl::Grid(size_t(pw) * ph), 256, 0, s->stream>>>(d_dest, pw, ph, d_psf,
+                                                           width, height);
+  RDL_HIP_CHECK(hipGetLastError());
+  return RDL_OK;
+}
+
+int rdl_trim_subtract_f64(rdl_session* s, float* d_residual, uint32_t width,
+                          uint32_t height, const double* d_padded, uint32_t pw,
+                          uint32_t ph) {
+  RDL_ARG_CHECK(s && d_residual && d_padded, "NULL argument");
+  RDL_ARG_CHECK(pw >= width && ph >= height, "padded size smaller than image");
+  rdl::ScopedTiming t(s, "trim_subtract", double(width) * height * 16.0);
+  rdl::TrimSubtractF64<<<rdl::Grid(size_t(width) * height), 256, 0, s->stream>>>(
+      d_residual, width, height, d_padded, pw, ph);
   RDL_HIP_CHECK(hipGetLastError());
   return RDL_OK;
 }

@@ -68,6 +68,9 @@ struct rdl_session {
   void* h_small = nullptr;       // 64 KiB pinned host
   rdl::Scratch partials;         // per-block partial keys
   rdl::Scratch radix;            // radix-select histograms
+  bool poison = false;            // RDL_POISON=1: NaN-fill fresh allocations
+  rdl::Scratch kernel;           // host-provided kernels (H2D destination)
+  rdl::Scratch loop_state;       // Högbom loop state / partials / trace
   void* comm = nullptr;          // ncclComm_t when initialised
 
   hipEvent_t GetEvent();
@@ -100,12 +103,14 @@ template <typename Get>
 __device__ __forceinline__ float IntegratePixel(const rdl_integration& g,
                                                 Get get) {
   if (g.copy_fast_path) return get(0);
+  const uint32_t np = g.n_pol;
   if (g.mode == RDL_INTEGRATE_LINEAR) {
+    // image_set.cc:432-460: AssignMultiply, then AddWithFactor (FMA), then *=
     float acc = 0.0f;
     bool first = true;
     for (uint32_t i = 0; i < g.n_images; ++i) {
       const float w = g.weights[i];
-      if (w != 0.0f) {
+      if (w != 0.0f && ((g.pol_mask >> (i % np)) & 1u)) {
         const float v = get(i);
         acc = first ? v * w : __builtin_fmaf(v, w, acc);
         first = false;
@@ -114,41 +119,49 @@ __device__ __forceinline__ float IntegratePixel(const rdl_integration& g,
     return first ? 0.0f : acc * g.factor;
   }
   if (g.mode == RDL_INTEGRATE_SQUARE) {
-    if (g.n_channels == 1) {
-      float acc = get(0) * get(0);
-      for (uint32_t p = 1; p < g.n_pol; ++p) {
-        const float v = get(p);
-        acc = __builtin_fmaf(v, v, acc);
+    if (g.n_channels == 1) {  // image_set.cc:361-386
+      float acc = 0.0f;
+      bool first = true;
+      for (uint32_t p = 0; p < np; ++p) {
+        if ((g.pol_mask >> p) & 1u) {
+          const float v = get(p);
+          acc = first ? v * v : __builtin_fmaf(v, v, acc);
+          first = false;
+        }
       }
       return __builtin_sqrtf(acc) * g.factor;
     }
-    float dest = 0.0f;
+    float dest = 0.0f;  // image_set.cc:388-421
     for (uint32_t ch = 0; ch < g.n_channels; ++ch) {
-      const float w = g.weights[ch * g.n_pol];
+      const float w = g.weights[ch * np];
       float scratch = 0.0f;
       if (w != 0.0f) {
-        if (g.n_pol == 1) {
+        if (np == 1) {
           scratch = get(ch);
         } else {
-          const float v0 = get(ch * g.n_pol);
-          float acc = v0 * v0;
-          for (uint32_t p = 1; p < g.n_pol; ++p) {
-            const float v = get(ch * g.n_pol + p);
-            acc = __builtin_fmaf(v, v, acc);
+          float acc = 0.0f;
+          bool first = true;
+          for (uint32_t p = 0; p < np; ++p) {
+            if ((g.pol_mask >> p) & 1u) {
+              const float v = get(ch * np + p);
+              acc = first ? v * v : __builtin_fmaf(v, v, acc);
+              first = false;
+            }
           }
-          scratch = __builtin_sqrtf(acc);
+          scratch = first ? 0.0f : __builtin_sqrtf(acc);
         }
       }
       dest = ch == 0 ? scratch * w : __builtin_fmaf(scratch, w, dest);
     }
     return dest * g.factor;
   }
-  // RDL_INTEGRATE_SQUARED_JOINS (aocommon op order unpinned)
+  // RDL_INTEGRATE_SQUARED_JOINS, image_set.cc:429-455 (aocommon SquareWithFactor
+  // / AddSquared operation order is not in /root/reference: parity unpinned)
   float acc = 0.0f;
   bool first = true;
   for (uint32_t i = 0; i < g.n_images; ++i) {
     const float w = g.weights[i];
-    if (w != 0.0f) {
+    if (w != 0.0f && ((g.pol_mask >> (i % np)) & 1u)) {
       const float v = get(i);
       acc = first ? v * v * w : __builtin_fmaf(v * v, w, acc);
       first = false;

@@ -1,4 +1,5 @@
 // Session / runtime part of the C-ABI (rdl_hip.h "runtime" section).
+#include <cstdlib>
 #include <cstring>
 
 #include "rdl_internal.h"
@@ -62,6 +63,7 @@ int rdl_session::EnsureScratch(rdl::Scratch& s, size_t bytes) {
   }
   RDL_HIP_CHECK(hipMalloc(&s.ptr, bytes));
   s.bytes = bytes;
+  if (poison) RDL_HIP_CHECK(hipMemsetAsync(s.ptr, 0xff, bytes, stream));
   return RDL_OK;
 }
 
@@ -89,6 +91,9 @@ int rdl_session_create(int device, rdl_session** out) {
   hipDeviceProp_t prop;
   RDL_HIP_CHECK(hipGetDeviceProperties(&prop, device));
   s->n_cus = prop.multiProcessorCount;
+  // debug aid: fill every fresh allocation with NaN bytes (0xff)
+  const char* poison = std::getenv("RDL_POISON");
+  s->poison = poison && poison[0] == '1';
   RDL_HIP_CHECK(hipMalloc(&s->d_small, 1 << 16));
   RDL_HIP_CHECK(hipHostMalloc(&s->h_small, 1 << 16, hipHostMallocDefault));
   *out = s.release();
@@ -107,6 +112,8 @@ int rdl_session_destroy(rdl_session* s) {
   for (hipEvent_t e : s->event_pool) (void)hipEventDestroy(e);
   if (s->partials.ptr) (void)hipFree(s->partials.ptr);
   if (s->radix.ptr) (void)hipFree(s->radix.ptr);
+  if (s->kernel.ptr) (void)hipFree(s->kernel.ptr);
+  if (s->loop_state.ptr) (void)hipFree(s->loop_state.ptr);
   if (s->d_small) (void)hipFree(s->d_small);
   if (s->h_small) (void)hipHostFree(s->h_small);
   if (s->comm) rdl_comm_destroy(s);
@@ -129,6 +136,10 @@ int rdl_malloc(rdl_session* s, size_t bytes, void** d_out) {
   *d_out = nullptr;
   if (bytes == 0) return RDL_OK;
   RDL_HIP_CHECK(hipMalloc(d_out, bytes));
+  if (s->poison) {
+    RDL_HIP_CHECK(hipMemsetAsync(*d_out, 0xff, bytes, s->stream));
+    RDL_HIP_CHECK(hipStreamSynchronize(s->stream));
+  }
   return RDL_OK;
 }
 

@@ -446,10 +446,11 @@ __global__ __launch_bounds__(kLoopThreads) void SubminorLoop(LoopArgs a) {
   }
 }
 
+template <typename T>
 __global__ __launch_bounds__(256) void ScatterModel(const uint32_t* pos,
                                                     const float* m,
                                                     uint64_t n_sel,
-                                                    float* dest, uint32_t dw,
+                                                    T* dest, uint32_t dw,
                                                     uint32_t ox, uint32_t oy,
                                                     int add) {
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n_sel;
@@ -457,9 +458,9 @@ __global__ __launch_bounds__(256) void ScatterModel(const uint32_t* pos,
     const uint32_t pk = pos[i];
     const size_t d = size_t((pk >> 16) + oy) * dw + (pk & 0xffffu) + ox;
     if (add)
-      dest[d] += m[i];
+      dest[d] += T(m[i]);
     else
-      dest[d] = m[i];
+      dest[d] = T(m[i]);
   }
 }
 
@@ -699,9 +700,29 @@ int rdl_subminor_model(rdl_subminor* h, uint32_t image_index, float* d_dest,
                                  s->stream));
   if (h->n_selected == 0) return RDL_OK;
   const unsigned grid = std::min<uint64_t>(4096, rdl::DivUp(h->n_selected, 256));
-  rdl::ScatterModel<<<grid, 256, 0, s->stream>>>(
+  rdl::ScatterModel<float><<<grid, 256, 0, s->stream>>>(
       h->d_pos, h->d_m + size_t(image_index) * h->n_selected, h->n_selected,
       d_dest, dest_w, ox, oy, mode == 1);
+  RDL_HIP_CHECK(hipGetLastError());
+  return RDL_OK;
+}
+
+int rdl_subminor_model_f64(rdl_subminor* h, uint32_t image_index,
+                           double* d_dest, uint32_t dest_w, uint32_t dest_h,
+                           uint32_t ox, uint32_t oy) {
+  RDL_ARG_CHECK(h && d_dest, "NULL argument");
+  RDL_ARG_CHECK(image_index < h->n_images || h->n_selected == 0,
+                "image index out of range");
+  RDL_ARG_CHECK(dest_w >= h->width + ox && dest_h >= h->height + oy,
+                "destination too small");
+  rdl_session* s = h->s;
+  RDL_HIP_CHECK(hipMemsetAsync(d_dest, 0, size_t(dest_w) * dest_h * sizeof(double),
+                               s->stream));
+  if (h->n_selected == 0) return RDL_OK;
+  const unsigned grid = std::min<uint64_t>(4096, rdl::DivUp(h->n_selected, 256));
+  rdl::ScatterModel<double><<<grid, 256, 0, s->stream>>>(
+      h->d_pos, h->d_m + size_t(image_index) * h->n_selected, h->n_selected,
+      d_dest, dest_w, ox, oy, 0);
   RDL_HIP_CHECK(hipGetLastError());
   return RDL_OK;
 }

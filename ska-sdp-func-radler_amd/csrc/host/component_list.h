@@ -1,0 +1,56 @@
+// radler::ComponentList (reference: cpp/component_list.{h,cc}): per-scale
+// component positions with one value per image. Built from the model images
+// for single-scale algorithms; recorded by MultiScaleAlgorithm otherwise.
+#pragma once
+
+#include <cstddef>
+#include <vector>
+
+namespace radler {
+
+class ImageSet;
+
+class ComponentList {
+ public:
+  ComponentList() = default;
+  ComponentList(size_t width, size_t height, size_t n_scales,
+                size_t n_frequencies)
+      : width_(width),
+        height_(height),
+        n_frequencies_(n_frequencies),
+        list_per_scale_(n_scales) {}
+  /// Every non-zero model pixel becomes a scale-0 component
+  /// (component_list.h:46-55 LoadFromImageSet).
+  ComponentList(size_t width, size_t height, const ImageSet& model_set);
+
+  struct Position {
+    size_t x, y;
+  };
+
+  void Add(size_t x, size_t y, size_t scale_index, const float* values);
+  void Add(const ComponentList& other, int offset_x, int offset_y);
+  void MergeDuplicates();
+  void Clear();
+  size_t Width() const { return width_; }
+  size_t Height() const { return height_; }
+  size_t NScales() const { return list_per_scale_.size(); }
+  void SetNScales(size_t n) { list_per_scale_.resize(n); }
+  size_t NFrequencies() const { return n_frequencies_; }
+  size_t ComponentCount(size_t scale_index) const {
+    return list_per_scale_[scale_index].positions.size();
+  }
+  void GetComponent(size_t scale_index, size_t index, size_t& x, size_t& y,
+                    float* values) const;
+
+ private:
+  struct ScaleList {
+    std::vector<Position> positions;
+    std::vector<float> values;
+  };
+  void MergeDuplicates(size_t scale_index);
+  size_t width_ = 0, height_ = 0, n_frequencies_ = 0;
+  size_t added_since_merge_ = 0;
+  std::vector<ScaleList> list_per_scale_;
+};
+
+}  // namespace radler

@@ -1,0 +1,105 @@
+// radler::algorithms::DeconvolutionAlgorithm — the plugin interface of the
+// reference (cpp/algorithms/deconvolution_algorithm.h:31-210), with the same
+// settings, setters and result struct. The GPU build passes device-resident
+// image sets and PSF planes instead of host aocommon::Images; everything
+// else (defaults, Clone(), iteration bookkeeping) is unchanged.
+#pragma once
+
+#include <memory>
+#include <optional>
+#include <vector>
+
+#include "device.h"
+#include "image_set.h"
+#include "settings.h"
+
+namespace radler::algorithms {
+
+struct DeconvolutionResult {
+  std::optional<float> starting_peak_value;
+  float final_peak_value = 0.0;
+  bool another_iteration_required = false;
+  bool is_diverging = false;
+};
+
+class DeconvolutionAlgorithm {
+ public:
+  virtual ~DeconvolutionAlgorithm() = default;
+  DeconvolutionAlgorithm& operator=(const DeconvolutionAlgorithm&) = delete;
+
+  virtual DeconvolutionResult ExecuteMajorIteration(
+      ImageSet& data_image, ImageSet& model_image,
+      const gpu::Planes& psf_images) = 0;
+  virtual std::unique_ptr<DeconvolutionAlgorithm> Clone() const = 0;
+
+  void SetMaxIterations(size_t v) { settings_.max_iterations = v; }
+  void SetThreshold(float v) { settings_.threshold = v; }
+  void SetMajorIterationThreshold(float v) {
+    settings_.major_iteration_threshold = v;
+  }
+  void SetMinorLoopGain(float v) { settings_.minor_loop_gain = v; }
+  void SetMajorLoopGain(float v) { settings_.major_loop_gain = v; }
+  void SetAllowNegativeComponents(bool v) {
+    settings_.allow_negative_components = v;
+  }
+  void SetStopOnNegativeComponents(bool v) {
+    settings_.stop_on_negative_component = v;
+  }
+  void SetCleanBorderRatio(float v) { settings_.clean_border_ratio = v; }
+  void SetCleanMask(const bool* mask) { settings_.clean_mask = mask; }
+  void SetDivergenceLimit(float v) { settings_.divergence_limit = v; }
+  void SetComponentOptimizationAlgorithm(OptimizationAlgorithm a) {
+    settings_.component_optimization_algorithm = a;
+  }
+
+  size_t MaxIterations() const { return settings_.max_iterations; }
+  float Threshold() const { return settings_.threshold; }
+  float MajorIterationThreshold() const {
+    return settings_.major_iteration_threshold;
+  }
+  float MinorLoopGain() const { return settings_.minor_loop_gain; }
+  float MajorLoopGain() const { return settings_.major_loop_gain; }
+  float CleanBorderRatio() const { return settings_.clean_border_ratio; }
+  bool AllowNegativeComponents() const {
+    return settings_.allow_negative_components;
+  }
+  bool StopOnNegativeComponents() const {
+    return settings_.stop_on_negative_component;
+  }
+  OptimizationAlgorithm ComponentOptimizationAlgorithm() const {
+    return settings_.component_optimization_algorithm;
+  }
+  const bool* CleanMask() const { return settings_.clean_mask; }
+  float DivergenceLimit() const { return settings_.divergence_limit; }
+  size_t IterationNumber() const { return iteration_number_; }
+  void SetIterationNumber(size_t n) { iteration_number_ = n; }
+
+ protected:
+  DeconvolutionAlgorithm() = default;
+  // Clones share settings and iteration count, not device scratch.
+  DeconvolutionAlgorithm(const DeconvolutionAlgorithm& o)
+      : settings_(o.settings_), iteration_number_(o.iteration_number_) {}
+
+  /// Device copy (uint8) of CleanMask() for the current call, or nullptr.
+  const uint8_t* DeviceCleanMask(gpu::Session& s, size_t width, size_t height);
+
+ private:
+  struct {
+    float threshold = 0.0;
+    float major_iteration_threshold = 0.0;
+    float minor_loop_gain = 0.1;
+    float major_loop_gain = 1.0;
+    float clean_border_ratio = 0.05;
+    size_t max_iterations = 500;
+    float divergence_limit = 4.0;
+    bool allow_negative_components = true;
+    bool stop_on_negative_component = false;
+    OptimizationAlgorithm component_optimization_algorithm =
+        OptimizationAlgorithm::kClean;
+    const bool* clean_mask = nullptr;
+  } settings_;
+  size_t iteration_number_ = 0;
+  std::shared_ptr<gpu::Buffer> mask_buffer_;
+};
+
+}  // namespace radler::algorithms

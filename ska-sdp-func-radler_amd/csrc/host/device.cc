@@ -1,0 +1,154 @@
+#include "device.h"
+
+#include <cstdlib>
+#include <mutex>
+
+namespace radler::gpu {
+
+void Check(int rc, const char* what) {
+  if (rc != RDL_OK)
+    throw std::runtime_error(std::string(what) + ": " + rdl_last_error());
+}
+
+Buffer::Buffer(Session& s, size_t bytes) { Resize(s, bytes); }
+
+Buffer::~Buffer() {
+  if (ptr_) rdl_free(s_->Handle(), ptr_);
+}
+
+Buffer& Buffer::operator=(Buffer&& o) noexcept {
+  if (this != &o) {
+    if (ptr_) rdl_free(s_->Handle(), ptr_);
+    s_ = o.s_;
+    ptr_ = o.ptr_;
+    bytes_ = o.bytes_;
+    o.ptr_ = nullptr;
+    o.bytes_ = 0;
+  }
+  return *this;
+}
+
+void Buffer::Resize(Session& s, size_t bytes) {
+  if (ptr_ && bytes <= bytes_) return;
+  if (ptr_) Check(rdl_free(s_->Handle(), ptr_), "rdl_free");
+  s_ = &s;
+  ptr_ = nullptr;
+  bytes_ = 0;
+  // 256-byte granularity keeps every plane start 16-byte aligned
+  const size_t alloc = (std::max<size_t>(bytes, 16) + 255) / 256 * 256;
+  Check(rdl_malloc(s.Handle(), alloc, &ptr_), "rdl_malloc");
+  bytes_ = alloc;
+}
+
+void Buffer::Zero() {
+  if (ptr_) Check(rdl_memset_zero(s_->Handle(), ptr_, bytes_), "rdl_memset_zero");
+}
+
+Fft::Fft(Session& s, size_t width, size_t height, bool f64)
+    : s_(s), width_(width), height_(height), f64_(f64) {
+  if (f64)
+    Check(rdl_fft_create_f64(s.Handle(), uint32_t(width), uint32_t(height), &f_),
+          "rdl_fft_create_f64");
+  else
+    Check(rdl_fft_create(s.Handle(), uint32_t(width), uint32_t(height), &f_),
+          "rdl_fft_create");
+  spectrum_bytes_ = rdl_fft_spectrum_bytes(f_);
+  work_.Resize(s, spectrum_bytes_);
+}
+
+Fft::~Fft() { rdl_fft_destroy(f_); }
+
+void Fft::Forward(const float* d_in, void* d_spectrum) {
+  Check(rdl_fft_forward(f_, d_in, d_spectrum), "rdl_fft_forward");
+}
+
+void Fft::Inverse(void* d_spectrum, float* d_out) {
+  Check(rdl_fft_inverse(f_, d_spectrum, d_out), "rdl_fft_inverse");
+}
+
+void Fft::Convolve(float* d_image, const void* d_kernel_spectrum) {
+  Check(rdl_fft_convolve(f_, d_image, d_kernel_spectrum, work_.Ptr()),
+        "rdl_fft_convolve");
+}
+
+void Fft::Forward64(const double* d_in, void* d_spectrum) {
+  Check(rdl_fft64_forward(f_, d_in, d_spectrum), "rdl_fft64_forward");
+}
+
+void Fft::Convolve64(double* d_image, const void* d_kernel_spectrum) {
+  Check(rdl_fft64_convolve(f_, d_image, d_kernel_spectrum, work_.Ptr()),
+        "rdl_fft64_convolve");
+}
+
+Session::Session(int device) : device_(device) {
+  Check(rdl_session_create(device, &s_), "rdl_session_create");
+}
+
+Session::~Session() {
+  ffts_.clear();
+  rdl_session_destroy(s_);
+}
+
+Fft& Session::GetFft(size_t width, size_t height, bool f64) {
+  auto key = std::make_tuple(width, height, f64);
+  auto it = ffts_.find(key);
+  if (it == ffts_.end())
+    it = ffts_.emplace(key, std::make_unique<Fft>(*this, width, height, f64)).first;
+  return *it->second;
+}
+
+void Session::Sync() { Check(rdl_session_sync(s_), "rdl_session_sync"); }
+
+void Session::H2D(void* d, const void* h, size_t bytes) {
+  Check(rdl_memcpy_h2d(s_, d, h, bytes), "rdl_memcpy_h2d");
+}
+void Session::D2H(void* h, const void* d, size_t bytes) {
+  Check(rdl_memcpy_d2h(s_, h, d, bytes), "rdl_memcpy_d2h");
+}
+void Session::D2D(void* d, const void* src, size_t bytes) {
+  Check(rdl_memcpy_d2d(s_, d, src, bytes), "rdl_memcpy_d2d");
+}
+void Session::Zero(void* d, size_t bytes) {
+  Check(rdl_memset_zero(s_, d, bytes), "rdl_memset_zero");
+}
+float Session::ReadFloat(const float* d) {
+  float v;
+  D2H(&v, d, sizeof(float));
+  return v;
+}
+
+std::shared_ptr<Session> Session::ForDevice(int device) {
+  static std::mutex mutex;
+  static std::map<int, std::weak_ptr<Session>> sessions;
+  std::lock_guard<std::mutex> lock(mutex);
+  auto it = sessions.find(device);
+  if (it != sessions.end())
+    if (auto s = it->second.lock()) return s;
+  auto s = std::make_shared<Session>(device);
+  sessions[device] = s;
+  return s;
+}
+
+int Session::DefaultDevice() {
+  for (const char* var : {"RADLER_DEVICE", "LOCAL_RANK"}) {
+    if (const char* v = std::getenv(var)) {
+      int count = 0;
+      Check(rdl_device_count(&count), "rdl_device_count");
+      const int d = std::atoi(v);
+      if (count > 0) return d % count;
+    }
+  }
+  return 0;
+}
+
+Planes Planes::Make(Session& s, size_t width, size_t height, size_t count) {
+  Planes p;
+  p.width = width;
+  p.height = height;
+  p.count = count;
+  p.buffer = std::make_shared<Buffer>(s, std::max<size_t>(1, width * height * count) *
+                                             sizeof(float));
+  return p;
+}
+
+}  // namespace radler::gpu

@@ -1,0 +1,114 @@
+// C++ side of the boundary: RAII wrappers over the rdl_hip.h C-ABI. Every
+// non-zero status becomes std::runtime_error carrying rdl_last_error(), which
+// is how the reference reports failures (cpp/radler.cc:52-112).
+#pragma once
+
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <tuple>
+#include <utility>
+#include <vector>
+
+#include "rdl_hip.h"
+
+namespace radler::gpu {
+
+void Check(int rc, const char* what);
+
+class Session;
+
+/// A device allocation owned by one session.
+class Buffer {
+ public:
+  Buffer() = default;
+  Buffer(Session& s, size_t bytes);
+  ~Buffer();
+  Buffer(const Buffer&) = delete;
+  Buffer& operator=(const Buffer&) = delete;
+  Buffer(Buffer&& o) noexcept { *this = std::move(o); }
+  Buffer& operator=(Buffer&& o) noexcept;
+  void* Ptr() const { return ptr_; }
+  float* F() const { return static_cast<float*>(ptr_); }
+  double* D() const { return static_cast<double*>(ptr_); }
+  size_t Bytes() const { return bytes_; }
+  void Resize(Session& s, size_t bytes);  // grow-only, contents discarded
+  void Zero();
+
+ private:
+  Session* s_ = nullptr;
+  void* ptr_ = nullptr;
+  size_t bytes_ = 0;
+};
+
+/// Real 2-D FFT pair of one size (rocFFT plans live in the C-ABI object).
+class Fft {
+ public:
+  Fft(Session& s, size_t width, size_t height, bool f64 = false);
+  ~Fft();
+  Fft(const Fft&) = delete;
+  Fft& operator=(const Fft&) = delete;
+  size_t Width() const { return width_; }
+  size_t Height() const { return height_; }
+  size_t SpectrumBytes() const { return spectrum_bytes_; }
+  size_t ComplexCount() const { return size_t(width_ / 2 + 1) * height_; }
+  bool IsF64() const { return f64_; }
+  void Forward(const float* d_in, void* d_spectrum);
+  void Inverse(void* d_spectrum, float* d_out);
+  /// In-place circular convolution with a cached kernel spectrum.
+  void Convolve(float* d_image, const void* d_kernel_spectrum);
+  /// Double-precision plan only.
+  void Forward64(const double* d_in, void* d_spectrum);
+  void Convolve64(double* d_image, const void* d_kernel_spectrum);
+  rdl_fft* Handle() { return f_; }
+
+ private:
+  Session& s_;
+  rdl_fft* f_ = nullptr;
+  size_t width_, height_, spectrum_bytes_;
+  bool f64_;
+  Buffer work_;
+};
+
+/// One HIP device + stream, with cached FFT plans.
+class Session {
+ public:
+  explicit Session(int device);
+  ~Session();
+  Session(const Session&) = delete;
+  Session& operator=(const Session&) = delete;
+  rdl_session* Handle() const { return s_; }
+  int Device() const { return device_; }
+  Fft& GetFft(size_t width, size_t height, bool f64 = false);
+  void Sync();
+  void H2D(void* d, const void* h, size_t bytes);
+  void D2H(void* h, const void* d, size_t bytes);
+  void D2D(void* d, const void* s, size_t bytes);
+  void Zero(void* d, size_t bytes);
+  float ReadFloat(const float* d);
+
+  /// Process-wide session for a device (one per GPU, shared by the Radler
+  /// objects of this process).
+  static std::shared_ptr<Session> ForDevice(int device);
+  /// The device a Radler instance uses when Settings::gpu_device == -1.
+  static int DefaultDevice();
+
+ private:
+  rdl_session* s_ = nullptr;
+  int device_;
+  std::map<std::tuple<size_t, size_t, bool>, std::unique_ptr<Fft>> ffts_;
+};
+
+/// A stack of `count` planes of width x height floats, contiguous.
+struct Planes {
+  std::shared_ptr<Buffer> buffer;
+  size_t width = 0, height = 0, count = 0;
+  size_t PlaneSize() const { return width * height; }
+  float* Plane(size_t i) const { return buffer->F() + i * PlaneSize(); }
+  float* Base() const { return buffer ? buffer->F() : nullptr; }
+  static Planes Make(Session& s, size_t width, size_t height, size_t count);
+};
+
+}  // namespace radler::gpu

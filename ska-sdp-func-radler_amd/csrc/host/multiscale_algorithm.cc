@@ -1,0 +1,459 @@
+// MultiScaleAlgorithm on the device. Line references are to the reference's
+// cpp/algorithms/multiscale_algorithm.cc unless stated.
+#include "multiscale_algorithm.h"
+
+#include <cmath>
+#include <cstdio>
+#include <map>
+#include <set>
+#include <stdexcept>
+
+#include "fft_sizes.h"
+#include "logger.h"
+#include "subminor.h"
+
+namespace radler::algorithms {
+
+using multiscale::MultiScaleTransforms;
+
+void InitializeScales(std::vector<MultiScaleAlgorithm::ScaleInfo>& scales,
+                      double beam_size_in_pixels, size_t min_width_height,
+                      MultiscaleShape shape, size_t max_scales,
+                      const std::vector<double>& scale_list) {  // :90-131
+  if (scale_list.empty()) {
+    if (scales.empty()) {
+      size_t scale_index = 0;
+      double scale = beam_size_in_pixels * 2.0;
+      do {
+        MultiScaleAlgorithm::ScaleInfo& e = scales.emplace_back();
+        e.scale = scale_index == 0 ? 0.0f : float(scale);
+        e.kernel_peak =
+            MultiScaleTransforms::KernelPeakValue(scale, min_width_height, shape);
+        scale *= 2.0;
+        ++scale_index;
+      } while (scale < min_width_height * 0.5 &&
+               (max_scales == 0 || scale_index < max_scales));
+    } else {
+      while (!scales.empty() && scales.back().scale >= min_width_height * 0.5) {
+        log::Info() << "Scale size " << scales.back().scale
+                    << " does not fit in cleaning region: removing scale.\n";
+        scales.pop_back();
+      }
+    }
+  } else if (scales.empty()) {
+    std::multiset<double> sorted(scale_list.begin(), scale_list.end());
+    for (double s : sorted) {
+      MultiScaleAlgorithm::ScaleInfo& e = scales.emplace_back();
+      e.scale = float(s);
+      e.kernel_peak =
+          MultiScaleTransforms::KernelPeakValue(e.scale, min_width_height, shape);
+    }
+  }
+}
+
+std::optional<size_t> SelectMaximumScale(
+    const std::vector<MultiScaleAlgorithm::ScaleInfo>& scales) {  // :133-151
+  std::map<float, size_t> peak_to_scale;
+  for (size_t i = 0; i != scales.size(); ++i)
+    if (scales[i].is_active)
+      peak_to_scale.insert(std::make_pair(
+          std::fabs(scales[i].max_unnormalized_image_value *
+                    scales[i].bias_factor),
+          i));
+  if (peak_to_scale.empty()) return std::nullopt;
+  return peak_to_scale.rbegin()->second;
+}
+
+MultiScaleAlgorithm::MultiScaleAlgorithm(const Settings::Multiscale& settings,
+                                         double beam_size, double pixel_scale_x,
+                                         double pixel_scale_y,
+                                         bool track_components)
+    : settings_(settings),
+      beam_size_in_pixels_(beam_size / std::max(pixel_scale_x, pixel_scale_y)),
+      track_components_(track_components) {
+  if (!(beam_size_in_pixels_ > 0.0)) beam_size_in_pixels_ = 1;  // :162
+}
+
+MultiScaleAlgorithm::MultiScaleAlgorithm(const MultiScaleAlgorithm& o)
+    : DeconvolutionAlgorithm(o),
+      settings_(o.settings_),
+      beam_size_in_pixels_(o.beam_size_in_pixels_),
+      track_components_(o.track_components_),
+      scale_infos_(o.scale_infos_) {}
+
+void MultiScaleAlgorithm::FindPeakDirect(const float* d_image,
+                                         size_t scale_index) {  // :700-748
+  ScaleInfo& info = scale_infos_[scale_index];
+  const size_t w = transforms_->Width(), h = transforms_->Height();
+  const uint32_t hb = uint32_t(std::round(w * CleanBorderRatio()));
+  const uint32_t vb = uint32_t(std::round(h * CleanBorderRatio()));
+  rdl_peak p;
+  gpu::Check(rdl_find_peak(session_->Handle(), d_image, uint32_t(w), uint32_t(h),
+                           0, uint32_t(h), hb, vb, AllowNegativeComponents(),
+                           d_mask_, 1, &p),
+             "rdl_find_peak");
+  info.max_image_value_x = p.x;
+  info.max_image_value_y = p.y;
+  info.max_unnormalized_image_value = p.found ? p.value : 0.0f;
+  info.max_normalized_image_value = p.found ? p.value : 0.0f;
+}
+
+void MultiScaleAlgorithm::FindActiveScaleConvolvedMaxima(
+    const ImageSet& image_set, float* d_integrated, bool report_rms) {
+  // :578-634 with ThreadedDeconvolutionTools::FindMultiScalePeak /
+  // FindSingleScalePeak (threaded_deconvolution_tools.cc:30-107): one forward
+  // FFT of the integrated image feeds every active scale.
+  rdl_session* s = session_->Handle();
+  const size_t w = image_set.Width(), h = image_set.Height();
+  image_set.GetLinearIntegrated(d_integrated);
+  bool need_fft = false;
+  for (size_t si = 0; si != scale_infos_.size(); ++si) {
+    ScaleInfo& e = scale_infos_[si];
+    if (!e.is_active) continue;
+    if (e.scale == 0.0f) {
+      FindPeakDirect(d_integrated, si);
+      if (report_rms)
+        gpu::Check(rdl_rms(s, d_integrated, w * h, &e.rms), "rdl_rms");
+    } else {
+      need_fft = true;
+    }
+  }
+  if (!need_fft) return;
+  gpu::Fft& fft = transforms_->Fft();
+  fft.Forward(d_integrated, spectrum_->Ptr());
+  const float norm = 1.0f / float(double(w) * h);
+  for (size_t si = 0; si != scale_infos_.size(); ++si) {
+    ScaleInfo& e = scale_infos_[si];
+    if (!e.is_active || e.scale == 0.0f) continue;
+    gpu::Check(rdl_spectrum_multiply(s, spectrum_work_->Ptr(), spectrum_->Ptr(),
+                                     transforms_->KernelSpectrum(e.scale),
+                                     fft.ComplexCount(), norm),
+               "rdl_spectrum_multiply");
+    fft.Inverse(spectrum_work_->Ptr(), scratch_->F());
+    const size_t border_scale = size_t(std::ceil(e.scale * 0.5));
+    const uint32_t xb = uint32_t(
+        std::max<size_t>(size_t(std::round(w * CleanBorderRatio())), border_scale));
+    const uint32_t yb = uint32_t(
+        std::max<size_t>(size_t(std::round(h * CleanBorderRatio())), border_scale));
+    if (report_rms)
+      gpu::Check(rdl_rms(s, scratch_->F(), w * h, &e.rms), "rdl_rms");
+    rdl_peak p;
+    gpu::Check(rdl_find_peak(s, scratch_->F(), uint32_t(w), uint32_t(h), 0,
+                             uint32_t(h), xb, yb, AllowNegativeComponents(),
+                             d_mask_, 1, &p),
+               "rdl_find_peak");
+    e.max_normalized_image_value = p.found ? p.value : 0.0f;
+    e.max_unnormalized_image_value = p.found ? p.value : 0.0f;
+    e.max_image_value_x = p.x;
+    e.max_image_value_y = p.y;
+  }
+}
+
+void MultiScaleAlgorithm::ActivateScales(size_t last) {  // :636-656
+  for (size_t i = 0; i != scale_infos_.size(); ++i) {
+    const bool activate =
+        i == last ||
+        std::fabs(scale_infos_[i].max_unnormalized_image_value) *
+                scale_infos_[i].bias_factor >
+            std::fabs(scale_infos_[last].max_unnormalized_image_value) *
+                (1.0 - MinorLoopGain()) * scale_infos_[last].bias_factor;
+    scale_infos_[i].is_active = activate;
+  }
+}
+
+DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
+    ImageSet& data_image, ImageSet& model_image, const gpu::Planes& psfs) {
+  gpu::Session& session = data_image.Session();
+  session_ = &session;
+  rdl_session* s = session.Handle();
+  const size_t width = data_image.Width();
+  const size_t height = data_image.Height();
+  const size_t npx = width * height;
+  trace_.clear();
+  if (StopOnNegativeComponents()) SetAllowNegativeComponents(true);
+  InitializeScales(scale_infos_, beam_size_in_pixels_, std::min(width, height),
+                   settings_.shape, settings_.max_scales, settings_.scale_list);
+  if (ComponentOptimizationAlgorithm() != OptimizationAlgorithm::kClean)
+    throw std::runtime_error(
+        "Component optimisation is not available in the MI355X build");
+
+  bool has_hit_threshold_in_sub_loop = false;
+  size_t threshold_countdown = std::max(size_t{8}, scale_infos_.size() * 3 / 2);
+
+  if (!transforms_ || transforms_->Width() != width ||
+      transforms_->Height() != height)
+    transforms_ = std::make_unique<MultiScaleTransforms>(session, width, height,
+                                                         settings_.shape);
+  d_mask_ = DeviceCleanMask(session, width, height);
+  scratch_ = std::make_shared<gpu::Buffer>(session, npx * sizeof(float));
+  gpu::Buffer integrated(session, npx * sizeof(float));
+  const size_t spectrum_bytes = transforms_->Fft().SpectrumBytes();
+  spectrum_ = std::make_shared<gpu::Buffer>(session, spectrum_bytes);
+  spectrum_work_ = std::make_shared<gpu::Buffer>(session, spectrum_bytes);
+
+  // ConvolvePsfs (:29-88): convolved[psf][scale]
+  const size_t n_psf = data_image.PsfCount();
+  const size_t n_scales = scale_infos_.size();
+  std::vector<gpu::Planes> convolved(n_psf);
+  auto convolve_psfs = [&](gpu::Planes& out, const float* d_psf,
+                           bool is_integrated) {
+    out = gpu::Planes::Make(session, width, height, n_scales);
+    const double first_auto_scale_size = beam_size_in_pixels_ * 2.0;
+    for (size_t si = 0; si != n_scales; ++si) {
+      ScaleInfo& e = scale_infos_[si];
+      session.D2D(out.Plane(si), d_psf, npx * sizeof(float));
+      if (e.scale != 0.0f) transforms_->Transform(out.Plane(si), e.scale);
+      if (is_integrated) {
+        e.psf_peak = session.ReadFloat(out.Plane(si) + width / 2 +
+                                       (height / 2) * width);
+        double exp_term;
+        if (e.scale == 0.0f || n_scales < 2)
+          exp_term = 0.0;
+        else
+          exp_term = std::log2(e.scale / first_auto_scale_size);
+        e.bias_factor = float(std::pow(settings_.scale_bias, -exp_term));
+        e.gain = float(double(MinorLoopGain()) / e.psf_peak);
+        e.is_active = true;
+        log::Info() << "- Scale " << std::round(e.scale)
+                    << ", bias factor=" << std::round(e.bias_factor * 10.0) / 10.0
+                    << ", psfpeak=" << e.psf_peak << ", gain=" << e.gain
+                    << ", kernel peak=" << e.kernel_peak << '\n';
+      }
+    }
+  };
+  data_image.GetIntegratedPsf(integrated.F(), psfs);
+  convolve_psfs(convolved[0], integrated.F(), true);
+  if (n_psf > 1)
+    for (size_t i = 0; i != n_psf; ++i)
+      convolve_psfs(convolved[i], psfs.Plane(i), false);
+
+  FindActiveScaleConvolvedMaxima(data_image, integrated.F(), true);
+  DeconvolutionResult result;
+  std::optional<size_t> optional_scale = SelectMaximumScale(scale_infos_);
+  if (!optional_scale) {
+    log::Warn() << "No peak found during multi-scale cleaning! Aborting "
+                   "deconvolution.\n";
+    result.another_iteration_required = false;
+    return result;
+  }
+  size_t scale_with_peak = *optional_scale;
+
+  bool is_final_threshold = false;
+  const float initial_peak_value =
+      std::fabs(scale_infos_[scale_with_peak].max_unnormalized_image_value *
+                scale_infos_[scale_with_peak].bias_factor);
+  float m_gain_threshold = initial_peak_value * (1.0 - MajorLoopGain());
+  m_gain_threshold = std::max(m_gain_threshold, MajorIterationThreshold());
+  float first_threshold = m_gain_threshold;
+  if (Threshold() > first_threshold) {
+    first_threshold = Threshold();
+    is_final_threshold = true;
+  }
+  log::Info() << "Starting multi-scale cleaning. Start peak=" << initial_peak_value
+              << ", major iteration threshold=" << first_threshold
+              << (is_final_threshold ? " (final)\n" : "\n");
+
+  ImageSet individual(data_image, width, height);
+  std::map<size_t, gpu::Planes> twice_cache;
+  std::map<std::pair<size_t, size_t>, std::shared_ptr<gpu::Buffer>> padded_cache;
+  bool diverging = false;
+
+  while (IterationNumber() < MaxIterations() &&
+         std::fabs(scale_infos_[scale_with_peak].max_unnormalized_image_value *
+                   scale_infos_[scale_with_peak].bias_factor) > first_threshold &&
+         (!StopOnNegativeComponents() ||
+          scale_infos_[scale_with_peak].max_unnormalized_image_value >= 0.0) &&
+         threshold_countdown > 0 && !diverging) {  // :323-543
+    ScaleInfo& info = scale_infos_[scale_with_peak];
+    // twice-convolved PSFs for this scale (:331-350), cached per major iteration
+    auto tw = twice_cache.find(scale_with_peak);
+    if (tw == twice_cache.end()) {
+      gpu::Planes t = gpu::Planes::Make(session, width, height, n_psf);
+      for (size_t i = 0; i != n_psf; ++i) {
+        session.D2D(t.Plane(i), convolved[i].Plane(scale_with_peak),
+                    npx * sizeof(float));
+        if (info.scale != 0.0f) transforms_->Transform(t.Plane(i), info.scale);
+      }
+      tw = twice_cache.emplace(scale_with_peak, std::move(t)).first;
+    }
+    const gpu::Planes& twice = tw->second;
+    // individually convolved images (:336-354)
+    individual.CopyFrom(data_image);
+    if (info.scale != 0.0f)
+      for (size_t i = 0; i != data_image.Size(); ++i)
+        transforms_->Transform(individual.Data(i), info.scale);
+
+    const float sub_iteration_gain_threshold =
+        std::fabs(info.max_unnormalized_image_value * info.bias_factor) *
+        (1.0 - settings_.sub_minor_loop_gain);
+    float first_sub_iteration_threshold = sub_iteration_gain_threshold;
+    if (first_threshold > first_sub_iteration_threshold) {
+      first_sub_iteration_threshold = first_threshold;
+      if (!has_hit_threshold_in_sub_loop) {
+        log::Info() << "Subminor loop is near minor loop threshold. "
+                       "Initiating countdown.\n";
+        has_hit_threshold_in_sub_loop = true;
+      }
+      threshold_countdown--;
+    }
+
+    if (settings_.fast_sub_minor_loop) {  // :377-462
+      const size_t sub_start = IterationNumber();
+      const size_t conv_w = utils::GetConvolutionSize(
+          info.scale, width, settings_.convolution_padding);
+      const size_t conv_h = utils::GetConvolutionSize(
+          info.scale, height, settings_.convolution_padding);
+      SubMinorLoop sub(session, width, height, conv_w, conv_h);
+      sub.SetIterationInfo(IterationNumber(), MaxIterations());
+      sub.SetThreshold(first_sub_iteration_threshold / info.bias_factor);
+      sub.SetGain(info.gain);
+      sub.SetDivergenceLimit(DivergenceLimit());
+      sub.SetAllowNegativeComponents(AllowNegativeComponents());
+      sub.SetStopOnNegativeComponent(StopOnNegativeComponents());
+      const size_t scale_border = size_t(std::ceil(info.scale * 0.5));
+      sub.SetCleanBorders(
+          std::max<size_t>(size_t(std::round(width * CleanBorderRatio())),
+                           scale_border),
+          std::max<size_t>(size_t(std::round(height * CleanBorderRatio())),
+                           scale_border));
+      sub.SetMask(d_mask_);
+      std::vector<uint32_t> xy;
+      sub.SetTrace(&xy);
+      const SubMinorLoop::RunResult r = sub.Run(individual, twice);
+      for (size_t c = 0; c + 1 < xy.size(); c += 2) {
+        trace_.push_back(xy[c]);
+        trace_.push_back(xy[c + 1]);
+        trace_.push_back(uint32_t(scale_with_peak));
+      }
+      diverging = r.diverging;
+      if (DivergenceLimit() != 0.0f && r.has_peak)
+        diverging = diverging ||
+                    std::fabs(r.peak) > initial_peak_value * DivergenceLimit();
+      if (!r.has_peak) {
+        log::Warn() << "Could not continue multi-scale clean, because the "
+                       "sub-minor loop failed to find components.\n";
+        break;
+      }
+      SetIterationNumber(sub.CurrentIteration());
+      info.n_components_cleaned += IterationNumber() - sub_start;
+      info.total_flux_cleaned += sub.FluxCleaned();
+      for (size_t i = 0; i != data_image.Size(); ++i) {
+        const size_t psf_index = data_image.PsfIndex(i);
+        auto key = std::make_pair(psf_index, scale_with_peak);
+        auto pc = padded_cache.find(key);
+        if (pc == padded_cache.end())
+          pc = padded_cache
+                   .emplace(key, SubMinorLoop::MakePaddedPsfSpectrum(
+                                     session, convolved[psf_index].Plane(scale_with_peak),
+                                     width, height, conv_w, conv_h))
+                   .first;
+        sub.CorrectResidualDirtyWithSpectrum(i, data_image.Data(i),
+                                             pc->second->Ptr());
+        if (info.scale != 0.0f) {
+          sub.GetFullIndividualModel(i, scratch_->F());
+          transforms_->Transform(scratch_->F(), info.scale);
+          gpu::Check(rdl_add(s, model_image.Data(i), scratch_->F(), npx),
+                     "rdl_add");
+        } else {
+          sub.AddIndividualModel(i, model_image.Data(i));
+        }
+      }
+    } else {  // :463-519
+      size_t n_kernel = 0;
+      std::vector<float> shape_kernel;
+      if (info.scale != 0.0f)
+        shape_kernel = MultiScaleTransforms::MakeShapeFunction(
+            info.scale, n_kernel, std::min(width, height), settings_.shape);
+      else
+        shape_kernel = {1.0f}, n_kernel = 1;
+      std::vector<float> cv(data_image.Size());
+      while (IterationNumber() < MaxIterations() &&
+             std::fabs(info.max_unnormalized_image_value * info.bias_factor) >
+                 first_sub_iteration_threshold &&
+             (!StopOnNegativeComponents() ||
+              info.max_unnormalized_image_value >= 0.0) &&
+             !diverging) {
+        const size_t x = info.max_image_value_x, y = info.max_image_value_y;
+        for (size_t i = 0; i != data_image.Size(); ++i)
+          cv[i] = session.ReadFloat(individual.Data(i) + x + y * width);
+        trace_.push_back(uint32_t(x));
+        trace_.push_back(uint32_t(y));
+        trace_.push_back(uint32_t(scale_with_peak));
+        for (size_t i = 0; i != data_image.Size(); ++i) {
+          cv[i] = cv[i] * info.gain;
+          const size_t pi = data_image.PsfIndex(i);
+          gpu::Check(rdl_subtract_psf(s, data_image.Data(i),
+                                      convolved[pi].Plane(scale_with_peak),
+                                      uint32_t(width), uint32_t(height),
+                                      uint32_t(x), uint32_t(y), cv[i]),
+                     "rdl_subtract_psf");
+          gpu::Check(rdl_subtract_psf(s, individual.Data(i), twice.Plane(pi),
+                                      uint32_t(width), uint32_t(height),
+                                      uint32_t(x), uint32_t(y), cv[i]),
+                     "rdl_subtract_psf");
+          // AddComponentToModel (:676-698): scale 0 adds the value itself
+          // (fma(1, v, m) == m + v), larger scales stamp the shape kernel.
+          gpu::Check(rdl_add_shape_component(
+                         s, model_image.Data(i), uint32_t(width),
+                         uint32_t(height), shape_kernel.data(),
+                         uint32_t(n_kernel), uint32_t(x), uint32_t(y), cv[i]),
+                     "rdl_add_shape_component");
+          info.n_components_cleaned++;
+          info.total_flux_cleaned += cv[i];
+        }
+        individual.GetLinearIntegrated(integrated.F());
+        FindPeakDirect(integrated.F(), scale_with_peak);
+        const float abs_peak =
+            std::fabs(info.max_unnormalized_image_value * info.bias_factor);
+        if (DivergenceLimit() != 0.0f)
+          diverging = abs_peak > initial_peak_value * DivergenceLimit();
+        SetIterationNumber(IterationNumber() + 1);
+      }
+    }
+
+    ActivateScales(scale_with_peak);
+    FindActiveScaleConvolvedMaxima(data_image, integrated.F(), false);
+    if (log::Verbosity() >= 3) {
+      char buf[256];
+      std::string line = "[ms] it=" + std::to_string(IterationNumber());
+      for (const ScaleInfo& e : scale_infos_) {
+        std::snprintf(buf, sizeof(buf), " | s=%g a=%d v=%.9g x=%zu y=%zu", e.scale,
+                      int(e.is_active), e.max_unnormalized_image_value * e.bias_factor,
+                      e.max_image_value_x, e.max_image_value_y);
+        line += buf;
+      }
+      std::fprintf(stderr, "%s\n", line.c_str());
+    }
+    optional_scale = SelectMaximumScale(scale_infos_);
+    if (!optional_scale) {
+      log::Warn() << "No peak found in main loop of multi-scale cleaning! "
+                     "Aborting deconvolution.\n";
+      result.another_iteration_required = false;
+      return result;
+    }
+    scale_with_peak = *optional_scale;
+    log::Info() << "Iteration " << IterationNumber() << ", scale "
+                << std::round(scale_infos_[scale_with_peak].scale) << " px : "
+                << scale_infos_[scale_with_peak].max_unnormalized_image_value *
+                       scale_infos_[scale_with_peak].bias_factor
+                << " at " << scale_infos_[scale_with_peak].max_image_value_x
+                << ',' << scale_infos_[scale_with_peak].max_image_value_y << '\n';
+  }
+
+  const bool max_iter_reached = IterationNumber() >= MaxIterations();
+  const bool negative_reached =
+      StopOnNegativeComponents() &&
+      scale_infos_[scale_with_peak].max_unnormalized_image_value < 0.0;
+  if (diverging)
+    log::Warn() << "WARNING: Multiscale clean diverged.\n";
+  result.is_diverging = diverging;
+  result.another_iteration_required =
+      !max_iter_reached && !is_final_threshold && !negative_reached && !diverging;
+  result.final_peak_value =
+      scale_infos_[scale_with_peak].max_unnormalized_image_value *
+      scale_infos_[scale_with_peak].bias_factor;
+  session.Sync();
+  return result;
+}
+
+}  // namespace radler::algorithms

@@ -1,0 +1,125 @@
+#include "multiscale_transforms.h"
+
+#include <cmath>
+
+namespace radler::algorithms::multiscale {
+
+namespace {
+// multiscale_transforms.h:186-194
+float HannWindow(float x, size_t n) {
+  return (x * 2 <= float(n + 1))
+             ? float(0.5 * (1.0 + std::cos(2.0 * M_PI * x / double(n + 1))))
+             : 0.0f;
+}
+float ShapeFunction(float x) {
+  if (x < 1.0f) {
+    const float xx = x * x;
+    return float(1.0 - double(xx));
+  }
+  return 0.0f;
+}
+// multiscale_transforms.h:118-185. The reference's GCC build contracts
+// dx*dx + dydy into an FMA (exact here: dx is a half-integer).
+std::vector<float> TaperedQuadratic(double scale, size_t& n) {
+  n = size_t(std::ceil(scale * 0.5) * 2.0) + 1;
+  std::vector<float> out(n * n, 0.0f);
+  if (scale == 0.0) {
+    out[0] = 1.0f;
+    return out;
+  }
+  float sum = 0.0f;
+  for (int y = 0; y != int(n); ++y) {
+    const float dy = float(y - 0.5 * double(n - 1));
+    const float dydy = dy * dy;
+    for (int x = 0; x != int(n); ++x) {
+      const float dx = float(x - 0.5 * double(n - 1));
+      const float r = std::sqrt(std::fma(dx, dx, dydy));
+      const float v = HannWindow(r, n) * ShapeFunction(float(double(r) / scale));
+      out[x + y * n] = v;
+      sum += v;
+    }
+  }
+  const float norm = float(1.0 / double(sum));
+  for (float& v : out) v *= norm;
+  return out;
+}
+// multiscale_transforms.h:127-161
+std::vector<float> Gaussian(double scale, size_t& n, size_t max_n) {
+  float sigma = MultiScaleTransforms::GaussianSigma(float(scale));
+  n = int(std::ceil(sigma * 12.0 / 2.0)) * 2 + 1;
+  if (n > max_n) {
+    n = max_n;
+    if ((n % 2) == 0 && n > 0) --n;
+  }
+  if (n < 1) n = 1;
+  if (sigma == 0.0f) {
+    sigma = 1.0f;
+    n = 1;
+  }
+  std::vector<float> out(n * n);
+  const float mu = float(int(n / 2));
+  const float two_sigma_sq = float(2.0 * sigma * sigma);
+  std::vector<float> g(n);
+  for (int i = 0; i != int(n); ++i) {
+    const float v = float(i) - mu;
+    g[i] = std::exp(-v * v / two_sigma_sq);
+  }
+  float sum = 0.0f;
+  for (size_t y = 0; y != n; ++y)
+    for (size_t x = 0; x != n; ++x) {
+      const float v = g[x] * g[y];
+      out[x + y * n] = v;
+      sum += v;
+    }
+  const float norm = float(1.0 / double(sum));
+  for (float& v : out) v *= norm;
+  return out;
+}
+}  // namespace
+
+std::vector<float> MultiScaleTransforms::MakeShapeFunction(float scale,
+                                                           size_t& n,
+                                                           size_t max_n,
+                                                           Shape shape) {
+  if (shape == Shape::kGaussianShape) return Gaussian(scale, n, max_n);
+  return TaperedQuadratic(scale, n);
+}
+
+float MultiScaleTransforms::KernelPeakValue(double scale, size_t max_n,
+                                            Shape shape) {
+  size_t n;
+  const std::vector<float> k = MakeShapeFunction(float(scale), n, max_n, shape);
+  return k[n / 2 + (n / 2) * n];
+}
+
+MultiScaleTransforms::MultiScaleTransforms(gpu::Session& s, size_t width,
+                                           size_t height, Shape shape)
+    : s_(s),
+      width_(width),
+      height_(height),
+      shape_(shape),
+      fft_(s.GetFft(width, height)) {}
+
+const void* MultiScaleTransforms::KernelSpectrum(float scale) {
+  auto it = spectra_.find(scale);
+  if (it != spectra_.end()) return it->second->Ptr();
+  size_t n;
+  const std::vector<float> k =
+      MakeShapeFunction(scale, n, std::min(width_, height_), shape_);
+  gpu::Buffer placed(s_, width_ * height_ * sizeof(float));
+  // schaapcommon::math::PrepareSmallConvolutionKernel
+  gpu::Check(rdl_prepare_small_kernel(s_.Handle(), placed.F(), uint32_t(width_),
+                                      uint32_t(height_), k.data(), uint32_t(n)),
+             "rdl_prepare_small_kernel");
+  auto spectrum = std::make_shared<gpu::Buffer>(s_, fft_.SpectrumBytes());
+  fft_.Forward(placed.F(), spectrum->Ptr());
+  s_.Sync();
+  spectra_[scale] = spectrum;
+  return spectrum->Ptr();
+}
+
+void MultiScaleTransforms::Transform(float* d_image, float scale) {
+  fft_.Convolve(d_image, KernelSpectrum(scale));
+}
+
+}  // namespace radler::algorithms::multiscale

@@ -1,0 +1,71 @@
+// radler::algorithms::ParallelDeconvolution (reference:
+// cpp/algorithms/parallel_deconvolution.{h,cc}). One subimage runs the
+// algorithm on the whole device-resident image set; a grid splits the image
+// into subimages (Dijkstra minimum-flux boundaries), finds the global start
+// peak, and deconvolves every subimage on the device.
+#pragma once
+
+#include <memory>
+#include <optional>
+#include <vector>
+
+#include "deconvolution_algorithm.h"
+#include "psf_offset.h"
+#include "settings.h"
+
+namespace radler::algorithms {
+
+struct ParallelDeconvolutionResult {
+  bool another_iteration_required = false;
+  std::optional<float> start_peak;
+  std::optional<float> end_peak;
+};
+
+class ParallelDeconvolution {
+ public:
+  explicit ParallelDeconvolution(const Settings& settings);
+  ~ParallelDeconvolution();
+
+  DeconvolutionAlgorithm& FirstAlgorithm() { return *algorithms_.front(); }
+  const DeconvolutionAlgorithm& FirstAlgorithm() const {
+    return *algorithms_.front();
+  }
+  const DeconvolutionAlgorithm& MaxScaleCountAlgorithm() const;
+  void SetAlgorithm(std::unique_ptr<DeconvolutionAlgorithm> algorithm);
+  void SetThreshold(double threshold);
+  void SetMinorLoopGain(double gain);
+  void SetCleanMask(const bool* mask);
+  bool IsInitialized() const { return !algorithms_.empty(); }
+  size_t SubImageCount() const { return algorithms_.size(); }
+  DeconvolutionAlgorithm& Algorithm(size_t i) { return *algorithms_[i]; }
+
+  ParallelDeconvolutionResult ExecuteMajorIteration(
+      ImageSet& data_image, ImageSet& model_image,
+      const std::vector<gpu::Planes>& psf_images,
+      const std::vector<PsfOffset>& psf_offsets, double major_loop_gain);
+
+  void FreeDeconvolutionAlgorithms() {
+    algorithms_.clear();
+    mask_ = nullptr;
+  }
+
+ private:
+  ParallelDeconvolutionResult ExecuteSingleThreadedRun(
+      ImageSet& data_image, ImageSet& model_image,
+      const std::vector<gpu::Planes>& psf_images,
+      const std::vector<PsfOffset>& psf_offsets, double major_loop_gain);
+  ParallelDeconvolutionResult ExecuteParallelRun(
+      ImageSet& data_image, ImageSet& model_image,
+      const std::vector<gpu::Planes>& psf_images,
+      const std::vector<PsfOffset>& psf_offsets, double major_loop_gain);
+
+  std::vector<std::unique_ptr<DeconvolutionAlgorithm>> algorithms_;
+  const Settings& settings_;
+  const bool* mask_ = nullptr;
+};
+
+/// parallel_deconvolution.cc:34-55 (first index on equal distance).
+size_t NearestPsfIndex(const std::vector<PsfOffset>& psf_offsets, size_t x,
+                       size_t y) noexcept;
+
+}  // namespace radler::algorithms

@@ -1,0 +1,238 @@
+// Line references are to the reference's cpp/radler.cc.
+#include "radler.h"
+
+#include <cmath>
+#include <stdexcept>
+
+#include "device.h"
+#include "generic_clean.h"
+#include "image_accessors.h"
+#include "image_set.h"
+#include "logger.h"
+#include "multiscale_algorithm.h"
+#include "parallel_deconvolution.h"
+
+namespace radler {
+
+namespace {
+[[noreturn]] void Unsupported(const char* what) {
+  throw std::runtime_error(std::string(what) +
+                           " is not available in the MI355X build of Radler");
+}
+}  // namespace
+
+Radler::Radler(const Settings& settings, std::unique_ptr<WorkTable> table,
+               double beam_size)
+    : Radler(settings, beam_size) {
+  InitializeDeconvolutionAlgorithm(std::move(table));
+}
+
+Radler::Radler(const Settings& settings, const aocommon::Image& psf_image,
+               aocommon::Image& residual_image, aocommon::Image& model_image,
+               double beam_size, aocommon::PolarizationEnum polarization)
+    : Radler(settings, beam_size) {
+  // :52-91
+  if (psf_image.Width() != settings.trimmed_image_width ||
+      psf_image.Height() != settings.trimmed_image_height)
+    throw std::runtime_error("Mismatch in PSF image size");
+  if (residual_image.Width() != settings.trimmed_image_width ||
+      residual_image.Height() != settings.trimmed_image_height)
+    throw std::runtime_error("Mismatch in residual image size");
+  if (model_image.Width() != settings.trimmed_image_width ||
+      model_image.Height() != settings.trimmed_image_height)
+    throw std::runtime_error("Mismatch in model image size");
+  auto table = std::make_unique<WorkTable>(std::vector<PsfOffset>{}, 1, 1);
+  auto e = std::make_unique<WorkTableEntry>();
+  e->polarization = polarization;
+  e->image_weight = 1.0;
+  e->psf_accessors.emplace_back(
+      std::make_unique<utils::LoadOnlyImageAccessor>(psf_image));
+  e->residual_accessor =
+      std::make_unique<utils::LoadAndStoreImageAccessor>(residual_image);
+  e->model_accessor =
+      std::make_unique<utils::LoadAndStoreImageAccessor>(model_image);
+  table->AddEntry(std::move(e));
+  InitializeDeconvolutionAlgorithm(std::move(table));
+}
+
+Radler::Radler(const Settings& settings, double beam_size)
+    : settings_(settings),
+      image_width_(settings.trimmed_image_width),
+      image_height_(settings.trimmed_image_height),
+      pixel_scale_x_(settings.pixel_scale.x),
+      pixel_scale_y_(settings.pixel_scale.y),
+      beam_size_(beam_size) {
+  // :93-117
+  if (settings.spectral_fitting.mode ==
+          schaapcommon::fitters::SpectralFittingMode::kForcedTerms &&
+      settings.spectral_fitting.forced_filename.empty())
+    throw std::runtime_error(
+        "Forced fitting filename is required when forced fitting is enabled.");
+  if (settings.parallel.grid_width == 0)
+    throw std::runtime_error("parallel.grid_width must be larger than zero");
+  if (settings.parallel.grid_height == 0)
+    throw std::runtime_error("parallel.grid_height must be larger than zero");
+  if (settings.parallel.max_threads == 0)
+    throw std::runtime_error("parallel.max_threads must be larger than zero");
+  parallel_deconvolution_ =
+      std::make_unique<algorithms::ParallelDeconvolution>(settings_);
+}
+
+Radler::~Radler() { FreeDeconvolutionAlgorithms(); }
+
+ComponentList Radler::GetComponentList() const {
+  // ParallelDeconvolution::GetComponentList (parallel_deconvolution.cc:185-210)
+  if (settings_.algorithm_type == AlgorithmType::kMultiscale)
+    Unsupported("A multiscale component list (save_source_list)");
+  ImageSet model_set(*table_, settings_.squared_joins,
+                     settings_.linked_polarizations, image_width_,
+                     image_height_, DeviceSession());
+  model_set.LoadAndAverage(false);
+  ComponentList list(image_width_, image_height_, model_set);
+  list.MergeDuplicates();
+  return list;
+}
+
+const algorithms::DeconvolutionAlgorithm& Radler::MaxScaleCountAlgorithm()
+    const {
+  return parallel_deconvolution_->MaxScaleCountAlgorithm();
+}
+
+void Radler::Perform(bool& another_iteration_required,
+                     size_t major_iteration_number) {  // :130-316
+  if (!table_) throw std::runtime_error("Radler: not initialized");
+  table_->ValidatePsfs();
+  log::Info() << " == Deconvolving (" << major_iteration_number << ") ==\n";
+  gpu::Session& s = DeviceSession();
+  ImageSet residual_set(*table_, settings_.squared_joins,
+                        settings_.linked_polarizations, image_width_,
+                        image_height_, s);
+  ImageSet model_set(*table_, settings_.squared_joins,
+                     settings_.linked_polarizations, image_width_,
+                     image_height_, s);
+  residual_set.LoadAndAverage(true);
+  model_set.LoadAndAverage(false);
+
+  const bool auto_mask_is_enabled =
+      settings_.auto_mask_sigma || settings_.absolute_auto_mask_threshold;
+  if (auto_mask_is_enabled) Unsupported("Auto-masking");
+  if (settings_.local_rms.method != LocalRmsMethod::kNone ||
+      !settings_.local_rms.image.empty())
+    Unsupported("Local-RMS thresholding");
+  parallel_deconvolution_->SetMinorLoopGain(settings_.minor_loop_gain);
+
+  if (settings_.auto_threshold_sigma) {
+    // integrated.MedianAndStdDevFromMAD() (:162-166) on the device
+    gpu::Buffer integrated(s, image_width_ * image_height_ * sizeof(float));
+    residual_set.GetLinearIntegrated(integrated.F());
+    const size_t n = image_width_ * image_height_;
+    float median = 0.0f, mad = 0.0f;
+    gpu::Check(rdl_median(s.Handle(), integrated.F(), n, 0, 0.0f, &median),
+               "rdl_median");
+    gpu::Check(rdl_median(s.Handle(), integrated.F(), n, 1, median, &mad),
+               "rdl_median");
+    const double stddev = double(mad) * 1.48260221850560;
+    log::Info() << "Estimated standard deviation of background noise: "
+                << stddev << '\n';
+    const double threshold_bias = settings_.squared_joins ? median : 0.0;
+    parallel_deconvolution_->SetThreshold(
+        std::max(stddev * (*settings_.auto_threshold_sigma) + threshold_bias,
+                 settings_.absolute_threshold));
+  }
+
+  const std::vector<gpu::Planes> psf_images = residual_set.LoadAndAveragePsfs();
+  const algorithms::ParallelDeconvolutionResult result =
+      parallel_deconvolution_->ExecuteMajorIteration(
+          residual_set, model_set, psf_images, table_->PsfOffsets(),
+          settings_.major_loop_gain);
+  another_iteration_required = result.another_iteration_required;
+
+  if (another_iteration_required && settings_.major_iteration_count != 0 &&
+      major_iteration_number >= settings_.major_iteration_count) {
+    another_iteration_required = false;
+    log::Info() << "Maximum number of major iterations was reached: not "
+                   "continuing deconvolution.\n";
+  }
+  if (another_iteration_required && settings_.minor_iteration_count != 0 &&
+      parallel_deconvolution_->FirstAlgorithm().IterationNumber() >=
+          settings_.minor_iteration_count) {
+    another_iteration_required = false;
+    log::Info() << "Maximum number of minor deconvolution iterations was "
+                   "reached: not continuing deconvolution.\n";
+  }
+  residual_set.AssignAndStoreResidual();
+  model_set.InterpolateAndStoreModel();
+}
+
+void Radler::InitializeDeconvolutionAlgorithm(
+    std::unique_ptr<WorkTable> table) {  // :333-395
+  FreeDeconvolutionAlgorithms();
+  table_ = std::move(table);
+  if (table_->OriginalGroups().empty()) throw std::runtime_error("Nothing to clean");
+  if (!std::isfinite(beam_size_)) {
+    log::Warn() << "No proper beam size available in deconvolution!\n";
+    beam_size_ = 0.0;
+  }
+  if (settings_.spectral_fitting.mode !=
+      schaapcommon::fitters::SpectralFittingMode::kNoFitting)
+    Unsupported("Spectral fitting");
+  if (!settings_.fits_mask.empty() || !settings_.casa_mask.empty() ||
+      settings_.horizon_mask_distance)
+    Unsupported("Mask files / horizon masks");
+  std::unique_ptr<algorithms::DeconvolutionAlgorithm> algorithm;
+  switch (settings_.algorithm_type) {
+    case AlgorithmType::kGenericClean:
+      algorithm = std::make_unique<algorithms::GenericClean>(
+          settings_.generic.use_sub_minor_optimization);
+      break;
+    case AlgorithmType::kMultiscale:
+      if (settings_.save_source_list) Unsupported("save_source_list");
+      algorithm = std::make_unique<algorithms::MultiScaleAlgorithm>(
+          settings_.multiscale, beam_size_, pixel_scale_x_, pixel_scale_y_,
+          settings_.save_source_list);
+      break;
+    case AlgorithmType::kIuwt:
+      Unsupported("The IUWT algorithm");
+    case AlgorithmType::kAdaptiveScalePixel:
+      Unsupported("The adaptive scale pixel algorithm");
+    case AlgorithmType::kMoreSane:
+      Unsupported("MoreSane");
+    case AlgorithmType::kPython:
+      Unsupported("Python deconvolution");
+  }
+  algorithm->SetMaxIterations(settings_.minor_iteration_count);
+  algorithm->SetThreshold(settings_.absolute_threshold);
+  algorithm->SetMinorLoopGain(settings_.minor_loop_gain);
+  algorithm->SetMajorLoopGain(settings_.major_loop_gain);
+  algorithm->SetCleanBorderRatio(settings_.border_ratio);
+  algorithm->SetDivergenceLimit(settings_.divergence_limit);
+  algorithm->SetAllowNegativeComponents(settings_.allow_negative_components);
+  algorithm->SetStopOnNegativeComponents(settings_.stop_on_negative_components);
+  parallel_deconvolution_->SetAlgorithm(std::move(algorithm));
+}
+
+void Radler::FreeDeconvolutionAlgorithms() {
+  parallel_deconvolution_->FreeDeconvolutionAlgorithms();
+  table_.reset();
+}
+
+gpu::Session& Radler::DeviceSession() const {
+  // The device is opened on first use, so constructing a Radler (argument
+  // validation) needs no GPU; Perform() fails loudly without one.
+  if (!session_) {
+    const int device = settings_.gpu_device >= 0 ? settings_.gpu_device
+                                                 : gpu::Session::DefaultDevice();
+    session_ = gpu::Session::ForDevice(device);
+  }
+  return *session_;
+}
+
+bool Radler::IsInitialized() const {
+  return parallel_deconvolution_->IsInitialized();
+}
+
+size_t Radler::IterationNumber() const {
+  return parallel_deconvolution_->FirstAlgorithm().IterationNumber();
+}
+
+}  // namespace radler

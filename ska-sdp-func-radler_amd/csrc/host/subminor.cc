@@ -1,0 +1,128 @@
+#include "subminor.h"
+
+#include <stdexcept>
+
+namespace radler::algorithms {
+
+SubMinorLoop::SubMinorLoop(gpu::Session& s, size_t width, size_t height,
+                           size_t padded_width, size_t padded_height)
+    : s_(s),
+      width_(width),
+      height_(height),
+      padded_width_(padded_width),
+      padded_height_(padded_height) {
+  gpu::Check(rdl_subminor_create(s.Handle(), &h_), "rdl_subminor_create");
+}
+
+SubMinorLoop::~SubMinorLoop() { rdl_subminor_destroy(h_); }
+
+SubMinorLoop::RunResult SubMinorLoop::Run(ImageSet& residual,
+                                          const gpu::Planes& psfs) {
+  rdl_subminor_params p{};
+  p.width = uint32_t(width_);
+  p.height = uint32_t(height_);
+  p.n_images = uint32_t(residual.Size());
+  p.n_pol = uint32_t(residual.NPolarizations());
+  p.integ = residual.Integration(false);  // GetLinearIntegrated
+  p.h_border = uint32_t(horizontal_border_);
+  p.v_border = uint32_t(vertical_border_);
+  p.allow_negative = allow_negative_;
+  p.stop_on_negative = stop_on_negative_;
+  p.threshold = threshold_;
+  p.gain = gain_;
+  p.divergence_limit = divergence_limit_;
+  p.iteration_start = current_iteration_;
+  p.max_iterations = max_iterations_;
+  p.d_mask = d_mask_;
+  n_images_ = residual.Size();
+  uint64_t cap = 0;
+  if (trace_) {
+    cap = max_iterations_ > current_iteration_ ? max_iterations_ - current_iteration_ : 0;
+    cap = std::min<uint64_t>(cap, uint64_t(1) << 22);
+  }
+  std::vector<uint32_t> tr(2 * cap);
+  rdl_subminor_result r;
+  gpu::Check(rdl_subminor_run(h_, residual.Base(), psfs.Base(), &p, &r,
+                              cap ? tr.data() : nullptr, cap),
+             "rdl_subminor_run");
+  n_selected_ = r.n_selected;
+  const size_t done = r.iteration - current_iteration_;
+  current_iteration_ = r.iteration;
+  flux_cleaned_ += r.flux_cleaned;
+  if (trace_)
+    trace_->insert(trace_->end(), tr.begin(),
+                   tr.begin() + 2 * std::min<uint64_t>(done, cap));
+  return {r.diverging != 0, r.has_peak != 0, r.peak};
+}
+
+std::shared_ptr<gpu::Buffer> SubMinorLoop::MakePaddedPsfSpectrum(
+    gpu::Session& s, const float* d_psf, size_t width, size_t height,
+    size_t pw, size_t ph) {
+  // float64 plan: see rdl_fft_create_f64 / DESIGN.md
+  gpu::Fft& fft = s.GetFft(pw, ph, true);
+  gpu::Buffer kernel(s, pw * ph * sizeof(double));
+  // Image::Untrim + PrepareConvolutionKernel (subminor_loop.cc:199-202)
+  gpu::Check(rdl_prepare_psf_kernel_f64(s.Handle(), kernel.D(), uint32_t(pw),
+                                        uint32_t(ph), d_psf, uint32_t(width),
+                                        uint32_t(height)),
+             "rdl_prepare_psf_kernel_f64");
+  auto spectrum = std::make_shared<gpu::Buffer>(s, fft.SpectrumBytes());
+  fft.Forward64(kernel.D(), spectrum->Ptr());
+  s.Sync();
+  return spectrum;
+}
+
+void SubMinorLoop::CorrectResidualDirty(size_t image_index, float* d_residual,
+                                        const float* d_psf, size_t psf_key) {
+  auto it = psf_spectra_.find(psf_key);
+  if (it == psf_spectra_.end())
+    it = psf_spectra_
+             .emplace(psf_key, MakePaddedPsfSpectrum(s_, d_psf, width_, height_,
+                                                     padded_width_,
+                                                     padded_height_))
+             .first;
+  CorrectResidualDirtyWithSpectrum(image_index, d_residual, it->second->Ptr());
+}
+
+void SubMinorLoop::CorrectResidualDirtyWithSpectrum(size_t image_index,
+                                                    float* d_residual,
+                                                    const void* d_spectrum) {
+  gpu::Fft& fft = s_.GetFft(padded_width_, padded_height_, true);
+  padded_.Resize(s_, padded_width_ * padded_height_ * sizeof(double));
+  // GetFullIndividualModel + Image::Untrim, fused scatter into a zero plane
+  const uint32_t ox = uint32_t((padded_width_ - width_) / 2);
+  const uint32_t oy = uint32_t((padded_height_ - height_) / 2);
+  gpu::Check(rdl_subminor_model_f64(h_, uint32_t(image_index), padded_.D(),
+                                    uint32_t(padded_width_),
+                                    uint32_t(padded_height_), ox, oy),
+             "rdl_subminor_model_f64");
+  fft.Convolve64(padded_.D(), d_spectrum);
+  // Image::Trim (to float) + residual -= (subminor_loop.cc:214-217)
+  gpu::Check(rdl_trim_subtract_f64(s_.Handle(), d_residual, uint32_t(width_),
+                                   uint32_t(height_), padded_.D(),
+                                   uint32_t(padded_width_),
+                                   uint32_t(padded_height_)),
+             "rdl_trim_subtract_f64");
+}
+
+void SubMinorLoop::GetFullIndividualModel(size_t image_index, float* d_dest) {
+  gpu::Check(rdl_subminor_model(h_, uint32_t(image_index), d_dest,
+                                uint32_t(width_), uint32_t(height_), 0, 0, 0),
+             "rdl_subminor_model");
+}
+
+void SubMinorLoop::AddIndividualModel(size_t image_index, float* d_model) {
+  gpu::Check(rdl_subminor_model(h_, uint32_t(image_index), d_model,
+                                uint32_t(width_), uint32_t(height_), 0, 0, 1),
+             "rdl_subminor_model");
+}
+
+void SubMinorLoop::GetSelection(std::vector<uint32_t>& positions,
+                                std::vector<float>& models) const {
+  positions.resize(n_selected_);
+  models.resize(n_selected_ * n_images_);
+  gpu::Check(rdl_subminor_get(h_, positions.data(), models.data(), n_selected_),
+             "rdl_subminor_get");
+}
+
+}  // namespace radler::algorithms

@@ -1,0 +1,402 @@
+// The `radler` Python module of the MI355X build: the reference's pybind11
+// surface (python/pywrappers.cc, pysettings.cc, pywork_table.cc,
+// pyradler.cc, pycomponent_list.cc) over libradler_amd, plus `radler.gpu`
+// helpers for device-resident runs (bench / tests).
+#include <pybind11/iostream.h>
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <sstream>
+
+#include "device.h"
+#include "device_run.h"
+#include "image_accessors.h"
+#include "logger.h"
+#include "radler.h"
+
+namespace py = pybind11;
+using AccessorList = std::vector<std::unique_ptr<aocommon::ImageAccessor>>;
+PYBIND11_MAKE_OPAQUE(AccessorList)
+
+namespace {
+
+using FloatArray = py::array_t<float, py::array::c_style>;
+
+template <class T>
+std::unique_ptr<T> MakeAccessor(FloatArray& data) {
+  if (data.ndim() != 2)
+    throw std::runtime_error("Provided array should have 2 dimensions.");
+  aocommon::Image view(data.mutable_data(), size_t(data.shape(1)),
+                       size_t(data.shape(0)));
+  return std::make_unique<T>(view);
+}
+
+void InitSettings(py::module& m) {  // python/pysettings.cc
+  py::enum_<radler::AlgorithmType>(m, "AlgorithmType")
+      .value("generic_clean", radler::AlgorithmType::kGenericClean)
+      .value("multiscale", radler::AlgorithmType::kMultiscale)
+      .value("iuwt", radler::AlgorithmType::kIuwt)
+      .value("more_sane", radler::AlgorithmType::kMoreSane)
+      .value("python", radler::AlgorithmType::kPython);
+  py::enum_<radler::LocalRmsMethod>(m, "LocalRmsMethod")
+      .value("none", radler::LocalRmsMethod::kNone)
+      .value("rms_window", radler::LocalRmsMethod::kRmsWindow)
+      .value("rms_and_minimum_window", radler::LocalRmsMethod::kRmsAndMinimumWindow);
+  py::enum_<radler::MultiscaleShape>(m, "MultiscaleShape")
+      .value("tapered_quadratic", radler::MultiscaleShape::kTaperedQuadraticShape)
+      .value("gaussian", radler::MultiscaleShape::kGaussianShape);
+
+  py::class_<radler::Settings> settings(m, "Settings");
+  settings.def(py::init<>())
+      .def_readwrite("trimmed_image_width", &radler::Settings::trimmed_image_width)
+      .def_readwrite("trimmed_image_height", &radler::Settings::trimmed_image_height)
+      .def_readwrite("channels_out", &radler::Settings::channels_out)
+      .def_readwrite("pixel_scale", &radler::Settings::pixel_scale)
+      .def_readwrite("thread_count", &radler::Settings::thread_count)
+      .def_readwrite("prefix_name", &radler::Settings::prefix_name)
+      .def_readwrite("linked_polarizations", &radler::Settings::linked_polarizations)
+      .def_readwrite("parallel", &radler::Settings::parallel)
+      .def_readwrite("absolute_threshold", &radler::Settings::absolute_threshold)
+      .def_readwrite("minor_loop_gain", &radler::Settings::minor_loop_gain)
+      .def_readwrite("major_loop_gain", &radler::Settings::major_loop_gain)
+      .def_readwrite("auto_threshold_sigma", &radler::Settings::auto_threshold_sigma)
+      .def_readwrite("auto_mask_sigma", &radler::Settings::auto_mask_sigma)
+      .def_readwrite("absolute_auto_mask_threshold",
+                     &radler::Settings::absolute_auto_mask_threshold)
+      .def_readwrite("save_source_list", &radler::Settings::save_source_list)
+      .def_readwrite("minor_iteration_count", &radler::Settings::minor_iteration_count)
+      .def_readwrite("major_iteration_count", &radler::Settings::major_iteration_count)
+      .def_readwrite("divergence_limit", &radler::Settings::divergence_limit)
+      .def_readwrite("allow_negative_components",
+                     &radler::Settings::allow_negative_components)
+      .def_readwrite("stop_on_negative_components",
+                     &radler::Settings::stop_on_negative_components)
+      .def_readwrite("squared_joins", &radler::Settings::squared_joins)
+      .def_readwrite("spectral_correction_frequency",
+                     &radler::Settings::spectral_correction_frequency)
+      .def_readwrite("spectral_correction", &radler::Settings::spectral_correction)
+      .def_readwrite("border_ratio", &radler::Settings::border_ratio)
+      .def_readwrite("fits_mask", &radler::Settings::fits_mask)
+      .def_readwrite("casa_mask", &radler::Settings::casa_mask)
+      .def_readwrite("horizon_mask_distance", &radler::Settings::horizon_mask_distance)
+      .def_readwrite("horizon_mask_filename", &radler::Settings::horizon_mask_filename)
+      .def_readwrite("local_rms", &radler::Settings::local_rms)
+      .def_readwrite("spectral_fitting", &radler::Settings::spectral_fitting)
+      .def_readwrite("algorithm_type", &radler::Settings::algorithm_type)
+      .def_readwrite("generic", &radler::Settings::generic)
+      .def_readwrite("multiscale", &radler::Settings::multiscale)
+      .def_readwrite("more_sane", &radler::Settings::more_sane)
+      .def_readwrite("python", &radler::Settings::python);
+
+  py::class_<radler::Settings::Generic>(settings, "Generic")
+      .def_readwrite("use_sub_minor_optimization",
+                     &radler::Settings::Generic::use_sub_minor_optimization);
+  py::class_<radler::Settings::Multiscale>(settings, "Multiscale")
+      .def_readwrite("fast_sub_minor_loop", &radler::Settings::Multiscale::fast_sub_minor_loop)
+      .def_readwrite("sub_minor_loop_gain", &radler::Settings::Multiscale::sub_minor_loop_gain)
+      .def_readwrite("scale_bias", &radler::Settings::Multiscale::scale_bias)
+      .def_readwrite("max_scales", &radler::Settings::Multiscale::max_scales)
+      .def_readwrite("convolution_padding", &radler::Settings::Multiscale::convolution_padding)
+      .def_readwrite("scale_list", &radler::Settings::Multiscale::scale_list)
+      .def_readwrite("shape", &radler::Settings::Multiscale::shape);
+  py::class_<radler::Settings::MoreSane>(settings, "MoreSane")
+      .def_readwrite("location", &radler::Settings::MoreSane::location)
+      .def_readwrite("arguments", &radler::Settings::MoreSane::arguments)
+      .def_readwrite("sigma_levels", &radler::Settings::MoreSane::sigma_levels);
+  py::class_<radler::Settings::Python>(settings, "Python")
+      .def_readwrite("filename", &radler::Settings::Python::filename);
+  py::class_<radler::Settings::Parallel>(settings, "Parallel")
+      .def_readwrite("grid_width", &radler::Settings::Parallel::grid_width)
+      .def_readwrite("grid_height", &radler::Settings::Parallel::grid_height)
+      .def_readwrite("max_threads", &radler::Settings::Parallel::max_threads);
+  py::class_<radler::Settings::PixelScale>(settings, "PixelScale")
+      .def_readwrite("x", &radler::Settings::PixelScale::x)
+      .def_readwrite("y", &radler::Settings::PixelScale::y);
+  py::class_<radler::Settings::LocalRms>(settings, "LocalRms")
+      .def_readwrite("method", &radler::Settings::LocalRms::method)
+      .def_readwrite("window", &radler::Settings::LocalRms::window)
+      .def_readwrite("image", &radler::Settings::LocalRms::image)
+      .def_readwrite("strength", &radler::Settings::LocalRms::strength);
+  py::class_<radler::Settings::SpectralFitting>(settings, "SpectralFitting")
+      .def_readwrite("mode", &radler::Settings::SpectralFitting::mode)
+      .def_readwrite("terms", &radler::Settings::SpectralFitting::terms)
+      .def_readwrite("forced_filename", &radler::Settings::SpectralFitting::forced_filename);
+
+  py::enum_<aocommon::PolarizationEnum>(m, "Polarization")
+      .value("stokes_i", aocommon::PolarizationEnum::StokesI)
+      .value("stokes_q", aocommon::PolarizationEnum::StokesQ)
+      .value("stokes_u", aocommon::PolarizationEnum::StokesU)
+      .value("stokes_v", aocommon::PolarizationEnum::StokesV)
+      .value("rr", aocommon::PolarizationEnum::RR)
+      .value("rl", aocommon::PolarizationEnum::RL)
+      .value("lr", aocommon::PolarizationEnum::LR)
+      .value("ll", aocommon::PolarizationEnum::LL)
+      .value("xx", aocommon::PolarizationEnum::XX)
+      .value("xy", aocommon::PolarizationEnum::XY)
+      .value("yx", aocommon::PolarizationEnum::YX)
+      .value("yy", aocommon::PolarizationEnum::YY)
+      .value("full_stokes", aocommon::PolarizationEnum::FullStokes)
+      .value("instrumental", aocommon::PolarizationEnum::Instrumental)
+      .value("diagonal_instrumental", aocommon::PolarizationEnum::DiagonalInstrumental);
+  py::enum_<schaapcommon::fitters::SpectralFittingMode>(m, "SpectralFittingMode")
+      .value("no_fitting", schaapcommon::fitters::SpectralFittingMode::kNoFitting)
+      .value("polynomial", schaapcommon::fitters::SpectralFittingMode::kPolynomial)
+      .value("log_polynomial", schaapcommon::fitters::SpectralFittingMode::kLogPolynomial)
+      .value("forced_terms", schaapcommon::fitters::SpectralFittingMode::kForcedTerms);
+}
+
+void InitWorkTable(py::module& m) {  // python/pywork_table.cc
+  py::class_<AccessorList>(m, "VectorUniquePtrImageAccessor")
+      .def("__len__", [](const AccessorList& self) { return self.size(); })
+      .def("append", [](AccessorList& self, FloatArray& psf) {
+        self.emplace_back(MakeAccessor<radler::utils::LoadOnlyImageAccessor>(psf));
+      });
+
+  py::class_<radler::WorkTable>(m, "WorkTable")
+      .def(py::init([](py::array_t<size_t> py_psf_offsets, size_t n_original_groups,
+                       size_t n_deconvolution_groups, size_t channel_index_offset) {
+             std::vector<radler::PsfOffset> offsets;
+             if (py::len(py_psf_offsets)) {
+               if (py_psf_offsets.ndim() != 2)
+                 throw py::type_error(
+                     "Non-empty PSF offsets must have two dimensions.");
+               if (py_psf_offsets.shape(1) != 2)
+                 throw py::type_error("PSF entries must have two values.");
+               auto u = py_psf_offsets.unchecked<2>();
+               for (py::ssize_t i = 0; i != py_psf_offsets.shape(0); ++i)
+                 offsets.emplace_back(u(i, 0), u(i, 1));
+             }
+             return std::make_unique<radler::WorkTable>(
+                 std::move(offsets), n_original_groups, n_deconvolution_groups,
+                 channel_index_offset);
+           }),
+           py::arg("py_psf_offsets"), py::arg("n_original_groups"),
+           py::arg("n_deconvolution_groups"), py::arg("channel_index_offset") = 0)
+      .def_property_readonly("original_groups", [](const radler::WorkTable& t) {
+        std::vector<std::vector<const radler::WorkTableEntry*>> g = t.OriginalGroups();
+        return g;
+      }, py::return_value_policy::reference_internal)
+      .def_property_readonly("deconvolution_groups",
+                             &radler::WorkTable::DeconvolutionGroups)
+      .def("__len__", &radler::WorkTable::Size)
+      .def("__str__", [](const radler::WorkTable& self) {
+        std::stringstream s;
+        s << self;
+        return s.str();
+      })
+      .def_property_readonly("channel_index_offset",
+                             &radler::WorkTable::GetChannelIndexOffset)
+      .def("add_entry",
+           [](radler::WorkTable& self, radler::WorkTableEntry& entry) {
+             self.AddEntry(std::make_unique<radler::WorkTableEntry>(std::move(entry)));
+           },
+           py::arg("entry"))
+      .def("__iter__",
+           [](const radler::WorkTable& self) {
+             return py::make_iterator(self.Begin(), self.End());
+           },
+           py::keep_alive<0, 1>());
+
+  py::class_<radler::WorkTableEntry>(m, "WorkTableEntry")
+      .def(py::init<>())
+      .def_property_readonly("central_frequency",
+                             &radler::WorkTableEntry::CentralFrequency)
+      .def_readwrite("index", &radler::WorkTableEntry::index)
+      .def_readwrite("band_start_frequency", &radler::WorkTableEntry::band_start_frequency)
+      .def_readwrite("band_end_frequency", &radler::WorkTableEntry::band_end_frequency)
+      .def_readwrite("polarization", &radler::WorkTableEntry::polarization)
+      .def_readwrite("original_channel_index",
+                     &radler::WorkTableEntry::original_channel_index)
+      .def_readwrite("original_interval_index",
+                     &radler::WorkTableEntry::original_interval_index)
+      .def_readwrite("mask_channel_index", &radler::WorkTableEntry::mask_channel_index)
+      .def_readwrite("image_weight", &radler::WorkTableEntry::image_weight)
+      .def_property_readonly(
+          "psfs",
+          [](radler::WorkTableEntry& self) -> AccessorList& {
+            return self.psf_accessors;
+          },
+          py::return_value_policy::reference)
+      .def_property("residual", nullptr,
+                    [](radler::WorkTableEntry& self, FloatArray& residual) {
+                      self.residual_accessor =
+                          MakeAccessor<radler::utils::LoadAndStoreImageAccessor>(residual);
+                    })
+      .def_property("model", nullptr,
+                    [](radler::WorkTableEntry& self, FloatArray& model) {
+                      self.model_accessor =
+                          MakeAccessor<radler::utils::LoadAndStoreImageAccessor>(model);
+                    });
+}
+
+void InitRadler(py::module& m) {  // python/pyradler.cc
+  py::class_<radler::Radler>(m, "Radler")
+      .def(py::init([](const radler::Settings& settings,
+                       radler::WorkTable& work_table, double beam_size) {
+             if (settings.thread_count == 0)
+               throw std::runtime_error("Number of threads should be > 0.");
+             return std::make_unique<radler::Radler>(
+                 settings, std::make_unique<radler::WorkTable>(std::move(work_table)),
+                 beam_size);
+           }),
+           py::arg("settings"), py::arg("work_table"), py::arg("beam_size"))
+      .def(py::init([](const radler::Settings& settings, FloatArray& psf,
+                       FloatArray& residual, FloatArray& model, double beam_size,
+                       size_t n_deconvolution_groups, py::array_t<double>& frequencies,
+                       py::array_t<double>& weights,
+                       aocommon::PolarizationEnum polarization) {
+             if (settings.thread_count == 0)
+               throw std::runtime_error("Number of threads should be > 0.");
+             if (psf.ndim() != residual.ndim() || psf.ndim() != model.ndim())
+               throw std::runtime_error(
+                   "Provided arrays should have equal dimension count.");
+             for (py::ssize_t d = 0; d < psf.ndim(); ++d)
+               if (residual.shape(d) != psf.shape(d) || model.shape(d) != psf.shape(d))
+                 throw std::runtime_error("Provided arrays should have equal shape.");
+             if (psf.ndim() != 2 && psf.ndim() != 3)
+               throw std::runtime_error("Provided arrays should have 2 or 3 dimensions.");
+             const size_t height = psf.shape(psf.ndim() - 2);
+             const size_t width = psf.shape(psf.ndim() - 1);
+             const size_t n_images = psf.ndim() == 2 ? 1 : psf.shape(0);
+             if (settings.spectral_fitting.mode !=
+                     schaapcommon::fitters::SpectralFittingMode::kNoFitting &&
+                 frequencies.size() == 0)
+               throw std::runtime_error(
+                   "Frequencies are required when spectral fitting is enabled.");
+             if (frequencies.size() > 0 &&
+                 (frequencies.ndim() != 2 || size_t(frequencies.shape(0)) != n_images ||
+                  frequencies.shape(1) != 2))
+               throw std::runtime_error(
+                   "Provided frequencies should have shape (n_images, 2).");
+             if (weights.size() > 0 &&
+                 (weights.ndim() != 1 || size_t(weights.shape(0)) != n_images))
+               throw std::runtime_error("Provided weights should have shape (n_images).");
+             auto table = std::make_unique<radler::WorkTable>(
+                 std::vector<radler::PsfOffset>{}, n_images, n_deconvolution_groups);
+             const size_t plane = width * height;
+             for (size_t i = 0; i < n_images; ++i) {
+               aocommon::Image p(psf.mutable_data() + i * plane, width, height);
+               aocommon::Image r(residual.mutable_data() + i * plane, width, height);
+               aocommon::Image mo(model.mutable_data() + i * plane, width, height);
+               auto e = std::make_unique<radler::WorkTableEntry>();
+               if (frequencies.size() > 0) {
+                 auto u = frequencies.unchecked<2>();
+                 e->band_start_frequency = u(i, 0);
+                 e->band_end_frequency = u(i, 1);
+               }
+               e->polarization = polarization;
+               e->original_channel_index = i;
+               e->image_weight = weights.size() > 0 ? weights.unchecked<1>()(i) : 1.0;
+               e->psf_accessors.emplace_back(
+                   std::make_unique<radler::utils::LoadOnlyImageAccessor>(p));
+               e->residual_accessor =
+                   std::make_unique<radler::utils::LoadAndStoreImageAccessor>(r);
+               e->model_accessor =
+                   std::make_unique<radler::utils::LoadAndStoreImageAccessor>(mo);
+               table->AddEntry(std::move(e));
+             }
+             return std::make_unique<radler::Radler>(settings, std::move(table),
+                                                     beam_size);
+           }),
+           py::arg("settings"), py::arg("psf").noconvert(),
+           py::arg("residual").noconvert(), py::arg("model").noconvert(),
+           py::arg("beam_size"), py::arg("n_deconvolution_groups") = 0,
+           py::arg("frequencies") = py::array_t<double>(),
+           py::arg("weights") = py::array_t<double>(),
+           py::arg("polarization") = aocommon::PolarizationEnum::StokesI)
+      .def("perform",
+           [](radler::Radler& self, size_t major_iteration_number) {
+             py::gil_scoped_release release;
+             bool another = false;
+             self.Perform(another, major_iteration_number);
+             return another;
+           },
+           py::arg("major_iteration_number"))
+      .def_property_readonly("iteration_number", &radler::Radler::IterationNumber)
+      .def_property_readonly("component_list", &radler::Radler::GetComponentList);
+}
+
+void InitComponentList(py::module& m) {  // python/pycomponent_list.cc
+  py::class_<radler::ComponentList>(m, "ComponentList")
+      .def(py::init<>())
+      .def(py::init<size_t, size_t, size_t, size_t>())
+      .def_property("n_scales", &radler::ComponentList::NScales,
+                    &radler::ComponentList::SetNScales)
+      .def_property_readonly("n_frequencies", &radler::ComponentList::NFrequencies)
+      .def("clear", &radler::ComponentList::Clear)
+      .def_property_readonly("width", &radler::ComponentList::Width)
+      .def_property_readonly("height", &radler::ComponentList::Height)
+      .def("component_count", [](const radler::ComponentList& self, size_t s) {
+        if (s >= self.NScales())
+          throw std::out_of_range("Scale index out of range in component count");
+        return self.ComponentCount(s);
+      });
+}
+
+py::dict ResultDict(const radler::algorithms::ParallelDeconvolutionResult& r,
+                    size_t iterations) {
+  py::dict d;
+  d["another_iteration_required"] = r.another_iteration_required;
+  d["start_peak"] = r.start_peak ? py::cast(*r.start_peak) : py::none();
+  d["end_peak"] = r.end_peak ? py::cast(*r.end_peak) : py::none();
+  d["iterations"] = iterations;
+  return d;
+}
+
+void InitGpu(py::module& m) {
+  py::module g = m.def_submodule("gpu", "MI355X device helpers (bench/tests)");
+  g.def("set_verbosity", &radler::log::SetVerbosity);
+  py::class_<radler::DeviceRun>(g, "DeviceRun")
+      .def(py::init([](const radler::Settings& settings, FloatArray psf,
+                       FloatArray residual, std::vector<double> weights,
+                       double beam_size) {
+             const size_t n = psf.ndim() == 2 ? 1 : psf.shape(0);
+             return std::make_unique<radler::DeviceRun>(
+                 settings, psf.data(), residual.data(), n, weights, beam_size);
+           }),
+           py::arg("settings"), py::arg("psf"), py::arg("residual"),
+           py::arg("weights") = std::vector<double>(), py::arg("beam_size") = 0.0)
+      .def("restore", &radler::DeviceRun::Restore)
+      .def("execute",
+           [](radler::DeviceRun& self) {
+             radler::algorithms::ParallelDeconvolutionResult r;
+             {
+               py::gil_scoped_release release;
+               r = self.Execute();
+             }
+             return ResultDict(r, self.LastIterations());
+           })
+      .def("sync", &radler::DeviceRun::Sync)
+      .def("residual", [](const radler::DeviceRun& self) {
+        std::vector<float> v = self.Residual();
+        return py::array_t<float>(v.size(), v.data());
+      })
+      .def("model", [](const radler::DeviceRun& self) {
+        std::vector<float> v = self.Model();
+        return py::array_t<float>(v.size(), v.data());
+      })
+      .def("trace", [](const radler::DeviceRun& self) {
+        const std::vector<uint32_t>& t = self.Trace();
+        py::array_t<uint32_t> a({py::ssize_t(t.size() / 3), py::ssize_t(3)});
+        std::copy(t.begin(), t.end(), a.mutable_data());
+        return a;
+      })
+      .def("session_handle", [](radler::DeviceRun& self) {
+        return reinterpret_cast<uintptr_t>(self.Session().Handle());
+      })
+      .def("stream_handle", [](radler::DeviceRun& self) {
+        return reinterpret_cast<uintptr_t>(rdl_session_stream(self.Session().Handle()));
+      });
+}
+
+}  // namespace
+
+PYBIND11_MODULE(radler, m) {  // python/pywrappers.cc
+  m.doc() = "MI355X-native Radio Astronomical Deconvolution Library (radler API)";
+  InitSettings(m);
+  InitWorkTable(m);
+  InitRadler(m);
+  InitComponentList(m);
+  InitGpu(m);
+}

@@ -25,7 +25,7 @@ def declared_symbols(header=HEADER):
 class Integration(C.Structure):
     _fields_ = [("n_images", C.c_uint32), ("n_pol", C.c_uint32),
                 ("n_channels", C.c_uint32), ("mode", C.c_uint32),
-                ("copy_fast_path", C.c_uint32),
+                ("copy_fast_path", C.c_uint32), ("pol_mask", C.c_uint32),
                 ("weights", C.c_float * MAX_IMAGES), ("factor", C.c_float)]
 
 
@@ -36,6 +36,7 @@ def integration(n_channels=1, n_pol=1, weights=None, pol_factor=1.0, mode=0):
     g.n_images, g.n_pol, g.n_channels, g.mode = n, n_pol, n_channels, mode
     w = np.ones(n_channels, np.float32) if weights is None else np.asarray(weights, np.float32)
     g.copy_fast_path = int(n_channels == 1 and n_pol == 1 and mode != 2)
+    g.pol_mask = (1 << n_pol) - 1
     for i in range(n):
         g.weights[i] = float(w[i // n_pol])
     wsum = float(sum(float(x) for x in w if x != 0.0))

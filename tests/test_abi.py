@@ -41,6 +41,6 @@ def test_library_reports_version_and_errors_without_gpu():
 def test_struct_layouts_match_header():
     # offsets the C compiler uses (checked against sizeof in the library build
     # would need a GPU-free helper; here: natural alignment expectations)
-    assert C.sizeof(Integration) == 4 * 5 + 4 * 64 + 4
+    assert C.sizeof(Integration) == 4 * 6 + 4 * 64 + 4
     assert C.sizeof(HogbomParams) % 8 == 0
     assert C.sizeof(SubminorParams) % 8 == 0

@@ -146,6 +146,47 @@ def test_fft_convolve(sess, orc, w, h):
     assert np.abs(g - o).max() <= tol
 
 
+@pytest.mark.parametrize("w,h", [(64, 64), (94, 47), (1128, 96)])
+def test_fft64_residual_correction(sess, orc, w, h):
+    """rdl_fft64_convolve + rdl_trim_subtract_f64: residual -= float(model (*) psf)
+    on a padded plane; against the oracle (float64 FFT, rounded to float), the
+    result agrees to float rounding (|err| <= 2 ulp of max(|conv|, |residual|))."""
+    rng = np.random.default_rng(21)
+    pw, ph = w + 10, h + 6
+    psf = rng.standard_normal((h, w)).astype(np.float32)
+    model = np.zeros((h, w), np.float32)
+    idx = rng.choice(w * h, 40, replace=False)
+    model.flat[idx] = rng.standard_normal(40).astype(np.float32)
+    residual = rng.standard_normal((h, w)).astype(np.float32)
+    f = C.c_void_p()
+    sess.rdl.rdl_fft_create_f64(sess.h, pw, ph, C.byref(f))
+    nb = sess.rdl.lib.rdl_fft_spectrum_bytes(f)
+    assert nb == (pw // 2 + 1) * ph * 16
+    dpsf, dres = sess.array(psf), sess.array(residual)
+    kern = sess.array(shape=(ph, pw), dtype=np.float64)
+    spec, work = sess.array(shape=(nb // 8,), dtype=np.float64), sess.array(shape=(nb // 8,), dtype=np.float64)
+    sess.rdl.rdl_prepare_psf_kernel_f64(sess.h, kern.vp, pw, ph, dpsf.vp, w, h)
+    sess.rdl.rdl_fft64_forward(f, kern.vp, spec.vp)
+    unt = np.zeros((ph, pw), np.float64)
+    unt[(ph - h) // 2:(ph - h) // 2 + h, (pw - w) // 2:(pw - w) // 2 + w] = model
+    dm = sess.array(unt)
+    sess.rdl.rdl_fft64_convolve(f, dm.vp, spec.vp, work.vp)
+    sess.rdl.rdl_trim_subtract_f64(sess.h, dres.vp, w, h, dm.vp, pw, ph)
+    # oracle: Untrim, PrepareConvolutionKernel, Convolve, Trim, subtract
+    k = np.zeros((ph, pw), np.float32)
+    k[(ph - h) // 2:(ph - h) // 2 + h, (pw - w) // 2:(pw - w) // 2 + w] = psf
+    k = np.roll(k, (-(ph // 2), -(pw // 2)), axis=(0, 1)).copy()
+    o = unt.astype(np.float32)
+    orc.convolve(o, k)
+    trimmed = o[(ph - h) // 2:(ph - h) // 2 + h, (pw - w) // 2:(pw - w) // 2 + w]
+    expect = residual - trimmed
+    err = np.abs(dres.get() - expect).max()
+    assert err <= 2.4e-7 * max(np.abs(trimmed).max(), np.abs(residual).max())
+    for x in (dpsf, dres, kern, spec, work, dm):
+        x.free()
+    sess.rdl.rdl_fft_destroy(f)
+
+
 def test_prepare_kernels(sess, orc):
     w, h, pw, ph = 40, 30, 48, 36
     rng = np.random.default_rng(2)
@@ -164,6 +205,33 @@ def test_prepare_kernels(sess, orc):
     assert np.array_equal(dk.get(), np.roll(full, (-(n // 2), -(n // 2)), axis=(0, 1)))
     dp.free()
     dk.free()
+
+
+@pytest.mark.parametrize("w,h", [(128, 128), (200, 150), (520, 300)])
+@pytest.mark.parametrize("scale", [8.0, 16.0, 32.0, 64.0, 128.0])
+@pytest.mark.parametrize("shape", [0, 1])
+def test_small_kernel_and_shape_component(sess, orc, w, h, scale, shape):
+    """Kernels of every multiscale size (n up to 257 -> 264 KiB uploads):
+    placement is exact, AddShapeComponent bit-exact vs the oracle."""
+    k = orc.shape_function(scale, min(w, h), shape)
+    n = k.shape[0]
+    if n > min(w, h):
+        pytest.skip("kernel larger than image")
+    d = sess.array(shape=(h, w))
+    sess.rdl.rdl_prepare_small_kernel(sess.h, d.vp, w, h, k.ctypes.data_as(C.c_void_p), n)
+    full = np.zeros((h, w), np.float32)
+    full[:n, :n] = k
+    assert np.array_equal(d.get(), np.roll(full, (-(n // 2), -(n // 2)), axis=(0, 1)))
+    rng = np.random.default_rng(n)
+    img = rng.standard_normal((h, w)).astype(np.float32)
+    d.upload(img)
+    expect = img.copy()
+    for (x, y, g) in ((w // 2, h // 2, 0.25), (1, h - 2, -0.5), (w - 1, 0, 1.5)):
+        sess.rdl.rdl_add_shape_component(sess.h, d.vp, w, h, k.ctypes.data_as(C.c_void_p), n,
+                                         x, y, C.c_float(g))
+        orc.add_shape_component(expect, scale, x, y, g, shape)
+    assert np.array_equal(bits(d.get()), bits(expect))
+    d.free()
 
 
 def test_median(sess):
