@@ -39,8 +39,8 @@ SEED = 20251015
 
 
 def make_problem(size, seed, n_points, n_blobs, fwhm=4.0):
-    from synthetic import make_dirty, make_psf, make_sky
-    psf = make_psf(size, size, fwhm=fwhm)
+    from synthetic import make_dirty, make_psf_uv, make_sky
+    psf = make_psf_uv(size, size, fwhm=fwhm)
     sky = make_sky(size, size, n_points, n_blobs, seed, flux_range=(1e-3, 1.0),
                    blob_sigma=(2.0, 40.0))
     dirty = make_dirty(psf, sky, NOISE, seed)
@@ -63,7 +63,7 @@ def settings_for(rd, size, max_iter, max_scales, threshold):
 
 
 # algorithmic bytes per launch are accumulated by the C-ABI per family
-FAMILIES = ["fft", "spectrum_multiply", "find_peak", "subminor_loop", "subminor_select",
+FAMILIES = ["fft", "fft64", "spectrum_multiply", "spectrum_multiply64", "find_peak", "subminor_loop", "subminor_select",
             "trim_subtract", "add", "integrate", "rms", "axpy", "radix_select"]
 
 

@@ -68,7 +68,8 @@ struct rdl_session {
   void* h_small = nullptr;       // 64 KiB pinned host
   rdl::Scratch partials;         // per-block partial keys
   rdl::Scratch radix;            // radix-select histograms
-  bool poison = false;            // RDL_POISON=1: NaN-fill fresh allocations
+  bool poison = false;
+  bool trace_subminor = false;    // RDL_TRACE_SUBMINOR=1: per-launch stats            // RDL_POISON=1: NaN-fill fresh allocations
   rdl::Scratch kernel;           // host-provided kernels (H2D destination)
   rdl::Scratch loop_state;       // Högbom loop state / partials / trace
   void* comm = nullptr;          // ncclComm_t when initialised
@@ -82,6 +83,12 @@ struct rdl_session {
 
 namespace rdl {
 // RAII-less helper used by launchers: records start/end events when timing.
+// Adds algorithmic bytes to a family after the fact (e.g. the sub-minor loop,
+// whose iteration count is known only when it returns).
+inline void AddTimingBytes(rdl_session* s, const char* family, double bytes) {
+  if (s->timing) s->timings[family].bytes += bytes;
+}
+
 struct ScopedTiming {
   rdl_session* s;
   const char* family;

@@ -94,6 +94,8 @@ int rdl_session_create(int device, rdl_session** out) {
   // debug aid: fill every fresh allocation with NaN bytes (0xff)
   const char* poison = std::getenv("RDL_POISON");
   s->poison = poison && poison[0] == '1';
+  const char* trace = std::getenv("RDL_TRACE_SUBMINOR");
+  s->trace_subminor = trace && trace[0] == '1';
   RDL_HIP_CHECK(hipMalloc(&s->d_small, 1 << 16));
   RDL_HIP_CHECK(hipHostMalloc(&s->h_small, 1 << 16, hipHostMallocDefault));
   *out = s.release();

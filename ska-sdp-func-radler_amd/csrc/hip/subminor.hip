@@ -20,6 +20,8 @@
 // "start at scratch[0], strict '>'" scan.
 #include <cmath>
 
+#include <cstdio>
+
 #include "rdl_internal.h"
 
 struct rdl_subminor {
@@ -672,6 +674,14 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
     rdl::SetError("sub-minor loop: grid exchange timed out");
     return RDL_ERR_TIMEOUT;
   }
+  // algorithmic bytes: 12 B x N_img x N_sel per iteration
+  rdl::AddTimingBytes(s, "subminor_loop",
+                      12.0 * double(ni) * double(n_sel) *
+                          double(res.iteration - p->iteration_start));
+  if (s->trace_subminor)
+    std::fprintf(stderr, "[subminor] n_sel=%llu g=%u lds=%d iters=%llu\n",
+                 (unsigned long long)n_sel, g, int(use_lds),
+                 (unsigned long long)(res.iteration - p->iteration_start));
   out->iteration = res.iteration;
   out->has_peak = 1;
   out->peak = res.peak;

@@ -21,6 +21,32 @@ def make_psf(w, h, fwhm=4.0, pa_deg=30.0, axis_ratio=0.7, sidelobe=0.05):
     return out
 
 
+def make_psf_uv(w, h, fwhm=4.0, pa_deg=30.0, axis_ratio=0.7, ring_px=9.0, ring_depth=0.4):
+    """Dirty beam synthesised from a non-negative uv weighting, as an
+    interferometer's is: W(u,v) = elliptical Gaussian taper (the FWHM-`fwhm`
+    core) x (1 - ring_depth/2 + ring_depth/2 cos(2 pi ring_px |uv|)) >= 0, whose
+    inverse FFT gives ring sidelobes at ~ring_px with a peak at the centre.
+    A non-negative spectrum keeps CLEAN convergent (make_psf's ring sidelobes
+    have a negative spectrum and make long CLEAN runs diverge).
+    psf[h//2, w//2] == 1.0 exactly."""
+    u = np.fft.fftfreq(w)[None, :]
+    v = np.fft.fftfreq(h)[:, None]
+    pa = np.deg2rad(pa_deg)
+    # image-plane sigma along the two axes -> uv-plane sigma 1/(2 pi sigma)
+    sx = fwhm / 2.3548
+    sy = sx * axis_ratio
+    uu = u * np.cos(pa) + v * np.sin(pa)
+    vv = -u * np.sin(pa) + v * np.cos(pa)
+    taper = np.exp(-2.0 * np.pi ** 2 * ((uu * sx) ** 2 + (vv * sy) ** 2))
+    r = np.hypot(u, v)
+    cover = 1.0 - ring_depth / 2 + ring_depth / 2 * np.cos(2.0 * np.pi * ring_px * r)
+    psf = np.fft.fftshift(np.fft.ifft2(taper * cover).real)
+    psf /= psf[h // 2, w // 2]
+    out = psf.astype(np.float32)
+    out[h // 2, w // 2] = 1.0
+    return out
+
+
 def make_sky(w, h, n_points, n_blobs, seed, margin=16, flux_range=(1e-3, 1.0),
              blob_sigma=(2.0, 40.0)):
     rng = np.random.default_rng(seed)
