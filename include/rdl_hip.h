@@ -216,6 +216,12 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
                      rdl_subminor_result* out, uint32_t* h_trace,
                      uint64_t trace_cap);
 
+/* Kernel choice for rdl_subminor_run (results are identical): mode 0 picks
+ * automatically, 1 forces the LDS-resident loop, 2 the register-resident
+ * loop; target_per_block (0 = keep) sets the selected pixels per workgroup
+ * above which the register loop spreads over more workgroups. */
+int rdl_subminor_set_tuning(rdl_subminor* h, int mode, uint32_t target_per_block);
+
 /* SubMinorLoop::GetFullIndividualModel (subminor_loop.cc:186-193), fused
  * with the caller's use: mode 0 writes the model of image `image_index` into
  * a zeroed dest (dest_w x dest_h, placed at offset ox,oy — Image::Untrim);

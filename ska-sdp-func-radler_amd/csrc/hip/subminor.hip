@@ -38,6 +38,9 @@ struct rdl_subminor {
   uint32_t* d_pos = nullptr;
   float* d_r = nullptr;
   float* d_m = nullptr;
+  int mode = 0;                  // 0 auto, 1 LDS kernel, 2 register kernel
+  uint32_t target_per_block = 1024;  // pixels per workgroup (multi-workgroup)
+  uint32_t single_max = 2048;         // largest selection kept on one workgroup
 };
 
 namespace rdl {
@@ -168,6 +171,7 @@ struct LoopArgs {
   uint64_t iteration_start, max_iterations;
   int32_t allow_negative, stop_on_negative;
   int32_t use_lds;
+  int32_t prof;           // accumulate per-phase cycles (block 0, wave 0)
 };
 
 struct LoopResult {
@@ -466,6 +470,410 @@ __global__ __launch_bounds__(256) void ScatterModel(const uint32_t* pos,
   }
 }
 
+// ------------------------------------------------- register-resident loop
+// SubminorLoopReg: the same loop with each thread's ITEMS selected pixels
+// (positions, residuals, model values) held in VGPRs, so one iteration is
+//   * ITEMS x N_img PSF gathers issued back to back (one memory round trip),
+//   * FMAs + integration + per-thread argmax in registers,
+//   * a wave argmax, the wave winner's payload into a parity slot in LDS,
+//   * ONE workgroup barrier; every wave then reduces the slots itself.
+// With G > 1 workgroups the block winners are exchanged through epoch-tagged
+// 8-byte granules ({epoch, word}, single-copy-atomic sc1 stores/loads): wave 0
+// sweeps all G records until every tag matches, so the data is the flag and
+// no counter or fence round trip is needed (parity-double-buffered so a fast
+// block never overwrites a record a slow one has not read).
+constexpr uint32_t kRegThreads = 512;
+constexpr uint32_t kRegWaves = kRegThreads / 64;
+
+// DPP cross-lane moves (gfx9 family): a 64-lane max in 6 VALU steps instead
+// of 6 ds_bpermute round trips; the result is read from lane 63 (or lane 0
+// for the 8-lane form) into a scalar.
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ uint64_t DppU64(uint64_t v) {
+  const uint32_t lo = uint32_t(__builtin_amdgcn_update_dpp(
+      0, int(uint32_t(v)), CTRL, ROW_MASK, 0xf, false));
+  const uint32_t hi = uint32_t(__builtin_amdgcn_update_dpp(
+      0, int(uint32_t(v >> 32)), CTRL, ROW_MASK, 0xf, false));
+  return (uint64_t(hi) << 32) | lo;
+}
+__device__ __forceinline__ uint64_t ReadLaneU64(uint64_t v, int lane) {
+  const uint32_t lo = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v)), lane));
+  const uint32_t hi = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v >> 32)), lane));
+  return (uint64_t(hi) << 32) | lo;
+}
+// Max over lanes 0..7 (others must hold 0); uniform result.
+__device__ __forceinline__ uint64_t Max8U64(uint64_t v) {
+  uint64_t t;
+  t = DppU64<0xb1>(v);  // quad_perm [1,0,3,2]
+  v = t > v ? t : v;
+  t = DppU64<0x4e>(v);  // quad_perm [2,3,0,1]
+  v = t > v ? t : v;
+  t = DppU64<0x141>(v);  // row_half_mirror
+  v = t > v ? t : v;
+  return ReadLaneU64(v, 0);
+}
+// Max over the 64 lanes; uniform result.
+__device__ __forceinline__ uint64_t Max64U64(uint64_t v) {
+  uint64_t t;
+  t = DppU64<0xb1>(v);
+  v = t > v ? t : v;
+  t = DppU64<0x4e>(v);
+  v = t > v ? t : v;
+  t = DppU64<0x141>(v);
+  v = t > v ? t : v;
+  t = DppU64<0x140>(v);  // row_mirror
+  v = t > v ? t : v;
+  t = DppU64<0x142, 0xa>(v);  // row_bcast:15 into rows 1 and 3
+  v = t > v ? t : v;
+  t = DppU64<0x143, 0xc>(v);  // row_bcast:31 into rows 2 and 3
+  v = t > v ? t : v;
+  return ReadLaneU64(v, 63);
+}
+// Workgroup barrier that orders LDS only: __syncthreads() also drains vmcnt,
+// which would make every iteration wait for its own trace/granule stores.
+__device__ __forceinline__ void LdsBarrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+__device__ __forceinline__ int FirstLane(bool pred) {
+  const uint64_t b = __ballot(pred);
+  return b ? __builtin_ctzll(b) : 0;
+}
+
+template <int NI>
+struct RegSlot {
+  uint64_t key;
+  uint32_t pos;
+  float r[NI];
+};
+
+__device__ __forceinline__ void StoreGranule(uint64_t* g, uint32_t epoch,
+                                             uint32_t v) {
+  __hip_atomic_store(g, (uint64_t(epoch) << 32) | v, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t LoadGranule(uint64_t* g) {
+  return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int NI, int ITEMS>
+__global__ __launch_bounds__(kRegThreads) void SubminorLoopReg(LoopArgs a) {
+  constexpr int REC = 3 + NI;  // granules per record: key hi, key lo, pos, r[NI]
+  __shared__ RegSlot<NI> slots[2][kRegWaves];
+  __shared__ RegSlot<NI> gwin;
+  __shared__ uint32_t gflag;
+
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint64_t base = uint64_t(blockIdx.x) * a.per_block;
+  const uint32_t cnt =
+      base >= a.n_sel ? 0u : uint32_t(min<uint64_t>(a.per_block, a.n_sel - base));
+  const int n_img = int(a.n_img);
+  const int n_pol = int(a.n_pol);
+
+  uint32_t pos[ITEMS];
+  float R[ITEMS][NI];
+  float M[ITEMS][NI];
+#pragma unroll
+  for (int i = 0; i < ITEMS; ++i) {
+    const uint32_t j = tid + uint32_t(i) * kRegThreads;
+    const bool valid = j < cnt;
+    pos[i] = valid ? a.pos[base + j] : 0u;
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+      R[i][k] = (valid && k < n_img) ? a.r[size_t(k) * a.n_sel + base + j] : 0.0f;
+      M[i][k] = 0.0f;
+    }
+  }
+
+  const int W = int(a.width), H = int(a.height);
+  const size_t plane = size_t(a.width) * a.height;
+  float c[NI];
+#pragma unroll
+  for (int k = 0; k < NI; ++k) c[k] = 0.0f;
+  int cx = 0, cy = 0;
+  bool have_component = false;
+  float start_abs = 0.0f;
+  bool diverging = false;
+  float flux = 0.0f;
+  uint64_t iteration = a.iteration_start;
+  float m = 0.0f;
+  uint32_t epoch = 0;
+  uint64_t* gran = reinterpret_cast<uint64_t*>(a.records);
+
+  uint64_t ph[6] = {0, 0, 0, 0, 0, 0};
+  const bool prof = a.prof && blockIdx.x == 0 && wave == 0;
+  uint64_t t_prev = prof ? __builtin_amdgcn_s_memtime() : 0;
+#define RDL_PHASE(i)                                       \
+  if (prof) {                                              \
+    const uint64_t t_now = __builtin_amdgcn_s_memtime();   \
+    ph[i] += t_now - t_prev;                               \
+    t_prev = t_now;                                        \
+  }
+  while (true) {
+    // ---- subtract the current component: all gathers first, then FMAs
+    if (have_component) {
+      float pv[ITEMS][NI];
+      bool in[ITEMS];
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        const uint32_t j = tid + uint32_t(i) * kRegThreads;
+        const int px = int(pos[i] & 0xffffu), py = int(pos[i] >> 16);
+        const int dx = px - cx + W / 2, dy = py - cy + H / 2;
+        in[i] = j < cnt && dx >= 0 && dx < W && dy >= 0 && dy < H;
+        const size_t off = in[i] ? size_t(dy) * a.width + size_t(dx) : 0;
+#pragma unroll
+        for (int k = 0; k < NI; ++k)
+          pv[i][k] = k < n_img ? a.psfs[size_t(k / n_pol) * plane + off] : 0.0f;
+      }
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i)
+#pragma unroll
+        for (int k = 0; k < NI; ++k)
+          if (in[i] && k < n_img) R[i][k] = __builtin_fmaf(-pv[i][k], c[k], R[i][k]);
+    }
+    RDL_PHASE(0)
+    // ---- integrate + per-thread argmax
+    uint64_t best = 0;
+    int best_i = 0;
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+      const uint32_t j = tid + uint32_t(i) * kRegThreads;
+      if (j < cnt) {
+        const float integ = IntegratePixel(a.integ, [&](uint32_t kk) {
+          float r = R[i][0];
+#pragma unroll
+          for (int q = 1; q < NI; ++q) r = (uint32_t(q) == kk) ? R[i][q] : r;
+          return r;
+        });
+        uint64_t key = MaxKey(integ, a.allow_negative, base + j);
+        if (base + j == 0 && integ != integ) key = ~0ull;  // scratch[0] is NaN
+        if (key > best) {
+          best = key;
+          best_i = i;
+        }
+      }
+    }
+    // ---- wave argmax; the owner (or lane 0 when nothing qualifies, which
+    // stands for selection index 0) writes the wave's slot
+    RDL_PHASE(1)
+    const uint64_t wmax = Max64U64(best);
+    const uint32_t par = epoch & 1u;
+    const int owner_lane = wmax != 0 ? FirstLane(best == wmax) : 0;
+    if (int(lane) == owner_lane) {
+      RegSlot<NI>& sl = slots[par][wave];
+      sl.key = wmax;
+      uint32_t pp = pos[0];
+      float rr[NI];
+#pragma unroll
+      for (int k = 0; k < NI; ++k) rr[k] = R[0][k];
+#pragma unroll
+      for (int i = 1; i < ITEMS; ++i)
+        if (i == best_i && wmax != 0) {
+          pp = pos[i];
+#pragma unroll
+          for (int k = 0; k < NI; ++k) rr[k] = R[i][k];
+        }
+      sl.pos = pp;
+#pragma unroll
+      for (int k = 0; k < NI; ++k) sl.r[k] = rr[k];
+    }
+    RDL_PHASE(2)
+    LdsBarrier();
+    RDL_PHASE(3)
+    // ---- block winner: every wave reduces the slots (ties -> lowest wave,
+    // which only matters for the all-zero case)
+    const uint64_t sk = lane < kRegWaves ? slots[par][lane].key : 0ull;
+    const uint64_t bkey = Max8U64(sk);
+    const uint32_t bw = bkey != 0 ? uint32_t(FirstLane(sk == bkey && lane < kRegWaves)) : 0u;
+    uint64_t gkey = bkey;
+    uint32_t wpos = slots[par][bw].pos;
+    float wr[NI];
+#pragma unroll
+    for (int k = 0; k < NI; ++k) wr[k] = slots[par][bw].r[k];
+
+    if (a.n_blocks > 1) {
+      ++epoch;  // 1, 2, ... (never 0: granules are zeroed per launch)
+      uint64_t* mine = gran + (size_t(par) * a.n_blocks + blockIdx.x) * REC;
+      // wave 1 publishes (its stores drain off wave 0's vmcnt) while wave 0
+      // sweeps
+      if (wave == 1 && lane < uint32_t(REC)) {
+        uint32_t v;
+        if (lane == 0) v = uint32_t(gkey >> 32);
+        else if (lane == 1) v = uint32_t(gkey);
+        else if (lane == 2) v = wpos;
+        else {
+          v = __float_as_uint(wr[0]);
+#pragma unroll
+          for (int k = 1; k < NI; ++k)
+            if (int(lane) - 3 == k) v = __float_as_uint(wr[k]);
+        }
+        StoreGranule(mine + lane, epoch, v);
+      }
+      if (wave == 0) {
+        // sweep: lane b handles blocks b, b+64, ...; all tags must match
+        const uint32_t nb = a.n_blocks;
+        uint64_t lk = 0;
+        uint32_t lb = 0xffffffffu;
+        uint32_t lrec[REC] = {};
+        uint64_t spins = 0;
+        bool failed = false;
+        while (true) {
+          bool ok = true;
+          lk = 0;
+          lb = 0xffffffffu;
+          for (uint32_t b = lane; b < nb; b += 64) {
+            uint64_t* rec = gran + (size_t(par) * nb + b) * REC;
+            uint32_t v[REC];
+#pragma unroll
+            for (int w = 0; w < REC; ++w) {
+              const uint64_t x = LoadGranule(rec + w);
+              ok &= uint32_t(x >> 32) == epoch;
+              v[w] = uint32_t(x);
+            }
+            const uint64_t key = (uint64_t(v[0]) << 32) | v[1];
+            if (lb == 0xffffffffu || key > lk) {
+              lk = key;
+              lb = b;
+#pragma unroll
+              for (int w = 0; w < REC; ++w) lrec[w] = v[w];
+            }
+          }
+          if (__all(ok)) break;
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > (uint64_t(1) << 26)) {
+            failed = true;
+            break;
+          }
+        }
+        // wave argmax over (key, block): keys are unique unless 0, and 0
+        // means block 0 (lane 0 holds it first)
+        const uint64_t kmax = Max64U64(lk);
+        const int src = kmax != 0 ? FirstLane(lk == kmax) : 0;
+        uint32_t rec[REC];
+#pragma unroll
+        for (int w = 0; w < REC; ++w)
+          rec[w] = uint32_t(__builtin_amdgcn_readlane(int(lrec[w]), src));
+        if (lane == 0) {
+          gwin.key = (uint64_t(rec[0]) << 32) | rec[1];
+          gwin.pos = rec[2];
+#pragma unroll
+          for (int kk = 0; kk < NI; ++kk) gwin.r[kk] = __uint_as_float(rec[3 + kk]);
+          gflag = failed ? 1u : 0u;
+        }
+      }
+      LdsBarrier();
+      if (gflag) {
+        if (tid == 0) StoreSc1(&a.result[8], 1u);
+        return;
+      }
+      gkey = gwin.key;
+      wpos = gwin.pos;
+#pragma unroll
+      for (int k = 0; k < NI; ++k) wr[k] = gwin.r[k];
+    } else {
+      ++epoch;
+    }
+
+    RDL_PHASE(4)
+    // ---- identical decisions everywhere (subminor_loop.cc:56-89)
+    const uint64_t winner_p = (gkey == 0 || gkey == ~0ull)
+                                  ? 0ull
+                                  : uint64_t(0xffffffffu - uint32_t(gkey));
+    m = IntegratePixel(a.integ, [&](uint32_t kk) {
+      float r = wr[0];
+#pragma unroll
+      for (int q = 1; q < NI; ++q) r = (uint32_t(q) == kk) ? wr[q] : r;
+      return r;
+    });
+    if (!have_component) {
+      start_abs = fabsf(m);
+    } else {
+      if (a.divergence_limit != 0.0f)
+        diverging = fabsf(m) > start_abs * a.divergence_limit;
+      ++iteration;
+    }
+    const bool go = fabsf(m) > a.threshold && iteration < a.max_iterations &&
+                    (!a.stop_on_negative || m >= 0.0f) && !diverging;
+    if (!go) break;
+#pragma unroll
+    for (int k = 0; k < NI; ++k) c[k] = k < n_img ? wr[k] * a.gain : 0.0f;
+    flux += m * a.gain;
+    cx = int(wpos & 0xffffu);
+    cy = int(wpos >> 16);
+    if (winner_p >= base && winner_p < base + cnt) {
+      const uint32_t j = uint32_t(winner_p - base);
+      if (j % kRegThreads == tid) {
+        const int wi = int(j / kRegThreads);
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i)
+          if (i == wi)
+#pragma unroll
+            for (int k = 0; k < NI; ++k)
+              if (k < n_img) M[i][k] += c[k];
+      }
+    }
+    if (blockIdx.x == 0 && tid == 0 && a.trace) {
+      const uint64_t t = iteration - a.iteration_start;
+      if (t < a.trace_cap) {
+        a.trace[2 * t] = uint32_t(cx);
+        a.trace[2 * t + 1] = uint32_t(cy);
+      }
+    }
+    have_component = true;
+    RDL_PHASE(5)
+  }
+#undef RDL_PHASE
+  if (prof && lane == 0) {
+    uint64_t* out = reinterpret_cast<uint64_t*>(a.result + 16);
+    for (int i = 0; i < 6; ++i) out[i] = ph[i];
+  }
+
+#pragma unroll
+  for (int i = 0; i < ITEMS; ++i) {
+    const uint32_t j = tid + uint32_t(i) * kRegThreads;
+    if (j < cnt)
+#pragma unroll
+      for (int k = 0; k < NI; ++k)
+        if (k < n_img) a.m[size_t(k) * a.n_sel + base + j] = M[i][k];
+  }
+  if (blockIdx.x == 0 && tid == 0) {
+    LoopResult* r = reinterpret_cast<LoopResult*>(a.result);
+    r->iteration = iteration;
+    r->peak = m;
+    r->diverging = diverging ? 1 : 0;
+    r->flux = flux;
+  }
+}
+
+template <int NI, int ITEMS>
+int LaunchReg(const LoopArgs& a, hipStream_t stream) {
+  auto kernel = SubminorLoopReg<NI, ITEMS>;
+  if (a.n_blocks > 1) {
+    void* args[] = {const_cast<LoopArgs*>(&a)};
+    RDL_HIP_CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(kernel),
+                                             dim3(a.n_blocks), dim3(kRegThreads),
+                                             args, 0, stream));
+  } else {
+    kernel<<<1, kRegThreads, 0, stream>>>(a);
+    RDL_HIP_CHECK(hipGetLastError());
+  }
+  return RDL_OK;
+}
+
+// Register budget: ITEMS x N_img residuals + model values + gathers per lane.
+constexpr uint32_t RegMaxItems(uint32_t ni) {
+  return ni <= 2 ? 8 : ni <= 4 ? 4 : 2;
+}
+
+template <int NI>
+int LaunchRegItems(const LoopArgs& a, uint32_t items, hipStream_t stream) {
+  constexpr uint32_t kMax = RegMaxItems(NI);
+  if (items <= 1) return LaunchReg<NI, 1>(a, stream);
+  if (items <= 2 || kMax == 2) return LaunchReg<NI, 2>(a, stream);
+  if (items <= 4 || kMax == 4) return LaunchReg<NI, (kMax >= 4 ? 4 : 2)>(a, stream);
+  return LaunchReg<NI, (kMax >= 8 ? 8 : 2)>(a, stream);
+}
+
 int Grow(void** p, size_t* have, size_t need, hipStream_t stream) {
   if (*have >= need) return RDL_OK;
   if (*p) {
@@ -599,22 +1007,48 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   RDL_HIP_CHECK(hipGetLastError());
 
   // ---------------- partition and loop
-  const size_t bytes_per_px = 4 + 8 * size_t(ni);
-  const size_t lds_cap = 150 * 1024;
   const uint32_t max_blocks = std::max(1, std::min(s->n_cus, 256));
-  uint32_t g;
-  if (n_sel <= 4096)
-    g = 1;
-  else
-    g = std::min<uint64_t>(max_blocks, (n_sel + 4095) / 4096);
-  uint64_t per = (n_sel + g - 1) / g;
-  bool use_lds = per * bytes_per_px <= lds_cap;
-  if (!use_lds) {
-    g = max_blocks;
+  // register kernel: N_img <= 8, <= 4096 pixels per workgroup
+  uint32_t ni_t = ni <= 1 ? 1 : ni <= 2 ? 2 : ni <= 4 ? 4 : 8;
+  uint32_t g = 1;
+  uint64_t per = n_sel;
+  bool use_reg = ni <= 8 && h->mode != 1;
+  const uint64_t reg_cap = uint64_t(rdl::kRegThreads) * rdl::RegMaxItems(ni_t);
+  if (use_reg) {
+    if (n_sel > std::min<uint64_t>(reg_cap, h->single_max)) {
+      const uint64_t target = std::max<uint32_t>(h->target_per_block, 512);
+      g = uint32_t(std::min<uint64_t>(max_blocks, (n_sel + target - 1) / target));
+      g = std::max<uint32_t>(g, 2);
+      per = (n_sel + g - 1) / g;
+      use_reg = per <= reg_cap;
+    }
+  }
+  if (!use_reg && h->mode == 2) {
+    rdl::SetError("register sub-minor kernel cannot hold this selection");
+    return RDL_ERR_ARG;
+  }
+  uint32_t items = 0;
+  bool use_lds = false;
+  size_t lds_bytes = 0;
+  if (use_reg) {
+    const uint64_t need = (per + rdl::kRegThreads - 1) / rdl::kRegThreads;
+    items = need <= 1 ? 1 : need <= 2 ? 2 : need <= 4 ? 4 : 8;
+  } else {
+    const size_t bytes_per_px = 4 + 8 * size_t(ni);
+    const size_t lds_cap = 150 * 1024;
+    if (n_sel <= 4096)
+      g = 1;
+    else
+      g = std::min<uint64_t>(max_blocks, (n_sel + 4095) / 4096);
     per = (n_sel + g - 1) / g;
     use_lds = per * bytes_per_px <= lds_cap;
+    if (!use_lds) {
+      g = max_blocks;
+      per = (n_sel + g - 1) / g;
+      use_lds = per * bytes_per_px <= lds_cap;
+    }
+    lds_bytes = use_lds ? per * bytes_per_px : 0;
   }
-  const size_t lds_bytes = use_lds ? per * bytes_per_px : 0;
   rdl::LoopArgs la{};
   la.pos = h->d_pos;
   la.r = h->d_r;
@@ -637,8 +1071,11 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   la.allow_negative = p->allow_negative;
   la.stop_on_negative = p->stop_on_negative;
   la.use_lds = use_lds ? 1 : 0;
+  la.prof = s->trace_subminor ? 1 : 0;
   const uint64_t n_trace = (h_trace && trace_cap) ? trace_cap : 0;
-  const size_t rec_bytes = size_t(2) * g * la.rec_words * sizeof(uint32_t);
+  const size_t rec_bytes =
+      use_reg ? (size_t(2) * g * (3 + ni_t) * sizeof(uint64_t) + 15) / 16 * 16
+              : size_t(2) * g * la.rec_words * sizeof(uint32_t);
   const size_t sync_need = 256 + 256 + rec_bytes + n_trace * 8;
   RDL_TRY(rdl::Grow(&h->sync, &h->sync_bytes, sync_need, st));
   char* sb = static_cast<char*>(h->sync);
@@ -647,22 +1084,40 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   la.records = reinterpret_cast<uint32_t*>(sb + 512);
   la.trace = n_trace ? reinterpret_cast<uint32_t*>(sb + 512 + rec_bytes) : nullptr;
   la.trace_cap = n_trace;
-  RDL_HIP_CHECK(hipMemsetAsync(sb, 0, 512, st));
+  // zero counter, result and (register kernel) the epoch-tagged granules
+  RDL_HIP_CHECK(hipMemsetAsync(sb, 0, use_reg ? 512 + rec_bytes : 512, st));
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  if (s->trace_subminor) {
+    ev0 = s->GetEvent();
+    ev1 = s->GetEvent();
+    RDL_HIP_CHECK(hipEventRecord(ev0, st));
+  }
   {
     rdl::ScopedTiming t(s, "subminor_loop", 0.0);
-    if (ni == 1)
+    if (use_reg) {
+      if (ni_t == 1)
+        RDL_TRY(rdl::LaunchRegItems<1>(la, items, st));
+      else if (ni_t == 2)
+        RDL_TRY(rdl::LaunchRegItems<2>(la, items, st));
+      else if (ni_t == 4)
+        RDL_TRY(rdl::LaunchRegItems<4>(la, items, st));
+      else
+        RDL_TRY(rdl::LaunchRegItems<8>(la, items, st));
+    } else if (ni == 1) {
       RDL_TRY(rdl::LaunchLoop<1>(la, lds_bytes, st));
-    else if (ni <= 2)
+    } else if (ni <= 2) {
       RDL_TRY(rdl::LaunchLoop<2>(la, lds_bytes, st));
-    else if (ni <= 4)
+    } else if (ni <= 4) {
       RDL_TRY(rdl::LaunchLoop<4>(la, lds_bytes, st));
-    else if (ni <= 8)
+    } else if (ni <= 8) {
       RDL_TRY(rdl::LaunchLoop<8>(la, lds_bytes, st));
-    else if (ni <= 16)
+    } else if (ni <= 16) {
       RDL_TRY(rdl::LaunchLoop<16>(la, lds_bytes, st));
-    else
+    } else {
       RDL_TRY(rdl::LaunchLoop<RDL_MAX_IMAGES>(la, lds_bytes, st));
+    }
   }
+  if (s->trace_subminor) RDL_HIP_CHECK(hipEventRecord(ev1, st));
   rdl::LoopResult res{};
   uint32_t err = 0;
   RDL_HIP_CHECK(hipMemcpyAsync(&res, la.result, sizeof(res),
@@ -678,10 +1133,22 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   rdl::AddTimingBytes(s, "subminor_loop",
                       12.0 * double(ni) * double(n_sel) *
                           double(res.iteration - p->iteration_start));
-  if (s->trace_subminor)
-    std::fprintf(stderr, "[subminor] n_sel=%llu g=%u lds=%d iters=%llu\n",
-                 (unsigned long long)n_sel, g, int(use_lds),
-                 (unsigned long long)(res.iteration - p->iteration_start));
+  if (s->trace_subminor) {
+    float ms = 0.0f;
+    RDL_HIP_CHECK(hipEventElapsedTime(&ms, ev0, ev1));
+    s->event_pool.push_back(ev0);
+    s->event_pool.push_back(ev1);
+    uint64_t ph[6] = {};
+    RDL_HIP_CHECK(hipMemcpy(ph, la.result + 16, sizeof(ph), hipMemcpyDeviceToHost));
+    std::fprintf(stderr,
+                 "[subminor] n_sel=%llu g=%u kind=%d iters=%llu us=%.1f "
+                 "gather=%llu integ=%llu wred=%llu bar=%llu xchg=%llu dec=%llu\n",
+                 (unsigned long long)n_sel, g, use_reg ? 10 + int(items) : int(use_lds),
+                 (unsigned long long)(res.iteration - p->iteration_start),
+                 double(ms) * 1e3, (unsigned long long)ph[0], (unsigned long long)ph[1],
+                 (unsigned long long)ph[2], (unsigned long long)ph[3],
+                 (unsigned long long)ph[4], (unsigned long long)ph[5]);
+  }
   out->iteration = res.iteration;
   out->has_peak = 1;
   out->peak = res.peak;
@@ -693,6 +1160,15 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
                                  hipMemcpyDeviceToHost, st));
     RDL_HIP_CHECK(hipStreamSynchronize(st));
   }
+  return RDL_OK;
+}
+
+int rdl_subminor_set_tuning(rdl_subminor* h, int mode,
+                            uint32_t target_per_block) {
+  RDL_ARG_CHECK(h, "NULL argument");
+  RDL_ARG_CHECK(mode >= 0 && mode <= 2, "mode must be 0, 1 or 2");
+  h->mode = mode;
+  if (target_per_block) h->target_per_block = target_per_block;
   return RDL_OK;
 }
 

@@ -301,33 +301,54 @@ def test_hogbom_bit_exact(sess, orc):
         a.free()
 
 
-@pytest.mark.parametrize("w,n_src,threshold_frac,mgain,max_iter", [
-    (128, 10, 0.0, 0.8, 300),       # small set: one workgroup
-    (512, 200, 0.002, 1.0, 2000),   # noise-level selection: multi-workgroup exchange
-])
-def test_subminor_loop_bit_exact(sess, orc, w, n_src, threshold_frac, mgain, max_iter):
+SUBMINOR_CASES = [
+    # w, n_src, threshold_frac, mgain, max_iter, n_ch, mode, target
+    (128, 10, 0.0, 0.8, 300, 1, 0, 0),        # small set: one workgroup
+    (512, 200, 0.002, 1.0, 2000, 1, 0, 0),    # noise-level selection: multi-workgroup
+    (128, 10, 0.0, 0.8, 300, 1, 1, 0),        # LDS-resident kernel forced
+    (512, 200, 0.002, 1.0, 2000, 1, 1, 0),
+    (256, 60, 0.001, 1.0, 1500, 1, 2, 512),   # register kernel spread over many blocks
+    (256, 60, 0.001, 1.0, 1500, 1, 2, 4096),
+    (200, 30, 0.002, 0.9, 800, 2, 0, 0),      # joined channels
+    (200, 30, 0.002, 0.9, 800, 3, 2, 700),
+    (160, 20, 0.003, 0.9, 600, 5, 0, 0),
+    (160, 20, 0.003, 0.9, 600, 8, 2, 600),
+    (160, 20, 0.003, 0.9, 600, 5, 1, 0),
+]
+
+
+@pytest.mark.parametrize("w,n_src,threshold_frac,mgain,max_iter,n_ch,mode,target",
+                         SUBMINOR_CASES)
+def test_subminor_loop_bit_exact(sess, orc, w, n_src, threshold_frac, mgain, max_iter,
+                                 n_ch, mode, target):
     """GenericClean's Clark path: the sub-minor loop's component trace and
-    model values are bit-exact; the residual after CorrectResidualDirty is
-    FFT-based (rocFFT vs float64), |err| <= 5e-6 * max|dirty|."""
+    model values are bit-exact (every kernel variant, 1..8 joined channels);
+    the residual after CorrectResidualDirty is FFT-based (rocFFT vs float64),
+    |err| <= 5e-6 * max|dirty|."""
     h = w
     psf, dirty = synthetic(w, h, n_src, 7)
-    res_o, mod_o = dirty[None].copy(), np.zeros((1, h, w), np.float32)
-    pk = float(np.abs(dirty).max())
+    dirties = np.stack([dirty * np.float32(1.0 + 0.15 * k) + np.float32(1e-3 * k) *
+                        np.roll(dirty, 3 * k, axis=1) for k in range(n_ch)]).astype(np.float32)
+    psfs = np.stack([psf] * n_ch)
+    res_o, mod_o = dirties.copy(), np.zeros((n_ch, h, w), np.float32)
+    integ = orc.integrate(dirties) if n_ch > 1 else dirties[0]
+    pk = float(np.abs(integ).max())
     thr = threshold_frac * pk
     alg = OracleAlgorithm(orc, 0, threshold=thr, max_iterations=max_iter, border_ratio=0.0,
                           use_sub_minor=1, major_loop_gain=mgain)
-    r, trace_o = alg.execute(res_o, mod_o, psf[None])
+    r, trace_o = alg.execute(res_o, mod_o, psfs)
     # GPU, as GenericClean::ExecuteMajorIteration with sub-minor optimisation
-    dres, dpsf = sess.array(dirty), sess.array(psf)
-    found, x, y, v = sess.find_peak(dres, w, h)
+    dres, dpsf = sess.array(dirties), sess.array(psfs)
+    _, _, _, v = orc.find_peak(integ, True)
     # generic_clean.cc:99-112 in float arithmetic
     first = max(np.float32(thr),
                 np.float32(abs(v)) * (np.float32(1.0) - np.float32(mgain)))
     sm = C.c_void_p()
     sess.rdl.rdl_subminor_create(sess.h, C.byref(sm))
+    sess.rdl.rdl_subminor_set_tuning(sm, mode, target)
     p = SubminorParams()
-    p.width, p.height, p.n_images, p.n_pol = w, h, 1, 1
-    p.integ = integration(1, 1, mode=0)
+    p.width, p.height, p.n_images, p.n_pol = w, h, n_ch, 1
+    p.integ = integration(n_ch, 1, mode=0)
     p.allow_negative, p.stop_on_negative = 1, 0
     p.threshold, p.gain, p.divergence_limit = np.float32(first), 0.1, 4.0
     p.iteration_start, p.max_iterations = 0, max_iter
@@ -338,6 +359,15 @@ def test_subminor_loop_bit_exact(sess, orc, w, n_src, threshold_frac, mgain, max
     n_it = out.iteration
     assert n_it == r.iteration_number
     assert np.array_equal(trace[:n_it], trace_o[:n_it, :2])
+    if n_ch > 1:
+        dmod = sess.array(shape=(h, w))
+        for k in range(n_ch):
+            sess.rdl.rdl_subminor_model(sm, k, dmod.vp, w, h, 0, 0, 0)
+            assert np.array_equal(bits(dmod.get()), bits(mod_o[k]))
+        sess.rdl.rdl_subminor_destroy(sm)
+        for a in (dres, dpsf, dmod):
+            a.free()
+        return
     # model via the scatter path; CorrectResidualDirty on the padded grid
     dmod = sess.array(shape=(h, w))
     sess.rdl.rdl_subminor_model(sm, 0, dmod.vp, w, h, 0, 0, 1)
