@@ -90,13 +90,13 @@ class Timing:
         return out
 
 
-def cpu_baseline(size, n_points, n_blobs, max_scales, threshold, sample_components, threads):
+def cpu_baseline(psf, dirty, max_scales, threshold, sample_components, threads):
     """The oracle (tests/oracle_lib -> oracle/build/liboracle.so) on the first
-    `sample_components` components of the same workload."""
+    `sample_components` components of the same workload (same inputs)."""
     from oracle_lib import OracleAlgorithm, get_oracle
     orc = get_oracle()
     orc.set_threads(threads)
-    psf, dirty = make_problem(size, SEED, n_points, n_blobs)
+    size = dirty.shape[0]
     res, mod = dirty[None].copy(), np.zeros_like(dirty)[None]
     alg = OracleAlgorithm(orc, 1, threshold=threshold, max_iterations=sample_components,
                           border_ratio=0.0, max_scales=max_scales, beam_size_in_pixels=BEAM_PX,
@@ -122,7 +122,7 @@ def main():
     ap.add_argument("--blobs", type=int, default=200)
     ap.add_argument("--max-iter", type=int, default=1000000)
     ap.add_argument("--sigma", type=float, default=5.0)
-    ap.add_argument("--cpu-sample", type=int, default=200,
+    ap.add_argument("--cpu-sample", type=int, default=2000,
                     help="components in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--breakdown", action="store_true", help="per-kernel times to stderr")
@@ -186,6 +186,7 @@ def main():
         max_elapsed, total_comps = float(t.item()), int(c.item())
 
     if rank != 0:
+        del run, timing
         if dist is not None:
             dist.destroy_process_group()
         return
@@ -215,8 +216,8 @@ def main():
 
     cpu = None
     if args.cpu_sample > 0 and world == 1:
-        cpu = cpu_baseline(args.size, args.points, args.blobs, args.scales, threshold,
-                           args.cpu_sample, args.cpu_threads)
+        cpu = cpu_baseline(psf, dirty, args.scales, threshold, args.cpu_sample,
+                           args.cpu_threads)
 
     line = {
         "metric": "CLEAN components/sec (multiscale, to 5-sigma threshold)",
@@ -241,7 +242,10 @@ def main():
         "roofline": roofline,
         "cpu_baseline": cpu,
     }
-    print(json.dumps(line))
+    print(json.dumps(line), flush=True)
+    del run, timing
+    import gc
+    gc.collect()  # release device buffers while the runtime is fully alive
     if dist is not None:
         dist.destroy_process_group()
 
