@@ -63,7 +63,7 @@ def settings_for(rd, size, max_iter, max_scales, threshold):
 
 
 # algorithmic bytes per launch are accumulated by the C-ABI per family
-FAMILIES = ["fft", "fft64", "spectrum_multiply", "spectrum_multiply64", "find_peak", "subminor_loop", "subminor_select",
+FAMILIES = ["conv_rows", "conv_cols", "conv64_rows", "conv64_cols", "fft", "fft64", "spectrum_multiply", "spectrum_multiply64", "find_peak", "subminor_loop", "subminor_select",
             "trim_subtract", "add", "integrate", "rms", "axpy", "radix_select"]
 
 

@@ -261,6 +261,37 @@ int rdl_fft64_inverse(rdl_fft* f, void* d_spectrum, double* d_out);
 /* In-place circular convolution in double precision (see rdl_fft_convolve). */
 int rdl_fft64_convolve(rdl_fft* f, double* d_image, const void* d_kernel_spectrum,
                        void* d_work);
+/* ---------------------------------------- LDS-resident FFT convolution */
+/* A width x height real 2-D transform pair built from three HBM passes
+ * (rows / columns / rows, each transform held in LDS), replacing rocFFT for
+ * the convolutions of multiscale_transforms.cc:9-21 and
+ * subminor_loop.cc:195-218. Lengths must be 2^a 3^b 5^c 7^d and fit in LDS
+ * (<= 20480 float, <= 10240 double); otherwise RDL_ERR_UNSUPPORTED.
+ * Spectra are (width/2+1) x height complex (float or double) in natural
+ * row-major order, like rocFFT's. Inputs and outputs are float images. */
+typedef struct rdl_conv rdl_conv;
+int rdl_conv_create(rdl_session* s, uint32_t width, uint32_t height, int f64,
+                    rdl_conv** out);
+int rdl_conv_destroy(rdl_conv* c);
+size_t rdl_conv_spectrum_bytes(const rdl_conv* c);
+/* Row transforms of the plane holding the in_w x in_h image d_in at offset
+ * (ox, oy) and zeros elsewhere (Image::Untrim fused). */
+int rdl_conv_rows_forward(rdl_conv* c, const float* d_in, uint32_t in_w,
+                          uint32_t in_h, uint32_t ox, uint32_t oy, void* d_spec);
+/* Column transforms, in or out of place. mode 0: forward; mode 1: forward,
+ * x kernel spectrum x scale, inverse; mode 2: input already column-
+ * transformed: x kernel spectrum x scale, inverse. */
+int rdl_conv_columns(rdl_conv* c, const void* d_in, void* d_out,
+                     const void* d_kernel, int mode, double scale);
+/* Inverse row transforms; the window (ox, oy, out_w, out_h) of the real plane
+ * is written to d_out (out_w wide) or, with subtract != 0, subtracted from
+ * it after rounding to float (Image::Trim + residual -= fused). */
+int rdl_conv_rows_inverse(rdl_conv* c, const void* d_spec, float* d_out,
+                          uint32_t out_w, uint32_t out_h, uint32_t ox,
+                          uint32_t oy, int subtract);
+/* Full 2-D forward transform of a width x height float image. */
+int rdl_conv_forward(rdl_conv* c, const float* d_in, void* d_spec);
+
 /* dst = a * b * scale, complex, n_complex elements. */
 int rdl_spectrum_multiply(rdl_session* s, void* d_dst, const void* d_a,
                           const void* d_b, size_t n_complex, float scale);

@@ -1,0 +1,671 @@
+// LDS-resident FFT convolution engine: the multiscale scale convolutions and
+// SubMinorLoop::CorrectResidualDirty (cpp/algorithms/multiscale/
+// multiscale_transforms.cc:9-21, cpp/algorithms/subminor_loop.cc:195-218;
+// schaapcommon::math::Convolve contract restated in oracle/oracle.cc) as
+// three HBM passes instead of rocFFT's transpose-heavy plans:
+//
+//   rows forward   : two real rows per transform packed as z = a + i b, one
+//                    complex Stockham FFT of the row length in LDS, split into
+//                    the two half spectra (W/2+1 bins) -> row-major spectrum.
+//                    The input is read from a w x h float image placed at an
+//                    offset inside the (possibly padded) plane (Image::Untrim
+//                    fused; rows outside it are zero and never loaded).
+//   columns        : `count` spectrum columns per workgroup, complex FFT of the
+//                    column length in LDS; optionally x kernel spectrum x 1/N
+//                    and the inverse column FFT in the same pass.
+//   rows inverse   : Hermitian half rows -> packed complex row -> inverse FFT
+//                    in LDS -> two real rows, written (Image::Trim fused) or
+//                    subtracted from the residual.
+//
+// Lengths must be 2^a 3^b 5^c 7^d (every CalculateGoodFFTSize output is) and
+// fit in LDS (160 KiB: 20480 float / 10240 double complex); otherwise
+// rdl_conv_create returns RDL_ERR_UNSUPPORTED and callers use rocFFT.
+// Twiddles come from a float64 table (rounded to T for float plans).
+#include <cmath>
+#include <cstring>
+
+#include "rdl_internal.h"
+
+namespace rdl {
+
+template <typename T>
+struct Cx {
+  T x, y;
+};
+
+template <typename T>
+__device__ __forceinline__ Cx<T> Add(Cx<T> a, Cx<T> b) {
+  return {a.x + b.x, a.y + b.y};
+}
+template <typename T>
+__device__ __forceinline__ Cx<T> Sub(Cx<T> a, Cx<T> b) {
+  return {a.x - b.x, a.y - b.y};
+}
+template <typename T>
+__device__ __forceinline__ Cx<T> Mul(Cx<T> a, Cx<T> b) {
+  return {a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x};
+}
+template <typename T>
+__device__ __forceinline__ Cx<T> MulMinusI(Cx<T> a) {  // a * (-i)
+  return {a.y, -a.x};
+}
+template <typename T>
+__device__ __forceinline__ Cx<T> Conj(Cx<T> a) {
+  return {a.x, -a.y};
+}
+template <typename T>
+__device__ __forceinline__ Cx<T> Scale(Cx<T> a, T s) {
+  return {a.x * s, a.y * s};
+}
+
+constexpr uint32_t kFftThreads = 1024;
+constexpr uint32_t kFftMaxPasses = 24;
+constexpr size_t kFftLdsBytes = 160 * 1024;
+
+// Complex elements one workgroup transforms at a time (count x length):
+// bounds the butterflies per thread, hence registers (no spills at 512 threads).
+constexpr uint32_t kMaxWgElems = 10240;
+template <typename T>
+constexpr uint32_t MaxElems() {
+  return kMaxWgElems;
+}
+
+struct LdsPlan {
+  uint32_t n;       // transform length
+  uint32_t n_pass;
+  uint8_t radix[kFftMaxPasses];
+  const void* tw;   // n twiddles exp(-2 pi i k / n), Cx<T>
+};
+
+// ---- radix-R DFT (forward, e^{-2 pi i jk/R}) on registers
+template <typename T, int R>
+struct Dft;
+
+template <typename T>
+struct Dft<T, 2> {
+  __device__ __forceinline__ static void Run(Cx<T>* a) {
+    const Cx<T> t = a[1];
+    a[1] = Sub(a[0], t);
+    a[0] = Add(a[0], t);
+  }
+};
+
+template <typename T>
+struct Dft<T, 4> {
+  __device__ __forceinline__ static void Run(Cx<T>* a) {
+    const Cx<T> t0 = Add(a[0], a[2]), t1 = Sub(a[0], a[2]);
+    const Cx<T> t2 = Add(a[1], a[3]), t3 = MulMinusI(Sub(a[1], a[3]));
+    a[0] = Add(t0, t2);
+    a[2] = Sub(t0, t2);
+    a[1] = Add(t1, t3);
+    a[3] = Sub(t1, t3);
+  }
+};
+
+template <typename T>
+struct Dft<T, 8> {
+  __device__ __forceinline__ static void Run(Cx<T>* a) {
+    Cx<T> e[4] = {a[0], a[2], a[4], a[6]};
+    Cx<T> o[4] = {a[1], a[3], a[5], a[7]};
+    Dft<T, 4>::Run(e);
+    Dft<T, 4>::Run(o);
+    const T c = T(0.70710678118654752440084436210485);
+    // o[k] *= W8^k, W8 = (c, -c)
+    o[1] = {c * (o[1].x + o[1].y), c * (o[1].y - o[1].x)};
+    o[2] = MulMinusI(o[2]);
+    o[3] = {c * (o[3].y - o[3].x), -c * (o[3].x + o[3].y)};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      a[k] = Add(e[k], o[k]);
+      a[k + 4] = Sub(e[k], o[k]);
+    }
+  }
+};
+
+// odd radix: pairs (a_j, a_{R-j})
+template <int R>
+struct OddTables;
+template <>
+struct OddTables<3> {
+  static constexpr double c[3] = {1.0, -0.5, -0.5};
+  static constexpr double s[3] = {0.0, 0.86602540378443864676372317075294,
+                                  -0.86602540378443864676372317075294};
+};
+template <>
+struct OddTables<5> {
+  static constexpr double c[5] = {1.0, 0.30901699437494742410229341718282,
+                                  -0.80901699437494742410229341718282,
+                                  -0.80901699437494742410229341718282,
+                                  0.30901699437494742410229341718282};
+  static constexpr double s[5] = {0.0, 0.95105651629515357211643933337938,
+                                  0.58778525229247312916870595463907,
+                                  -0.58778525229247312916870595463907,
+                                  -0.95105651629515357211643933337938};
+};
+template <>
+struct OddTables<7> {
+  static constexpr double c[7] = {1.0,
+                                  0.62348980185873353052500488400424,
+                                  -0.22252093395631440428890256449679,
+                                  -0.90096886790241912623610231950745,
+                                  -0.90096886790241912623610231950745,
+                                  -0.22252093395631440428890256449679,
+                                  0.62348980185873353052500488400424};
+  static constexpr double s[7] = {0.0,
+                                  0.78183148246802980870844452667406,
+                                  0.97492791218182360701813168299393,
+                                  0.43388373911755812047576833284836,
+                                  -0.43388373911755812047576833284836,
+                                  -0.97492791218182360701813168299393,
+                                  -0.78183148246802980870844452667406};
+};
+
+template <typename T, int R>
+struct DftOdd {
+  __device__ __forceinline__ static void Run(Cx<T>* a) {
+    constexpr int H = (R - 1) / 2;
+    Cx<T> sp[H], sm[H];
+#pragma unroll
+    for (int j = 1; j <= H; ++j) {
+      sp[j - 1] = Add(a[j], a[R - j]);
+      sm[j - 1] = Sub(a[j], a[R - j]);
+    }
+    const Cx<T> a0 = a[0];
+    Cx<T> y0 = a0;
+#pragma unroll
+    for (int j = 0; j < H; ++j) y0 = Add(y0, sp[j]);
+#pragma unroll
+    for (int k = 1; k <= H; ++k) {
+      Cx<T> re = a0, im = {T(0), T(0)};
+#pragma unroll
+      for (int j = 1; j <= H; ++j) {
+        const T cj = T(OddTables<R>::c[(j * k) % R]);
+        const T sj = T(OddTables<R>::s[(j * k) % R]);
+        re = {re.x + cj * sp[j - 1].x, re.y + cj * sp[j - 1].y};
+        im = {im.x + sj * sm[j - 1].x, im.y + sj * sm[j - 1].y};
+      }
+      // y_k = re - i im, y_{R-k} = re + i im
+      a[k] = {re.x + im.y, re.y - im.x};
+      a[R - k] = {re.x - im.y, re.y + im.x};
+    }
+    a[0] = y0;
+  }
+};
+template <typename T>
+struct Dft<T, 3> : DftOdd<T, 3> {};
+template <typename T>
+struct Dft<T, 5> : DftOdd<T, 5> {};
+template <typename T>
+struct Dft<T, 7> : DftOdd<T, 7> {};
+
+// ---- one Stockham pass over `count` transforms of length n held in LDS
+// (in place: all butterfly inputs are read to registers before the barrier)
+template <typename T, int R>
+__device__ __forceinline__ void StockhamPass(Cx<T>* buf, uint32_t n,
+                                             uint32_t count, uint32_t ns,
+                                             const Cx<T>* __restrict__ tw,
+                                             uint32_t tid) {
+  constexpr uint32_t BPT = (MaxElems<T>() / R + kFftThreads - 1) / kFftThreads;
+  const uint32_t nb = n / R;
+  const uint32_t total = nb * count;
+  const uint32_t m = n / (ns * R);
+  Cx<T> v[BPT][R];
+#pragma unroll
+  for (uint32_t i = 0; i < BPT; ++i) {
+    const uint32_t b = tid + i * kFftThreads;
+    if (b < total) {
+      const uint32_t t = b / nb, j = b - t * nb;
+      const Cx<T>* base = buf + size_t(t) * n;
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[i][r] = base[j + r * nb];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t i = 0; i < BPT; ++i) {
+    const uint32_t b = tid + i * kFftThreads;
+    if (b < total) {
+      const uint32_t t = b / nb, j = b - t * nb;
+      const uint32_t k = j % ns;
+      if (ns > 1) {
+#pragma unroll
+        for (int r = 1; r < R; ++r) v[i][r] = Mul(v[i][r], tw[k * r * m]);
+      }
+      Dft<T, R>::Run(v[i]);
+      Cx<T>* base = buf + size_t(t) * n;
+      const uint32_t d = (j / ns) * ns * R + k;
+#pragma unroll
+      for (int r = 0; r < R; ++r) base[d + r * ns] = v[i][r];
+    }
+  }
+  __syncthreads();
+}
+
+// Forward complex FFT (natural order in and out) of `count` transforms.
+template <typename T>
+__device__ void LdsFftForward(Cx<T>* buf, const LdsPlan& p, uint32_t count,
+                              uint32_t tid) {
+  const Cx<T>* tw = static_cast<const Cx<T>*>(p.tw);
+  uint32_t ns = 1;
+  for (uint32_t q = 0; q < p.n_pass; ++q) {
+    const uint32_t r = p.radix[q];
+    switch (r) {
+      case 8: StockhamPass<T, 8>(buf, p.n, count, ns, tw, tid); break;
+      case 4: StockhamPass<T, 4>(buf, p.n, count, ns, tw, tid); break;
+      case 2: StockhamPass<T, 2>(buf, p.n, count, ns, tw, tid); break;
+      case 3: StockhamPass<T, 3>(buf, p.n, count, ns, tw, tid); break;
+      case 5: StockhamPass<T, 5>(buf, p.n, count, ns, tw, tid); break;
+      default: StockhamPass<T, 7>(buf, p.n, count, ns, tw, tid); break;
+    }
+    ns *= r;
+  }
+}
+
+// ---------------------------------------------------------------- kernels
+struct RowArgs {
+  LdsPlan plan;        // row length n = plane width
+  uint32_t height;     // plane rows
+  uint32_t count;      // row pairs per workgroup
+  uint32_t ld;         // spectrum row stride (complex) = n/2+1
+  // forward input / inverse output window inside the plane
+  uint32_t img_w, img_h, ox, oy;
+};
+
+// rows forward: float image window -> half spectra (T)
+template <typename T>
+__global__ __launch_bounds__(kFftThreads) void RowsForward(RowArgs a,
+                                                           const float* __restrict__ in,
+                                                           Cx<T>* __restrict__ spec) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  Cx<T>* buf = reinterpret_cast<Cx<T>*>(lds_raw);
+  const uint32_t tid = threadIdx.x;
+  const uint32_t n = a.plan.n;
+  const uint32_t pair0 = blockIdx.x * a.count;
+  const uint32_t n_pairs = (a.height + 1) / 2;
+  const uint32_t count = min(a.count, n_pairs - pair0);
+  for (uint32_t idx = tid; idx < count * n; idx += kFftThreads) {
+    const uint32_t t = idx / n, x = idx - t * n;
+    const uint32_t y0 = 2 * (pair0 + t), y1 = y0 + 1;
+    T va = T(0), vb = T(0);
+    const int64_t ix = int64_t(x) - a.ox;
+    if (ix >= 0 && ix < a.img_w) {
+      const int64_t iy0 = int64_t(y0) - a.oy, iy1 = int64_t(y1) - a.oy;
+      if (iy0 >= 0 && iy0 < a.img_h) va = T(in[size_t(iy0) * a.img_w + ix]);
+      if (y1 < a.height && iy1 >= 0 && iy1 < a.img_h)
+        vb = T(in[size_t(iy1) * a.img_w + ix]);
+    }
+    buf[idx] = {va, vb};
+  }
+  __syncthreads();
+  LdsFftForward<T>(buf, a.plan, count, tid);
+  const uint32_t nh = n / 2 + 1;
+  for (uint32_t idx = tid; idx < count * nh; idx += kFftThreads) {
+    const uint32_t t = idx / nh, k = idx - t * nh;
+    const Cx<T> zk = buf[size_t(t) * n + k];
+    const Cx<T> zc = Conj(buf[size_t(t) * n + (k == 0 ? 0 : n - k)]);
+    const T h = T(0.5);
+    const Cx<T> A = {h * (zk.x + zc.x), h * (zk.y + zc.y)};
+    const Cx<T> B = {h * (zk.y - zc.y), -h * (zk.x - zc.x)};
+    const uint32_t y0 = 2 * (pair0 + t), y1 = y0 + 1;
+    spec[size_t(y0) * a.ld + k] = A;
+    if (y1 < a.height) spec[size_t(y1) * a.ld + k] = B;
+  }
+}
+
+// rows inverse: half spectra -> real rows; write (mode 0) or subtract
+// (mode 1) the window [ox, ox+img_w) x [oy, oy+img_h) into out (img_w wide)
+template <typename T>
+__global__ __launch_bounds__(kFftThreads) void RowsInverse(RowArgs a,
+                                                           const Cx<T>* __restrict__ spec,
+                                                           float* __restrict__ out,
+                                                           int subtract) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  Cx<T>* buf = reinterpret_cast<Cx<T>*>(lds_raw);
+  const uint32_t tid = threadIdx.x;
+  const uint32_t n = a.plan.n;
+  const uint32_t pair0 = blockIdx.x * a.count;
+  const uint32_t n_pairs = (a.height + 1) / 2;
+  const uint32_t count = min(a.count, n_pairs - pair0);
+  const uint32_t nh = n / 2 + 1;
+  const bool even = (n & 1u) == 0;
+  for (uint32_t idx = tid; idx < count * nh; idx += kFftThreads) {
+    const uint32_t t = idx / nh, k = idx - t * nh;
+    const uint32_t y0 = 2 * (pair0 + t), y1 = y0 + 1;
+    Cx<T> A = spec[size_t(y0) * a.ld + k];
+    Cx<T> B = y1 < a.height ? spec[size_t(y1) * a.ld + k] : Cx<T>{T(0), T(0)};
+    if (k == 0 || (even && k == n / 2)) {  // C2R ignores these imaginary parts
+      A.y = T(0);
+      B.y = T(0);
+    }
+    // Z[k] = A + iB ; Z[n-k] = conj(A) + i conj(B). Stored conjugated (inverse
+    // FFT = conj(FFT(conj)))
+    Cx<T>* row = buf + size_t(t) * n;
+    row[k] = {A.x - B.y, -(A.y + B.x)};
+    if (k != 0 && !(even && k == n / 2)) row[n - k] = {A.x + B.y, -(B.x - A.y)};
+  }
+  __syncthreads();
+  LdsFftForward<T>(buf, a.plan, count, tid);
+  for (uint32_t idx = tid; idx < count * n; idx += kFftThreads) {
+    const uint32_t t = idx / n, x = idx - t * n;
+    const int64_t ix = int64_t(x) - a.ox;
+    if (ix < 0 || ix >= a.img_w) continue;
+    const Cx<T> z = buf[idx];  // conj(result): a = z.x, b = -z.y
+    const uint32_t y0 = 2 * (pair0 + t), y1 = y0 + 1;
+    const int64_t iy0 = int64_t(y0) - a.oy, iy1 = int64_t(y1) - a.oy;
+    if (iy0 >= 0 && iy0 < a.img_h) {
+      float* o = out + size_t(iy0) * a.img_w + ix;
+      if (subtract)
+        *o -= float(z.x);
+      else
+        *o = float(z.x);
+    }
+    if (y1 < a.height && iy1 >= 0 && iy1 < a.img_h) {
+      float* o = out + size_t(iy1) * a.img_w + ix;
+      if (subtract)
+        *o -= float(-z.y);
+      else
+        *o = float(-z.y);
+    }
+  }
+}
+
+struct ColArgs {
+  LdsPlan plan;      // column length n = plane height
+  uint32_t n_cols;   // spectrum columns = width/2+1
+  uint32_t count;    // columns per workgroup
+  uint32_t ld;       // spectrum row stride
+  uint32_t tiles_per_xcd;
+  int mode;          // 0 fwd, 1 fwd*K*s+inv, 2 (already fwd) *K*s+inv
+  double scale;
+};
+
+template <typename T>
+__global__ __launch_bounds__(kFftThreads) void Columns(ColArgs a,
+                                                       const Cx<T>* __restrict__ in,
+                                                       Cx<T>* __restrict__ out,
+                                                       const Cx<T>* __restrict__ kern) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  Cx<T>* buf = reinterpret_cast<Cx<T>*>(lds_raw);
+  // XCD-aware tiles: consecutive column tiles run on the same XCD so the
+  // 128-byte lines they share are fetched into one L2
+  const uint32_t xcd = blockIdx.x & 7u, slot = blockIdx.x >> 3;
+  const uint32_t tile = xcd * a.tiles_per_xcd + slot;
+  const uint32_t k0 = tile * a.count;
+  if (k0 >= a.n_cols) return;
+  const uint32_t count = min(a.count, a.n_cols - k0);
+  const uint32_t tid = threadIdx.x;
+  const uint32_t n = a.plan.n;
+  const T s = T(a.scale);
+  for (uint32_t idx = tid; idx < count * n; idx += kFftThreads) {
+    const uint32_t y = idx / count, j = idx - y * count;
+    Cx<T> v = in[size_t(y) * a.ld + k0 + j];
+    if (a.mode == 2) v = Conj(Scale(Mul(v, kern[size_t(y) * a.ld + k0 + j]), s));
+    buf[size_t(j) * n + y] = v;
+  }
+  __syncthreads();
+  if (a.mode != 2) LdsFftForward<T>(buf, a.plan, count, tid);
+  if (a.mode == 1) {
+    for (uint32_t idx = tid; idx < count * n; idx += kFftThreads) {
+      const uint32_t y = idx / count, j = idx - y * count;
+      Cx<T>& v = buf[size_t(j) * n + y];
+      v = Conj(Scale(Mul(v, kern[size_t(y) * a.ld + k0 + j]), s));
+    }
+    __syncthreads();
+  }
+  if (a.mode != 0) LdsFftForward<T>(buf, a.plan, count, tid);
+  for (uint32_t idx = tid; idx < count * n; idx += kFftThreads) {
+    const uint32_t y = idx / count, j = idx - y * count;
+    const Cx<T> v = buf[size_t(j) * n + y];
+    out[size_t(y) * a.ld + k0 + j] = a.mode == 0 ? v : Conj(v);
+  }
+}
+
+// ---------------------------------------------------------------- planning
+bool Factorize(uint32_t n, std::vector<uint8_t>& radix) {
+  radix.clear();
+  uint32_t m = n;
+  uint32_t twos = 0;
+  while (m % 2 == 0) {
+    m /= 2;
+    ++twos;
+  }
+  while (twos >= 3) {
+    radix.push_back(8);
+    twos -= 3;
+  }
+  if (twos == 2) radix.push_back(4);
+  if (twos == 1) radix.push_back(2);
+  for (uint32_t r : {7u, 5u, 3u})
+    while (m % r == 0) {
+      m /= r;
+      radix.push_back(uint8_t(r));
+    }
+  return m == 1 && radix.size() <= kFftMaxPasses;
+}
+
+}  // namespace rdl
+
+struct rdl_conv {
+  rdl_session* s = nullptr;
+  uint32_t width = 0, height = 0;
+  bool f64 = false;
+  void* tw_row = nullptr;
+  void* tw_col = nullptr;
+  rdl::LdsPlan row_plan{}, col_plan{};
+  uint32_t row_count = 1, col_count = 1;
+};
+
+namespace {
+
+int MakePlan(rdl_conv* c, uint32_t n, bool f64, rdl::LdsPlan* plan, void** tw) {
+  std::vector<uint8_t> radix;
+  if (!rdl::Factorize(n, radix)) {
+    rdl::SetError("LDS FFT: length " + std::to_string(n) + " is not 2/3/5/7-smooth");
+    return RDL_ERR_UNSUPPORTED;
+  }
+  plan->n = n;
+  plan->n_pass = uint32_t(radix.size());
+  std::memset(plan->radix, 0, sizeof(plan->radix));
+  for (size_t i = 0; i < radix.size(); ++i) plan->radix[i] = radix[i];
+  const size_t esz = f64 ? 16 : 8;
+  std::vector<unsigned char> host(size_t(n) * esz);
+  for (uint32_t k = 0; k < n; ++k) {
+    // exp(-2 pi i k/n) with the angle reduced to the first octant in double
+    const long double ang = -2.0L * 3.14159265358979323846264338327950288L * k / n;
+    const double cr = double(std::cos(ang)), ci = double(std::sin(ang));
+    if (f64) {
+      double v[2] = {cr, ci};
+      std::memcpy(&host[k * esz], v, 16);
+    } else {
+      float v[2] = {float(cr), float(ci)};
+      std::memcpy(&host[k * esz], v, 8);
+    }
+  }
+  RDL_HIP_CHECK(hipMalloc(tw, host.size()));
+  RDL_HIP_CHECK(hipMemcpy(*tw, host.data(), host.size(), hipMemcpyHostToDevice));
+  plan->tw = *tw;
+  (void)c;
+  return RDL_OK;
+}
+
+template <typename T>
+int LaunchRowsForward(rdl_conv* c, const float* in, uint32_t in_w, uint32_t in_h,
+                      uint32_t ox, uint32_t oy, void* spec) {
+  rdl::RowArgs a{};
+  a.plan = c->row_plan;
+  a.height = c->height;
+  a.count = c->row_count;
+  a.ld = c->width / 2 + 1;
+  a.img_w = in_w;
+  a.img_h = in_h;
+  a.ox = ox;
+  a.oy = oy;
+  const uint32_t n_pairs = (c->height + 1) / 2;
+  const uint32_t grid = (n_pairs + a.count - 1) / a.count;
+  const size_t lds = size_t(a.count) * c->width * sizeof(rdl::Cx<T>);
+  auto k = rdl::RowsForward<T>;
+  static bool attr_set = false;  // once per instantiation (the call can stall)
+  if (!attr_set) {
+    RDL_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      int(rdl::kFftLdsBytes)));
+    attr_set = true;
+  }
+  k<<<grid, rdl::kFftThreads, lds, c->s->stream>>>(a, in,
+                                                   static_cast<rdl::Cx<T>*>(spec));
+  RDL_HIP_CHECK(hipGetLastError());
+  return RDL_OK;
+}
+
+template <typename T>
+int LaunchRowsInverse(rdl_conv* c, const void* spec, float* out, uint32_t out_w,
+                      uint32_t out_h, uint32_t ox, uint32_t oy, int subtract) {
+  rdl::RowArgs a{};
+  a.plan = c->row_plan;
+  a.height = c->height;
+  a.count = c->row_count;
+  a.ld = c->width / 2 + 1;
+  a.img_w = out_w;
+  a.img_h = out_h;
+  a.ox = ox;
+  a.oy = oy;
+  const uint32_t n_pairs = (c->height + 1) / 2;
+  const uint32_t grid = (n_pairs + a.count - 1) / a.count;
+  const size_t lds = size_t(a.count) * c->width * sizeof(rdl::Cx<T>);
+  auto k = rdl::RowsInverse<T>;
+  static bool attr_set = false;  // once per instantiation (the call can stall)
+  if (!attr_set) {
+    RDL_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      int(rdl::kFftLdsBytes)));
+    attr_set = true;
+  }
+  k<<<grid, rdl::kFftThreads, lds, c->s->stream>>>(
+      a, static_cast<const rdl::Cx<T>*>(spec), out, subtract);
+  RDL_HIP_CHECK(hipGetLastError());
+  return RDL_OK;
+}
+
+template <typename T>
+int LaunchColumns(rdl_conv* c, const void* in, void* out, const void* kern,
+                  int mode, double scale) {
+  rdl::ColArgs a{};
+  a.plan = c->col_plan;
+  a.n_cols = c->width / 2 + 1;
+  a.count = c->col_count;
+  a.ld = a.n_cols;
+  a.mode = mode;
+  a.scale = scale;
+  const uint32_t n_tiles = (a.n_cols + a.count - 1) / a.count;
+  a.tiles_per_xcd = (n_tiles + 7) / 8;
+  const uint32_t grid = 8 * a.tiles_per_xcd;
+  const size_t lds = size_t(a.count) * c->height * sizeof(rdl::Cx<T>);
+  auto k = rdl::Columns<T>;
+  static bool attr_set = false;  // once per instantiation (the call can stall)
+  if (!attr_set) {
+    RDL_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      int(rdl::kFftLdsBytes)));
+    attr_set = true;
+  }
+  k<<<grid, rdl::kFftThreads, lds, c->s->stream>>>(
+      a, static_cast<const rdl::Cx<T>*>(in), static_cast<rdl::Cx<T>*>(out),
+      static_cast<const rdl::Cx<T>*>(kern));
+  RDL_HIP_CHECK(hipGetLastError());
+  return RDL_OK;
+}
+
+double SpectrumBytes(const rdl_conv* c) {
+  return double(c->width / 2 + 1) * c->height * (c->f64 ? 16.0 : 8.0);
+}
+
+}  // namespace
+
+extern "C" {
+
+int rdl_conv_create(rdl_session* s, uint32_t width, uint32_t height, int f64,
+                    rdl_conv** out) {
+  RDL_ARG_CHECK(s && out, "NULL argument");
+  RDL_ARG_CHECK(width >= 2 && height >= 2, "bad size");
+  *out = nullptr;
+  const size_t esz = f64 ? 16 : 8;
+  const size_t max_elems = std::min<size_t>(rdl::kFftLdsBytes / esz, rdl::kMaxWgElems);
+  if (width > max_elems || height > max_elems) {
+    rdl::SetError("LDS FFT: size exceeds LDS capacity");
+    return RDL_ERR_UNSUPPORTED;
+  }
+  auto c = std::make_unique<rdl_conv>();
+  c->s = s;
+  c->width = width;
+  c->height = height;
+  c->f64 = f64 != 0;
+  RDL_HIP_CHECK(hipSetDevice(s->device));
+  RDL_TRY(MakePlan(c.get(), width, c->f64, &c->row_plan, &c->tw_row));
+  RDL_TRY(MakePlan(c.get(), height, c->f64, &c->col_plan, &c->tw_col));
+  // transforms per workgroup: fill ~64 KiB (float) / the LDS (double) so small
+  // planes still give each workgroup enough work; never more than LDS holds
+  const size_t budget = c->f64 ? rdl::kFftLdsBytes : 64 * 1024;
+  c->row_count = uint32_t(std::max<size_t>(1, std::min<size_t>(budget / (width * esz), 64)));
+  c->col_count = uint32_t(std::max<size_t>(1, std::min<size_t>(budget / (height * esz), 64)));
+  c->row_count = std::min<uint32_t>(c->row_count, uint32_t(max_elems / width));
+  c->col_count = std::min<uint32_t>(c->col_count, uint32_t(max_elems / height));
+  *out = c.release();
+  return RDL_OK;
+}
+
+int rdl_conv_destroy(rdl_conv* c) {
+  if (!c) return RDL_OK;
+  (void)hipStreamSynchronize(c->s->stream);
+  if (c->tw_row) (void)hipFree(c->tw_row);
+  if (c->tw_col) (void)hipFree(c->tw_col);
+  delete c;
+  return RDL_OK;
+}
+
+size_t rdl_conv_spectrum_bytes(const rdl_conv* c) {
+  return c ? size_t(SpectrumBytes(c)) : 0;
+}
+
+int rdl_conv_rows_forward(rdl_conv* c, const float* d_in, uint32_t in_w,
+                          uint32_t in_h, uint32_t ox, uint32_t oy, void* d_spec) {
+  RDL_ARG_CHECK(c && d_in && d_spec, "NULL argument");
+  RDL_ARG_CHECK(uint64_t(ox) + in_w <= c->width && uint64_t(oy) + in_h <= c->height,
+                "input window outside the plane");
+  rdl::ScopedTiming t(c->s, c->f64 ? "conv64_rows" : "conv_rows",
+                      double(in_w) * in_h * 4.0 + SpectrumBytes(c));
+  return c->f64 ? LaunchRowsForward<double>(c, d_in, in_w, in_h, ox, oy, d_spec)
+                : LaunchRowsForward<float>(c, d_in, in_w, in_h, ox, oy, d_spec);
+}
+
+int rdl_conv_columns(rdl_conv* c, const void* d_in, void* d_out,
+                     const void* d_kernel, int mode, double scale) {
+  RDL_ARG_CHECK(c && d_in && d_out, "NULL argument");
+  RDL_ARG_CHECK(mode >= 0 && mode <= 2, "mode must be 0, 1 or 2");
+  RDL_ARG_CHECK(mode == 0 || d_kernel, "kernel spectrum required");
+  const double sb = SpectrumBytes(c);
+  rdl::ScopedTiming t(c->s, c->f64 ? "conv64_cols" : "conv_cols",
+                      mode == 0 ? 2.0 * sb : 3.0 * sb);
+  return c->f64 ? LaunchColumns<double>(c, d_in, d_out, d_kernel, mode, scale)
+                : LaunchColumns<float>(c, d_in, d_out, d_kernel, mode, scale);
+}
+
+int rdl_conv_rows_inverse(rdl_conv* c, const void* d_spec, float* d_out,
+                          uint32_t out_w, uint32_t out_h, uint32_t ox, uint32_t oy,
+                          int subtract) {
+  RDL_ARG_CHECK(c && d_spec && d_out, "NULL argument");
+  RDL_ARG_CHECK(uint64_t(ox) + out_w <= c->width && uint64_t(oy) + out_h <= c->height,
+                "output window outside the plane");
+  rdl::ScopedTiming t(c->s, c->f64 ? "conv64_rows" : "conv_rows",
+                      SpectrumBytes(c) + double(out_w) * out_h * (subtract ? 8.0 : 4.0));
+  return c->f64 ? LaunchRowsInverse<double>(c, d_spec, d_out, out_w, out_h, ox, oy,
+                                            subtract)
+                : LaunchRowsInverse<float>(c, d_spec, d_out, out_w, out_h, ox, oy,
+                                           subtract);
+}
+
+int rdl_conv_forward(rdl_conv* c, const float* d_in, void* d_spec) {
+  RDL_TRY(rdl_conv_rows_forward(c, d_in, c->width, c->height, 0, 0, d_spec));
+  return rdl_conv_columns(c, d_spec, d_spec, nullptr, 0, 1.0);
+}
+
+}  // extern "C"

@@ -46,29 +46,99 @@ void Buffer::Zero() {
 
 Fft::Fft(Session& s, size_t width, size_t height, bool f64)
     : s_(s), width_(width), height_(height), f64_(f64) {
-  if (f64)
-    Check(rdl_fft_create_f64(s.Handle(), uint32_t(width), uint32_t(height), &f_),
-          "rdl_fft_create_f64");
-  else
-    Check(rdl_fft_create(s.Handle(), uint32_t(width), uint32_t(height), &f_),
-          "rdl_fft_create");
-  spectrum_bytes_ = rdl_fft_spectrum_bytes(f_);
+  // The LDS engine wins for the float64 padded residual correction (mixed-radix
+  // sizes, where rocFFT needs many transpose passes); rocFFT's single-precision
+  // power-of-two kernels are faster for the scale convolutions
+  // (tools/bench_fft.py). RADLER_FFT=rocfft / lds overrides.
+  const char* force = std::getenv("RADLER_FFT");
+  const std::string mode = force ? force : "";
+  const bool want_lds = mode == "lds" || (mode != "rocfft" && f64);
+  const bool lds_ok = want_lds &&
+                      rdl_conv_create(s.Handle(), uint32_t(width), uint32_t(height),
+                                      f64 ? 1 : 0, &conv_) == RDL_OK;
+  if (lds_ok) {
+    spectrum_bytes_ = rdl_conv_spectrum_bytes(conv_);
+  } else {
+    conv_ = nullptr;
+    if (f64)
+      Check(rdl_fft_create_f64(s.Handle(), uint32_t(width), uint32_t(height), &f_),
+            "rdl_fft_create_f64");
+    else
+      Check(rdl_fft_create(s.Handle(), uint32_t(width), uint32_t(height), &f_),
+            "rdl_fft_create");
+    spectrum_bytes_ = rdl_fft_spectrum_bytes(f_);
+  }
   work_.Resize(s, spectrum_bytes_);
 }
 
-Fft::~Fft() { rdl_fft_destroy(f_); }
+Fft::~Fft() {
+  if (conv_) rdl_conv_destroy(conv_);
+  if (f_) rdl_fft_destroy(f_);
+}
 
 void Fft::Forward(const float* d_in, void* d_spectrum) {
-  Check(rdl_fft_forward(f_, d_in, d_spectrum), "rdl_fft_forward");
+  if (conv_)
+    Check(rdl_conv_forward(conv_, d_in, d_spectrum), "rdl_conv_forward");
+  else
+    Check(rdl_fft_forward(f_, d_in, d_spectrum), "rdl_fft_forward");
 }
 
 void Fft::Inverse(void* d_spectrum, float* d_out) {
+  if (conv_)
+    throw std::logic_error("Fft::Inverse: use ConvolveSpectrum with the LDS engine");
   Check(rdl_fft_inverse(f_, d_spectrum, d_out), "rdl_fft_inverse");
 }
 
 void Fft::Convolve(float* d_image, const void* d_kernel_spectrum) {
-  Check(rdl_fft_convolve(f_, d_image, d_kernel_spectrum, work_.Ptr()),
-        "rdl_fft_convolve");
+  if (conv_) {
+    const double norm = 1.0 / (double(width_) * double(height_));
+    Check(rdl_conv_rows_forward(conv_, d_image, uint32_t(width_), uint32_t(height_),
+                                0, 0, work_.Ptr()),
+          "rdl_conv_rows_forward");
+    Check(rdl_conv_columns(conv_, work_.Ptr(), work_.Ptr(), d_kernel_spectrum, 1,
+                           f64_ ? norm : double(float(norm))),
+          "rdl_conv_columns");
+    Check(rdl_conv_rows_inverse(conv_, work_.Ptr(), d_image, uint32_t(width_),
+                                uint32_t(height_), 0, 0, 0),
+          "rdl_conv_rows_inverse");
+  } else {
+    Check(rdl_fft_convolve(f_, d_image, d_kernel_spectrum, work_.Ptr()),
+          "rdl_fft_convolve");
+  }
+}
+
+void Fft::ConvolveSpectrum(const void* d_spectrum, const void* d_kernel_spectrum,
+                           void* d_work, float* d_out) {
+  const double norm = 1.0 / (double(width_) * double(height_));
+  if (conv_) {
+    Check(rdl_conv_columns(conv_, d_spectrum, d_work, d_kernel_spectrum, 2,
+                           f64_ ? norm : double(float(norm))),
+          "rdl_conv_columns");
+    Check(rdl_conv_rows_inverse(conv_, d_work, d_out, uint32_t(width_),
+                                uint32_t(height_), 0, 0, 0),
+          "rdl_conv_rows_inverse");
+  } else {
+    Check(rdl_spectrum_multiply(s_.Handle(), d_work, d_spectrum, d_kernel_spectrum,
+                                ComplexCount(), float(norm)),
+          "rdl_spectrum_multiply");
+    Check(rdl_fft_inverse(f_, d_work, d_out), "rdl_fft_inverse");
+  }
+}
+
+void Fft::ConvolveSubtract(const float* d_image, size_t img_w, size_t img_h,
+                           size_t ox, size_t oy, const void* d_kernel_spectrum,
+                           void* d_work, float* d_residual) {
+  if (!conv_) throw std::logic_error("Fft::ConvolveSubtract needs the LDS engine");
+  const double norm = 1.0 / (double(width_) * double(height_));
+  Check(rdl_conv_rows_forward(conv_, d_image, uint32_t(img_w), uint32_t(img_h),
+                              uint32_t(ox), uint32_t(oy), d_work),
+        "rdl_conv_rows_forward");
+  Check(rdl_conv_columns(conv_, d_work, d_work, d_kernel_spectrum, 1,
+                         f64_ ? norm : double(float(norm))),
+        "rdl_conv_columns");
+  Check(rdl_conv_rows_inverse(conv_, d_work, d_residual, uint32_t(img_w),
+                              uint32_t(img_h), uint32_t(ox), uint32_t(oy), 1),
+        "rdl_conv_rows_inverse");
 }
 
 void Fft::Forward64(const double* d_in, void* d_spectrum) {
@@ -86,6 +156,8 @@ Session::Session(int device) : device_(device) {
 
 Session::~Session() {
   ffts_.clear();
+  for (Buffer& b : scratch_) b = Buffer();
+  if (subminor_) rdl_subminor_destroy(subminor_);
   rdl_session_destroy(s_);
 }
 
@@ -95,6 +167,16 @@ Fft& Session::GetFft(size_t width, size_t height, bool f64) {
   if (it == ffts_.end())
     it = ffts_.emplace(key, std::make_unique<Fft>(*this, width, height, f64)).first;
   return *it->second;
+}
+
+Buffer& Session::Scratch(ScratchSlot slot, size_t bytes) {
+  scratch_[slot].Resize(*this, bytes);
+  return scratch_[slot];
+}
+
+rdl_subminor* Session::SharedSubminor() {
+  if (!subminor_) Check(rdl_subminor_create(s_, &subminor_), "rdl_subminor_create");
+  return subminor_;
 }
 
 void Session::Sync() { Check(rdl_session_sync(s_), "rdl_session_sync"); }

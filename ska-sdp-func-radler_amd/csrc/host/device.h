@@ -43,7 +43,9 @@ class Buffer {
   size_t bytes_ = 0;
 };
 
-/// Real 2-D FFT pair of one size (rocFFT plans live in the C-ABI object).
+/// Real 2-D FFT pair of one size. Uses the LDS-resident convolution engine
+/// (rdl_conv_*) when the size allows, rocFFT (rdl_fft_*) otherwise; spectra
+/// have the same layout either way (RADLER_FFT=rocfft|lds overrides the choice).
 class Fft {
  public:
   Fft(Session& s, size_t width, size_t height, bool f64 = false);
@@ -59,7 +61,17 @@ class Fft {
   void Inverse(void* d_spectrum, float* d_out);
   /// In-place circular convolution with a cached kernel spectrum.
   void Convolve(float* d_image, const void* d_kernel_spectrum);
-  /// Double-precision plan only.
+  /// out = image whose spectrum is d_spectrum x d_kernel_spectrum / N
+  /// (d_spectrum is preserved; d_work is spectrum-sized scratch).
+  void ConvolveSpectrum(const void* d_spectrum, const void* d_kernel_spectrum,
+                        void* d_work, float* d_out);
+  /// LDS engine only: residual(window) -= Trim(conv(Untrim(image), kernel)),
+  /// the image (img_w x img_h) placed at (ox, oy) in the plane.
+  void ConvolveSubtract(const float* d_image, size_t img_w, size_t img_h,
+                        size_t ox, size_t oy, const void* d_kernel_spectrum,
+                        void* d_work, float* d_residual);
+  bool UsesLds() const { return conv_ != nullptr; }
+  /// Double-precision rocFFT plan only.
   void Forward64(const double* d_in, void* d_spectrum);
   void Convolve64(double* d_image, const void* d_kernel_spectrum);
   rdl_fft* Handle() { return f_; }
@@ -67,6 +79,7 @@ class Fft {
  private:
   Session& s_;
   rdl_fft* f_ = nullptr;
+  rdl_conv* conv_ = nullptr;
   size_t width_, height_, spectrum_bytes_;
   bool f64_;
   Buffer work_;
@@ -89,6 +102,15 @@ class Session {
   void Zero(void* d, size_t bytes);
   float ReadFloat(const float* d);
 
+  /// Grow-only scratch buffers that outlive the algorithm objects (a
+  /// SubMinorLoop is created per outer iteration; allocating its ~1 GB of
+  /// planes each time costs a hipMalloc/hipFree pair and a device sync).
+  enum ScratchSlot { kCorrectionModel = 0, kCorrectionSpectrum, kNumScratch };
+  Buffer& Scratch(ScratchSlot slot, size_t bytes);
+  /// The session's sub-minor loop state (selection, model values), reused by
+  /// consecutive SubMinorLoop objects.
+  rdl_subminor* SharedSubminor();
+
   /// Process-wide session for a device (one per GPU, shared by the Radler
   /// objects of this process).
   static std::shared_ptr<Session> ForDevice(int device);
@@ -99,6 +121,8 @@ class Session {
   rdl_session* s_ = nullptr;
   int device_;
   std::map<std::tuple<size_t, size_t, bool>, std::unique_ptr<Fft>> ffts_;
+  Buffer scratch_[kNumScratch];
+  rdl_subminor* subminor_ = nullptr;
 };
 
 /// A stack of `count` planes of width x height floats, contiguous.

@@ -121,15 +121,11 @@ void MultiScaleAlgorithm::FindActiveScaleConvolvedMaxima(
   if (!need_fft) return;
   gpu::Fft& fft = transforms_->Fft();
   fft.Forward(d_integrated, spectrum_->Ptr());
-  const float norm = 1.0f / float(double(w) * h);
   for (size_t si = 0; si != scale_infos_.size(); ++si) {
     ScaleInfo& e = scale_infos_[si];
     if (!e.is_active || e.scale == 0.0f) continue;
-    gpu::Check(rdl_spectrum_multiply(s, spectrum_work_->Ptr(), spectrum_->Ptr(),
-                                     transforms_->KernelSpectrum(e.scale),
-                                     fft.ComplexCount(), norm),
-               "rdl_spectrum_multiply");
-    fft.Inverse(spectrum_work_->Ptr(), scratch_->F());
+    fft.ConvolveSpectrum(spectrum_->Ptr(), transforms_->KernelSpectrum(e.scale),
+                         spectrum_work_->Ptr(), scratch_->F());
     const size_t border_scale = size_t(std::ceil(e.scale * 0.5));
     const uint32_t xb = uint32_t(
         std::max<size_t>(size_t(std::round(w * CleanBorderRatio())), border_scale));

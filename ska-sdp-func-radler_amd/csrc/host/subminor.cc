@@ -11,10 +11,10 @@ SubMinorLoop::SubMinorLoop(gpu::Session& s, size_t width, size_t height,
       height_(height),
       padded_width_(padded_width),
       padded_height_(padded_height) {
-  gpu::Check(rdl_subminor_create(s.Handle(), &h_), "rdl_subminor_create");
+  h_ = s.SharedSubminor();
 }
 
-SubMinorLoop::~SubMinorLoop() { rdl_subminor_destroy(h_); }
+SubMinorLoop::~SubMinorLoop() = default;
 
 SubMinorLoop::RunResult SubMinorLoop::Run(ImageSet& residual,
                                           const gpu::Planes& psfs) {
@@ -58,16 +58,25 @@ SubMinorLoop::RunResult SubMinorLoop::Run(ImageSet& residual,
 std::shared_ptr<gpu::Buffer> SubMinorLoop::MakePaddedPsfSpectrum(
     gpu::Session& s, const float* d_psf, size_t width, size_t height,
     size_t pw, size_t ph) {
-  // float64 plan: see rdl_fft_create_f64 / DESIGN.md
+  // float64 transforms: see rdl_fft_create_f64 / DESIGN.md
   gpu::Fft& fft = s.GetFft(pw, ph, true);
-  gpu::Buffer kernel(s, pw * ph * sizeof(double));
-  // Image::Untrim + PrepareConvolutionKernel (subminor_loop.cc:199-202)
-  gpu::Check(rdl_prepare_psf_kernel_f64(s.Handle(), kernel.D(), uint32_t(pw),
-                                        uint32_t(ph), d_psf, uint32_t(width),
-                                        uint32_t(height)),
-             "rdl_prepare_psf_kernel_f64");
   auto spectrum = std::make_shared<gpu::Buffer>(s, fft.SpectrumBytes());
-  fft.Forward64(kernel.D(), spectrum->Ptr());
+  if (fft.UsesLds()) {
+    // Image::Untrim + PrepareConvolutionKernel (subminor_loop.cc:199-202)
+    gpu::Buffer kernel(s, pw * ph * sizeof(float));
+    gpu::Check(rdl_prepare_psf_kernel(s.Handle(), kernel.F(), uint32_t(pw),
+                                      uint32_t(ph), d_psf, uint32_t(width),
+                                      uint32_t(height)),
+               "rdl_prepare_psf_kernel");
+    fft.Forward(kernel.F(), spectrum->Ptr());
+  } else {
+    gpu::Buffer kernel(s, pw * ph * sizeof(double));
+    gpu::Check(rdl_prepare_psf_kernel_f64(s.Handle(), kernel.D(), uint32_t(pw),
+                                          uint32_t(ph), d_psf, uint32_t(width),
+                                          uint32_t(height)),
+               "rdl_prepare_psf_kernel_f64");
+    fft.Forward64(kernel.D(), spectrum->Ptr());
+  }
   s.Sync();
   return spectrum;
 }
@@ -88,10 +97,22 @@ void SubMinorLoop::CorrectResidualDirtyWithSpectrum(size_t image_index,
                                                     float* d_residual,
                                                     const void* d_spectrum) {
   gpu::Fft& fft = s_.GetFft(padded_width_, padded_height_, true);
-  padded_.Resize(s_, padded_width_ * padded_height_ * sizeof(double));
-  // GetFullIndividualModel + Image::Untrim, fused scatter into a zero plane
   const uint32_t ox = uint32_t((padded_width_ - width_) / 2);
   const uint32_t oy = uint32_t((padded_height_ - height_) / 2);
+  if (fft.UsesLds()) {
+    // GetFullIndividualModel into a W x H plane; Untrim, Convolve, Trim and
+    // the subtraction run inside the three transform passes
+    gpu::Buffer& model = s_.Scratch(gpu::Session::kCorrectionModel,
+                                    width_ * height_ * sizeof(float));
+    gpu::Buffer& work = s_.Scratch(gpu::Session::kCorrectionSpectrum, fft.SpectrumBytes());
+    GetFullIndividualModel(image_index, model.F());
+    fft.ConvolveSubtract(model.F(), width_, height_, ox, oy, d_spectrum, work.Ptr(),
+                         d_residual);
+    return;
+  }
+  gpu::Buffer& padded_ = s_.Scratch(gpu::Session::kCorrectionSpectrum,
+                                    padded_width_ * padded_height_ * sizeof(double));
+  // GetFullIndividualModel + Image::Untrim, fused scatter into a zero plane
   gpu::Check(rdl_subminor_model_f64(h_, uint32_t(image_index), padded_.D(),
                                     uint32_t(padded_width_),
                                     uint32_t(padded_height_), ox, oy),

@@ -84,7 +84,6 @@ class SubMinorLoop {
   size_t n_selected_ = 0, n_images_ = 0;
   std::vector<uint32_t>* trace_ = nullptr;
   std::map<size_t, std::shared_ptr<gpu::Buffer>> psf_spectra_;
-  gpu::Buffer padded_;
 };
 
 }  // namespace radler::algorithms

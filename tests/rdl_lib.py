@@ -108,6 +108,8 @@ class Rdl:
         self.lib.rdl_session_stream.argtypes = [C.c_void_p]
         self.lib.rdl_fft_spectrum_bytes.restype = C.c_size_t
         self.lib.rdl_fft_spectrum_bytes.argtypes = [C.c_void_p]
+        self.lib.rdl_conv_spectrum_bytes.restype = C.c_size_t
+        self.lib.rdl_conv_spectrum_bytes.argtypes = [C.c_void_p]
 
     def __getattr__(self, name):
         fn = getattr(self.lib, name)

@@ -187,6 +187,117 @@ def test_fft64_residual_correction(sess, orc, w, h):
     sess.rdl.rdl_fft_destroy(f)
 
 
+CONV_SIZES = [(64, 64), (128, 200), (210, 150), (96, 7), (2, 48), (1134, 96), (8, 1536),
+              (2016, 10)]
+
+
+def conv_create(sess, w, h, f64):
+    c = C.c_void_p()
+    rc = sess.rdl.lib.rdl_conv_create(sess.h, w, h, int(f64), C.byref(c))
+    return c if rc == 0 else None
+
+
+@pytest.mark.parametrize("w,h", CONV_SIZES)
+@pytest.mark.parametrize("f64", [False, True])
+def test_lds_fft_forward(sess, w, h, f64):
+    """Full 2-D forward transform vs numpy's float64 rfft2 (same layout and
+    normalisation): |err| <= eps_T * 8 * sqrt(log2 N) * sum|x|^(1/2)-scale."""
+    c = conv_create(sess, w, h, f64)
+    assert c is not None
+    rng = np.random.default_rng(w * 31 + h)
+    img = rng.standard_normal((h, w)).astype(np.float32)
+    nb = sess.rdl.lib.rdl_conv_spectrum_bytes(c)
+    assert nb == (w // 2 + 1) * h * (16 if f64 else 8)
+    di = sess.array(img)
+    spec = sess.array(shape=(h, w // 2 + 1), dtype=np.complex128 if f64 else np.complex64)
+    sess.rdl.rdl_conv_forward(c, di.vp, spec.vp)
+    got = spec.get()
+    ref = np.fft.rfft2(img.astype(np.float64))
+    eps = 2.3e-16 if f64 else 1.2e-7
+    tol = eps * 8 * np.sqrt(np.log2(w * h)) * np.sqrt(w * h)
+    assert np.abs(got - ref).max() <= tol
+    di.free()
+    spec.free()
+    sess.rdl.rdl_conv_destroy(c)
+
+
+def test_lds_fft_unsupported(sess):
+    for w, h in [(94, 47), (11, 64), (64, 22)]:
+        assert conv_create(sess, w, h, False) is None
+    assert conv_create(sess, 20480 * 2, 8, False) is None
+    assert conv_create(sess, 8, 10240 * 2, True) is None
+
+
+@pytest.mark.parametrize("w,h", [(64, 64), (210, 150), (96, 7), (1134, 96)])
+@pytest.mark.parametrize("f64", [False, True])
+def test_lds_fft_convolutions(sess, orc, w, h, f64):
+    """In-place convolution (rows, columns mode 1, rows) and the shared-spectrum
+    form (columns mode 2) against the oracle's float64 circular convolution."""
+    c = conv_create(sess, w, h, f64)
+    rng = np.random.default_rng(5 + w)
+    img = rng.standard_normal((h, w)).astype(np.float32)
+    ker = rng.standard_normal((h, w)).astype(np.float32)
+    o = img.copy()
+    orc.convolve(o, ker)
+    cdt = np.complex128 if f64 else np.complex64
+    dk, di = sess.array(ker), sess.array(img)
+    kspec = sess.array(shape=(h, w // 2 + 1), dtype=cdt)
+    work = sess.array(shape=(h, w // 2 + 1), dtype=cdt)
+    sspec = sess.array(shape=(h, w // 2 + 1), dtype=cdt)
+    out = sess.array(shape=(h, w))
+    sess.rdl.rdl_conv_forward(c, dk.vp, kspec.vp)
+    norm = 1.0 / (w * h) if f64 else float(np.float32(1.0 / (w * h)))
+    sess.rdl.rdl_conv_rows_forward(c, di.vp, w, h, 0, 0, work.vp)
+    sess.rdl.rdl_conv_columns(c, work.vp, work.vp, kspec.vp, 1, C.c_double(norm))
+    sess.rdl.rdl_conv_rows_inverse(c, work.vp, di.vp, w, h, 0, 0, 0)
+    tol = (1e-12 if f64 else 2e-6) * np.abs(o).max() * np.sqrt(np.log2(w * h))
+    assert np.abs(di.get() - o).max() <= max(tol, 1.2e-7 * np.abs(o).max())
+    di.upload(img)
+    sess.rdl.rdl_conv_forward(c, di.vp, sspec.vp)
+    sess.rdl.rdl_conv_columns(c, sspec.vp, work.vp, kspec.vp, 2, C.c_double(norm))
+    sess.rdl.rdl_conv_rows_inverse(c, work.vp, out.vp, w, h, 0, 0, 0)
+    assert np.abs(out.get() - o).max() <= max(tol, 1.2e-7 * np.abs(o).max())
+    for x in (dk, di, kspec, work, sspec, out):
+        x.free()
+    sess.rdl.rdl_conv_destroy(c)
+
+
+@pytest.mark.parametrize("w,h,pw,ph", [(64, 64, 72, 72), (200, 150, 224, 168), (90, 60, 98, 64)])
+def test_lds_fft_correction(sess, orc, w, h, pw, ph):
+    """SubMinorLoop::CorrectResidualDirty in one call sequence: model placed at
+    the centred offset of the padded plane, x padded PSF spectrum, trimmed and
+    subtracted from the residual (float64 transforms): agrees with the oracle
+    to float rounding."""
+    c = conv_create(sess, pw, ph, True)
+    rng = np.random.default_rng(pw)
+    psf = rng.standard_normal((h, w)).astype(np.float32)
+    model = np.zeros((h, w), np.float32)
+    model.flat[rng.choice(w * h, 50, replace=False)] = rng.standard_normal(50).astype(np.float32)
+    residual = rng.standard_normal((h, w)).astype(np.float32)
+    dpsf, dmod, dres = sess.array(psf), sess.array(model), sess.array(residual)
+    kplane = sess.array(shape=(ph, pw))
+    kspec = sess.array(shape=(ph, pw // 2 + 1), dtype=np.complex128)
+    work = sess.array(shape=(ph, pw // 2 + 1), dtype=np.complex128)
+    sess.rdl.rdl_prepare_psf_kernel(sess.h, kplane.vp, pw, ph, dpsf.vp, w, h)
+    sess.rdl.rdl_conv_forward(c, kplane.vp, kspec.vp)
+    ox, oy = (pw - w) // 2, (ph - h) // 2
+    sess.rdl.rdl_conv_rows_forward(c, dmod.vp, w, h, ox, oy, work.vp)
+    sess.rdl.rdl_conv_columns(c, work.vp, work.vp, kspec.vp, 1, C.c_double(1.0 / (pw * ph)))
+    sess.rdl.rdl_conv_rows_inverse(c, work.vp, dres.vp, w, h, ox, oy, 1)
+    k = np.zeros((ph, pw), np.float32)
+    k[oy:oy + h, ox:ox + w] = psf
+    k = np.roll(k, (-(ph // 2), -(pw // 2)), axis=(0, 1)).copy()
+    o = np.zeros((ph, pw), np.float32)
+    o[oy:oy + h, ox:ox + w] = model
+    orc.convolve(o, k)
+    expect = residual - o[oy:oy + h, ox:ox + w]
+    err = np.abs(dres.get() - expect).max()
+    assert err <= 2.4e-7 * max(np.abs(o).max(), np.abs(residual).max())
+    for x in (dpsf, dmod, dres, kplane, kspec, work):
+        x.free()
+    sess.rdl.rdl_conv_destroy(c)
+
+
 def test_prepare_kernels(sess, orc):
     w, h, pw, ph = 40, 30, 48, 36
     rng = np.random.default_rng(2)
