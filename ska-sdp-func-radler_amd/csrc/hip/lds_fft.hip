@@ -198,6 +198,79 @@ struct Dft<T, 5> : DftOdd<T, 5> {};
 template <typename T>
 struct Dft<T, 7> : DftOdd<T, 7> {};
 
+// composite radices R = P x Q (Cooley-Tukey in registers):
+// X[k2 + Q k3] = sum_k1 W_P^{k1 k3} W_R^{k1 k2} sum_n2 x[k1 + P n2] W_Q^{n2 k2}
+template <typename T, int P, int Q>
+struct DftComposite {
+  __device__ __forceinline__ static void Run(Cx<T>* a, const double (*w)[2]) {
+    constexpr int R = P * Q;
+    Cx<T> t[P][Q];
+#pragma unroll
+    for (int k1 = 0; k1 < P; ++k1) {
+#pragma unroll
+      for (int n2 = 0; n2 < Q; ++n2) t[k1][n2] = a[k1 + P * n2];
+      Dft<T, Q>::Run(t[k1]);
+#pragma unroll
+      for (int k2 = 1; k2 < Q; ++k2)
+        if (k1 > 0) {
+          const int m = (k1 * k2) % R;
+          t[k1][k2] = Mul(t[k1][k2], Cx<T>{T(w[m][0]), T(w[m][1])});
+        }
+    }
+#pragma unroll
+    for (int k2 = 0; k2 < Q; ++k2) {
+      Cx<T> u[P];
+#pragma unroll
+      for (int k1 = 0; k1 < P; ++k1) u[k1] = t[k1][k2];
+      Dft<T, P>::Run(u);
+#pragma unroll
+      for (int k3 = 0; k3 < P; ++k3) a[k2 + Q * k3] = u[k3];
+    }
+  }
+};
+
+// exp(-2 pi i m / 16), exp(-2 pi i m / 9)
+__device__ constexpr double kW16[16][2] = {
+    {1.0, 0.0},
+    {0.92387953251128675612818318939679, -0.38268343236508977172845998403040},
+    {0.70710678118654752440084436210485, -0.70710678118654752440084436210485},
+    {0.38268343236508977172845998403040, -0.92387953251128675612818318939679},
+    {0.0, -1.0},
+    {-0.38268343236508977172845998403040, -0.92387953251128675612818318939679},
+    {-0.70710678118654752440084436210485, -0.70710678118654752440084436210485},
+    {-0.92387953251128675612818318939679, -0.38268343236508977172845998403040},
+    {-1.0, 0.0},
+    {-0.92387953251128675612818318939679, 0.38268343236508977172845998403040},
+    {-0.70710678118654752440084436210485, 0.70710678118654752440084436210485},
+    {-0.38268343236508977172845998403040, 0.92387953251128675612818318939679},
+    {0.0, 1.0},
+    {0.38268343236508977172845998403040, 0.92387953251128675612818318939679},
+    {0.70710678118654752440084436210485, 0.70710678118654752440084436210485},
+    {0.92387953251128675612818318939679, 0.38268343236508977172845998403040}};
+__device__ constexpr double kW9[9][2] = {
+    {1.0, 0.0},
+    {0.76604444311897803520239265055542, -0.64278760968653932632264340990726},
+    {0.17364817766693034885171662676931, -0.98480775301220805936674302458952},
+    {-0.5, -0.86602540378443864676372317075294},
+    {-0.93969262078590838405410927732473, -0.34202014332566873304409961468226},
+    {-0.93969262078590838405410927732473, 0.34202014332566873304409961468226},
+    {-0.5, 0.86602540378443864676372317075294},
+    {0.17364817766693034885171662676931, 0.98480775301220805936674302458952},
+    {0.76604444311897803520239265055542, 0.64278760968653932632264340990726}};
+
+template <typename T>
+struct Dft<T, 16> {
+  __device__ __forceinline__ static void Run(Cx<T>* a) {
+    DftComposite<T, 4, 4>::Run(a, kW16);
+  }
+};
+template <typename T>
+struct Dft<T, 9> {
+  __device__ __forceinline__ static void Run(Cx<T>* a) {
+    DftComposite<T, 3, 3>::Run(a, kW9);
+  }
+};
+
 // ---- one Stockham pass over `count` transforms of length n held in LDS
 // (in place: all butterfly inputs are read to registers before the barrier)
 template <typename T, int R>
@@ -250,6 +323,8 @@ __device__ void LdsFftForward(Cx<T>* buf, const LdsPlan& p, uint32_t count,
   for (uint32_t q = 0; q < p.n_pass; ++q) {
     const uint32_t r = p.radix[q];
     switch (r) {
+      case 16: StockhamPass<T, 16>(buf, p.n, count, ns, tw, tid); break;
+      case 9: StockhamPass<T, 9>(buf, p.n, count, ns, tw, tid); break;
       case 8: StockhamPass<T, 8>(buf, p.n, count, ns, tw, tid); break;
       case 4: StockhamPass<T, 4>(buf, p.n, count, ns, tw, tid); break;
       case 2: StockhamPass<T, 2>(buf, p.n, count, ns, tw, tid); break;
@@ -429,12 +504,17 @@ bool Factorize(uint32_t n, std::vector<uint8_t>& radix) {
     m /= 2;
     ++twos;
   }
-  while (twos >= 3) {
-    radix.push_back(8);
-    twos -= 3;
+  while (twos >= 4) {
+    radix.push_back(16);
+    twos -= 4;
   }
+  if (twos == 3) radix.push_back(8);
   if (twos == 2) radix.push_back(4);
   if (twos == 1) radix.push_back(2);
+  while (m % 9 == 0) {
+    m /= 9;
+    radix.push_back(9);
+  }
   for (uint32_t r : {7u, 5u, 3u})
     while (m % r == 0) {
       m /= r;

@@ -38,8 +38,12 @@ def main():
                                          C.POINTER(C.c_uint64), C.POINTER(C.c_double)]
     s.rdl.lib.rdl_conv_spectrum_bytes.restype = C.c_size_t
     reps = 10
-    for (w, h, f64) in ((8192, 8192, False), (9072, 9072, True), (4096, 4096, False),
-                        (4536, 4536, True)):
+    cases = ((8192, 8192, False), (9072, 9072, True), (4096, 4096, False), (4536, 4536, True))
+    if len(sys.argv) > 1:  # e.g. "9072,9072,1"
+        w, h, f = (int(v) for v in sys.argv[1].split(","))
+        cases = ((w, h, bool(f)),)
+        reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    for (w, h, f64) in cases:
         img = np.random.default_rng(1).standard_normal((h, w)).astype(np.float32)
         di = s.array(img)
         cdt = np.complex128 if f64 else np.complex64
