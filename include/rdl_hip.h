@@ -336,6 +336,22 @@ int rdl_add_shape_component(rdl_session* s, float* d_image, uint32_t width,
                             uint32_t height, const float* h_kernel, uint32_t n,
                             uint32_t x, uint32_t y, float gain);
 
+/* ------------------------------------------------------- box transfers */
+/* w x h box from src (row stride src_w, origin src_x,src_y) to dst (stride
+ * dst_w, origin dst_x,dst_y); d_mask (box-local w x h bytes, may be NULL):
+ *   RDL_BOX_COPY         dst = src                 (ImageSet::Trim)
+ *   RDL_BOX_COPY_MASKED  dst = src where mask      (ImageSet::CopyMasked)
+ *   RDL_BOX_COPY_ZERO    dst = mask ? src : 0      (ImageSet::TrimMasked)
+ *   RDL_BOX_ADD          dst += src                (ImageSet::AddSubImage)
+ * (cpp/image_set.h:216-262, parallel_deconvolution.cc:308-318, 475-482). */
+#define RDL_BOX_COPY 0
+#define RDL_BOX_COPY_MASKED 1
+#define RDL_BOX_COPY_ZERO 2
+#define RDL_BOX_ADD 3
+int rdl_box(rdl_session* s, float* d_dst, uint32_t dst_w, uint32_t dst_x,
+            uint32_t dst_y, const float* d_src, uint32_t src_w, uint32_t src_x,
+            uint32_t src_y, uint32_t w, uint32_t h, const uint8_t* d_mask, int op);
+
 /* -------------------------------------------------- IUWT (à-trous) */
 /* IuwtDecomposition::DecomposeMt / Recompose
  * (cpp/algorithms/iuwt/iuwt_decomposition.cc:9-237, .h:121-261).

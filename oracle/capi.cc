@@ -9,6 +9,7 @@
 
 #include "fft.h"
 #include "oracle.h"
+#include "tiling.h"
 
 using namespace oracle;
 
@@ -235,6 +236,123 @@ int orc_algo_execute(void* h, const orc_set_desc* d, float* residual,
         trace[3 * i + 2] = tr[i].scale;
       }
     }
+    return 0;
+  } catch (std::exception& e) {
+    g_error = e.what();
+    return 1;
+  }
+}
+
+struct orc_parallel_result {
+  int32_t another_iteration_required;
+  int32_t n_subimages;
+  double start_peak, end_peak;
+  uint64_t first_iteration_number, total_iterations;
+  uint64_t n_trace;
+};
+
+struct OrcParallel {
+  size_t grid_w, grid_h;
+  double major_loop_gain_unused = 0.0;
+  std::vector<TiledAlgorithm> algorithms;
+};
+
+// MakeSubImages alone (no user mask): boxes 4 x u32 per subimage, labels
+// W*H u16 (subimage index + 1 in its boundary mask).
+int orc_make_subimages(const float* image, uint64_t w, uint64_t h, uint64_t grid_w,
+                       uint64_t grid_h, uint32_t* boxes, uint16_t* labels) {
+  try {
+    std::vector<SubImage> subs = MakeSubImages(image, w, h, nullptr, grid_w, grid_h);
+    std::fill(labels, labels + w * h, uint16_t(0));
+    for (const SubImage& s : subs) {
+      boxes[4 * s.index] = uint32_t(s.x);
+      boxes[4 * s.index + 1] = uint32_t(s.y);
+      boxes[4 * s.index + 2] = uint32_t(s.width);
+      boxes[4 * s.index + 3] = uint32_t(s.height);
+      for (size_t y = 0; y != s.height; ++y)
+        for (size_t x = 0; x != s.width; ++x)
+          if (s.boundary_mask[y * s.width + x])
+            labels[(y + s.y) * w + x + s.x] = uint16_t(s.index + 1);
+    }
+    return 0;
+  } catch (std::exception& e) {
+    g_error = e.what();
+    return 1;
+  }
+}
+
+void* orc_parallel_create(int kind, const orc_algo_settings* a, uint64_t grid_w,
+                          uint64_t grid_h) {
+  auto* p = new OrcParallel();
+  p->grid_w = grid_w;
+  p->grid_h = grid_h;
+  p->algorithms.resize(grid_w * grid_h);
+  for (TiledAlgorithm& t : p->algorithms) {
+    t.kind = kind;
+    t.settings = MakeSettings(a);
+    t.settings.clean_mask = nullptr;
+  }
+  return p;
+}
+
+void orc_parallel_destroy(void* h) { delete static_cast<OrcParallel*>(h); }
+
+// sub_boxes: 4 x u32 (x, y, w, h) per subimage; labels (may be NULL): W*H
+// u16, subimage index + 1 where the pixel is in that subimage's boundary
+// mask; trace: 4 x u32 (subimage, x, y, scale) per component of the run pass.
+int orc_parallel_execute(void* h, const orc_set_desc* d, float* residual,
+                         float* model, const float* psfs, double major_loop_gain,
+                         const uint8_t* user_mask, orc_parallel_result* out,
+                         uint32_t* sub_boxes, uint16_t* labels, uint32_t* trace,
+                         uint64_t trace_cap) {
+  try {
+    auto* p = static_cast<OrcParallel*>(h);
+    SetDesc desc = MakeDesc(d);
+    ImageSet res = MakeSet(desc, d, residual);
+    ImageSet mod = MakeSet(desc, d, model);
+    std::vector<const float*> psf_ptrs;
+    for (uint64_t c = 0; c != d->n_channels; ++c)
+      psf_ptrs.push_back(psfs + c * d->width * d->height);
+    std::vector<SubImage> subs;
+    std::vector<std::vector<Component>> traces;
+    const double limit = p->algorithms.front().settings.divergence_limit;
+    ParallelResult r = ParallelRun(p->algorithms, p->grid_w, p->grid_h, desc, res,
+                                   mod, psf_ptrs, major_loop_gain, limit,
+                                   reinterpret_cast<const bool*>(user_mask), &subs,
+                                   &traces);
+    out->another_iteration_required = r.another_iteration_required;
+    out->n_subimages = int32_t(subs.size());
+    out->start_peak = r.start_peak;
+    out->end_peak = r.end_peak;
+    out->first_iteration_number = p->algorithms.front().iteration_number;
+    out->total_iterations = 0;
+    for (const TiledAlgorithm& t : p->algorithms)
+      out->total_iterations += t.iteration_number;
+    if (labels) std::fill(labels, labels + d->width * d->height, uint16_t(0));
+    uint64_t n_trace = 0;
+    for (const SubImage& s : subs) {
+      if (sub_boxes) {
+        sub_boxes[4 * s.index] = uint32_t(s.x);
+        sub_boxes[4 * s.index + 1] = uint32_t(s.y);
+        sub_boxes[4 * s.index + 2] = uint32_t(s.width);
+        sub_boxes[4 * s.index + 3] = uint32_t(s.height);
+      }
+      if (labels)
+        for (size_t y = 0; y != s.height; ++y)
+          for (size_t x = 0; x != s.width; ++x)
+            if (s.boundary_mask[y * s.width + x])
+              labels[(y + s.y) * d->width + x + s.x] = uint16_t(s.index + 1);
+      for (const Component& c : traces[s.index]) {
+        if (trace && n_trace < trace_cap) {
+          trace[4 * n_trace] = uint32_t(s.index);
+          trace[4 * n_trace + 1] = c.x;
+          trace[4 * n_trace + 2] = c.y;
+          trace[4 * n_trace + 3] = c.scale;
+        }
+        ++n_trace;
+      }
+    }
+    out->n_trace = n_trace;
     return 0;
   } catch (std::exception& e) {
     g_error = e.what();

@@ -83,6 +83,33 @@ inline unsigned GridFor(size_t n) {
 
 }  // namespace rdl
 
+
+namespace rdl {
+// Box transfer between two planes (ImageSet::Trim / TrimMasked / CopyMasked /
+// AddSubImage, cpp/image_set.h:216-262, aocommon Image box helpers).
+__global__ __launch_bounds__(256) void BoxKernel(float* dst, uint32_t dst_w,
+                                                 uint32_t dst_x, uint32_t dst_y,
+                                                 const float* src, uint32_t src_w,
+                                                 uint32_t src_x, uint32_t src_y,
+                                                 uint32_t w, uint32_t h,
+                                                 const uint8_t* mask, int op) {
+  const size_t total = size_t(w) * h;
+  for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < total;
+       i += size_t(gridDim.x) * blockDim.x) {
+    const uint32_t x = uint32_t(i % w), y = uint32_t(i / w);
+    const float v = src[size_t(y + src_y) * src_w + x + src_x];
+    float& d = dst[size_t(y + dst_y) * dst_w + x + dst_x];
+    const bool m = mask ? mask[i] != 0 : true;
+    switch (op) {
+      case RDL_BOX_COPY: d = v; break;
+      case RDL_BOX_COPY_MASKED: if (m) d = v; break;
+      case RDL_BOX_COPY_ZERO: d = m ? v : 0.0f; break;
+      default: d += v; break;
+    }
+  }
+}
+}  // namespace rdl
+
 extern "C" {
 
 int rdl_integrate(rdl_session* s, const rdl_integration* integ,
@@ -163,6 +190,24 @@ int rdl_add_shape_component(rdl_session* s, float* d_image, uint32_t width,
     RDL_HIP_CHECK(hipGetLastError());
   }
   RDL_HIP_CHECK(hipStreamSynchronize(s->stream));
+  return RDL_OK;
+}
+
+
+int rdl_box(rdl_session* s, float* d_dst, uint32_t dst_w, uint32_t dst_x,
+            uint32_t dst_y, const float* d_src, uint32_t src_w, uint32_t src_x,
+            uint32_t src_y, uint32_t w, uint32_t h, const uint8_t* d_mask, int op) {
+  RDL_ARG_CHECK(s && d_dst && d_src, "NULL argument");
+  RDL_ARG_CHECK(op >= RDL_BOX_COPY && op <= RDL_BOX_ADD, "bad box op");
+  RDL_ARG_CHECK(uint64_t(dst_x) + w <= dst_w && uint64_t(src_x) + w <= src_w,
+                "box outside the row");
+  if (w == 0 || h == 0) return RDL_OK;
+  rdl::ScopedTiming t(s, "box", double(w) * h * (op == RDL_BOX_ADD ? 12.0 : 8.0));
+  const size_t total = size_t(w) * h;
+  rdl::BoxKernel<<<unsigned(std::min<size_t>(16384, (total + 255) / 256)), 256, 0,
+                   s->stream>>>(d_dst, dst_w, dst_x, dst_y, d_src, src_w, src_x,
+                                src_y, w, h, d_mask, op);
+  RDL_HIP_CHECK(hipGetLastError());
   return RDL_OK;
 }
 

@@ -116,9 +116,10 @@ std::vector<float> DeviceRun::Model() const {
   return out;
 }
 
-const std::vector<uint32_t>& DeviceRun::Trace() const {
+const std::vector<uint32_t>& DeviceRun::Trace(size_t index) const {
   static const std::vector<uint32_t> empty;
-  const algorithms::DeconvolutionAlgorithm& a = parallel_->FirstAlgorithm();
+  if (index >= parallel_->SubImageCount()) return empty;
+  const algorithms::DeconvolutionAlgorithm& a = parallel_->Algorithm(index);
   if (auto* m = dynamic_cast<const algorithms::MultiScaleAlgorithm*>(&a))
     return m->LastTrace();
   if (auto* g = dynamic_cast<const algorithms::GenericClean*>(&a))

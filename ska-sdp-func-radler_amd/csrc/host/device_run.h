@@ -34,7 +34,12 @@ class DeviceRun {
   size_t LastIterations() const { return last_iterations_; }
   std::vector<float> Residual() const;
   std::vector<float> Model() const;
-  const std::vector<uint32_t>& Trace() const;
+  /// Component trace (x, y, scale triples) of subimage `index`'s algorithm.
+  const std::vector<uint32_t>& Trace(size_t index = 0) const;
+  /// Tiles of the last Execute (empty for a 1x1 grid).
+  const std::vector<algorithms::SubImage>& SubImages() const {
+    return parallel_->SubImages();
+  }
   gpu::Session& Session() { return *session_; }
   void Sync() { session_->Sync(); }
 

@@ -1,0 +1,45 @@
+// radler::math::DijkstraSplitter (reference: cpp/math/dijkstra_splitter.{h,cc}):
+// minimum-|flux| paths that split the integrated image into subimages for
+// ParallelDeconvolution. Runs on the host (a priority-queue search, not
+// data-parallel); the image comes from the device once per major iteration.
+#pragma once
+
+#include <cstddef>
+#include <vector>
+
+namespace radler::math {
+
+class DijkstraSplitter {
+ public:
+  DijkstraSplitter(size_t width, size_t height) : width_(width), height_(height) {}
+
+  /// Shortest top-to-bottom path of sum |image| inside columns [x1, x2);
+  /// output (a width x height plane) gets 1 on the path, 0 elsewhere in the
+  /// band, untouched outside it (dijkstra_splitter.cc:32-84).
+  void DivideVertically(const float* image, float* output, size_t x1,
+                        size_t x2) const;
+  /// Left-to-right path inside rows [y1, y2) (dijkstra_splitter.cc:86-136).
+  void DivideHorizontally(const float* image, float* output, size_t y1,
+                          size_t y2) const;
+  /// Area between the dividers around column subimage_x
+  /// (dijkstra_splitter.cc:138-172).
+  void FloodVerticalArea(const float* subdivision, size_t subimage_x, bool* mask,
+                         size_t& x, size_t& subwidth) const;
+  /// Area between the dividers around row subimage_y (:174-208).
+  void FloodHorizontalArea(const float* subdivision, size_t subimage_y,
+                           bool* mask, size_t& y, size_t& subheight) const;
+  /// Overlap of a vertical area (trimmed to its columns) and a horizontal
+  /// area; bounding box kept even when the image is (:210-285).
+  void GetBoundingMask(const bool* vertical_mask, size_t vertical_mask_x,
+                       size_t vertical_mask_width, const bool* horizontal_mask,
+                       bool* mask, size_t& sub_x, size_t& sub_y, size_t& subwidth,
+                       size_t& subheight) const;
+
+ private:
+  template <bool kVertical>
+  void Divide(const float* image, float* output, size_t lo, size_t hi) const;
+
+  size_t width_, height_;
+};
+
+}  // namespace radler::math

@@ -15,6 +15,14 @@
 
 namespace radler::algorithms {
 
+/// One tile of the grid (parallel_deconvolution.h SubImage).
+struct SubImage {
+  size_t index = 0, x = 0, y = 0, width = 0, height = 0;
+  std::vector<bool> mask, boundary_mask;
+  double peak = 0.0;
+  bool reached_major_threshold = false;
+};
+
 struct ParallelDeconvolutionResult {
   bool another_iteration_required = false;
   std::optional<float> start_peak;
@@ -38,11 +46,15 @@ class ParallelDeconvolution {
   bool IsInitialized() const { return !algorithms_.empty(); }
   size_t SubImageCount() const { return algorithms_.size(); }
   DeconvolutionAlgorithm& Algorithm(size_t i) { return *algorithms_[i]; }
+  const DeconvolutionAlgorithm& Algorithm(size_t i) const { return *algorithms_[i]; }
 
   ParallelDeconvolutionResult ExecuteMajorIteration(
       ImageSet& data_image, ImageSet& model_image,
       const std::vector<gpu::Planes>& psf_images,
       const std::vector<PsfOffset>& psf_offsets, double major_loop_gain);
+
+  /// Tiles of the last ExecuteParallelRun (empty for a 1x1 grid).
+  const std::vector<SubImage>& SubImages() const { return subimages_; }
 
   void FreeDeconvolutionAlgorithms() {
     algorithms_.clear();
@@ -59,10 +71,22 @@ class ParallelDeconvolution {
       const std::vector<gpu::Planes>& psf_images,
       const std::vector<PsfOffset>& psf_offsets, double major_loop_gain);
 
+  void RunSubImage(SubImage& sub, ImageSet& data_image, const ImageSet& model_image,
+                   ImageSet& result_model, const gpu::Planes& psfs,
+                   double major_iteration_threshold, bool find_peak_only);
+
   std::vector<std::unique_ptr<DeconvolutionAlgorithm>> algorithms_;
+  std::vector<SubImage> subimages_;
   const Settings& settings_;
   const bool* mask_ = nullptr;
 };
+
+/// Subimage geometry of the grid (parallel_deconvolution.cc:57-166).
+std::vector<SubImage> MakeSubImages(const std::vector<float>& image, size_t width,
+                                    size_t height, const bool* user_mask,
+                                    const std::vector<PsfOffset>& psf_offsets,
+                                    const Settings& settings,
+                                    std::vector<size_t>& psf_indices);
 
 /// parallel_deconvolution.cc:34-55 (first index on equal distance).
 size_t NearestPsfIndex(const std::vector<PsfOffset>& psf_offsets, size_t x,

@@ -344,6 +344,37 @@ py::dict ResultDict(const radler::algorithms::ParallelDeconvolutionResult& r,
   return d;
 }
 
+void InitTiling(py::module& m) {
+  py::module t = m.def_submodule("tiling", "ParallelDeconvolution subimage geometry");
+  t.def("make_subimages", [](py::array_t<float, py::array::c_style | py::array::forcecast> image,
+                             size_t grid_w, size_t grid_h) {
+    if (image.ndim() != 2) throw std::runtime_error("image must be 2-D");
+    const size_t h = image.shape(0), w = image.shape(1);
+    radler::Settings settings;
+    settings.parallel.grid_width = grid_w;
+    settings.parallel.grid_height = grid_h;
+    std::vector<float> img(image.data(), image.data() + w * h);
+    std::vector<size_t> psf_indices;
+    const auto subs = radler::algorithms::MakeSubImages(img, w, h, nullptr, {}, settings,
+                                                        psf_indices);
+    py::array_t<uint32_t> boxes({py::ssize_t(subs.size()), py::ssize_t(4)});
+    py::array_t<uint16_t> labels({py::ssize_t(h), py::ssize_t(w)});
+    std::fill(labels.mutable_data(), labels.mutable_data() + w * h, 0);
+    for (const auto& sub : subs) {
+      uint32_t* b = boxes.mutable_data(py::ssize_t(sub.index), 0);
+      b[0] = uint32_t(sub.x);
+      b[1] = uint32_t(sub.y);
+      b[2] = uint32_t(sub.width);
+      b[3] = uint32_t(sub.height);
+      for (size_t y = 0; y != sub.height; ++y)
+        for (size_t x = 0; x != sub.width; ++x)
+          if (sub.boundary_mask[y * sub.width + x])
+            labels.mutable_data()[(y + sub.y) * w + x + sub.x] = uint16_t(sub.index + 1);
+    }
+    return py::make_tuple(boxes, labels);
+  }, py::arg("image"), py::arg("grid_width"), py::arg("grid_height"));
+}
+
 void InitGpu(py::module& m) {
   py::module g = m.def_submodule("gpu", "MI355X device helpers (bench/tests)");
   g.def("set_verbosity", &radler::log::SetVerbosity);
@@ -376,12 +407,33 @@ void InitGpu(py::module& m) {
         std::vector<float> v = self.Model();
         return py::array_t<float>(v.size(), v.data());
       })
-      .def("trace", [](const radler::DeviceRun& self) {
-        const std::vector<uint32_t>& t = self.Trace();
+      .def("trace", [](const radler::DeviceRun& self, size_t index) {
+        const std::vector<uint32_t>& t = self.Trace(index);
         py::array_t<uint32_t> a({py::ssize_t(t.size() / 3), py::ssize_t(3)});
         std::copy(t.begin(), t.end(), a.mutable_data());
         return a;
-      })
+      }, py::arg("index") = 0)
+      .def("subimages", [](const radler::DeviceRun& self, size_t width, size_t height) {
+        // (boxes [n][x, y, w, h], labels [h][w]: subimage index + 1 inside its
+        // boundary mask)
+        const auto& subs = self.SubImages();
+        py::array_t<uint32_t> boxes({py::ssize_t(subs.size()), py::ssize_t(4)});
+        py::array_t<uint16_t> labels({py::ssize_t(height), py::ssize_t(width)});
+        std::fill(labels.mutable_data(), labels.mutable_data() + width * height, 0);
+        for (const auto& sub : subs) {
+          uint32_t* b = boxes.mutable_data(py::ssize_t(sub.index), 0);
+          b[0] = uint32_t(sub.x);
+          b[1] = uint32_t(sub.y);
+          b[2] = uint32_t(sub.width);
+          b[3] = uint32_t(sub.height);
+          for (size_t y = 0; y != sub.height; ++y)
+            for (size_t x = 0; x != sub.width; ++x)
+              if (sub.boundary_mask[y * sub.width + x])
+                labels.mutable_data()[(y + sub.y) * width + x + sub.x] =
+                    uint16_t(sub.index + 1);
+        }
+        return py::make_tuple(boxes, labels);
+      }, py::arg("width"), py::arg("height"))
       .def("session_handle", [](radler::DeviceRun& self) {
         return reinterpret_cast<uintptr_t>(self.Session().Handle());
       })
@@ -399,4 +451,5 @@ PYBIND11_MODULE(radler, m) {  // python/pywrappers.cc
   InitRadler(m);
   InitComponentList(m);
   InitGpu(m);
+  InitTiling(m);
 }

@@ -213,6 +213,70 @@ class OracleAlgorithm:
             pass
 
 
+def make_subimages(oracle, image, grid_w, grid_h):
+    """oracle MakeSubImages: (boxes [n, 4] x,y,w,h; labels [h, w])."""
+    image = np.ascontiguousarray(image, np.float32)
+    h, w = image.shape
+    boxes = np.zeros((grid_w * grid_h, 4), np.uint32)
+    labels = np.zeros((h, w), np.uint16)
+    L = oracle.lib
+    L.orc_make_subimages.argtypes = [f32p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
+                                     C.c_void_p, C.c_void_p]
+    if L.orc_make_subimages(image, w, h, grid_w, grid_h, boxes.ctypes.data,
+                            labels.ctypes.data) != 0:
+        raise RuntimeError(L.orc_last_error().decode())
+    return boxes, labels
+
+
+class ParallelResult(C.Structure):
+    _fields_ = [("another_iteration_required", C.c_int32), ("n_subimages", C.c_int32),
+                ("start_peak", C.c_double), ("end_peak", C.c_double),
+                ("first_iteration_number", C.c_uint64), ("total_iterations", C.c_uint64),
+                ("n_trace", C.c_uint64)]
+
+
+class OracleParallel:
+    """ParallelDeconvolution tiling restatement (oracle/tiling.cc): a grid of
+    per-subimage algorithms (GenericClean=0, MultiScale=1)."""
+
+    def __init__(self, oracle, kind, grid_w, grid_h, **settings):
+        self.o = oracle
+        self.settings = algo_settings(**settings)
+        L = oracle.lib
+        L.orc_parallel_create.restype = C.c_void_p
+        L.orc_parallel_create.argtypes = [C.c_int, C.POINTER(AlgoSettings), C.c_uint64,
+                                          C.c_uint64]
+        L.orc_parallel_destroy.argtypes = [C.c_void_p]
+        L.orc_parallel_execute.argtypes = [C.c_void_p, C.POINTER(SetDesc), f32p, f32p, f32p,
+                                           C.c_double, C.c_void_p, C.POINTER(ParallelResult),
+                                           C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]
+        self.h = L.orc_parallel_create(kind, C.byref(self.settings), grid_w, grid_h)
+        self.n_sub = grid_w * grid_h
+
+    def execute(self, residual, model, psfs, major_loop_gain, user_mask=None,
+                trace_cap=1 << 22):
+        n, h, w = residual.shape
+        d = Oracle.set_desc(w, h, psfs.shape[0], n // psfs.shape[0], None)
+        r = ParallelResult()
+        boxes = np.zeros((self.n_sub, 4), np.uint32)
+        labels = np.zeros((h, w), np.uint16)
+        trace = np.zeros((trace_cap, 4), np.uint32)
+        um = None if user_mask is None else np.ascontiguousarray(user_mask, np.uint8)
+        rc = self.o.lib.orc_parallel_execute(
+            self.h, C.byref(d), residual, model, np.ascontiguousarray(psfs, np.float32),
+            major_loop_gain, None if um is None else um.ctypes.data, C.byref(r),
+            boxes.ctypes.data, labels.ctypes.data, trace.ctypes.data, trace_cap)
+        if rc != 0:
+            raise RuntimeError(self.o.lib.orc_last_error().decode())
+        return r, boxes, labels, trace[: min(r.n_trace, trace_cap)].copy()
+
+    def __del__(self):
+        try:
+            self.o.lib.orc_parallel_destroy(self.h)
+        except Exception:
+            pass
+
+
 _ORACLE = None
 
 

@@ -1,0 +1,89 @@
+"""ParallelDeconvolution tiling.
+
+CPU: the product's host splitter (radler.tiling.make_subimages ->
+libradler_amd.so MakeSubImages / DijkstraSplitter) produces exactly the
+oracle's subimage geometry (boxes and boundary masks), the masks partition the
+image, boxes are even-sized on even images.
+GPU: Radler's tiled major iteration (device box transfers + per-subimage
+algorithms) matches the oracle's tiled run: same tiles, same per-subimage
+component traces, residual/model within 2e-5 * max|dirty|.
+"""
+import numpy as np
+import pytest
+
+from oracle_lib import OracleParallel, get_oracle, make_subimages
+from radler_import import radler as rd
+from synthetic import problem
+
+PIXEL_SCALE = 1.0 / 3600.0 * np.pi / 180.0
+
+GEOMETRY_CASES = [(256, 256, 3, 2, 1), (200, 160, 2, 2, 2), (301, 257, 4, 3, 3),
+                  (128, 512, 2, 4, 4), (512, 512, 8, 8, 5)]
+
+
+@pytest.mark.parametrize("w,h,gw,gh,seed", GEOMETRY_CASES)
+def test_splitter_matches_oracle(w, h, gw, gh, seed):
+    _, dirty = problem(w, h, 30, 3, seed=seed)
+    boxes_o, labels_o = make_subimages(get_oracle(), dirty, gw, gh)
+    boxes, labels = rd.tiling.make_subimages(dirty, gw, gh)
+    assert np.array_equal(boxes, boxes_o)
+    assert np.array_equal(labels, labels_o)
+    # every pixel belongs to exactly one subimage (boundary masks partition)
+    assert labels.min() >= 1 and set(np.unique(labels)) == set(range(1, gw * gh + 1))
+    for i, (x, y, bw, bh) in enumerate(boxes):
+        ys, xs = np.nonzero(labels == i + 1)
+        assert xs.min() >= x and xs.max() < x + bw and ys.min() >= y and ys.max() < y + bh
+        if w % 2 == 0:
+            assert bw % 2 == 0
+        if h % 2 == 0:
+            assert bh % 2 == 0
+
+
+def test_splitter_flat_image_is_deterministic():
+    """Equal costs everywhere: tie-breaking follows the heap order exactly."""
+    img = np.ones((96, 128), np.float32)
+    assert all(np.array_equal(a, b) for a, b in
+               zip(rd.tiling.make_subimages(img, 3, 3), make_subimages(get_oracle(), img, 3, 3)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,w,gw,gh", [(1, 256, 3, 2), (0, 192, 2, 2), (1, 320, 2, 3)])
+def test_tiled_run_matches_oracle(kind, w, gw, gh):
+    h = w
+    psf, dirty = problem(w, h, 40, 4, seed=w + gw)
+    thr, max_iter, mgain = 4e-3, 1500, 0.9
+    orc = get_oracle()
+    orc.set_threads(8)
+    st = dict(threshold=thr, max_iterations=max_iter, border_ratio=0.0,
+              major_loop_gain=mgain)
+    if kind == 1:
+        st.update(max_scales=4, beam_size_in_pixels=2.0)
+    par = OracleParallel(orc, kind, gw, gh, **st)
+    res_o, mod_o = dirty[None].copy(), np.zeros((1, h, w), np.float32)
+    r_o, boxes_o, labels_o, trace_o = par.execute(res_o, mod_o, psf[None], mgain)
+
+    s = rd.Settings()
+    s.algorithm_type = rd.AlgorithmType.multiscale if kind == 1 else rd.AlgorithmType.generic_clean
+    s.trimmed_image_width = s.trimmed_image_height = w
+    s.pixel_scale.x = s.pixel_scale.y = PIXEL_SCALE
+    s.minor_iteration_count = max_iter
+    s.absolute_threshold = thr
+    s.border_ratio = 0.0
+    s.major_loop_gain = mgain
+    s.parallel.grid_width, s.parallel.grid_height = gw, gh
+    if kind == 1:
+        s.multiscale.max_scales = 4
+    run = rd.gpu.DeviceRun(s, psf, dirty, [], 2.0 * PIXEL_SCALE if kind == 1 else 0.0)
+    r = run.execute()
+    boxes, labels = run.subimages(w, h)
+    assert np.array_equal(boxes, boxes_o)
+    assert np.array_equal(labels, labels_o)
+    for i in range(gw * gh):
+        t_o = trace_o[trace_o[:, 0] == i][:, 1:]
+        t_g = run.trace(i)
+        assert np.array_equal(t_g if kind == 1 else t_g[:, :2], t_o if kind == 1 else t_o[:, :2]), i
+    assert r["iterations"] == r_o.total_iterations
+    assert r["another_iteration_required"] == bool(r_o.another_iteration_required)
+    tol = 2e-5 * np.abs(dirty).max()
+    assert np.abs(run.residual().reshape(h, w) - res_o[0]).max() <= tol
+    assert np.abs(run.model().reshape(h, w) - mod_o[0]).max() <= tol
