@@ -353,16 +353,20 @@ int rdl_box(rdl_session* s, float* d_dst, uint32_t dst_w, uint32_t dst_x,
             uint32_t src_y, uint32_t w, uint32_t h, const uint8_t* d_mask, int op);
 
 /* -------------------------------------------------- IUWT (à-trous) */
-/* IuwtDecomposition::DecomposeMt / Recompose
- * (cpp/algorithms/iuwt/iuwt_decomposition.cc:9-237, .h:121-261).
- * d_coeffs: n_scales+1 planes (detail scales then the residual approx).
- * d_scratch: 2 planes. */
-int rdl_iuwt_decompose(rdl_session* s, const float* d_input, uint32_t width,
-                       uint32_t height, uint32_t n_scales, float* d_coeffs,
-                       float* d_scratch, int include_residual);
+/* IuwtDecomposition::DecomposeMt (cpp/algorithms/iuwt/iuwt_decomposition.cc:
+ * 9-54): d_coeffs receives n_scales detail planes and, as plane n_scales, the
+ * approximation (zeroed unless include_largest). d_scratch is one plane; it
+ * may be d_input itself, which reproduces the reference's Decompose(x, x, ..)
+ * calls (iuwt_deconvolution_algorithm.cc:342, 385, 686, 785): the input is
+ * overwritten and the first row pass runs in place. Bit-exact with the
+ * reference build's tap order and FMA contraction. */
+int rdl_iuwt_decompose(rdl_session* s, float* d_input, float* d_scratch,
+                       uint32_t width, uint32_t height, uint32_t n_scales,
+                       float* d_coeffs, int include_largest);
+/* IuwtDecomposition::Recompose (iuwt_decomposition.h:121-146). */
 int rdl_iuwt_recompose(rdl_session* s, const float* d_coeffs, uint32_t width,
-                       uint32_t height, uint32_t n_scales, float* d_out,
-                       float* d_scratch, int include_residual);
+                       uint32_t height, uint32_t n_scales, int include_largest,
+                       float* d_out);
 
 /* -------------------------------------------- multi-GPU (RCCL over xGMI) */
 /* Size of an RCCL unique id blob; rank 0 creates it and the host side

@@ -10,6 +10,7 @@
 #include "fft.h"
 #include "oracle.h"
 #include "tiling.h"
+#include "iuwt.h"
 
 using namespace oracle;
 
@@ -256,6 +257,32 @@ struct OrcParallel {
   double major_loop_gain_unused = 0.0;
   std::vector<TiledAlgorithm> algorithms;
 };
+
+// IUWT: coeffs (n_scales + 1) planes; aliased != 0 runs Decompose(x, x, ..)
+// with input as the scratch (input is overwritten, like the reference).
+int orc_iuwt_decompose(float* input, uint64_t w, uint64_t h, uint64_t n_scales,
+                       int aliased, int include_largest, float* coeffs) {
+  try {
+    std::vector<float> scratch(aliased ? 0 : w * h);
+    std::vector<std::vector<float>> c;
+    IuwtDecompose(input, aliased ? input : scratch.data(), w, h, n_scales, c,
+                  include_largest != 0);
+    for (size_t s = 0; s != c.size(); ++s)
+      if (!c[s].empty()) std::copy(c[s].begin(), c[s].end(), coeffs + s * w * h);
+    return 0;
+  } catch (std::exception& e) {
+    g_error = e.what();
+    return 1;
+  }
+}
+
+void orc_iuwt_recompose(const float* coeffs, uint64_t w, uint64_t h,
+                        uint64_t n_scales, int include_largest, float* out) {
+  std::vector<std::vector<float>> c(n_scales + 1);
+  for (size_t s = 0; s <= n_scales; ++s)
+    if (s < n_scales || include_largest) c[s].assign(coeffs + s * w * h, coeffs + (s + 1) * w * h);
+  IuwtRecompose(c, w, h, n_scales, include_largest != 0, out);
+}
 
 // MakeSubImages alone (no user mask): boxes 4 x u32 per subimage, labels
 // W*H u16 (subimage index + 1 in its boundary mask).

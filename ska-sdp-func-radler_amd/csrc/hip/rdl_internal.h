@@ -71,7 +71,8 @@ struct rdl_session {
   bool poison = false;
   bool trace_subminor = false;    // RDL_TRACE_SUBMINOR=1: per-launch stats            // RDL_POISON=1: NaN-fill fresh allocations
   rdl::Scratch kernel;           // host-provided kernels (H2D destination)
-  rdl::Scratch loop_state;       // Högbom loop state / partials / trace
+  rdl::Scratch loop_state;
+  rdl::Scratch iuwt;             // IUWT i0 / recompose accumulator plane       // Högbom loop state / partials / trace
   void* comm = nullptr;          // ncclComm_t when initialised
 
   hipEvent_t GetEvent();

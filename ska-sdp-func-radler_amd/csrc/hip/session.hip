@@ -116,6 +116,7 @@ int rdl_session_destroy(rdl_session* s) {
   if (s->radix.ptr) (void)hipFree(s->radix.ptr);
   if (s->kernel.ptr) (void)hipFree(s->kernel.ptr);
   if (s->loop_state.ptr) (void)hipFree(s->loop_state.ptr);
+  if (s->iuwt.ptr) (void)hipFree(s->iuwt.ptr);
   if (s->d_small) (void)hipFree(s->d_small);
   if (s->h_small) (void)hipHostFree(s->h_small);
   if (s->comm) rdl_comm_destroy(s);

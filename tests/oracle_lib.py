@@ -213,6 +213,31 @@ class OracleAlgorithm:
             pass
 
 
+def iuwt_decompose(oracle, image, n_scales, aliased=False, include_largest=True):
+    """oracle IUWT DecomposeMt: (coeffs [n_scales + 1, h, w], input after the
+    call — overwritten when aliased, as in Decompose(x, x, ..))."""
+    img = np.ascontiguousarray(image, np.float32).copy()
+    h, w = img.shape
+    coeffs = np.zeros((n_scales + 1, h, w), np.float32)
+    L = oracle.lib
+    L.orc_iuwt_decompose.argtypes = [f32p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int,
+                                     C.c_int, f32p]
+    if L.orc_iuwt_decompose(img, w, h, n_scales, int(aliased), int(include_largest),
+                            coeffs) != 0:
+        raise RuntimeError(L.orc_last_error().decode())
+    return coeffs, img
+
+
+def iuwt_recompose(oracle, coeffs, n_scales, include_largest=True):
+    coeffs = np.ascontiguousarray(coeffs, np.float32)
+    _, h, w = coeffs.shape
+    out = np.zeros((h, w), np.float32)
+    L = oracle.lib
+    L.orc_iuwt_recompose.argtypes = [f32p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, f32p]
+    L.orc_iuwt_recompose(coeffs, w, h, n_scales, int(include_largest), out)
+    return out
+
+
 def make_subimages(oracle, image, grid_w, grid_h):
     """oracle MakeSubImages: (boxes [n, 4] x,y,w,h; labels [h, w])."""
     image = np.ascontiguousarray(image, np.float32)
