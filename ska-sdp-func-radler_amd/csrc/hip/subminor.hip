@@ -556,7 +556,9 @@ __device__ __forceinline__ uint64_t LoadGranule(uint64_t* g) {
   return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int NI, int ITEMS>
+// FAST: one image whose integration is the identity (ImageSet copy fast path,
+// cpp/image_set.cc:425-430): the integrated value is the residual itself.
+template <int NI, int ITEMS, bool FAST>
 __global__ __launch_bounds__(kRegThreads) void SubminorLoopReg(LoopArgs a) {
   constexpr int REC = 3 + NI;  // granules per record: key hi, key lo, pos, r[NI]
   __shared__ RegSlot<NI> slots[2][kRegWaves];
@@ -639,7 +641,7 @@ __global__ __launch_bounds__(kRegThreads) void SubminorLoopReg(LoopArgs a) {
     for (int i = 0; i < ITEMS; ++i) {
       const uint32_t j = tid + uint32_t(i) * kRegThreads;
       if (j < cnt) {
-        const float integ = IntegratePixel(a.integ, [&](uint32_t kk) {
+        const float integ = FAST ? R[i][0] : IntegratePixel(a.integ, [&](uint32_t kk) {
           float r = R[i][0];
 #pragma unroll
           for (int q = 1; q < NI; ++q) r = (uint32_t(q) == kk) ? R[i][q] : r;
@@ -682,14 +684,28 @@ __global__ __launch_bounds__(kRegThreads) void SubminorLoopReg(LoopArgs a) {
     RDL_PHASE(3)
     // ---- block winner: every wave reduces the slots (ties -> lowest wave,
     // which only matters for the all-zero case)
-    const uint64_t sk = lane < kRegWaves ? slots[par][lane].key : 0ull;
+    // lanes 0..7 read a whole slot each (one LDS round trip); the winner's
+    // payload then comes from its lane by readlane
+    uint64_t sk = 0ull;
+    uint32_t spos = 0;
+    float sr[NI];
+#pragma unroll
+    for (int k = 0; k < NI; ++k) sr[k] = 0.0f;
+    if (lane < kRegWaves) {
+      const RegSlot<NI>& sl = slots[par][lane];
+      sk = sl.key;
+      spos = sl.pos;
+#pragma unroll
+      for (int k = 0; k < NI; ++k) sr[k] = sl.r[k];
+    }
     const uint64_t bkey = Max8U64(sk);
-    const uint32_t bw = bkey != 0 ? uint32_t(FirstLane(sk == bkey && lane < kRegWaves)) : 0u;
+    const int bw = bkey != 0 ? FirstLane(sk == bkey && lane < kRegWaves) : 0;
     uint64_t gkey = bkey;
-    uint32_t wpos = slots[par][bw].pos;
+    uint32_t wpos = uint32_t(__builtin_amdgcn_readlane(int(spos), bw));
     float wr[NI];
 #pragma unroll
-    for (int k = 0; k < NI; ++k) wr[k] = slots[par][bw].r[k];
+    for (int k = 0; k < NI; ++k)
+      wr[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sr[k]), bw));
 
     if (a.n_blocks > 1) {
       ++epoch;  // 1, 2, ... (never 0: granules are zeroed per launch)
@@ -779,7 +795,7 @@ __global__ __launch_bounds__(kRegThreads) void SubminorLoopReg(LoopArgs a) {
     const uint64_t winner_p = (gkey == 0 || gkey == ~0ull)
                                   ? 0ull
                                   : uint64_t(0xffffffffu - uint32_t(gkey));
-    m = IntegratePixel(a.integ, [&](uint32_t kk) {
+    m = FAST ? wr[0] : IntegratePixel(a.integ, [&](uint32_t kk) {
       float r = wr[0];
 #pragma unroll
       for (int q = 1; q < NI; ++q) r = (uint32_t(q) == kk) ? wr[q] : r;
@@ -847,7 +863,8 @@ __global__ __launch_bounds__(kRegThreads) void SubminorLoopReg(LoopArgs a) {
 
 template <int NI, int ITEMS>
 int LaunchReg(const LoopArgs& a, hipStream_t stream) {
-  auto kernel = SubminorLoopReg<NI, ITEMS>;
+  auto kernel = (NI == 1 && a.integ.copy_fast_path) ? SubminorLoopReg<NI, ITEMS, NI == 1>
+                                                    : SubminorLoopReg<NI, ITEMS, false>;
   if (a.n_blocks > 1) {
     void* args[] = {const_cast<LoopArgs*>(&a)};
     RDL_HIP_CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(kernel),
