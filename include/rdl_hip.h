@@ -47,6 +47,16 @@ int rdl_session_destroy(rdl_session* s);
 int rdl_session_sync(rdl_session* s);
 /* hipStream_t of the session, for callers that record events on it. */
 void* rdl_session_stream(rdl_session* s);
+/* Make the session's device current for the calling host thread (worker
+ * threads of the subimage pool call this once before allocating). */
+int rdl_session_bind(rdl_session* s);
+/* `n_sharing` sessions run concurrently on this session's device: grids of
+ * the workgroup-cooperative kernels (the multi-workgroup sub-minor loop) are
+ * capped to n_cus / n_sharing so every concurrent loop stays co-resident.
+ * The subimage pool of ParallelDeconvolution sets this
+ * (cpp/algorithms/parallel_deconvolution.cc:583-616 runs subimages on
+ * settings.parallel.max_threads threads). */
+int rdl_session_set_concurrency(rdl_session* s, uint32_t n_sharing);
 
 int rdl_malloc(rdl_session* s, size_t bytes, void** d_out);
 int rdl_free(rdl_session* s, void* d_ptr);
@@ -54,6 +64,10 @@ int rdl_memcpy_h2d(rdl_session* s, void* d_dst, const void* h_src, size_t bytes)
 int rdl_memcpy_d2h(rdl_session* s, void* h_dst, const void* d_src, size_t bytes);
 int rdl_memcpy_d2d(rdl_session* s, void* d_dst, const void* d_src, size_t bytes);
 int rdl_memset_zero(rdl_session* s, void* d_dst, size_t bytes);
+/* Device-to-device copy between GPUs (xGMI peer copy when the devices
+ * differ), ordered on the session's stream. */
+int rdl_memcpy_peer(rdl_session* s, void* d_dst, int dst_device,
+                    const void* d_src, int src_device, size_t bytes);
 
 /* Per-kernel device timing (HIP events around every launch of a kernel
  * family on the session stream). Used by bench.py's roofline. */

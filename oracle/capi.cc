@@ -255,6 +255,7 @@ struct orc_parallel_result {
 struct OrcParallel {
   size_t grid_w, grid_h;
   double major_loop_gain_unused = 0.0;
+  bool snapshot = false;
   std::vector<TiledAlgorithm> algorithms;
 };
 
@@ -324,6 +325,12 @@ void* orc_parallel_create(int kind, const orc_algo_settings* a, uint64_t grid_w,
 
 void orc_parallel_destroy(void* h) { delete static_cast<OrcParallel*>(h); }
 
+// 1: subimages of a pass all trim the residual as it was at the start of the
+// pass (the product's concurrent subimage pool, max_threads > 1)
+void orc_parallel_set_snapshot(void* h, int snapshot) {
+  static_cast<OrcParallel*>(h)->snapshot = snapshot != 0;
+}
+
 // sub_boxes: 4 x u32 (x, y, w, h) per subimage; labels (may be NULL): W*H
 // u16, subimage index + 1 where the pixel is in that subimage's boundary
 // mask; trace: 4 x u32 (subimage, x, y, scale) per component of the run pass.
@@ -346,7 +353,7 @@ int orc_parallel_execute(void* h, const orc_set_desc* d, float* residual,
     ParallelResult r = ParallelRun(p->algorithms, p->grid_w, p->grid_h, desc, res,
                                    mod, psf_ptrs, major_loop_gain, limit,
                                    reinterpret_cast<const bool*>(user_mask), &subs,
-                                   &traces);
+                                   &traces, p->snapshot);
     out->another_iteration_required = r.another_iteration_required;
     out->n_subimages = int32_t(subs.size());
     out->start_peak = r.start_peak;

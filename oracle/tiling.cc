@@ -253,7 +253,14 @@ ParallelResult ParallelRun(std::vector<TiledAlgorithm>& algorithms,
                            const std::vector<const float*>& psfs,
                            double major_loop_gain, double divergence_limit,
                            const bool* user_mask, std::vector<SubImage>* out_subs,
-                           std::vector<std::vector<Component>>* traces) {
+                           std::vector<std::vector<Component>>* traces,
+                           bool snapshot) {
+  // snapshot == false: subimages run one after another, each trimming the
+  // residual left by the ones before (the reference with one thread).
+  // snapshot == true: every subimage of a pass trims the residual as it was
+  // when the pass started (the reference's multi-threaded run when all
+  // threads trim before the first copy-back, parallel_deconvolution.cc:
+  // 583-616, 300-357 and 458-484).
   const size_t width = data.width, height = data.height;
   const size_t n_img = data.Size();
   std::vector<float> integrated(width * height);
@@ -265,13 +272,16 @@ ParallelResult ParallelRun(std::vector<TiledAlgorithm>& algorithms,
   std::vector<std::vector<float>> result_model(n_img,
                                                std::vector<float>(width * height, 0.0f));
 
+  std::vector<std::vector<float>> snapshot_store;
+  std::vector<const float*> source(data.images.begin(), data.images.end());
+
   // RunSubImage (parallel_deconvolution.cc:300-484)
   auto run = [&](SubImage& s, double major_threshold, bool find_peak_only) {
     TiledAlgorithm& alg = algorithms[s.index];
     const size_t sw = s.width, sh = s.height, n = sw * sh;
     std::vector<float> sub_data(n_img * n), sub_model(n_img * n);
     for (size_t i = 0; i != n_img; ++i) {
-      CopyBox(&sub_data[i * n], s.x, s.y, sw, sh, data.images[i], width);
+      CopyBox(&sub_data[i * n], s.x, s.y, sw, sh, source[i], width);
       CopyBox(&sub_model[i * n], s.x, s.y, sw, sh, model.images[i], width);
       for (size_t p = 0; p != n; ++p)
         if (!s.boundary_mask[p]) sub_model[i * n + p] = 0.0f;  // TrimMasked
@@ -335,6 +345,13 @@ ParallelResult ParallelRun(std::vector<TiledAlgorithm>& algorithms,
   for (const SubImage& s : subs)
     if (s.peak > start_peak) start_peak = s.peak;
   const double threshold = start_peak * (1.0 - major_loop_gain);
+  if (snapshot) {
+    snapshot_store.reserve(n_img);
+    for (size_t i = 0; i != n_img; ++i) {
+      snapshot_store.emplace_back(data.images[i], data.images[i] + width * height);
+      source[i] = snapshot_store.back().data();
+    }
+  }
   for (SubImage& s : subs) run(s, threshold, false);
   for (size_t i = 0; i != n_img; ++i)
     std::copy(result_model[i].begin(), result_model[i].end(), model.images[i]);

@@ -45,6 +45,7 @@ ParallelResult ParallelRun(std::vector<TiledAlgorithm>& algorithms,
                            const std::vector<const float*>& psfs,
                            double major_loop_gain, double divergence_limit,
                            const bool* user_mask, std::vector<SubImage>* out_subs,
-                           std::vector<std::vector<Component>>* traces);
+                           std::vector<std::vector<Component>>* traces,
+                           bool snapshot = false);
 
 }  // namespace oracle

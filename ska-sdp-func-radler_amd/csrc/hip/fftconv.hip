@@ -193,6 +193,10 @@ static int CreateFft(rdl_session* s, uint32_t width, uint32_t height, bool f64,
   RDL_ARG_CHECK(s && out, "NULL argument");
   RDL_ARG_CHECK(width >= 2 && height >= 1, "bad FFT size");
   std::call_once(g_rocfft_once, [] { rocfft_setup(); });
+  // plans are created from the subimage workers' threads; keep rocFFT's
+  // plan cache single-threaded
+  static std::mutex plan_mutex;
+  std::lock_guard<std::mutex> lock(plan_mutex);
   RDL_HIP_CHECK(hipSetDevice(s->device));
   auto f = std::make_unique<rdl_fft>();
   f->s = s;

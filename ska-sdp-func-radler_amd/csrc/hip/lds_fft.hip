@@ -584,13 +584,9 @@ int LaunchRowsForward(rdl_conv* c, const float* in, uint32_t in_w, uint32_t in_h
   const uint32_t grid = (n_pairs + a.count - 1) / a.count;
   const size_t lds = size_t(a.count) * c->width * sizeof(rdl::Cx<T>);
   auto k = rdl::RowsForward<T>;
-  static bool attr_set = false;  // once per instantiation (the call can stall)
-  if (!attr_set) {
-    RDL_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      int(rdl::kFftLdsBytes)));
-    attr_set = true;
-  }
+  static std::atomic<uint64_t> attr_done{0};  // per instantiation and device
+  RDL_TRY(rdl::SetMaxLdsOnce(reinterpret_cast<const void*>(k), int(rdl::kFftLdsBytes),
+                             c->s->device, attr_done));
   k<<<grid, rdl::kFftThreads, lds, c->s->stream>>>(a, in,
                                                    static_cast<rdl::Cx<T>*>(spec));
   RDL_HIP_CHECK(hipGetLastError());
@@ -613,13 +609,9 @@ int LaunchRowsInverse(rdl_conv* c, const void* spec, float* out, uint32_t out_w,
   const uint32_t grid = (n_pairs + a.count - 1) / a.count;
   const size_t lds = size_t(a.count) * c->width * sizeof(rdl::Cx<T>);
   auto k = rdl::RowsInverse<T>;
-  static bool attr_set = false;  // once per instantiation (the call can stall)
-  if (!attr_set) {
-    RDL_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      int(rdl::kFftLdsBytes)));
-    attr_set = true;
-  }
+  static std::atomic<uint64_t> attr_done{0};  // per instantiation and device
+  RDL_TRY(rdl::SetMaxLdsOnce(reinterpret_cast<const void*>(k), int(rdl::kFftLdsBytes),
+                             c->s->device, attr_done));
   k<<<grid, rdl::kFftThreads, lds, c->s->stream>>>(
       a, static_cast<const rdl::Cx<T>*>(spec), out, subtract);
   RDL_HIP_CHECK(hipGetLastError());
@@ -641,13 +633,9 @@ int LaunchColumns(rdl_conv* c, const void* in, void* out, const void* kern,
   const uint32_t grid = 8 * a.tiles_per_xcd;
   const size_t lds = size_t(a.count) * c->height * sizeof(rdl::Cx<T>);
   auto k = rdl::Columns<T>;
-  static bool attr_set = false;  // once per instantiation (the call can stall)
-  if (!attr_set) {
-    RDL_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      int(rdl::kFftLdsBytes)));
-    attr_set = true;
-  }
+  static std::atomic<uint64_t> attr_done{0};  // per instantiation and device
+  RDL_TRY(rdl::SetMaxLdsOnce(reinterpret_cast<const void*>(k), int(rdl::kFftLdsBytes),
+                             c->s->device, attr_done));
   k<<<grid, rdl::kFftThreads, lds, c->s->stream>>>(
       a, static_cast<const rdl::Cx<T>*>(in), static_cast<rdl::Cx<T>*>(out),
       static_cast<const rdl::Cx<T>*>(kern));

@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <map>
 #include <memory>
@@ -60,6 +61,7 @@ struct rdl_session {
   int device = 0;
   hipStream_t stream = nullptr;
   int n_cus = 256;
+  uint32_t coop_limit = 0;       // cap on cooperative grids (0: n_cus)
   bool timing = false;
   std::map<std::string, rdl::TimingEntry> timings;
   std::vector<hipEvent_t> event_pool;
@@ -218,4 +220,20 @@ __device__ __forceinline__ uint64_t BlockMaxU64(uint64_t v, uint64_t* lds) {
 
 inline unsigned DivUp(size_t a, size_t b) { return unsigned((a + b - 1) / b); }
 
+}  // namespace rdl
+
+namespace rdl {
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (call site,
+// device): the call can stall, and the attribute is per device, so a pool
+// of workers on several GPUs needs it on each. `done` is the call site's
+// device bitmask.
+inline int SetMaxLdsOnce(const void* fn, int bytes, int device,
+                         std::atomic<uint64_t>& done) {
+  const uint64_t bit = uint64_t(1) << (device & 63);
+  if (done.load(std::memory_order_acquire) & bit) return RDL_OK;
+  RDL_HIP_CHECK(
+      hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  done.fetch_or(bit, std::memory_order_acq_rel);
+  return RDL_OK;
+}
 }  // namespace rdl

@@ -1,4 +1,5 @@
 // Session / runtime part of the C-ABI (rdl_hip.h "runtime" section).
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -84,6 +85,14 @@ int rdl_session_create(int device, rdl_session** out) {
   int n = 0;
   RDL_HIP_CHECK(hipGetDeviceCount(&n));
   RDL_ARG_CHECK(device >= 0 && device < n, "invalid device index");
+  // leave the caller's current device as it was (a pool creates sessions
+  // for other GPUs from the main thread)
+  int prev = 0;
+  RDL_HIP_CHECK(hipGetDevice(&prev));
+  struct Restore {
+    int d;
+    ~Restore() { (void)hipSetDevice(d); }
+  } restore{prev};
   RDL_HIP_CHECK(hipSetDevice(device));
   auto s = std::make_unique<rdl_session>();
   s->device = device;
@@ -133,12 +142,29 @@ int rdl_session_sync(rdl_session* s) {
 
 void* rdl_session_stream(rdl_session* s) { return s ? s->stream : nullptr; }
 
+int rdl_session_bind(rdl_session* s) {
+  RDL_ARG_CHECK(s, "NULL session");
+  RDL_HIP_CHECK(hipSetDevice(s->device));
+  return RDL_OK;
+}
+
+int rdl_session_set_concurrency(rdl_session* s, uint32_t n_sharing) {
+  RDL_ARG_CHECK(s, "NULL session");
+  s->coop_limit =
+      n_sharing <= 1 ? 0 : std::max<uint32_t>(1, uint32_t(s->n_cus) / n_sharing);
+  return RDL_OK;
+}
+
 int rdl_malloc(rdl_session* s, size_t bytes, void** d_out) {
   RDL_ARG_CHECK(s && d_out, "NULL argument");
-  RDL_HIP_CHECK(hipSetDevice(s->device));
   *d_out = nullptr;
   if (bytes == 0) return RDL_OK;
-  RDL_HIP_CHECK(hipMalloc(d_out, bytes));
+  int prev = 0;
+  RDL_HIP_CHECK(hipGetDevice(&prev));
+  if (prev != s->device) RDL_HIP_CHECK(hipSetDevice(s->device));
+  const hipError_t e = hipMalloc(d_out, bytes);
+  if (prev != s->device) (void)hipSetDevice(prev);
+  RDL_HIP_CHECK(e);
   if (s->poison) {
     RDL_HIP_CHECK(hipMemsetAsync(*d_out, 0xff, bytes, s->stream));
     RDL_HIP_CHECK(hipStreamSynchronize(s->stream));
@@ -180,6 +206,19 @@ int rdl_memcpy_d2d(rdl_session* s, void* d_dst, const void* d_src,
   if (bytes == 0) return RDL_OK;
   RDL_HIP_CHECK(hipMemcpyAsync(d_dst, d_src, bytes, hipMemcpyDeviceToDevice,
                                s->stream));
+  return RDL_OK;
+}
+
+int rdl_memcpy_peer(rdl_session* s, void* d_dst, int dst_device,
+                    const void* d_src, int src_device, size_t bytes) {
+  RDL_ARG_CHECK(s, "NULL session");
+  if (bytes == 0) return RDL_OK;
+  if (dst_device == src_device)
+    RDL_HIP_CHECK(hipMemcpyAsync(d_dst, d_src, bytes, hipMemcpyDeviceToDevice,
+                                 s->stream));
+  else
+    RDL_HIP_CHECK(hipMemcpyPeerAsync(d_dst, dst_device, d_src, src_device, bytes,
+                                     s->stream));
   return RDL_OK;
 }
 

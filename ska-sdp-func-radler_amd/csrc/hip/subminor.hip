@@ -1024,7 +1024,8 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   RDL_HIP_CHECK(hipGetLastError());
 
   // ---------------- partition and loop
-  const uint32_t max_blocks = std::max(1, std::min(s->n_cus, 256));
+  uint32_t max_blocks = uint32_t(std::max(1, std::min(s->n_cus, 256)));
+  if (s->coop_limit) max_blocks = std::min(max_blocks, s->coop_limit);
   // register kernel: N_img <= 8, <= 4096 pixels per workgroup
   uint32_t ni_t = ni <= 1 ? 1 : ni <= 2 ? 2 : ni <= 4 ? 4 : 8;
   uint32_t g = 1;
@@ -1035,7 +1036,7 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
     if (n_sel > std::min<uint64_t>(reg_cap, h->single_max)) {
       const uint64_t target = std::max<uint32_t>(h->target_per_block, 512);
       g = uint32_t(std::min<uint64_t>(max_blocks, (n_sel + target - 1) / target));
-      g = std::max<uint32_t>(g, 2);
+      g = std::max<uint32_t>(g, std::min<uint32_t>(2, max_blocks));
       per = (n_sel + g - 1) / g;
       use_reg = per <= reg_cap;
     }

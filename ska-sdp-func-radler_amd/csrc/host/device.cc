@@ -180,6 +180,15 @@ rdl_subminor* Session::SharedSubminor() {
 }
 
 void Session::Sync() { Check(rdl_session_sync(s_), "rdl_session_sync"); }
+void Session::Bind() { Check(rdl_session_bind(s_), "rdl_session_bind"); }
+void Session::SetConcurrency(size_t n) {
+  Check(rdl_session_set_concurrency(s_, uint32_t(n)), "rdl_session_set_concurrency");
+}
+void Session::Peer(void* d, int dst_device, const void* src, int src_device,
+                   size_t bytes) {
+  Check(rdl_memcpy_peer(s_, d, dst_device, src, src_device, bytes),
+        "rdl_memcpy_peer");
+}
 
 void Session::H2D(void* d, const void* h, size_t bytes) {
   Check(rdl_memcpy_h2d(s_, d, h, bytes), "rdl_memcpy_h2d");

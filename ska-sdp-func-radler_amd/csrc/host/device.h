@@ -96,6 +96,12 @@ class Session {
   int Device() const { return device_; }
   Fft& GetFft(size_t width, size_t height, bool f64 = false);
   void Sync();
+  /// Make this session's device current for the calling thread.
+  void Bind();
+  /// `n` sessions share the device concurrently (caps cooperative grids).
+  void SetConcurrency(size_t n);
+  /// Copy between devices (or within one) on this session's stream.
+  void Peer(void* d, int dst_device, const void* s, int src_device, size_t bytes);
   void H2D(void* d, const void* h, size_t bytes);
   void D2H(void* h, const void* d, size_t bytes);
   void D2D(void* d, const void* s, size_t bytes);

@@ -35,6 +35,11 @@ ImageSet::ImageSet(const ImageSet& like, size_t width, size_t height)
     : ImageSet(like.table_, like.square_joined_channels_,
                like.linked_polarizations_, width, height, *like.session_) {}
 
+ImageSet::ImageSet(const ImageSet& like, size_t width, size_t height,
+                   gpu::Session& session)
+    : ImageSet(like.table_, like.square_joined_channels_,
+               like.linked_polarizations_, width, height, session) {}
+
 void ImageSet::InitializePolFactor() {  // image_set.h:298-324
   const WorkTable::Group& first = table_.OriginalGroups().front();
   std::set<aocommon::PolarizationEnum> pols;

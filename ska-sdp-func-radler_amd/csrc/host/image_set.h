@@ -22,6 +22,10 @@ class ImageSet {
            size_t width, size_t height, gpu::Session& session);
   /// Same configuration, different image size (image_set.cc:448-450).
   ImageSet(const ImageSet& like, size_t width, size_t height);
+  /// Same configuration, planes allocated on another session (a subimage
+  /// worker's device/stream).
+  ImageSet(const ImageSet& like, size_t width, size_t height,
+           gpu::Session& session);
   ImageSet(const ImageSet&) = delete;
   ImageSet& operator=(const ImageSet&) = delete;
 

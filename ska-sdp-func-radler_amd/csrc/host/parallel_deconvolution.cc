@@ -3,9 +3,13 @@
 #include "parallel_deconvolution.h"
 
 #include <algorithm>
-#include <stdexcept>
-
 #include <cmath>
+#include <cstdlib>
+#include <exception>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <thread>
 
 #include "dijkstra_splitter.h"
 #include "logger.h"
@@ -191,50 +195,74 @@ std::vector<SubImage> MakeSubImages(const std::vector<float>& image, size_t widt
   return subs;
 }
 
-void ParallelDeconvolution::RunSubImage(SubImage& sub, ImageSet& data_image,
-                                        const ImageSet& model_image,
-                                        ImageSet& result_model,
-                                        const gpu::Planes& psfs,
-                                        double major_iteration_threshold,
-                                        bool find_peak_only) {
-  // parallel_deconvolution.cc:300-484 on the device: the subimage's planes
-  // are box copies of the full image set's planes
-  gpu::Session& s = data_image.Session();
-  const size_t W = data_image.Width(), H = data_image.Height();
-  const size_t sw = sub.width, sh = sub.height, n = sw * sh;
-  const uint32_t uw = uint32_t(sw), uh = uint32_t(sh);
-  gpu::Buffer boundary(s, n);
-  {
-    std::vector<uint8_t> b(n);
-    for (size_t i = 0; i != n; ++i) b[i] = sub.boundary_mask[i] ? 1 : 0;
-    s.H2D(boundary.Ptr(), b.data(), n);
-  }
-  const uint8_t* d_boundary = static_cast<const uint8_t*>(boundary.Ptr());
-  ImageSet sub_data(data_image, sw, sh);
-  ImageSet sub_model(model_image, sw, sh);
+namespace {
+
+std::vector<uint8_t> MaskBytes(const std::vector<bool>& mask) {
+  std::vector<uint8_t> b(mask.size());
+  for (size_t i = 0; i != mask.size(); ++i) b[i] = mask[i] ? 1 : 0;
+  return b;
+}
+
+// ImageSet::Trim / TrimMasked of the data and model planes and the centred
+// Image::Resize of the PSFs into contiguous subimage planes, as box copies
+// ordered on `ops` (parallel_deconvolution.cc:300-357)
+void TrimSubImage(gpu::Session& ops, const SubImage& sub, const ImageSet& data_image,
+                  const ImageSet& model_image, const gpu::Planes& psfs,
+                  float* d_data, float* d_model, float* d_psfs,
+                  const uint8_t* d_boundary) {
+  const size_t W = data_image.Width();
+  const uint32_t uw = uint32_t(sub.width), uh = uint32_t(sub.height);
+  const size_t n = sub.width * sub.height;
+  if (psfs.width < sub.width || psfs.height < sub.height)
+    throw std::runtime_error("PSF smaller than a subimage");
   for (size_t i = 0; i != data_image.Size(); ++i) {
-    gpu::Check(rdl_box(s.Handle(), sub_data.Data(i), uw, 0, 0, data_image.Data(i),
+    gpu::Check(rdl_box(ops.Handle(), d_data + i * n, uw, 0, 0, data_image.Data(i),
                        uint32_t(W), uint32_t(sub.x), uint32_t(sub.y), uw, uh,
                        nullptr, RDL_BOX_COPY),
                "rdl_box");  // ImageSet::Trim
-    gpu::Check(rdl_box(s.Handle(), sub_model.Data(i), uw, 0, 0, model_image.Data(i),
+    gpu::Check(rdl_box(ops.Handle(), d_model + i * n, uw, 0, 0, model_image.Data(i),
                        uint32_t(W), uint32_t(sub.x), uint32_t(sub.y), uw, uh,
                        d_boundary, RDL_BOX_COPY_ZERO),
                "rdl_box");  // ImageSet::TrimMasked
   }
-  ImageSet initial_model(sub_model, sw, sh);
-  initial_model.CopyFrom(sub_model);
-  // Image::Resize of the PSFs to the subimage: centred trim (PSFs are never
-  // smaller than a subimage here)
-  if (psfs.width < sw || psfs.height < sh)
-    throw std::runtime_error("PSF smaller than a subimage");
-  gpu::Planes sub_psfs = gpu::Planes::Make(s, sw, sh, psfs.count);
   for (size_t i = 0; i != psfs.count; ++i)
-    gpu::Check(rdl_box(s.Handle(), sub_psfs.Plane(i), uw, 0, 0, psfs.Plane(i),
-                       uint32_t(psfs.width), uint32_t((psfs.width - sw) / 2),
-                       uint32_t((psfs.height - sh) / 2), uw, uh, nullptr,
+    gpu::Check(rdl_box(ops.Handle(), d_psfs + i * n, uw, 0, 0, psfs.Plane(i),
+                       uint32_t(psfs.width), uint32_t((psfs.width - sub.width) / 2),
+                       uint32_t((psfs.height - sub.height) / 2), uw, uh, nullptr,
                        RDL_BOX_COPY),
                "rdl_box");
+}
+
+// ImageSet::CopyMasked of the residual (only when the subimage converged) and
+// ImageSet::AddSubImage of the model (parallel_deconvolution.cc:458-484)
+void MergeSubImage(gpu::Session& ops, const SubImage& sub, ImageSet& data_image,
+                   ImageSet& result_model, const float* d_data,
+                   const float* d_model, const uint8_t* d_boundary,
+                   bool converging) {
+  const size_t W = data_image.Width();
+  const uint32_t uw = uint32_t(sub.width), uh = uint32_t(sub.height);
+  const size_t n = sub.width * sub.height;
+  for (size_t i = 0; i != data_image.Size(); ++i) {
+    if (converging)
+      gpu::Check(rdl_box(ops.Handle(), data_image.Data(i), uint32_t(W),
+                         uint32_t(sub.x), uint32_t(sub.y), d_data + i * n, uw, 0, 0,
+                         uw, uh, d_boundary, RDL_BOX_COPY_MASKED),
+                 "rdl_box");
+    gpu::Check(rdl_box(ops.Handle(), result_model.Data(i), uint32_t(W),
+                       uint32_t(sub.x), uint32_t(sub.y), d_model + i * n, uw, 0, 0,
+                       uw, uh, nullptr, RDL_BOX_ADD),
+               "rdl_box");
+  }
+}
+
+}  // namespace
+
+bool ParallelDeconvolution::DeconvolveSubImage(SubImage& sub, ImageSet& sub_data,
+                                               ImageSet& sub_model,
+                                               const gpu::Planes& sub_psfs,
+                                               double major_iteration_threshold,
+                                               bool find_peak_only) {
+  // parallel_deconvolution.cc:363-456
   DeconvolutionAlgorithm& alg = *algorithms_[sub.index];
   std::vector<char> mask_copy(sub.mask.begin(), sub.mask.end());
   alg.SetCleanMask(reinterpret_cast<const bool*>(mask_copy.data()));
@@ -253,27 +281,224 @@ void ParallelDeconvolution::RunSubImage(SubImage& sub, ImageSet& data_image,
       (settings_.divergence_limit == 0.0 ||
        std::fabs(sub.peak) <= peak_at_start * settings_.divergence_limit) &&
       std::isfinite(sub.peak) && !result.is_diverging;
-  if (!converging && !find_peak_only) {
+  if (find_peak_only) {
+    alg.SetMaxIterations(max_n_iter);
+  } else if (!converging) {
     log::Warn() << "Peak of sub-image " << sub.index << " increased from "
                 << peak_at_start << " to " << sub.peak
                 << " and deconvolution probably diverged: resetting.\n";
     sub.reached_major_threshold = false;
   }
-  if (find_peak_only) {
-    alg.SetMaxIterations(max_n_iter);
-    return;
+  return converging;
+}
+
+void ParallelDeconvolution::RunSubImage(SubImage& sub, ImageSet& data_image,
+                                        const ImageSet& model_image,
+                                        ImageSet& result_model,
+                                        const gpu::Planes& psfs,
+                                        double major_iteration_threshold,
+                                        bool find_peak_only) {
+  // parallel_deconvolution.cc:300-484 on the device: the subimage's planes
+  // are box copies of the full image set's planes
+  gpu::Session& s = data_image.Session();
+  const size_t sw = sub.width, sh = sub.height, n = sw * sh;
+  gpu::Buffer boundary(s, n);
+  s.H2D(boundary.Ptr(), MaskBytes(sub.boundary_mask).data(), n);
+  const uint8_t* d_boundary = static_cast<const uint8_t*>(boundary.Ptr());
+  ImageSet sub_data(data_image, sw, sh);
+  ImageSet sub_model(model_image, sw, sh);
+  gpu::Planes sub_psfs = gpu::Planes::Make(s, sw, sh, psfs.count);
+  TrimSubImage(s, sub, data_image, model_image, psfs, sub_data.Base(),
+               sub_model.Base(), sub_psfs.Base(), d_boundary);
+  ImageSet initial_model(sub_model, sw, sh);
+  initial_model.CopyFrom(sub_model);
+  const bool converging = DeconvolveSubImage(
+      sub, sub_data, sub_model, sub_psfs, major_iteration_threshold, find_peak_only);
+  if (find_peak_only) return;
+  MergeSubImage(s, sub, data_image, result_model, sub_data.Base(),
+                converging ? sub_model.Base() : initial_model.Base(), d_boundary,
+                converging);
+  s.Sync();
+}
+
+std::vector<int> ParallelDeconvolution::PoolDevices(int main_device) {
+  // RADLER_DEVICES="0,1,2,3" spreads the subimage workers over those GPUs;
+  // by default they share the device of the image set
+  std::vector<int> devices;
+  if (const char* env = std::getenv("RADLER_DEVICES")) {
+    int count = 0;
+    gpu::Check(rdl_device_count(&count), "rdl_device_count");
+    std::string list(env);
+    size_t pos = 0;
+    while (pos < list.size()) {
+      size_t end = list.find(',', pos);
+      if (end == std::string::npos) end = list.size();
+      const std::string item = list.substr(pos, end - pos);
+      if (!item.empty()) {
+        const int d = std::stoi(item);
+        if (d < 0 || d >= count)
+          throw std::runtime_error("RADLER_DEVICES names device " + item +
+                                   ", which does not exist");
+        devices.push_back(d);
+      }
+      pos = end + 1;
+    }
   }
-  const ImageSet& model_out = converging ? sub_model : initial_model;
-  for (size_t i = 0; i != data_image.Size(); ++i) {
-    if (converging)  // ImageSet::CopyMasked
-      gpu::Check(rdl_box(s.Handle(), data_image.Data(i), uint32_t(W),
-                         uint32_t(sub.x), uint32_t(sub.y), sub_data.Data(i), uw, 0,
-                         0, uw, uh, d_boundary, RDL_BOX_COPY_MASKED),
-                 "rdl_box");
-    gpu::Check(rdl_box(s.Handle(), result_model.Data(i), uint32_t(W),
-                       uint32_t(sub.x), uint32_t(sub.y), model_out.Data(i), uw, 0, 0,
-                       uw, uh, nullptr, RDL_BOX_ADD),
-               "rdl_box");  // ImageSet::AddSubImage
+  if (devices.empty()) devices.push_back(main_device);
+  return devices;
+}
+
+void ParallelDeconvolution::EnsureWorkers(gpu::Session& main, size_t n) {
+  if (workers_.size() == n && worker_main_device_ == main.Device()) return;
+  if (!workers_.empty())
+    throw std::runtime_error(
+        "ParallelDeconvolution: the subimage worker pool cannot change between "
+        "major iterations");
+  const std::vector<int> devices = PoolDevices(main.Device());
+  std::map<int, size_t> per_device;
+  for (size_t w = 0; w != n; ++w) {
+    const int d = devices[w % devices.size()];
+    workers_.push_back(std::make_unique<gpu::Session>(d));
+    ++per_device[d];
+  }
+  for (auto& w : workers_) w->SetConcurrency(per_device[w->Device()]);
+  worker_main_device_ = main.Device();
+  main.Bind();
+}
+
+void ParallelDeconvolution::RunSubImagesConcurrently(
+    ImageSet& data_image, const ImageSet& model_image, ImageSet& result_model,
+    const std::vector<gpu::Planes>& psf_images,
+    const std::vector<size_t>& psf_indices, double major_iteration_threshold,
+    bool find_peak_only) {
+  // The reference runs RunSubImage on settings.parallel.max_threads threads
+  // (parallel_deconvolution.cc:583-616), each trimming from the shared
+  // residual and copying back under a mutex. Here every subimage trims from
+  // the residual as it was when the pass started and the copy-backs are
+  // applied afterwards in subimage order: the schedule the reference takes
+  // when all its threads trim before the first one finishes, made
+  // deterministic. Boundary masks are disjoint and the model additions
+  // outside them add zeros, so the merged result does not depend on the
+  // number of workers or devices.
+  gpu::Session& s = data_image.Session();
+  const int main_device = s.Device();
+  const size_t n_sub = subimages_.size(), W = workers_.size();
+  const size_t n_img = data_image.Size();
+  // RADLER_POOL_STAGING=1 routes same-device workers through the staging
+  // buffers and peer copies a worker on another GPU uses (exercised by the
+  // one-GPU tests)
+  const char* staging_env = std::getenv("RADLER_POOL_STAGING");
+  const bool force_staging = staging_env && staging_env[0] == '1';
+  struct Slot {
+    gpu::Session* ws = nullptr;
+    bool remote = false;
+    // main-device staging of a remote worker's planes (data | model | psfs)
+    std::unique_ptr<gpu::Buffer> stage;
+    std::unique_ptr<gpu::Buffer> boundary;  // on the main device
+    std::unique_ptr<ImageSet> data, model, initial;
+    gpu::Planes psfs;
+    bool converging = false;
+  };
+  std::vector<Slot> slots(n_sub);
+  for (size_t i = 0; i != n_sub; ++i) {
+    Slot& slot = slots[i];
+    const SubImage& sub = subimages_[i];
+    const size_t n = sub.width * sub.height;
+    const gpu::Planes& psfs = psf_images[psf_indices[i]];
+    slot.ws = workers_[i % W].get();
+    slot.remote = force_staging || slot.ws->Device() != main_device;
+    slot.boundary = std::make_unique<gpu::Buffer>(s, n);
+    s.H2D(slot.boundary->Ptr(), MaskBytes(sub.boundary_mask).data(), n);
+    if (slot.remote) {
+      slot.stage = std::make_unique<gpu::Buffer>(
+          s, (2 * n_img + psfs.count) * n * sizeof(float));
+      float* base = slot.stage->F();
+      TrimSubImage(s, sub, data_image, model_image, psfs, base, base + n_img * n,
+                   base + 2 * n_img * n,
+                   static_cast<const uint8_t*>(slot.boundary->Ptr()));
+    }
+  }
+  s.Sync();
+
+  std::vector<std::exception_ptr> errors(W);
+  auto work = [&](size_t w) {
+    try {
+      gpu::Session& ws = *workers_[w];
+      ws.Bind();
+      for (size_t i = w; i < n_sub; i += W) {
+        Slot& slot = slots[i];
+        SubImage& sub = subimages_[i];
+        const size_t sw = sub.width, sh = sub.height, n = sw * sh;
+        const gpu::Planes& psfs = psf_images[psf_indices[i]];
+        slot.data = std::make_unique<ImageSet>(data_image, sw, sh, ws);
+        slot.model = std::make_unique<ImageSet>(model_image, sw, sh, ws);
+        slot.psfs = gpu::Planes::Make(ws, sw, sh, psfs.count);
+        if (slot.remote) {
+          const float* base = slot.stage->F();
+          ws.Peer(slot.data->Base(), ws.Device(), base, main_device,
+                  n_img * n * sizeof(float));
+          ws.Peer(slot.model->Base(), ws.Device(), base + n_img * n, main_device,
+                  n_img * n * sizeof(float));
+          ws.Peer(slot.psfs.Base(), ws.Device(), base + 2 * n_img * n, main_device,
+                  psfs.count * n * sizeof(float));
+        } else {
+          TrimSubImage(ws, sub, data_image, model_image, psfs, slot.data->Base(),
+                       slot.model->Base(), slot.psfs.Base(),
+                       static_cast<const uint8_t*>(slot.boundary->Ptr()));
+        }
+        if (!find_peak_only) {
+          slot.initial = std::make_unique<ImageSet>(*slot.model, sw, sh);
+          slot.initial->CopyFrom(*slot.model);
+        }
+        slot.converging = DeconvolveSubImage(sub, *slot.data, *slot.model,
+                                             slot.psfs, major_iteration_threshold,
+                                             find_peak_only);
+        if (slot.remote && !find_peak_only) {
+          float* base = slot.stage->F();
+          const ImageSet& model_out = slot.converging ? *slot.model : *slot.initial;
+          ws.Peer(base, main_device, slot.data->Base(), ws.Device(),
+                  n_img * n * sizeof(float));
+          ws.Peer(base + n_img * n, main_device, model_out.Base(), ws.Device(),
+                  n_img * n * sizeof(float));
+        }
+        ws.Sync();
+        if (find_peak_only || slot.remote) {
+          slot.data.reset();
+          slot.model.reset();
+          slot.initial.reset();
+          slot.psfs = gpu::Planes();
+        }
+      }
+      ws.Sync();
+    } catch (...) {
+      errors[w] = std::current_exception();
+    }
+  };
+  std::vector<std::thread> threads;
+  threads.reserve(W);
+  for (size_t w = 0; w != W; ++w) threads.emplace_back(work, w);
+  for (std::thread& t : threads) t.join();
+  s.Bind();
+  for (std::exception_ptr& e : errors)
+    if (e) std::rethrow_exception(e);
+  if (find_peak_only) return;
+
+  for (size_t i = 0; i != n_sub; ++i) {
+    Slot& slot = slots[i];
+    const SubImage& sub = subimages_[i];
+    const size_t n = sub.width * sub.height;
+    const float* d_data;
+    const float* d_model;
+    if (slot.remote) {
+      d_data = slot.stage->F();
+      d_model = d_data + n_img * n;
+    } else {
+      d_data = slot.data->Base();
+      d_model = (slot.converging ? slot.model : slot.initial)->Base();
+    }
+    MergeSubImage(s, sub, data_image, result_model, d_data, d_model,
+                  static_cast<const uint8_t*>(slot.boundary->Ptr()),
+                  slot.converging);
   }
   s.Sync();
 }
@@ -282,8 +507,11 @@ ParallelDeconvolutionResult ParallelDeconvolution::ExecuteParallelRun(
     ImageSet& data_image, ImageSet& model_image,
     const std::vector<gpu::Planes>& psf_images,
     const std::vector<PsfOffset>& psf_offsets, double major_loop_gain) {
-  // parallel_deconvolution.cc:556-654; subimages run one after another in
-  // index order on this session's device
+  // parallel_deconvolution.cc:556-654. One worker: subimages run one after
+  // another in index order, each seeing the copy-backs of the ones before
+  // (the reference with one thread). More workers (settings.parallel
+  // .max_threads): subimages run concurrently on their own streams / GPUs,
+  // see RunSubImagesConcurrently.
   gpu::Session& s = data_image.Session();
   const size_t width = data_image.Width(), height = data_image.Height();
   std::vector<float> image(width * height);
@@ -297,18 +525,31 @@ ParallelDeconvolutionResult ParallelDeconvolution::ExecuteParallelRun(
                              psf_indices);
   ImageSet result_model(model_image, width, height);
   result_model.Fill(0.0f);
-  for (SubImage& sub : subimages_)
-    RunSubImage(sub, data_image, model_image, result_model,
-                psf_images[psf_indices[sub.index]], 0.0, true);
+  const size_t n_workers =
+      std::min<size_t>(std::max<size_t>(settings_.parallel.max_threads, 1),
+                       subimages_.size());
+  const bool concurrent = n_workers > 1;
+  if (concurrent) EnsureWorkers(s, n_workers);
+  if (concurrent)
+    RunSubImagesConcurrently(data_image, model_image, result_model, psf_images,
+                             psf_indices, 0.0, true);
+  else
+    for (SubImage& sub : subimages_)
+      RunSubImage(sub, data_image, model_image, result_model,
+                  psf_images[psf_indices[sub.index]], 0.0, true);
   double start_peak = 0.0;
   for (const SubImage& sub : subimages_)
     if (sub.peak > start_peak) start_peak = sub.peak;
   const double threshold = start_peak * (1.0 - major_loop_gain);
   log::Info() << "Maximum start peak over " << subimages_.size()
               << " subimages: " << start_peak << '\n';
-  for (SubImage& sub : subimages_)
-    RunSubImage(sub, data_image, model_image, result_model,
-                psf_images[psf_indices[sub.index]], threshold, false);
+  if (concurrent)
+    RunSubImagesConcurrently(data_image, model_image, result_model, psf_images,
+                             psf_indices, threshold, false);
+  else
+    for (SubImage& sub : subimages_)
+      RunSubImage(sub, data_image, model_image, result_model,
+                  psf_images[psf_indices[sub.index]], threshold, false);
   model_image.CopyFrom(result_model);
 
   ParallelDeconvolutionResult result;

@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "deconvolution_algorithm.h"
+#include "device.h"
 #include "psf_offset.h"
 #include "settings.h"
 
@@ -58,8 +59,13 @@ class ParallelDeconvolution {
 
   void FreeDeconvolutionAlgorithms() {
     algorithms_.clear();
+    workers_.clear();
+    worker_main_device_ = -1;
     mask_ = nullptr;
   }
+  /// Worker streams of the concurrent subimage pool (0 until a gridded run
+  /// with settings.parallel.max_threads > 1).
+  size_t WorkerCount() const { return workers_.size(); }
 
  private:
   ParallelDeconvolutionResult ExecuteSingleThreadedRun(
@@ -74,7 +80,23 @@ class ParallelDeconvolution {
   void RunSubImage(SubImage& sub, ImageSet& data_image, const ImageSet& model_image,
                    ImageSet& result_model, const gpu::Planes& psfs,
                    double major_iteration_threshold, bool find_peak_only);
+  /// Runs the subimage's algorithm; returns whether it converged.
+  bool DeconvolveSubImage(SubImage& sub, ImageSet& sub_data, ImageSet& sub_model,
+                          const gpu::Planes& sub_psfs,
+                          double major_iteration_threshold, bool find_peak_only);
+  void RunSubImagesConcurrently(ImageSet& data_image, const ImageSet& model_image,
+                                ImageSet& result_model,
+                                const std::vector<gpu::Planes>& psf_images,
+                                const std::vector<size_t>& psf_indices,
+                                double major_iteration_threshold,
+                                bool find_peak_only);
+  void EnsureWorkers(gpu::Session& main, size_t n);
+  static std::vector<int> PoolDevices(int main_device);
 
+  // worker sessions (one stream each) outlive the algorithms, whose cached
+  // transforms and scratch live on them
+  std::vector<std::unique_ptr<gpu::Session>> workers_;
+  int worker_main_device_ = -1;
   std::vector<std::unique_ptr<DeconvolutionAlgorithm>> algorithms_;
   std::vector<SubImage> subimages_;
   const Settings& settings_;

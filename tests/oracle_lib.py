@@ -277,6 +277,12 @@ class OracleParallel:
                                            C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]
         self.h = L.orc_parallel_create(kind, C.byref(self.settings), grid_w, grid_h)
         self.n_sub = grid_w * grid_h
+        L.orc_parallel_set_snapshot.argtypes = [C.c_void_p, C.c_int]
+
+    def set_snapshot(self, snapshot):
+        """True: every subimage of a pass trims the residual as it was at the
+        start of the pass (the product's concurrent pool, max_threads > 1)."""
+        self.o.lib.orc_parallel_set_snapshot(self.h, 1 if snapshot else 0)
 
     def execute(self, residual, model, psfs, major_loop_gain, user_mask=None,
                 trace_cap=1 << 22):

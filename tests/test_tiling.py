@@ -46,22 +46,7 @@ def test_splitter_flat_image_is_deterministic():
                zip(rd.tiling.make_subimages(img, 3, 3), make_subimages(get_oracle(), img, 3, 3)))
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("kind,w,gw,gh", [(1, 256, 3, 2), (0, 192, 2, 2), (1, 320, 2, 3)])
-def test_tiled_run_matches_oracle(kind, w, gw, gh):
-    h = w
-    psf, dirty = problem(w, h, 40, 4, seed=w + gw)
-    thr, max_iter, mgain = 4e-3, 1500, 0.9
-    orc = get_oracle()
-    orc.set_threads(8)
-    st = dict(threshold=thr, max_iterations=max_iter, border_ratio=0.0,
-              major_loop_gain=mgain)
-    if kind == 1:
-        st.update(max_scales=4, beam_size_in_pixels=2.0)
-    par = OracleParallel(orc, kind, gw, gh, **st)
-    res_o, mod_o = dirty[None].copy(), np.zeros((1, h, w), np.float32)
-    r_o, boxes_o, labels_o, trace_o = par.execute(res_o, mod_o, psf[None], mgain)
-
+def _settings(kind, w, thr, max_iter, mgain, gw, gh, threads):
     s = rd.Settings()
     s.algorithm_type = rd.AlgorithmType.multiscale if kind == 1 else rd.AlgorithmType.generic_clean
     s.trimmed_image_width = s.trimmed_image_height = w
@@ -71,19 +56,77 @@ def test_tiled_run_matches_oracle(kind, w, gw, gh):
     s.border_ratio = 0.0
     s.major_loop_gain = mgain
     s.parallel.grid_width, s.parallel.grid_height = gw, gh
+    s.parallel.max_threads = threads
     if kind == 1:
         s.multiscale.max_scales = 4
+    return s
+
+
+def _check_tiled(kind, w, gw, gh, threads, majors=1, staging=False, monkeypatch=None):
+    h = w
+    psf, dirty = problem(w, h, 40, 4, seed=w + gw)
+    thr, max_iter, mgain = 4e-3, 1500, 0.9 if majors == 1 else 0.5
+    orc = get_oracle()
+    orc.set_threads(8)
+    st = dict(threshold=thr, max_iterations=max_iter, border_ratio=0.0,
+              major_loop_gain=mgain)
+    if kind == 1:
+        st.update(max_scales=4, beam_size_in_pixels=2.0)
+    par = OracleParallel(orc, kind, gw, gh, **st)
+    par.set_snapshot(threads > 1)
+    res_o, mod_o = dirty[None].copy(), np.zeros((1, h, w), np.float32)
+
+    if staging:
+        monkeypatch.setenv("RADLER_POOL_STAGING", "1")
+    s = _settings(kind, w, thr, max_iter, mgain, gw, gh, threads)
     run = rd.gpu.DeviceRun(s, psf, dirty, [], 2.0 * PIXEL_SCALE if kind == 1 else 0.0)
-    r = run.execute()
-    boxes, labels = run.subimages(w, h)
-    assert np.array_equal(boxes, boxes_o)
-    assert np.array_equal(labels, labels_o)
-    for i in range(gw * gh):
-        t_o = trace_o[trace_o[:, 0] == i][:, 1:]
-        t_g = run.trace(i)
-        assert np.array_equal(t_g if kind == 1 else t_g[:, :2], t_o if kind == 1 else t_o[:, :2]), i
-    assert r["iterations"] == r_o.total_iterations
-    assert r["another_iteration_required"] == bool(r_o.another_iteration_required)
-    tol = 2e-5 * np.abs(dirty).max()
-    assert np.abs(run.residual().reshape(h, w) - res_o[0]).max() <= tol
-    assert np.abs(run.model().reshape(h, w) - mod_o[0]).max() <= tol
+    iterations = 0
+    for major in range(majors):
+        r_o, boxes_o, labels_o, trace_o = par.execute(res_o, mod_o, psf[None], mgain)
+        r = run.execute()
+        boxes, labels = run.subimages(w, h)
+        assert np.array_equal(boxes, boxes_o)
+        assert np.array_equal(labels, labels_o)
+        for i in range(gw * gh):
+            t_o = trace_o[trace_o[:, 0] == i][:, 1:]
+            t_g = run.trace(i)
+            assert np.array_equal(t_g if kind == 1 else t_g[:, :2],
+                                  t_o if kind == 1 else t_o[:, :2]), (major, i)
+        iterations = r_o.total_iterations
+        assert r["iterations"] == iterations - (0 if major == 0 else prev)
+        prev = iterations
+        assert r["another_iteration_required"] == bool(r_o.another_iteration_required)
+        tol = 2e-5 * np.abs(dirty).max()
+        assert np.abs(run.residual().reshape(h, w) - res_o[0]).max() <= tol
+        assert np.abs(run.model().reshape(h, w) - mod_o[0]).max() <= tol
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,w,gw,gh", [(1, 256, 3, 2), (0, 192, 2, 2), (1, 320, 2, 3)])
+def test_tiled_run_matches_oracle(kind, w, gw, gh):
+    """One worker: subimages in index order (the reference with one thread)."""
+    _check_tiled(kind, w, gw, gh, threads=1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,w,gw,gh,threads", [(1, 256, 3, 2, 6), (0, 192, 2, 2, 2),
+                                                  (1, 320, 3, 3, 4), (1, 256, 2, 2, 64)])
+def test_concurrent_pool_matches_oracle_snapshot(kind, w, gw, gh, threads):
+    """max_threads > 1: subimages run concurrently on worker streams; every
+    subimage trims the pass-start residual (oracle snapshot mode)."""
+    _check_tiled(kind, w, gw, gh, threads=threads)
+
+
+@pytest.mark.gpu
+def test_concurrent_pool_staging_path(monkeypatch):
+    """The staging + peer-copy path of workers on another GPU, forced on one
+    device (RADLER_POOL_STAGING=1)."""
+    _check_tiled(1, 256, 3, 2, threads=3, staging=True, monkeypatch=monkeypatch)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("threads", [1, 4])
+def test_tiled_two_major_iterations(threads):
+    """The worker pool and per-subimage algorithms persist across major
+    iterations (iteration counts and scale state carry over)."""
+    _check_tiled(1, 256, 2, 2, threads=threads, majors=2)
