@@ -63,8 +63,11 @@ def settings_for(rd, size, max_iter, max_scales, threshold):
 
 
 # algorithmic bytes per launch are accumulated by the C-ABI per family
-FAMILIES = ["conv_rows", "conv_cols", "conv64_rows", "conv64_cols", "fft", "fft64", "spectrum_multiply", "spectrum_multiply64", "find_peak", "subminor_loop", "subminor_select",
-            "trim_subtract", "add", "integrate", "rms", "axpy", "radix_select"]
+FAMILIES = ["conv_rows", "conv_cols", "conv64_rows", "conv64_cols", "conv_rows_sparse",
+            "conv_cols_sparse", "conv64_rows_sparse", "conv64_cols_sparse", "fft", "fft64",
+            "spectrum_multiply", "spectrum_multiply64", "find_peak", "subminor_loop",
+            "subminor_select", "trim_subtract", "add", "integrate", "rms", "axpy",
+            "radix_select", "iuwt", "box"]
 
 
 class Timing:
@@ -88,6 +91,25 @@ class Timing:
             if n.value:
                 out[fam] = {"ms": ms.value, "launches": n.value, "bytes": b.value}
         return out
+
+
+def measured_traffic(family, bytes_per_launch):
+    """HBM bytes per launch of `family` from the committed PMC summary
+    (profiles/r*_traffic.json, made by tools/pmc_traffic.py from separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this benchmark): the
+    measured traffic/algorithmic ratio applied to this run's launch size."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")))
+    if not files:
+        return None, None
+    try:
+        fam = json.load(open(files[-1]))["families"].get(family)
+    except (OSError, ValueError, KeyError):
+        return None, None
+    if not fam or not fam.get("traffic_over_algorithmic"):
+        return None, None
+    return (round(fam["traffic_over_algorithmic"] * bytes_per_launch),
+            os.path.relpath(files[-1], ROOT))
 
 
 def cpu_baseline(psf, dirty, max_scales, threshold, sample_components, threads):
@@ -126,6 +148,9 @@ def main():
                     help="components in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--breakdown", action="store_true", help="per-kernel times to stderr")
+    ap.add_argument("--timing-all", action="store_true",
+                    help="count every launch of the process (PMC passes, tools/pmc_traffic.py)")
+    ap.add_argument("--dump-families", help="write the per-family launch/byte counts here")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -147,6 +172,8 @@ def main():
     s = settings_for(rd, args.size, args.max_iter, args.scales, threshold)
     run = rd.gpu.DeviceRun(s, psf, dirty, [], BEAM_PX * PIXEL_SCALE)
     timing = Timing(run.session_handle())
+    if args.timing_all:
+        timing.enable(True)
 
     for _ in range(args.warmup):
         run.restore()
@@ -159,7 +186,8 @@ def main():
             dist.barrier()
             torch.cuda.synchronize()
 
-    timing.reset()
+    if not args.timing_all:
+        timing.reset()
     timing.enable(True)
     barrier()
     run.sync()
@@ -175,6 +203,9 @@ def main():
     elapsed = time.perf_counter() - t0
     timing.enable(False)
     fams = timing.get()
+    if args.dump_families and rank == 0:
+        with open(args.dump_families, "w") as f:
+            json.dump(fams, f, indent=1)
 
     total_comps, max_elapsed = comps, elapsed
     if dist is not None:
@@ -200,9 +231,11 @@ def main():
         avg_ms = dom["ms"] / dom["launches"]
         bytes_per_launch = dom["bytes"] / dom["launches"]
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+        traffic, traffic_src = measured_traffic(dom_name, bytes_per_launch)
         roofline = {"bound": "hbm", "kernel": dom_name, "achieved": round(achieved, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "traffic_source": traffic_src,
                     "avg_launch_us": round(avg_ms * 1e3, 2),
                     "bytes_per_launch": bytes_per_launch,
                     "share_of_device_time": round(dom["ms"] / device_ms, 3) if device_ms else None}

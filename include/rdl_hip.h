@@ -245,6 +245,12 @@ int rdl_subminor_model(rdl_subminor* h, uint32_t image_index, float* d_dest,
                        uint32_t oy, int mode);
 /* As mode 0 of rdl_subminor_model, into a zeroed float64 plane (input of the
  * double-precision residual correction, rdl_fft64_convolve). */
+/* Row occupancy of that model in a plane with the model at row offset oy:
+ * d_rows[y] = 1 where row y holds a non-zero model value, else 0 (n_rows
+ * bytes). Lets the correction's transform skip the empty rows
+ * (rdl_conv_rows_forward_masked / rdl_conv_columns_ex). */
+int rdl_subminor_model_rows(rdl_subminor* h, uint32_t image_index,
+                            uint8_t* d_rows, uint32_t n_rows, uint32_t oy);
 int rdl_subminor_model_f64(rdl_subminor* h, uint32_t image_index,
                            double* d_dest, uint32_t dest_w, uint32_t dest_h,
                            uint32_t ox, uint32_t oy);
@@ -305,6 +311,24 @@ int rdl_conv_rows_inverse(rdl_conv* c, const void* d_spec, float* d_out,
                           uint32_t oy, int subtract);
 /* Full 2-D forward transform of a width x height float image. */
 int rdl_conv_forward(rdl_conv* c, const float* d_in, void* d_spec);
+/* Sparse / layout variants of the passes above.
+ * rdl_conv_rows_forward_masked: d_row_mask[y] == 0 declares plane row y zero;
+ * workgroups whose rows are all zero read and write nothing, so the column
+ * pass must be given the same mask (it substitutes zeros for those rows).
+ * rdl_conv_columns_ex: d_row_mask as above (NULL: dense); kernel_layout
+ * RDL_CONV_COL_MAJOR reads the kernel spectrum as columns (column k at
+ * d_kernel + k*height, contiguous: the strided kernel read of the row-major
+ * layout is the column pass's costliest access); out_layout
+ * RDL_CONV_COL_MAJOR writes a mode-0 spectrum that way (d_out != d_in). */
+#define RDL_CONV_ROW_MAJOR 0
+#define RDL_CONV_COL_MAJOR 1
+int rdl_conv_rows_forward_masked(rdl_conv* c, const float* d_in, uint32_t in_w,
+                                 uint32_t in_h, uint32_t ox, uint32_t oy,
+                                 void* d_spec, const uint8_t* d_row_mask);
+int rdl_conv_columns_ex(rdl_conv* c, const void* d_in, void* d_out,
+                        const void* d_kernel, int mode, double scale,
+                        const uint8_t* d_row_mask, int kernel_layout,
+                        int out_layout);
 
 /* dst = a * b * scale, complex, n_complex elements. */
 int rdl_spectrum_multiply(rdl_session* s, void* d_dst, const void* d_a,

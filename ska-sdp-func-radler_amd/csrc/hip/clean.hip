@@ -309,9 +309,8 @@ int rdl_hogbom_run(rdl_session* s, float* d_residuals, float* d_models,
       }
     }
     RDL_HIP_CHECK(hipGetLastError());
-    RDL_HIP_CHECK(hipMemcpyAsync(&st, a.state, sizeof(st),
-                                 hipMemcpyDeviceToHost, s->stream));
-    RDL_HIP_CHECK(hipStreamSynchronize(s->stream));
+    const rdl::SmallRead r{&st, a.state, sizeof(st)};
+    RDL_TRY(rdl::ReadSmall(s, &r, 1));
     if (st.done) break;
   }
   if (n_trace) {

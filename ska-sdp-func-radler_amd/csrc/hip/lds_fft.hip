@@ -344,6 +344,9 @@ struct RowArgs {
   uint32_t ld;         // spectrum row stride (complex) = n/2+1
   // forward input / inverse output window inside the plane
   uint32_t img_w, img_h, ox, oy;
+  // forward: per plane row, 0 = known zero. A workgroup whose rows are all
+  // zero neither reads nor writes (the column pass must get the same mask)
+  const uint8_t* row_mask;
 };
 
 // rows forward: float image window -> half spectra (T)
@@ -358,6 +361,19 @@ __global__ __launch_bounds__(kFftThreads) void RowsForward(RowArgs a,
   const uint32_t pair0 = blockIdx.x * a.count;
   const uint32_t n_pairs = (a.height + 1) / 2;
   const uint32_t count = min(a.count, n_pairs - pair0);
+  if (a.row_mask) {
+    // workgroup OR through the (not yet used) dynamic LDS: the engine owns
+    // all of it, so no static __shared__ flag or __syncthreads_or
+    volatile uint32_t* flag = reinterpret_cast<volatile uint32_t*>(lds_raw);
+    if (tid == 0) *flag = 0u;
+    __syncthreads();
+    const uint32_t y = 2 * pair0 + tid;
+    if (tid < 2 * count && y < a.height && a.row_mask[y] != 0) *flag = 1u;
+    __syncthreads();
+    const bool any = *flag != 0u;
+    __syncthreads();
+    if (!any) return;
+  }
   for (uint32_t idx = tid; idx < count * n; idx += kFftThreads) {
     const uint32_t t = idx / n, x = idx - t * n;
     const uint32_t y0 = 2 * (pair0 + t), y1 = y0 + 1;
@@ -452,6 +468,9 @@ struct ColArgs {
   uint32_t tiles_per_xcd;
   int mode;          // 0 fwd, 1 fwd*K*s+inv, 2 (already fwd) *K*s+inv
   double scale;
+  const uint8_t* row_mask;  // rows known zero are not read (NULL: dense)
+  uint32_t kern_cm;         // kernel spectrum column-major (column k at k*n)
+  uint32_t out_cm;          // mode 0: write the spectrum column-major
 };
 
 template <typename T>
@@ -473,21 +492,37 @@ __global__ __launch_bounds__(kFftThreads) void Columns(ColArgs a,
   const T s = T(a.scale);
   for (uint32_t idx = tid; idx < count * n; idx += kFftThreads) {
     const uint32_t y = idx / count, j = idx - y * count;
-    Cx<T> v = in[size_t(y) * a.ld + k0 + j];
-    if (a.mode == 2) v = Conj(Scale(Mul(v, kern[size_t(y) * a.ld + k0 + j]), s));
+    Cx<T> v = (a.row_mask && a.row_mask[y] == 0) ? Cx<T>{T(0), T(0)}
+                                                 : in[size_t(y) * a.ld + k0 + j];
+    if (a.mode == 2)
+      v = Conj(Scale(Mul(v, a.kern_cm ? kern[size_t(k0 + j) * n + y]
+                                      : kern[size_t(y) * a.ld + k0 + j]),
+                     s));
     buf[size_t(j) * n + y] = v;
   }
   __syncthreads();
   if (a.mode != 2) LdsFftForward<T>(buf, a.plan, count, tid);
   if (a.mode == 1) {
-    for (uint32_t idx = tid; idx < count * n; idx += kFftThreads) {
-      const uint32_t y = idx / count, j = idx - y * count;
-      Cx<T>& v = buf[size_t(j) * n + y];
-      v = Conj(Scale(Mul(v, kern[size_t(y) * a.ld + k0 + j]), s));
+    if (a.kern_cm) {  // contiguous kernel columns: walk each column
+      for (uint32_t idx = tid; idx < count * n; idx += kFftThreads) {
+        Cx<T>& v = buf[idx];  // idx = j*n + y
+        v = Conj(Scale(Mul(v, kern[size_t(k0) * n + idx]), s));
+      }
+    } else {
+      for (uint32_t idx = tid; idx < count * n; idx += kFftThreads) {
+        const uint32_t y = idx / count, j = idx - y * count;
+        Cx<T>& v = buf[size_t(j) * n + y];
+        v = Conj(Scale(Mul(v, kern[size_t(y) * a.ld + k0 + j]), s));
+      }
     }
     __syncthreads();
   }
   if (a.mode != 0) LdsFftForward<T>(buf, a.plan, count, tid);
+  if (a.out_cm) {  // column-major spectrum (mode 0 only)
+    for (uint32_t idx = tid; idx < count * n; idx += kFftThreads)
+      out[size_t(k0) * n + idx] = buf[idx];
+    return;
+  }
   for (uint32_t idx = tid; idx < count * n; idx += kFftThreads) {
     const uint32_t y = idx / count, j = idx - y * count;
     const Cx<T> v = buf[size_t(j) * n + y];
@@ -570,8 +605,9 @@ int MakePlan(rdl_conv* c, uint32_t n, bool f64, rdl::LdsPlan* plan, void** tw) {
 
 template <typename T>
 int LaunchRowsForward(rdl_conv* c, const float* in, uint32_t in_w, uint32_t in_h,
-                      uint32_t ox, uint32_t oy, void* spec) {
+                      uint32_t ox, uint32_t oy, void* spec, const uint8_t* row_mask) {
   rdl::RowArgs a{};
+  a.row_mask = row_mask;
   a.plan = c->row_plan;
   a.height = c->height;
   a.count = c->row_count;
@@ -620,8 +656,12 @@ int LaunchRowsInverse(rdl_conv* c, const void* spec, float* out, uint32_t out_w,
 
 template <typename T>
 int LaunchColumns(rdl_conv* c, const void* in, void* out, const void* kern,
-                  int mode, double scale) {
+                  int mode, double scale, const uint8_t* row_mask, int kern_cm,
+                  int out_cm) {
   rdl::ColArgs a{};
+  a.row_mask = row_mask;
+  a.kern_cm = kern_cm ? 1u : 0u;
+  a.out_cm = out_cm ? 1u : 0u;
   a.plan = c->col_plan;
   a.n_cols = c->width / 2 + 1;
   a.count = c->col_count;
@@ -701,8 +741,23 @@ int rdl_conv_rows_forward(rdl_conv* c, const float* d_in, uint32_t in_w,
                 "input window outside the plane");
   rdl::ScopedTiming t(c->s, c->f64 ? "conv64_rows" : "conv_rows",
                       double(in_w) * in_h * 4.0 + SpectrumBytes(c));
-  return c->f64 ? LaunchRowsForward<double>(c, d_in, in_w, in_h, ox, oy, d_spec)
-                : LaunchRowsForward<float>(c, d_in, in_w, in_h, ox, oy, d_spec);
+  return c->f64 ? LaunchRowsForward<double>(c, d_in, in_w, in_h, ox, oy, d_spec, nullptr)
+                : LaunchRowsForward<float>(c, d_in, in_w, in_h, ox, oy, d_spec, nullptr);
+}
+
+int rdl_conv_rows_forward_masked(rdl_conv* c, const float* d_in, uint32_t in_w,
+                                 uint32_t in_h, uint32_t ox, uint32_t oy,
+                                 void* d_spec, const uint8_t* d_row_mask) {
+  RDL_ARG_CHECK(c && d_in && d_spec && d_row_mask, "NULL argument");
+  RDL_ARG_CHECK(uint64_t(ox) + in_w <= c->width && uint64_t(oy) + in_h <= c->height,
+                "input window outside the plane");
+  // bytes depend on the mask's occupancy (known only on the device): the
+  // sparse family reports time and launches, not bandwidth
+  rdl::ScopedTiming t(c->s, c->f64 ? "conv64_rows_sparse" : "conv_rows_sparse", 0.0);
+  return c->f64 ? LaunchRowsForward<double>(c, d_in, in_w, in_h, ox, oy, d_spec,
+                                            d_row_mask)
+                : LaunchRowsForward<float>(c, d_in, in_w, in_h, ox, oy, d_spec,
+                                           d_row_mask);
 }
 
 int rdl_conv_columns(rdl_conv* c, const void* d_in, void* d_out,
@@ -713,8 +768,39 @@ int rdl_conv_columns(rdl_conv* c, const void* d_in, void* d_out,
   const double sb = SpectrumBytes(c);
   rdl::ScopedTiming t(c->s, c->f64 ? "conv64_cols" : "conv_cols",
                       mode == 0 ? 2.0 * sb : 3.0 * sb);
-  return c->f64 ? LaunchColumns<double>(c, d_in, d_out, d_kernel, mode, scale)
-                : LaunchColumns<float>(c, d_in, d_out, d_kernel, mode, scale);
+  return c->f64 ? LaunchColumns<double>(c, d_in, d_out, d_kernel, mode, scale,
+                                        nullptr, 0, 0)
+                : LaunchColumns<float>(c, d_in, d_out, d_kernel, mode, scale,
+                                       nullptr, 0, 0);
+}
+
+int rdl_conv_columns_ex(rdl_conv* c, const void* d_in, void* d_out,
+                        const void* d_kernel, int mode, double scale,
+                        const uint8_t* d_row_mask, int kernel_layout,
+                        int out_layout) {
+  RDL_ARG_CHECK(c && d_in && d_out, "NULL argument");
+  RDL_ARG_CHECK(mode >= 0 && mode <= 2, "mode must be 0, 1 or 2");
+  RDL_ARG_CHECK(mode == 0 || d_kernel, "kernel spectrum required");
+  RDL_ARG_CHECK(out_layout == RDL_CONV_ROW_MAJOR ||
+                    (mode == 0 && d_out != d_in),
+                "a column-major output needs mode 0 and a separate output");
+  RDL_ARG_CHECK(kernel_layout == RDL_CONV_ROW_MAJOR ||
+                    kernel_layout == RDL_CONV_COL_MAJOR,
+                "bad kernel layout");
+  const double sb = SpectrumBytes(c);
+  // with a row mask the input reads are skipped for the zero rows: count
+  // the kernel read and the output write only (a lower bound)
+  const char* fam = d_row_mask ? (c->f64 ? "conv64_cols_sparse" : "conv_cols_sparse")
+                               : (c->f64 ? "conv64_cols" : "conv_cols");
+  const double bytes = d_row_mask ? (mode == 0 ? sb : 2.0 * sb)
+                                  : (mode == 0 ? 2.0 * sb : 3.0 * sb);
+  rdl::ScopedTiming t(c->s, fam, bytes);
+  const int kcm = kernel_layout == RDL_CONV_COL_MAJOR;
+  const int ocm = out_layout == RDL_CONV_COL_MAJOR;
+  return c->f64 ? LaunchColumns<double>(c, d_in, d_out, d_kernel, mode, scale,
+                                        d_row_mask, kcm, ocm)
+                : LaunchColumns<float>(c, d_in, d_out, d_kernel, mode, scale,
+                                       d_row_mask, kcm, ocm);
 }
 
 int rdl_conv_rows_inverse(rdl_conv* c, const void* d_spec, float* d_out,

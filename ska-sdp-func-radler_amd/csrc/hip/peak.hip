@@ -194,9 +194,8 @@ int rdl_find_peak(rdl_session* s, const float* d_image, uint32_t width,
                               h_border, v_border, allow_negative, d_mask,
                               avx_semantics, s->d_small));
   rdl::PeakOut o;
-  RDL_HIP_CHECK(hipMemcpyAsync(&o, s->d_small, sizeof(o),
-                               hipMemcpyDeviceToHost, s->stream));
-  RDL_HIP_CHECK(hipStreamSynchronize(s->stream));
+  const rdl::SmallRead r{&o, s->d_small, sizeof(o)};
+  RDL_TRY(rdl::ReadSmall(s, &r, 1));
   out->value = o.value;
   out->x = o.x;
   out->y = o.y;
@@ -218,9 +217,8 @@ int rdl_rms(rdl_session* s, const float* d_image, size_t n, float* out) {
     rdl::SumSquaresFinal<<<1, 64, 0, s->stream>>>(partials, blocks, n, d_out);
   }
   RDL_HIP_CHECK(hipGetLastError());
-  RDL_HIP_CHECK(
-      hipMemcpyAsync(out, d_out, sizeof(float), hipMemcpyDeviceToHost, s->stream));
-  RDL_HIP_CHECK(hipStreamSynchronize(s->stream));
+  const rdl::SmallRead r{out, d_out, sizeof(float)};
+  RDL_TRY(rdl::ReadSmall(s, &r, 1));
   return RDL_OK;
 }
 

@@ -5,6 +5,7 @@
 
 #include <atomic>
 #include <cstdint>
+#include <cstring>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -234,6 +235,40 @@ inline int SetMaxLdsOnce(const void* fn, int bytes, int device,
   RDL_HIP_CHECK(
       hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
   done.fetch_or(bit, std::memory_order_acq_rel);
+  return RDL_OK;
+}
+}  // namespace rdl
+
+namespace rdl {
+// Small device->host reads go through the session's pinned 64 KiB buffer:
+// one DMA straight into pinned memory instead of the runtime's pageable
+// staging path (lower latency per outer iteration, and no shared staging
+// buffer between the worker threads of a subimage pool). Copies `n` regions
+// (device src, bytes) back to back, syncs the stream, then scatters them.
+struct SmallRead {
+  void* h_dst;
+  const void* d_src;
+  size_t bytes;
+};
+inline int ReadSmall(rdl_session* s, const SmallRead* reads, int n) {
+  size_t off = 0;
+  for (int i = 0; i < n; ++i) {
+    const size_t b = (reads[i].bytes + 15) / 16 * 16;
+    if (off + b > (size_t(1) << 16)) {
+      SetError("ReadSmall: more than 64 KiB");
+      return RDL_ERR_ARG;
+    }
+    RDL_HIP_CHECK(hipMemcpyAsync(static_cast<char*>(s->h_small) + off, reads[i].d_src,
+                                 reads[i].bytes, hipMemcpyDeviceToHost, s->stream));
+    off += b;
+  }
+  RDL_HIP_CHECK(hipStreamSynchronize(s->stream));
+  off = 0;
+  for (int i = 0; i < n; ++i) {
+    std::memcpy(reads[i].h_dst, static_cast<const char*>(s->h_small) + off,
+                reads[i].bytes);
+    off += (reads[i].bytes + 15) / 16 * 16;
+  }
   return RDL_OK;
 }
 }  // namespace rdl

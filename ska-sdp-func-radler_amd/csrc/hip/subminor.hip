@@ -470,6 +470,15 @@ __global__ __launch_bounds__(256) void ScatterModel(const uint32_t* pos,
   }
 }
 
+// rows of the (untrimmed) model plane that hold a non-zero component
+__global__ __launch_bounds__(256) void MarkModelRows(const uint32_t* pos,
+                                                     const float* m, uint64_t n_sel,
+                                                     uint8_t* rows, uint32_t oy) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n_sel;
+       i += uint64_t(gridDim.x) * blockDim.x)
+    if (m[i] != 0.0f) rows[(pos[i] >> 16) + oy] = 1;
+}
+
 // ------------------------------------------------- register-resident loop
 // SubminorLoopReg: the same loop with each thread's ITEMS selected pixels
 // (positions, residuals, model values) held in VGPRs, so one iteration is
@@ -996,9 +1005,10 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   }
   RDL_HIP_CHECK(hipGetLastError());
   uint64_t n_sel = 0;
-  RDL_HIP_CHECK(hipMemcpyAsync(&n_sel, d_total, sizeof(n_sel),
-                               hipMemcpyDeviceToHost, st));
-  RDL_HIP_CHECK(hipStreamSynchronize(st));
+  {
+    const rdl::SmallRead r{&n_sel, d_total, sizeof(n_sel)};
+    RDL_TRY(rdl::ReadSmall(s, &r, 1));
+  }
   h->n_selected = n_sel;
   out->n_selected = n_sel;
   out->iteration = p->iteration_start;
@@ -1138,11 +1148,11 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   if (s->trace_subminor) RDL_HIP_CHECK(hipEventRecord(ev1, st));
   rdl::LoopResult res{};
   uint32_t err = 0;
-  RDL_HIP_CHECK(hipMemcpyAsync(&res, la.result, sizeof(res),
-                               hipMemcpyDeviceToHost, st));
-  RDL_HIP_CHECK(hipMemcpyAsync(&err, la.result + 8, sizeof(err),
-                               hipMemcpyDeviceToHost, st));
-  RDL_HIP_CHECK(hipStreamSynchronize(st));
+  {
+    const rdl::SmallRead r[2] = {{&res, la.result, sizeof(res)},
+                                 {&err, la.result + 8, sizeof(err)}};
+    RDL_TRY(rdl::ReadSmall(s, r, 2));
+  }
   if (err) {
     rdl::SetError("sub-minor loop: grid exchange timed out");
     return RDL_ERR_TIMEOUT;
@@ -1157,7 +1167,8 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
     s->event_pool.push_back(ev0);
     s->event_pool.push_back(ev1);
     uint64_t ph[6] = {};
-    RDL_HIP_CHECK(hipMemcpy(ph, la.result + 16, sizeof(ph), hipMemcpyDeviceToHost));
+    const rdl::SmallRead r{ph, la.result + 16, sizeof(ph)};
+    RDL_TRY(rdl::ReadSmall(s, &r, 1));
     std::fprintf(stderr,
                  "[subminor] n_sel=%llu g=%u kind=%d iters=%llu us=%.1f "
                  "gather=%llu integ=%llu wred=%llu bar=%llu xchg=%llu dec=%llu\n",
@@ -1207,6 +1218,23 @@ int rdl_subminor_model(rdl_subminor* h, uint32_t image_index, float* d_dest,
   rdl::ScatterModel<float><<<grid, 256, 0, s->stream>>>(
       h->d_pos, h->d_m + size_t(image_index) * h->n_selected, h->n_selected,
       d_dest, dest_w, ox, oy, mode == 1);
+  RDL_HIP_CHECK(hipGetLastError());
+  return RDL_OK;
+}
+
+int rdl_subminor_model_rows(rdl_subminor* h, uint32_t image_index,
+                            uint8_t* d_rows, uint32_t n_rows, uint32_t oy) {
+  RDL_ARG_CHECK(h && d_rows, "NULL argument");
+  RDL_ARG_CHECK(image_index < h->n_images || h->n_selected == 0,
+                "image index out of range");
+  RDL_ARG_CHECK(n_rows >= h->height + oy, "row mask too short");
+  rdl_session* s = h->s;
+  RDL_HIP_CHECK(hipMemsetAsync(d_rows, 0, n_rows, s->stream));
+  if (h->n_selected == 0) return RDL_OK;
+  const unsigned grid = std::min<uint64_t>(4096, rdl::DivUp(h->n_selected, 256));
+  rdl::MarkModelRows<<<grid, 256, 0, s->stream>>>(
+      h->d_pos, h->d_m + size_t(image_index) * h->n_selected, h->n_selected, d_rows,
+      oy);
   RDL_HIP_CHECK(hipGetLastError());
   return RDL_OK;
 }

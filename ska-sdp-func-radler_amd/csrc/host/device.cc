@@ -125,17 +125,36 @@ void Fft::ConvolveSpectrum(const void* d_spectrum, const void* d_kernel_spectrum
   }
 }
 
+void Fft::ForwardColumnMajor(const float* d_in, void* d_spectrum) {
+  if (!conv_) throw std::logic_error("Fft::ForwardColumnMajor needs the LDS engine");
+  Check(rdl_conv_rows_forward(conv_, d_in, uint32_t(width_), uint32_t(height_), 0, 0,
+                              work_.Ptr()),
+        "rdl_conv_rows_forward");
+  Check(rdl_conv_columns_ex(conv_, work_.Ptr(), d_spectrum, nullptr, 0, 1.0, nullptr,
+                            RDL_CONV_ROW_MAJOR, RDL_CONV_COL_MAJOR),
+        "rdl_conv_columns_ex");
+}
+
 void Fft::ConvolveSubtract(const float* d_image, size_t img_w, size_t img_h,
                            size_t ox, size_t oy, const void* d_kernel_spectrum,
-                           void* d_work, float* d_residual) {
+                           void* d_work, float* d_residual,
+                           const uint8_t* d_row_mask, bool kernel_col_major) {
   if (!conv_) throw std::logic_error("Fft::ConvolveSubtract needs the LDS engine");
   const double norm = 1.0 / (double(width_) * double(height_));
-  Check(rdl_conv_rows_forward(conv_, d_image, uint32_t(img_w), uint32_t(img_h),
-                              uint32_t(ox), uint32_t(oy), d_work),
-        "rdl_conv_rows_forward");
-  Check(rdl_conv_columns(conv_, d_work, d_work, d_kernel_spectrum, 1,
-                         f64_ ? norm : double(float(norm))),
-        "rdl_conv_columns");
+  if (d_row_mask)
+    Check(rdl_conv_rows_forward_masked(conv_, d_image, uint32_t(img_w),
+                                       uint32_t(img_h), uint32_t(ox), uint32_t(oy),
+                                       d_work, d_row_mask),
+          "rdl_conv_rows_forward_masked");
+  else
+    Check(rdl_conv_rows_forward(conv_, d_image, uint32_t(img_w), uint32_t(img_h),
+                                uint32_t(ox), uint32_t(oy), d_work),
+          "rdl_conv_rows_forward");
+  Check(rdl_conv_columns_ex(conv_, d_work, d_work, d_kernel_spectrum, 1,
+                            f64_ ? norm : double(float(norm)), d_row_mask,
+                            kernel_col_major ? RDL_CONV_COL_MAJOR : RDL_CONV_ROW_MAJOR,
+                            RDL_CONV_ROW_MAJOR),
+        "rdl_conv_columns_ex");
   Check(rdl_conv_rows_inverse(conv_, d_work, d_residual, uint32_t(img_w),
                               uint32_t(img_h), uint32_t(ox), uint32_t(oy), 1),
         "rdl_conv_rows_inverse");

@@ -67,9 +67,16 @@ class Fft {
                         void* d_work, float* d_out);
   /// LDS engine only: residual(window) -= Trim(conv(Untrim(image), kernel)),
   /// the image (img_w x img_h) placed at (ox, oy) in the plane.
+  /// d_row_mask (plane rows, 0 = the image row is all zero) skips the empty
+  /// rows; kernel_col_major reads a spectrum made by ForwardColumnMajor.
   void ConvolveSubtract(const float* d_image, size_t img_w, size_t img_h,
                         size_t ox, size_t oy, const void* d_kernel_spectrum,
-                        void* d_work, float* d_residual);
+                        void* d_work, float* d_residual,
+                        const uint8_t* d_row_mask = nullptr,
+                        bool kernel_col_major = false);
+  /// LDS engine only: forward spectrum stored column by column (column k at
+  /// k * height), the layout the column pass reads contiguously.
+  void ForwardColumnMajor(const float* d_in, void* d_spectrum);
   bool UsesLds() const { return conv_ != nullptr; }
   /// Double-precision rocFFT plan only.
   void Forward64(const double* d_in, void* d_spectrum);
@@ -111,7 +118,12 @@ class Session {
   /// Grow-only scratch buffers that outlive the algorithm objects (a
   /// SubMinorLoop is created per outer iteration; allocating its ~1 GB of
   /// planes each time costs a hipMalloc/hipFree pair and a device sync).
-  enum ScratchSlot { kCorrectionModel = 0, kCorrectionSpectrum, kNumScratch };
+  enum ScratchSlot {
+    kCorrectionModel = 0,
+    kCorrectionSpectrum,
+    kCorrectionRows,
+    kNumScratch
+  };
   Buffer& Scratch(ScratchSlot slot, size_t bytes);
   /// The session's sub-minor loop state (selection, model values), reused by
   /// consecutive SubMinorLoop objects.

@@ -105,6 +105,10 @@ void MultiScaleAlgorithm::FindActiveScaleConvolvedMaxima(
   // FFT of the integrated image feeds every active scale.
   rdl_session* s = session_->Handle();
   const size_t w = image_set.Width(), h = image_set.Height();
+  const bool identity = image_set.Size() == 1 && image_set.Integration(false).copy_fast_path;
+  scale_image_valid_.assign(scale_infos_.size(), false);
+  if (identity && scale_images_.size() != scale_infos_.size())
+    scale_images_.assign(scale_infos_.size(), gpu::Planes());
   image_set.GetLinearIntegrated(d_integrated);
   bool need_fft = false;
   for (size_t si = 0; si != scale_infos_.size(); ++si) {
@@ -124,17 +128,25 @@ void MultiScaleAlgorithm::FindActiveScaleConvolvedMaxima(
   for (size_t si = 0; si != scale_infos_.size(); ++si) {
     ScaleInfo& e = scale_infos_[si];
     if (!e.is_active || e.scale == 0.0f) continue;
+    float* d_conv = scratch_->F();
+    if (identity) {
+      gpu::Planes& kept = scale_images_[si];
+      if (!kept.buffer || kept.width != w || kept.height != h)
+        kept = gpu::Planes::Make(*session_, w, h, 1);
+      d_conv = kept.Base();
+      scale_image_valid_[si] = true;
+    }
     fft.ConvolveSpectrum(spectrum_->Ptr(), transforms_->KernelSpectrum(e.scale),
-                         spectrum_work_->Ptr(), scratch_->F());
+                         spectrum_work_->Ptr(), d_conv);
     const size_t border_scale = size_t(std::ceil(e.scale * 0.5));
     const uint32_t xb = uint32_t(
         std::max<size_t>(size_t(std::round(w * CleanBorderRatio())), border_scale));
     const uint32_t yb = uint32_t(
         std::max<size_t>(size_t(std::round(h * CleanBorderRatio())), border_scale));
     if (report_rms)
-      gpu::Check(rdl_rms(s, scratch_->F(), w * h, &e.rms), "rdl_rms");
+      gpu::Check(rdl_rms(s, d_conv, w * h, &e.rms), "rdl_rms");
     rdl_peak p;
-    gpu::Check(rdl_find_peak(s, scratch_->F(), uint32_t(w), uint32_t(h), 0,
+    gpu::Check(rdl_find_peak(s, d_conv, uint32_t(w), uint32_t(h), 0,
                              uint32_t(h), xb, yb, AllowNegativeComponents(),
                              d_mask_, 1, &p),
                "rdl_find_peak");
@@ -274,10 +286,20 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
     }
     const gpu::Planes& twice = tw->second;
     // individually convolved images (:336-354)
-    individual.CopyFrom(data_image);
-    if (info.scale != 0.0f)
-      for (size_t i = 0; i != data_image.Size(); ++i)
-        transforms_->Transform(individual.Data(i), info.scale);
+    if (info.scale != 0.0f && scale_with_peak < scale_image_valid_.size() &&
+        scale_image_valid_[scale_with_peak]) {
+      // the residual has not changed since FindActiveScaleConvolvedMaxima
+      // convolved it with this scale: take that image
+      gpu::Planes previous = individual.Planes();
+      individual.SetPlanes(scale_images_[scale_with_peak]);
+      scale_images_[scale_with_peak] = previous;
+      scale_image_valid_[scale_with_peak] = false;
+    } else {
+      individual.CopyFrom(data_image);
+      if (info.scale != 0.0f)
+        for (size_t i = 0; i != data_image.Size(); ++i)
+          transforms_->Transform(individual.Data(i), info.scale);
+    }
 
     const float sub_iteration_gain_threshold =
         std::fabs(info.max_unnormalized_image_value * info.bias_factor) *

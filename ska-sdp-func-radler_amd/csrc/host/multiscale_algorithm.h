@@ -73,6 +73,14 @@ class MultiScaleAlgorithm final : public DeconvolutionAlgorithm {
   const uint8_t* d_mask_ = nullptr;
   std::shared_ptr<gpu::Buffer> scratch_;  // W x H
   std::shared_ptr<gpu::Buffer> spectrum_, spectrum_work_;
+  // One image with the identity integration (ImageSet copy fast path): the
+  // integrated image IS the residual, so the scale-convolved images that
+  // FindActiveScaleConvolvedMaxima computes are the next outer iteration's
+  // individually convolved image for that scale (same input, same FFT plan,
+  // same kernel spectrum: bit-identical to a fresh Transform). They are kept
+  // per scale and swapped in instead of convolving again.
+  std::vector<gpu::Planes> scale_images_;
+  std::vector<bool> scale_image_valid_;
 };
 
 // multiscale_algorithm.cc:90-151 (free functions in the reference)

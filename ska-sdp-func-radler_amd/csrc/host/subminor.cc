@@ -68,7 +68,7 @@ std::shared_ptr<gpu::Buffer> SubMinorLoop::MakePaddedPsfSpectrum(
                                       uint32_t(ph), d_psf, uint32_t(width),
                                       uint32_t(height)),
                "rdl_prepare_psf_kernel");
-    fft.Forward(kernel.F(), spectrum->Ptr());
+    fft.ForwardColumnMajor(kernel.F(), spectrum->Ptr());
   } else {
     gpu::Buffer kernel(s, pw * ph * sizeof(double));
     gpu::Check(rdl_prepare_psf_kernel_f64(s.Handle(), kernel.D(), uint32_t(pw),
@@ -105,9 +105,16 @@ void SubMinorLoop::CorrectResidualDirtyWithSpectrum(size_t image_index,
     gpu::Buffer& model = s_.Scratch(gpu::Session::kCorrectionModel,
                                     width_ * height_ * sizeof(float));
     gpu::Buffer& work = s_.Scratch(gpu::Session::kCorrectionSpectrum, fft.SpectrumBytes());
+    gpu::Buffer& rows = s_.Scratch(gpu::Session::kCorrectionRows, padded_height_);
     GetFullIndividualModel(image_index, model.F());
+    // the model holds a few hundred components per outer iteration: the
+    // transform skips its empty rows (exactly zero, so nothing changes)
+    gpu::Check(rdl_subminor_model_rows(h_, uint32_t(image_index),
+                                       static_cast<uint8_t*>(rows.Ptr()),
+                                       uint32_t(padded_height_), oy),
+               "rdl_subminor_model_rows");
     fft.ConvolveSubtract(model.F(), width_, height_, ox, oy, d_spectrum, work.Ptr(),
-                         d_residual);
+                         d_residual, static_cast<const uint8_t*>(rows.Ptr()), true);
     return;
   }
   gpu::Buffer& padded_ = s_.Scratch(gpu::Session::kCorrectionSpectrum,

@@ -16,6 +16,8 @@ from rdl_lib import (HogbomParams, HogbomResult, Session, SubminorParams, Submin
 
 pytestmark = pytest.mark.gpu
 
+RDL_CONV_ROW_MAJOR, RDL_CONV_COL_MAJOR = 0, 1  # rdl_hip.h
+
 
 @pytest.fixture(scope="module")
 def sess():
@@ -502,3 +504,53 @@ def test_subminor_loop_bit_exact(sess, orc, w, n_src, threshold_frac, mgain, max
     sess.rdl.rdl_subminor_destroy(sm)
     for a in (dres, dpsf, dmod, kern, spec_k, padded, work):
         a.free()
+
+
+@pytest.mark.parametrize("w,h,pw,ph,rows", [(64, 64, 72, 72, (3, 40)), (200, 150, 224, 168, (0, 1, 77, 149)),
+                                            (90, 60, 98, 64, ()), (90, 60, 98, 64, (59,))])
+def test_lds_fft_correction_sparse_rows(sess, w, h, pw, ph, rows):
+    """The correction with a row mask (empty model rows neither read nor
+    transformed) and a column-major PSF spectrum is bit-identical to the dense
+    row-major sequence: the skipped rows are exact zeros either way."""
+    c = conv_create(sess, pw, ph, True)
+    rng = np.random.default_rng(pw + len(rows))
+    psf = rng.standard_normal((h, w)).astype(np.float32)
+    model = np.zeros((h, w), np.float32)
+    for y in rows:
+        xs = rng.choice(w, 5, replace=False)
+        model[y, xs] = rng.standard_normal(5).astype(np.float32)
+    residual = rng.standard_normal((h, w)).astype(np.float32)
+    ox, oy = (pw - w) // 2, (ph - h) // 2
+    mask = np.zeros(ph, np.uint8)
+    for y in rows:
+        mask[y + oy] = 1
+    dpsf, dmod = sess.array(psf), sess.array(model)
+    dres_a, dres_b = sess.array(residual), sess.array(residual)
+    dmask = sess.array(mask, dtype=np.uint8)
+    kplane = sess.array(shape=(ph, pw))
+    kspec = sess.array(shape=(ph, pw // 2 + 1), dtype=np.complex128)
+    kspec_cm = sess.array(shape=(pw // 2 + 1, ph), dtype=np.complex128)
+    work = sess.array(shape=(ph, pw // 2 + 1), dtype=np.complex128)
+    sess.rdl.rdl_prepare_psf_kernel(sess.h, kplane.vp, pw, ph, dpsf.vp, w, h)
+    sess.rdl.rdl_conv_forward(c, kplane.vp, kspec.vp)
+    # column-major forward spectrum == the row-major one transposed
+    sess.rdl.rdl_conv_rows_forward(c, kplane.vp, pw, ph, 0, 0, work.vp)
+    sess.rdl.rdl_conv_columns_ex(c, work.vp, kspec_cm.vp, None, 0, C.c_double(1.0), None,
+                                 RDL_CONV_ROW_MAJOR, RDL_CONV_COL_MAJOR)
+    assert np.array_equal(kspec_cm.get(), kspec.get().T)
+    norm = C.c_double(1.0 / (pw * ph))
+    sess.rdl.rdl_conv_rows_forward(c, dmod.vp, w, h, ox, oy, work.vp)
+    sess.rdl.rdl_conv_columns(c, work.vp, work.vp, kspec.vp, 1, norm)
+    sess.rdl.rdl_conv_rows_inverse(c, work.vp, dres_a.vp, w, h, ox, oy, 1)
+    work.upload(np.full((ph, pw // 2 + 1), np.nan, np.complex128))  # skipped rows stay unread
+    sess.rdl.rdl_conv_rows_forward_masked(c, dmod.vp, w, h, ox, oy, work.vp, dmask.vp)
+    sess.rdl.rdl_conv_columns_ex(c, work.vp, work.vp, kspec_cm.vp, 1, norm, dmask.vp,
+                                 RDL_CONV_COL_MAJOR, RDL_CONV_ROW_MAJOR)
+    sess.rdl.rdl_conv_rows_inverse(c, work.vp, dres_b.vp, w, h, ox, oy, 1)
+    a, b = dres_a.get(), dres_b.get()
+    assert np.array_equal(a, b)
+    if not rows:
+        assert np.array_equal(b, residual)
+    for x in (dpsf, dmod, dres_a, dres_b, dmask, kplane, kspec, kspec_cm, work):
+        x.free()
+    sess.rdl.rdl_conv_destroy(c)
