@@ -67,7 +67,7 @@ FAMILIES = ["conv_rows", "conv_cols", "conv64_rows", "conv64_cols", "conv_rows_s
             "conv_cols_sparse", "conv64_rows_sparse", "conv64_cols_sparse", "fft", "fft64",
             "spectrum_multiply", "spectrum_multiply64", "find_peak", "subminor_loop",
             "subminor_select", "trim_subtract", "add", "integrate", "rms", "axpy",
-            "radix_select", "iuwt", "box"]
+            "radix_select", "iuwt", "box", "stamp_model"]
 
 
 class Timing:

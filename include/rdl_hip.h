@@ -245,6 +245,14 @@ int rdl_subminor_model(rdl_subminor* h, uint32_t image_index, float* d_dest,
                        uint32_t oy, int mode);
 /* As mode 0 of rdl_subminor_model, into a zeroed float64 plane (input of the
  * double-precision residual correction, rdl_fft64_convolve). */
+/* d_model += (that model convolved circularly with the odd n x n shape
+ * kernel centred at (n/2, n/2)): the scale > 0 model update of the multiscale
+ * fast sub-minor path (multiscale_algorithm.cc:442-460: GetFullIndividualModel,
+ * Transform, AddWithFactor) by direct stamping in a fixed component order
+ * instead of a pair of full-image FFTs. */
+int rdl_subminor_add_shape_model(rdl_subminor* h, uint32_t image_index,
+                                 const float* d_kernel, uint32_t n, float* d_model,
+                                 uint32_t width, uint32_t height);
 /* Row occupancy of that model in a plane with the model at row offset oy:
  * d_rows[y] = 1 where row y holds a non-zero model value, else 0 (n_rows
  * bytes). Lets the correction's transform skip the empty rows
@@ -292,6 +300,17 @@ int rdl_fft64_convolve(rdl_fft* f, double* d_image, const void* d_kernel_spectru
 typedef struct rdl_conv rdl_conv;
 int rdl_conv_create(rdl_session* s, uint32_t width, uint32_t height, int f64,
                     rdl_conv** out);
+/* As rdl_conv_create with an explicit column-pass strategy: AUTO (currently
+ * the one-pass kernel), SINGLE forces the one-pass column kernel, SPLIT the
+ * split (four-step, coalesced) passes (RDL_ERR_UNSUPPORTED
+ * when the column length has no split into two factors >= 4). Spectra have
+ * the same layout either way. rdl_conv_columns_split reports the choice. */
+#define RDL_CONV_COLUMNS_AUTO 0
+#define RDL_CONV_COLUMNS_SINGLE 1
+#define RDL_CONV_COLUMNS_SPLIT 2
+int rdl_conv_create_ex(rdl_session* s, uint32_t width, uint32_t height, int f64,
+                       int columns, rdl_conv** out);
+int rdl_conv_columns_split(const rdl_conv* c);
 int rdl_conv_destroy(rdl_conv* c);
 size_t rdl_conv_spectrum_bytes(const rdl_conv* c);
 /* Row transforms of the plane holding the in_w x in_h image d_in at offset

@@ -58,7 +58,10 @@ __device__ __forceinline__ Cx<T> Scale(Cx<T> a, T s) {
   return {a.x * s, a.y * s};
 }
 
-constexpr uint32_t kFftThreads = 1024;
+#ifndef RDL_FFT_THREADS
+#define RDL_FFT_THREADS 1024
+#endif
+constexpr uint32_t kFftThreads = RDL_FFT_THREADS;
 constexpr uint32_t kFftMaxPasses = 24;
 constexpr size_t kFftLdsBytes = 160 * 1024;
 
@@ -273,11 +276,15 @@ struct Dft<T, 9> {
 
 // ---- one Stockham pass over `count` transforms of length n held in LDS
 // (in place: all butterfly inputs are read to registers before the barrier)
+// Not inlined on purpose: with every radix inlined into one kernel the
+// register allocator spilled 150-300 bytes per lane (scratch traffic showed
+// up as 4-5x the algorithmic HBM writes); as separate functions each pass is
+// allocated on its own (no spills; the call saves a few callee-saved VGPRs).
 template <typename T, int R>
-__device__ __forceinline__ void StockhamPass(Cx<T>* buf, uint32_t n,
+__device__ __attribute__((noinline)) void StockhamPass(Cx<T>* buf, uint32_t n,
                                              uint32_t count, uint32_t ns,
                                              const Cx<T>* __restrict__ tw,
-                                             uint32_t tid) {
+                                             uint32_t tid, uint32_t stride) {
   constexpr uint32_t BPT = (MaxElems<T>() / R + kFftThreads - 1) / kFftThreads;
   const uint32_t nb = n / R;
   const uint32_t total = nb * count;
@@ -288,7 +295,7 @@ __device__ __forceinline__ void StockhamPass(Cx<T>* buf, uint32_t n,
     const uint32_t b = tid + i * kFftThreads;
     if (b < total) {
       const uint32_t t = b / nb, j = b - t * nb;
-      const Cx<T>* base = buf + size_t(t) * n;
+      const Cx<T>* base = buf + size_t(t) * stride;
 #pragma unroll
       for (int r = 0; r < R; ++r) v[i][r] = base[j + r * nb];
     }
@@ -305,7 +312,7 @@ __device__ __forceinline__ void StockhamPass(Cx<T>* buf, uint32_t n,
         for (int r = 1; r < R; ++r) v[i][r] = Mul(v[i][r], tw[k * r * m]);
       }
       Dft<T, R>::Run(v[i]);
-      Cx<T>* base = buf + size_t(t) * n;
+      Cx<T>* base = buf + size_t(t) * stride;
       const uint32_t d = (j / ns) * ns * R + k;
 #pragma unroll
       for (int r = 0; r < R; ++r) base[d + r * ns] = v[i][r];
@@ -314,23 +321,29 @@ __device__ __forceinline__ void StockhamPass(Cx<T>* buf, uint32_t n,
   __syncthreads();
 }
 
-// Forward complex FFT (natural order in and out) of `count` transforms.
+// Forward complex FFT (natural order in and out) of `count` transforms, each
+// `stride` elements apart (>= n; padding keeps transposing loads off one bank).
 template <typename T>
 __device__ void LdsFftForward(Cx<T>* buf, const LdsPlan& p, uint32_t count,
-                              uint32_t tid) {
+                              uint32_t tid, uint32_t stride = 0) {
+  if (stride == 0) stride = p.n;
   const Cx<T>* tw = static_cast<const Cx<T>*>(p.tw);
   uint32_t ns = 1;
   for (uint32_t q = 0; q < p.n_pass; ++q) {
     const uint32_t r = p.radix[q];
     switch (r) {
-      case 16: StockhamPass<T, 16>(buf, p.n, count, ns, tw, tid); break;
-      case 9: StockhamPass<T, 9>(buf, p.n, count, ns, tw, tid); break;
-      case 8: StockhamPass<T, 8>(buf, p.n, count, ns, tw, tid); break;
-      case 4: StockhamPass<T, 4>(buf, p.n, count, ns, tw, tid); break;
-      case 2: StockhamPass<T, 2>(buf, p.n, count, ns, tw, tid); break;
-      case 3: StockhamPass<T, 3>(buf, p.n, count, ns, tw, tid); break;
-      case 5: StockhamPass<T, 5>(buf, p.n, count, ns, tw, tid); break;
-      default: StockhamPass<T, 7>(buf, p.n, count, ns, tw, tid); break;
+      case 16:
+        if constexpr (sizeof(T) == 4) StockhamPass<T, 16>(buf, p.n, count, ns, tw, tid, stride);
+        break;
+      case 9:
+        if constexpr (sizeof(T) == 4) StockhamPass<T, 9>(buf, p.n, count, ns, tw, tid, stride);
+        break;
+      case 8: StockhamPass<T, 8>(buf, p.n, count, ns, tw, tid, stride); break;
+      case 4: StockhamPass<T, 4>(buf, p.n, count, ns, tw, tid, stride); break;
+      case 2: StockhamPass<T, 2>(buf, p.n, count, ns, tw, tid, stride); break;
+      case 3: StockhamPass<T, 3>(buf, p.n, count, ns, tw, tid, stride); break;
+      case 5: StockhamPass<T, 5>(buf, p.n, count, ns, tw, tid, stride); break;
+      default: StockhamPass<T, 7>(buf, p.n, count, ns, tw, tid, stride); break;
     }
     ns *= r;
   }
@@ -530,8 +543,136 @@ __global__ __launch_bounds__(kFftThreads) void Columns(ColArgs a,
   }
 }
 
+// ------------------------------------------- split (four-step) column passes
+// A column transform of length N = N1 * N2 in two coalesced passes instead of
+// one strided one (with one double column per workgroup the single-pass
+// column kernel touches a separate 128-byte line for every element):
+//   A  : for each n2, the N1 elements at rows N2*n1 + n2 (strided rows, but
+//        `cols` adjacent columns per row, so every load/store is a full
+//        line): length-N1 FFT, x W_N^(n2*k1), back to rows N2*k1 + n2.
+//   B  : for each k1, the N2 elements at rows N2*k1 + n2 (one contiguous
+//        block of rows): length-N2 FFT -> X[k1 + N1*k2].
+// The inverse runs the same passes backwards (B^-1 over the block, then A^-1
+// with conj twiddles). B stores/loads the spectrum in natural row order
+// (row k1 + N1*k2), so spectra keep the single-pass layout; the fused
+// convolution (forward, x K x s, inverse) keeps B and B^-1 in one pass over
+// the block.
+struct SplitArgs {
+  LdsPlan plan;        // sub-transform (N1 for A, N2 for B)
+  uint32_t n, n1, n2;  // column length and its split
+  uint32_t n_cols;     // spectrum columns (W/2+1)
+  uint32_t ld;         // spectrum row stride
+  uint32_t cols;       // adjacent columns per tile
+  uint32_t groups;     // sub-columns per tile (A: n2 values, B: k1 values)
+  uint32_t col_tiles;  // tiles across the columns
+  uint32_t n_groups;   // A: n2, B: n1
+  const void* tw_n;    // exp(-2 pi i k / N), k < N
+  const uint8_t* row_mask;  // A forward: rows known zero are not read
+  double scale;
+  int mode;            // A: 0 forward, 1 inverse. B: 0 fwd, 1 fwd*K*s+inv, 2 *K*s+inv
+};
+
+template <typename T>
+__global__ __launch_bounds__(kFftThreads) void ColumnsSplitA(SplitArgs a,
+                                                             const Cx<T>* in,
+                                                             Cx<T>* out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  Cx<T>* buf = reinterpret_cast<Cx<T>*>(lds_raw);
+  const uint32_t ct = blockIdx.x % a.col_tiles, gt = blockIdx.x / a.col_tiles;
+  const uint32_t k0 = ct * a.cols, g0 = gt * a.groups;
+  const uint32_t cnt = min(a.cols, a.n_cols - k0);
+  const uint32_t gcnt = min(a.groups, a.n_groups - g0);
+  const uint32_t tid = threadIdx.x, n1 = a.n1, n2 = a.n2, C = a.cols;
+  const bool inverse = a.mode == 1;
+  const Cx<T>* __restrict__ twn = static_cast<const Cx<T>*>(a.tw_n);
+  const uint32_t total = n1 * gcnt * C;
+  for (uint32_t idx = tid; idx < total; idx += kFftThreads) {
+    const uint32_t j = idx % C, rest = idx / C;
+    const uint32_t g = rest % gcnt, i1 = rest / gcnt;
+    const uint32_t sub = g0 + g;
+    const uint32_t row = n2 * i1 + sub;
+    Cx<T> v{T(0), T(0)};
+    if (j < cnt && !(a.row_mask && a.row_mask[row] == 0))
+      v = in[size_t(row) * a.ld + k0 + j];
+    if (inverse)  // conj(v * conj(w)) = conj(v) * w, w = W_N^(n2*k1)
+      v = Mul(Conj(v), twn[(uint64_t(sub) * i1) % a.n]);
+    buf[size_t(g * C + j) * (n1 + 1) + i1] = v;
+  }
+  __syncthreads();
+  LdsFftForward<T>(buf, a.plan, gcnt * C, tid, n1 + 1);
+  for (uint32_t idx = tid; idx < total; idx += kFftThreads) {
+    const uint32_t j = idx % C, rest = idx / C;
+    const uint32_t g = rest % gcnt, i1 = rest / gcnt;
+    const uint32_t sub = g0 + g;
+    Cx<T> v = buf[size_t(g * C + j) * (n1 + 1) + i1];
+    v = inverse ? Conj(v) : Mul(v, twn[(uint64_t(sub) * i1) % a.n]);
+    if (j < cnt) out[size_t(n2 * i1 + sub) * a.ld + k0 + j] = v;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kFftThreads) void ColumnsSplitB(SplitArgs a,
+                                                             const Cx<T>* in,
+                                                             Cx<T>* out,
+                                                             const Cx<T>* kern) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  Cx<T>* buf = reinterpret_cast<Cx<T>*>(lds_raw);
+  const uint32_t ct = blockIdx.x % a.col_tiles, gt = blockIdx.x / a.col_tiles;
+  const uint32_t k0 = ct * a.cols, g0 = gt * a.groups;
+  const uint32_t cnt = min(a.cols, a.n_cols - k0);
+  const uint32_t gcnt = min(a.groups, a.n_groups - g0);
+  const uint32_t tid = threadIdx.x, n1 = a.n1, n2 = a.n2, C = a.cols;
+  const T s = T(a.scale);
+  const uint32_t total = n2 * gcnt * C;
+  // mode 0/1 read the block (rows n2*k1 + i2), mode 2 the natural spectrum
+  // (rows k1 + n1*k2); mode 2 starts in the conjugated domain
+  for (uint32_t idx = tid; idx < total; idx += kFftThreads) {
+    const uint32_t j = idx % C, rest = idx / C;
+    const uint32_t g = rest % gcnt, i2 = rest / gcnt;
+    const uint32_t k1 = g0 + g;
+    Cx<T> v{T(0), T(0)};
+    if (a.mode == 2) {
+      const size_t at = size_t(k1 + n1 * i2) * a.ld + k0 + j;
+      if (j < cnt) v = Conj(Scale(Mul(in[at], kern[at]), s));
+    } else if (j < cnt) {
+      v = in[size_t(n2 * k1 + i2) * a.ld + k0 + j];
+    }
+    buf[size_t(g * C + j) * (n2 + 1) + i2] = v;
+  }
+  __syncthreads();
+  LdsFftForward<T>(buf, a.plan, gcnt * C, tid, n2 + 1);
+  if (a.mode == 1) {
+    for (uint32_t idx = tid; idx < total; idx += kFftThreads) {
+      const uint32_t j = idx % C, rest = idx / C;
+      const uint32_t g = rest % gcnt, i2 = rest / gcnt;
+      const uint32_t k1 = g0 + g;
+      Cx<T>& v = buf[size_t(g * C + j) * (n2 + 1) + i2];
+      const Cx<T> k = j < cnt ? kern[size_t(k1 + n1 * i2) * a.ld + k0 + j]
+                              : Cx<T>{T(0), T(0)};
+      v = Conj(Scale(Mul(v, k), s));
+    }
+    __syncthreads();
+    LdsFftForward<T>(buf, a.plan, gcnt * C, tid, n2 + 1);
+  }
+  for (uint32_t idx = tid; idx < total; idx += kFftThreads) {
+    const uint32_t j = idx % C, rest = idx / C;
+    const uint32_t g = rest % gcnt, i2 = rest / gcnt;
+    const uint32_t k1 = g0 + g;
+    const Cx<T> v = buf[size_t(g * C + j) * (n2 + 1) + i2];
+    if (j >= cnt) continue;
+    if (a.mode == 0)  // X[k1 + n1*k2] in natural order
+      out[size_t(k1 + n1 * i2) * a.ld + k0 + j] = v;
+    else  // back from the conjugated domain, block layout for A^-1
+      out[size_t(n2 * k1 + i2) * a.ld + k0 + j] = Conj(v);
+  }
+}
+
 // ---------------------------------------------------------------- planning
-bool Factorize(uint32_t n, std::vector<uint8_t>& radix) {
+// Double plans stop at radix 8 and 3: the composite radix-16 / radix-9
+// butterflies hold twice their inputs in registers, which in double spills
+// past the 128 VGPRs a 1024-thread workgroup leaves each wave (the spill
+// traffic showed up as 4-5x the algorithmic HBM writes).
+bool Factorize(uint32_t n, bool f64, std::vector<uint8_t>& radix) {
   radix.clear();
   uint32_t m = n;
   uint32_t twos = 0;
@@ -539,14 +680,15 @@ bool Factorize(uint32_t n, std::vector<uint8_t>& radix) {
     m /= 2;
     ++twos;
   }
-  while (twos >= 4) {
-    radix.push_back(16);
-    twos -= 4;
+  const uint32_t big2 = f64 ? 3 : 4;
+  while (twos >= big2) {
+    radix.push_back(uint8_t(1u << big2));
+    twos -= big2;
   }
   if (twos == 3) radix.push_back(8);
   if (twos == 2) radix.push_back(4);
   if (twos == 1) radix.push_back(2);
-  while (m % 9 == 0) {
+  while (!f64 && m % 9 == 0) {
     m /= 9;
     radix.push_back(9);
   }
@@ -568,13 +710,22 @@ struct rdl_conv {
   void* tw_col = nullptr;
   rdl::LdsPlan row_plan{}, col_plan{};
   uint32_t row_count = 1, col_count = 1;
+  // split (four-step) column passes
+  bool split = false;
+  uint32_t n1 = 0, n2 = 0;
+  rdl::LdsPlan plan_n1{}, plan_n2{};
+  void* tw_n1 = nullptr;
+  void* tw_n2 = nullptr;
+  uint32_t split_cols = 0;
+  void* scratch = nullptr;  // spectrum-sized, for the out-of-place B passes
+  size_t scratch_bytes = 0;
 };
 
 namespace {
 
 int MakePlan(rdl_conv* c, uint32_t n, bool f64, rdl::LdsPlan* plan, void** tw) {
   std::vector<uint8_t> radix;
-  if (!rdl::Factorize(n, radix)) {
+  if (!rdl::Factorize(n, f64, radix)) {
     rdl::SetError("LDS FFT: length " + std::to_string(n) + " is not 2/3/5/7-smooth");
     return RDL_ERR_UNSUPPORTED;
   }
@@ -683,6 +834,96 @@ int LaunchColumns(rdl_conv* c, const void* in, void* out, const void* kern,
   return RDL_OK;
 }
 
+// one A or B pass over the whole spectrum
+template <typename T>
+int LaunchSplit(rdl_conv* c, bool pass_b, int mode, const void* in, void* out,
+                const void* kern, double scale, const uint8_t* row_mask) {
+  rdl::SplitArgs a{};
+  a.plan = pass_b ? c->plan_n2 : c->plan_n1;
+  a.n = c->height;
+  a.n1 = c->n1;
+  a.n2 = c->n2;
+  a.n_cols = c->width / 2 + 1;
+  a.ld = a.n_cols;
+  a.cols = c->split_cols;
+  const uint32_t sub_len = pass_b ? c->n2 : c->n1;
+  // elements per workgroup: half the LDS for double (two workgroups per CU
+  // overlap one's loads with the other's transform), the engine's maximum
+  // for float; the padded stride must fit as well
+  const uint32_t target = c->f64 ? rdl::kMaxWgElems / 2 : rdl::kMaxWgElems;
+  a.groups = std::max<uint32_t>(1, target / (a.cols * (sub_len + 1)));
+  a.n_groups = pass_b ? c->n1 : c->n2;
+  a.groups = std::min(a.groups, a.n_groups);
+  a.col_tiles = (a.n_cols + a.cols - 1) / a.cols;
+  a.tw_n = c->col_plan.tw;
+  a.row_mask = row_mask;
+  a.scale = scale;
+  a.mode = mode;
+  const uint32_t grid = a.col_tiles * ((a.n_groups + a.groups - 1) / a.groups);
+  const size_t lds = size_t(a.groups) * a.cols * (sub_len + 1) * sizeof(rdl::Cx<T>);
+  if (pass_b) {
+    auto k = rdl::ColumnsSplitB<T>;
+    static std::atomic<uint64_t> attr_done{0};
+    RDL_TRY(rdl::SetMaxLdsOnce(reinterpret_cast<const void*>(k),
+                               int(rdl::kFftLdsBytes), c->s->device, attr_done));
+    k<<<grid, rdl::kFftThreads, lds, c->s->stream>>>(
+        a, static_cast<const rdl::Cx<T>*>(in), static_cast<rdl::Cx<T>*>(out),
+        static_cast<const rdl::Cx<T>*>(kern));
+  } else {
+    auto k = rdl::ColumnsSplitA<T>;
+    static std::atomic<uint64_t> attr_done{0};
+    RDL_TRY(rdl::SetMaxLdsOnce(reinterpret_cast<const void*>(k),
+                               int(rdl::kFftLdsBytes), c->s->device, attr_done));
+    k<<<grid, rdl::kFftThreads, lds, c->s->stream>>>(
+        a, static_cast<const rdl::Cx<T>*>(in), static_cast<rdl::Cx<T>*>(out));
+  }
+  RDL_HIP_CHECK(hipGetLastError());
+  return RDL_OK;
+}
+
+int EnsureSplitScratch(rdl_conv* c, size_t bytes) {
+  if (c->scratch_bytes >= bytes) return RDL_OK;
+  if (c->scratch) {
+    RDL_HIP_CHECK(hipStreamSynchronize(c->s->stream));
+    RDL_HIP_CHECK(hipFree(c->scratch));
+    c->scratch = nullptr;
+    c->scratch_bytes = 0;
+  }
+  RDL_HIP_CHECK(hipMalloc(&c->scratch, bytes));
+  c->scratch_bytes = bytes;
+  return RDL_OK;
+}
+
+// the column pass of any mode through the split passes (see SplitArgs)
+template <typename T>
+int LaunchColumnsSplit(rdl_conv* c, const void* in, void* out, const void* kern,
+                       int mode, double scale, const uint8_t* row_mask) {
+  const size_t bytes = size_t(c->width / 2 + 1) * c->height * sizeof(rdl::Cx<T>);
+  if (mode == 0) {  // A: in -> scratch, B: scratch -> out (natural order)
+    RDL_TRY(EnsureSplitScratch(c, bytes));
+    RDL_TRY(LaunchSplit<T>(c, false, 0, in, c->scratch, nullptr, 1.0, row_mask));
+    return LaunchSplit<T>(c, true, 0, c->scratch, out, nullptr, 1.0, nullptr);
+  }
+  if (mode == 1) {  // A: in -> out, B (fwd x K x s inv) and A^-1 in place
+    RDL_TRY(LaunchSplit<T>(c, false, 0, in, out, nullptr, 1.0, row_mask));
+    RDL_TRY(LaunchSplit<T>(c, true, 1, out, out, kern, scale, nullptr));
+    return LaunchSplit<T>(c, false, 1, out, out, nullptr, 1.0, nullptr);
+  }
+  // mode 2: B (x K x s inv) from the natural spectrum into scratch, A^-1 -> out
+  RDL_TRY(EnsureSplitScratch(c, bytes));
+  RDL_TRY(LaunchSplit<T>(c, true, 2, in, c->scratch, kern, scale, nullptr));
+  return LaunchSplit<T>(c, false, 1, c->scratch, out, nullptr, 1.0, nullptr);
+}
+
+template <typename T>
+int LaunchColumnsAny(rdl_conv* c, const void* in, void* out, const void* kern,
+                     int mode, double scale, const uint8_t* row_mask, int kern_cm,
+                     int out_cm) {
+  if (c->split)
+    return LaunchColumnsSplit<T>(c, in, out, kern, mode, scale, row_mask);
+  return LaunchColumns<T>(c, in, out, kern, mode, scale, row_mask, kern_cm, out_cm);
+}
+
 double SpectrumBytes(const rdl_conv* c) {
   return double(c->width / 2 + 1) * c->height * (c->f64 ? 16.0 : 8.0);
 }
@@ -693,7 +934,16 @@ extern "C" {
 
 int rdl_conv_create(rdl_session* s, uint32_t width, uint32_t height, int f64,
                     rdl_conv** out) {
+  return rdl_conv_create_ex(s, width, height, f64, RDL_CONV_COLUMNS_AUTO, out);
+}
+
+int rdl_conv_columns_split(const rdl_conv* c) { return c && c->split ? 1 : 0; }
+
+int rdl_conv_create_ex(rdl_session* s, uint32_t width, uint32_t height, int f64,
+                       int columns, rdl_conv** out) {
   RDL_ARG_CHECK(s && out, "NULL argument");
+  RDL_ARG_CHECK(columns >= RDL_CONV_COLUMNS_AUTO && columns <= RDL_CONV_COLUMNS_SPLIT,
+                "bad column strategy");
   RDL_ARG_CHECK(width >= 2 && height >= 2, "bad size");
   *out = nullptr;
   const size_t esz = f64 ? 16 : 8;
@@ -717,6 +967,32 @@ int rdl_conv_create(rdl_session* s, uint32_t width, uint32_t height, int f64,
   c->col_count = uint32_t(std::max<size_t>(1, std::min<size_t>(budget / (height * esz), 64)));
   c->row_count = std::min<uint32_t>(c->row_count, uint32_t(max_elems / width));
   c->col_count = std::min<uint32_t>(c->col_count, uint32_t(max_elems / height));
+  // split columns: N = N1 * N2 with N1 the largest divisor <= sqrt(N)
+  uint32_t n1 = 1;
+  for (uint32_t d = 1; uint64_t(d) * d <= height; ++d)
+    if (height % d == 0) n1 = d;
+  const uint32_t n2 = height / n1;
+  const bool can_split = n1 >= 4 && n2 >= 4;
+  // AUTO keeps the single pass: measured on MI355X (tools/bench_fft.py) the
+  // split passes are faster only for the shared-spectrum inverse in float
+  // (8192^2: 606 vs 909 us) and slower for the fused convolutions
+  const bool want_split = columns == RDL_CONV_COLUMNS_SPLIT;
+  if (columns == RDL_CONV_COLUMNS_SPLIT && !can_split) {
+    rdl::SetError("LDS FFT: column length " + std::to_string(height) +
+                  " has no split into two factors >= 4");
+    return RDL_ERR_UNSUPPORTED;
+  }
+  if (want_split && can_split) {
+    c->split = true;
+    c->n1 = n1;
+    c->n2 = n2;
+    RDL_TRY(MakePlan(c.get(), n1, c->f64, &c->plan_n1, &c->tw_n1));
+    RDL_TRY(MakePlan(c.get(), n2, c->f64, &c->plan_n2, &c->tw_n2));
+    // 256-byte row segments, as many as the sub-lengths allow
+    c->split_cols = std::max<uint32_t>(
+        1, std::min<uint32_t>(c->f64 ? 16 : 32,
+                              rdl::kMaxWgElems / (std::max(n1, n2) + 1)));
+  }
   *out = c.release();
   return RDL_OK;
 }
@@ -726,6 +1002,9 @@ int rdl_conv_destroy(rdl_conv* c) {
   (void)hipStreamSynchronize(c->s->stream);
   if (c->tw_row) (void)hipFree(c->tw_row);
   if (c->tw_col) (void)hipFree(c->tw_col);
+  if (c->tw_n1) (void)hipFree(c->tw_n1);
+  if (c->tw_n2) (void)hipFree(c->tw_n2);
+  if (c->scratch) (void)hipFree(c->scratch);
   delete c;
   return RDL_OK;
 }
@@ -768,10 +1047,10 @@ int rdl_conv_columns(rdl_conv* c, const void* d_in, void* d_out,
   const double sb = SpectrumBytes(c);
   rdl::ScopedTiming t(c->s, c->f64 ? "conv64_cols" : "conv_cols",
                       mode == 0 ? 2.0 * sb : 3.0 * sb);
-  return c->f64 ? LaunchColumns<double>(c, d_in, d_out, d_kernel, mode, scale,
-                                        nullptr, 0, 0)
-                : LaunchColumns<float>(c, d_in, d_out, d_kernel, mode, scale,
-                                       nullptr, 0, 0);
+  return c->f64 ? LaunchColumnsAny<double>(c, d_in, d_out, d_kernel, mode, scale,
+                                           nullptr, 0, 0)
+                : LaunchColumnsAny<float>(c, d_in, d_out, d_kernel, mode, scale,
+                                          nullptr, 0, 0);
 }
 
 int rdl_conv_columns_ex(rdl_conv* c, const void* d_in, void* d_out,
@@ -787,6 +1066,9 @@ int rdl_conv_columns_ex(rdl_conv* c, const void* d_in, void* d_out,
   RDL_ARG_CHECK(kernel_layout == RDL_CONV_ROW_MAJOR ||
                     kernel_layout == RDL_CONV_COL_MAJOR,
                 "bad kernel layout");
+  RDL_ARG_CHECK(!c->split || (kernel_layout == RDL_CONV_ROW_MAJOR &&
+                              out_layout == RDL_CONV_ROW_MAJOR),
+                "split column plans use the row-major layout only");
   const double sb = SpectrumBytes(c);
   // with a row mask the input reads are skipped for the zero rows: count
   // the kernel read and the output write only (a lower bound)
@@ -797,10 +1079,10 @@ int rdl_conv_columns_ex(rdl_conv* c, const void* d_in, void* d_out,
   rdl::ScopedTiming t(c->s, fam, bytes);
   const int kcm = kernel_layout == RDL_CONV_COL_MAJOR;
   const int ocm = out_layout == RDL_CONV_COL_MAJOR;
-  return c->f64 ? LaunchColumns<double>(c, d_in, d_out, d_kernel, mode, scale,
-                                        d_row_mask, kcm, ocm)
-                : LaunchColumns<float>(c, d_in, d_out, d_kernel, mode, scale,
-                                       d_row_mask, kcm, ocm);
+  return c->f64 ? LaunchColumnsAny<double>(c, d_in, d_out, d_kernel, mode, scale,
+                                           d_row_mask, kcm, ocm)
+                : LaunchColumnsAny<float>(c, d_in, d_out, d_kernel, mode, scale,
+                                          d_row_mask, kcm, ocm);
 }
 
 int rdl_conv_rows_inverse(rdl_conv* c, const void* d_spec, float* d_out,

@@ -479,6 +479,92 @@ __global__ __launch_bounds__(256) void MarkModelRows(const uint32_t* pos,
     if (m[i] != 0.0f) rows[(pos[i] >> 16) + oy] = 1;
 }
 
+// Model update of a scale > 0 outer iteration: model += the selection's
+// component values convolved (circularly, as the FFT convolution of the
+// reference does) with the scale's n x n shape kernel, by direct stamping.
+// One workgroup per 64 x 64 output tile walks the selection in index order,
+// keeps the components whose (wrapped) stamp reaches the tile, and sums
+// m_c * k[y - y_c + n/2][x - x_c + n/2] per pixel in that order: a fixed
+// summation order, so the result is reproducible.
+constexpr uint32_t kStampTile = 64;
+constexpr uint32_t kStampThreads = 256;
+constexpr uint32_t kStampRows = kStampTile * kStampTile / kStampThreads;  // 16
+
+// d in (-size, 2*size) -> d mod size
+__device__ __forceinline__ uint32_t WrapDist(int32_t d, uint32_t size) {
+  if (d < 0) d += int32_t(size);
+  if (d >= int32_t(size)) d -= int32_t(size);
+  return uint32_t(d);
+}
+
+__global__ __launch_bounds__(kStampThreads) void StampShapeModel(
+    const uint32_t* __restrict__ pos, const float* __restrict__ m, uint64_t n_sel,
+    const float* __restrict__ kern, uint32_t n, float* __restrict__ model,
+    uint32_t width, uint32_t height, uint32_t tiles_x) {
+  __shared__ uint32_t list[kStampThreads];
+  __shared__ uint32_t wave_count[kStampThreads / 64];
+  __shared__ uint32_t n_list;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t tx0 = (blockIdx.x % tiles_x) * kStampTile;
+  const uint32_t ty0 = (blockIdx.x / tiles_x) * kStampTile;
+  const uint32_t lx = min(kStampTile, width - tx0), ly = min(kStampTile, height - ty0);
+  const uint32_t h = n / 2;
+  const uint32_t px = tx0 + (tid % kStampTile);
+  const uint32_t py0 = ty0 + tid / kStampTile;
+  float acc[kStampRows];
+#pragma unroll
+  for (uint32_t r = 0; r < kStampRows; ++r) acc[r] = 0.0f;
+  bool any = false;
+  for (uint64_t base = 0; base < n_sel; base += kStampThreads) {
+    const uint64_t c = base + tid;
+    bool hit = false;
+    if (c < n_sel && m[c] != 0.0f) {
+      const uint32_t pk = pos[c];
+      const uint32_t xc = pk & 0xffffu, yc = pk >> 16;
+      const uint32_t dx0 = WrapDist(int32_t(tx0) - int32_t(xc) + int32_t(h), width);
+      const uint32_t dy0 = WrapDist(int32_t(ty0) - int32_t(yc) + int32_t(h), height);
+      hit = (dx0 < n || dx0 + lx - 1 >= width) && (dy0 < n || dy0 + ly - 1 >= height);
+    }
+    // order-preserving compaction of the hits (wave order, then lane order)
+    const uint64_t b = __ballot(hit);
+    if (lane == 0) wave_count[wave] = uint32_t(__popcll(b));
+    __syncthreads();
+    uint32_t off = 0, total = 0;
+    for (uint32_t w = 0; w < kStampThreads / 64; ++w) {
+      if (w < wave) off += wave_count[w];
+      total += wave_count[w];
+    }
+    if (hit) list[off + uint32_t(__popcll(b & ((uint64_t(1) << lane) - 1)))] = uint32_t(c - base);
+    if (tid == 0) n_list = total;
+    __syncthreads();
+    const uint32_t cnt = n_list;
+    any |= cnt != 0;
+    for (uint32_t i = 0; i < cnt; ++i) {
+      const uint64_t cc = base + list[i];
+      const uint32_t pk = pos[cc];
+      const float v = m[cc];
+      const uint32_t xc = pk & 0xffffu, yc = pk >> 16;
+      const uint32_t dx = WrapDist(int32_t(px) - int32_t(xc) + int32_t(h), width);
+      if (dx >= n || px >= width) continue;
+      constexpr uint32_t kStep = kStampThreads / kStampTile;
+      uint32_t dy = WrapDist(int32_t(py0) - int32_t(yc) + int32_t(h), height);
+#pragma unroll
+      for (uint32_t r = 0; r < kStampRows; ++r) {
+        if (dy < n && py0 + r * kStep < height) acc[r] += v * kern[dy * n + dx];
+        dy += kStep;
+        if (dy >= height) dy -= height;
+      }
+    }
+    __syncthreads();
+  }
+  if (!any || px >= width) return;
+#pragma unroll
+  for (uint32_t r = 0; r < kStampRows; ++r) {
+    const uint32_t py = py0 + r * (kStampThreads / kStampTile);
+    if (py < height) model[size_t(py) * width + px] += acc[r];
+  }
+}
+
 // ------------------------------------------------- register-resident loop
 // SubminorLoopReg: the same loop with each thread's ITEMS selected pixels
 // (positions, residuals, model values) held in VGPRs, so one iteration is
@@ -1218,6 +1304,31 @@ int rdl_subminor_model(rdl_subminor* h, uint32_t image_index, float* d_dest,
   rdl::ScatterModel<float><<<grid, 256, 0, s->stream>>>(
       h->d_pos, h->d_m + size_t(image_index) * h->n_selected, h->n_selected,
       d_dest, dest_w, ox, oy, mode == 1);
+  RDL_HIP_CHECK(hipGetLastError());
+  return RDL_OK;
+}
+
+int rdl_subminor_add_shape_model(rdl_subminor* h, uint32_t image_index,
+                                 const float* d_kernel, uint32_t n, float* d_model,
+                                 uint32_t width, uint32_t height) {
+  RDL_ARG_CHECK(h && d_kernel && d_model, "NULL argument");
+  RDL_ARG_CHECK(image_index < h->n_images || h->n_selected == 0,
+                "image index out of range");
+  RDL_ARG_CHECK(width == h->width && height == h->height, "model size differs");
+  RDL_ARG_CHECK(n >= 1 && n % 2 == 1 && n <= width && n <= height,
+                "shape kernel must be odd and no larger than the image");
+  if (h->n_selected == 0) return RDL_OK;
+  rdl_session* s = h->s;
+  const uint32_t tiles_x = rdl::DivUp(width, rdl::kStampTile);
+  const uint32_t tiles_y = rdl::DivUp(height, rdl::kStampTile);
+  {
+    // algorithmic bytes: the selection read per tile is cached; count the
+    // model read-modify-write of the whole plane
+    rdl::ScopedTiming t(s, "stamp_model", 8.0 * double(width) * height);
+    rdl::StampShapeModel<<<tiles_x * tiles_y, rdl::kStampThreads, 0, s->stream>>>(
+        h->d_pos, h->d_m + size_t(image_index) * h->n_selected, h->n_selected,
+        d_kernel, n, d_model, width, height, tiles_x);
+  }
   RDL_HIP_CHECK(hipGetLastError());
   return RDL_OK;
 }

@@ -53,9 +53,15 @@ Fft::Fft(Session& s, size_t width, size_t height, bool f64)
   const char* force = std::getenv("RADLER_FFT");
   const std::string mode = force ? force : "";
   const bool want_lds = mode == "lds" || (mode != "rocfft" && f64);
+  // RADLER_FFT_COLUMNS=single / split overrides the column-pass choice
+  const char* cols_env = std::getenv("RADLER_FFT_COLUMNS");
+  const std::string cols = cols_env ? cols_env : "";
+  const int strategy = cols == "single"  ? RDL_CONV_COLUMNS_SINGLE
+                       : cols == "split" ? RDL_CONV_COLUMNS_SPLIT
+                                         : RDL_CONV_COLUMNS_AUTO;
   const bool lds_ok = want_lds &&
-                      rdl_conv_create(s.Handle(), uint32_t(width), uint32_t(height),
-                                      f64 ? 1 : 0, &conv_) == RDL_OK;
+                      rdl_conv_create_ex(s.Handle(), uint32_t(width), uint32_t(height),
+                                         f64 ? 1 : 0, strategy, &conv_) == RDL_OK;
   if (lds_ok) {
     spectrum_bytes_ = rdl_conv_spectrum_bytes(conv_);
   } else {

@@ -78,6 +78,9 @@ class Fft {
   /// k * height), the layout the column pass reads contiguously.
   void ForwardColumnMajor(const float* d_in, void* d_spectrum);
   bool UsesLds() const { return conv_ != nullptr; }
+  /// LDS engine with the split (four-step) column passes: spectra are read
+  /// row-major, so ForwardColumnMajor is not used.
+  bool SplitColumns() const { return conv_ && rdl_conv_columns_split(conv_); }
   /// Double-precision rocFFT plan only.
   void Forward64(const double* d_in, void* d_spectrum);
   void Convolve64(double* d_image, const void* d_kernel_spectrum);

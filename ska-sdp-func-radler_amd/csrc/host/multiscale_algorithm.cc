@@ -368,10 +368,19 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
         sub.CorrectResidualDirtyWithSpectrum(i, data_image.Data(i),
                                              pc->second->Ptr());
         if (info.scale != 0.0f) {
-          sub.GetFullIndividualModel(i, scratch_->F());
-          transforms_->Transform(scratch_->F(), info.scale);
-          gpu::Check(rdl_add(s, model_image.Data(i), scratch_->F(), npx),
-                     "rdl_add");
+          // the sub-minor model is a few hundred components: stamping the
+          // shape kernel costs n_sel * n^2 multiply-adds against two
+          // full-image FFTs (:451-460 convolves with the same kernel)
+          size_t n_kernel = 0;
+          const float* d_kernel = transforms_->ShapeKernel(info.scale, n_kernel);
+          if (double(sub.NSelected()) * double(n_kernel) * double(n_kernel) <= 1e9) {
+            sub.AddShapeModel(i, d_kernel, n_kernel, model_image.Data(i));
+          } else {
+            sub.GetFullIndividualModel(i, scratch_->F());
+            transforms_->Transform(scratch_->F(), info.scale);
+            gpu::Check(rdl_add(s, model_image.Data(i), scratch_->F(), npx),
+                       "rdl_add");
+          }
         } else {
           sub.AddIndividualModel(i, model_image.Data(i));
         }

@@ -118,6 +118,20 @@ const void* MultiScaleTransforms::KernelSpectrum(float scale) {
   return spectrum->Ptr();
 }
 
+const float* MultiScaleTransforms::ShapeKernel(float scale, size_t& n) {
+  auto it = shapes_.find(scale);
+  if (it == shapes_.end()) {
+    size_t kn;
+    const std::vector<float> k =
+        MakeShapeFunction(scale, kn, std::min(width_, height_), shape_);
+    auto buf = std::make_shared<gpu::Buffer>(s_, k.size() * sizeof(float));
+    s_.H2D(buf->Ptr(), k.data(), k.size() * sizeof(float));
+    it = shapes_.emplace(scale, std::make_pair(buf, kn)).first;
+  }
+  n = it->second.second;
+  return it->second.first->F();
+}
+
 void MultiScaleTransforms::Transform(float* d_image, float scale) {
   fft_.Convolve(d_image, KernelSpectrum(scale));
 }

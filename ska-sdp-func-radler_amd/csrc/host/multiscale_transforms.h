@@ -26,6 +26,9 @@ class MultiScaleTransforms {
 
   /// Spectrum of the scale kernel placed at the origin (cached).
   const void* KernelSpectrum(float scale);
+  /// The scale's n x n shape kernel on the device (cached), for direct
+  /// stamping of sparse models.
+  const float* ShapeKernel(float scale, size_t& n);
   /// In-place convolution of one W x H plane with the scale kernel
   /// (multiscale_transforms.cc:9-21).
   void Transform(float* d_image, float scale);
@@ -42,6 +45,7 @@ class MultiScaleTransforms {
   Shape shape_;
   gpu::Fft& fft_;
   std::map<float, std::shared_ptr<gpu::Buffer>> spectra_;
+  std::map<float, std::pair<std::shared_ptr<gpu::Buffer>, size_t>> shapes_;
 };
 
 }  // namespace radler::algorithms::multiscale

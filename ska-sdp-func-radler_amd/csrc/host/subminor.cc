@@ -68,7 +68,10 @@ std::shared_ptr<gpu::Buffer> SubMinorLoop::MakePaddedPsfSpectrum(
                                       uint32_t(ph), d_psf, uint32_t(width),
                                       uint32_t(height)),
                "rdl_prepare_psf_kernel");
-    fft.ForwardColumnMajor(kernel.F(), spectrum->Ptr());
+    if (fft.SplitColumns())
+      fft.Forward(kernel.F(), spectrum->Ptr());
+    else
+      fft.ForwardColumnMajor(kernel.F(), spectrum->Ptr());
   } else {
     gpu::Buffer kernel(s, pw * ph * sizeof(double));
     gpu::Check(rdl_prepare_psf_kernel_f64(s.Handle(), kernel.D(), uint32_t(pw),
@@ -114,7 +117,8 @@ void SubMinorLoop::CorrectResidualDirtyWithSpectrum(size_t image_index,
                                        uint32_t(padded_height_), oy),
                "rdl_subminor_model_rows");
     fft.ConvolveSubtract(model.F(), width_, height_, ox, oy, d_spectrum, work.Ptr(),
-                         d_residual, static_cast<const uint8_t*>(rows.Ptr()), true);
+                         d_residual, static_cast<const uint8_t*>(rows.Ptr()),
+                         !fft.SplitColumns());
     return;
   }
   gpu::Buffer& padded_ = s_.Scratch(gpu::Session::kCorrectionSpectrum,
@@ -143,6 +147,14 @@ void SubMinorLoop::AddIndividualModel(size_t image_index, float* d_model) {
   gpu::Check(rdl_subminor_model(h_, uint32_t(image_index), d_model,
                                 uint32_t(width_), uint32_t(height_), 0, 0, 1),
              "rdl_subminor_model");
+}
+
+void SubMinorLoop::AddShapeModel(size_t image_index, const float* d_kernel,
+                                 size_t n, float* d_model) {
+  gpu::Check(rdl_subminor_add_shape_model(h_, uint32_t(image_index), d_kernel,
+                                          uint32_t(n), d_model, uint32_t(width_),
+                                          uint32_t(height_)),
+             "rdl_subminor_add_shape_model");
 }
 
 void SubMinorLoop::GetSelection(std::vector<uint32_t>& positions,

@@ -61,6 +61,10 @@ class SubMinorLoop {
   void GetFullIndividualModel(size_t image_index, float* d_dest);
   /// model += GetFullIndividualModel(...) (generic_clean.cc:145-148).
   void AddIndividualModel(size_t image_index, float* d_model);
+  /// model += GetFullIndividualModel(...) convolved with an odd n x n shape
+  /// kernel (circular), by direct stamping.
+  void AddShapeModel(size_t image_index, const float* d_kernel, size_t n,
+                     float* d_model);
   /// Selected positions and per-image model values (UpdateComponentList,
   /// UpdateAutoMask inputs).
   void GetSelection(std::vector<uint32_t>& positions,

@@ -193,19 +193,38 @@ CONV_SIZES = [(64, 64), (128, 200), (210, 150), (96, 7), (2, 48), (1134, 96), (8
               (2016, 10)]
 
 
-def conv_create(sess, w, h, f64):
+RDL_CONV_COLUMNS_AUTO, RDL_CONV_COLUMNS_SINGLE, RDL_CONV_COLUMNS_SPLIT = 0, 1, 2
+
+
+def conv_create(sess, w, h, f64, columns=None):
     c = C.c_void_p()
-    rc = sess.rdl.lib.rdl_conv_create(sess.h, w, h, int(f64), C.byref(c))
+    if columns is None:
+        rc = sess.rdl.lib.rdl_conv_create(sess.h, w, h, int(f64), C.byref(c))
+    else:
+        rc = sess.rdl.lib.rdl_conv_create_ex(sess.h, w, h, int(f64), columns, C.byref(c))
     return c if rc == 0 else None
+
+
+def split_ok(h):
+    """Column lengths the split passes accept (largest divisor <= sqrt >= 4)."""
+    n1 = max(d for d in range(1, int(h ** 0.5) + 1) if h % d == 0)
+    return n1 >= 4 and h // n1 >= 4
 
 
 @pytest.mark.parametrize("w,h", CONV_SIZES)
 @pytest.mark.parametrize("f64", [False, True])
-def test_lds_fft_forward(sess, w, h, f64):
+@pytest.mark.parametrize("columns", ["single", "split"])
+def test_lds_fft_forward(sess, w, h, f64, columns):
     """Full 2-D forward transform vs numpy's float64 rfft2 (same layout and
-    normalisation): |err| <= eps_T * 8 * sqrt(log2 N) * sum|x|^(1/2)-scale."""
-    c = conv_create(sess, w, h, f64)
+    normalisation): |err| <= eps_T * 8 * sqrt(log2 N) * sum|x|^(1/2)-scale.
+    Both column strategies (one strided pass / split four-step passes)."""
+    if columns == "split" and not split_ok(h):
+        assert conv_create(sess, w, h, f64, RDL_CONV_COLUMNS_SPLIT) is None
+        return
+    strategy = RDL_CONV_COLUMNS_SPLIT if columns == "split" else RDL_CONV_COLUMNS_SINGLE
+    c = conv_create(sess, w, h, f64, strategy)
     assert c is not None
+    assert sess.rdl.lib.rdl_conv_columns_split(c) == (columns == "split")
     rng = np.random.default_rng(w * 31 + h)
     img = rng.standard_normal((h, w)).astype(np.float32)
     nb = sess.rdl.lib.rdl_conv_spectrum_bytes(c)
@@ -230,12 +249,16 @@ def test_lds_fft_unsupported(sess):
     assert conv_create(sess, 8, 10240 * 2, True) is None
 
 
-@pytest.mark.parametrize("w,h", [(64, 64), (210, 150), (96, 7), (1134, 96)])
+@pytest.mark.parametrize("w,h", [(64, 64), (210, 150), (96, 7), (1134, 96), (40, 2048)])
 @pytest.mark.parametrize("f64", [False, True])
-def test_lds_fft_convolutions(sess, orc, w, h, f64):
+@pytest.mark.parametrize("columns", ["single", "split"])
+def test_lds_fft_convolutions(sess, orc, w, h, f64, columns):
     """In-place convolution (rows, columns mode 1, rows) and the shared-spectrum
     form (columns mode 2) against the oracle's float64 circular convolution."""
-    c = conv_create(sess, w, h, f64)
+    if columns == "split" and not split_ok(h):
+        return
+    c = conv_create(sess, w, h, f64,
+                    RDL_CONV_COLUMNS_SPLIT if columns == "split" else RDL_CONV_COLUMNS_SINGLE)
     rng = np.random.default_rng(5 + w)
     img = rng.standard_normal((h, w)).astype(np.float32)
     ker = rng.standard_normal((h, w)).astype(np.float32)
@@ -265,12 +288,13 @@ def test_lds_fft_convolutions(sess, orc, w, h, f64):
 
 
 @pytest.mark.parametrize("w,h,pw,ph", [(64, 64, 72, 72), (200, 150, 224, 168), (90, 60, 98, 64)])
-def test_lds_fft_correction(sess, orc, w, h, pw, ph):
+@pytest.mark.parametrize("columns", [RDL_CONV_COLUMNS_SINGLE, RDL_CONV_COLUMNS_SPLIT])
+def test_lds_fft_correction(sess, orc, w, h, pw, ph, columns):
     """SubMinorLoop::CorrectResidualDirty in one call sequence: model placed at
     the centred offset of the padded plane, x padded PSF spectrum, trimmed and
     subtracted from the residual (float64 transforms): agrees with the oracle
     to float rounding."""
-    c = conv_create(sess, pw, ph, True)
+    c = conv_create(sess, pw, ph, True, columns)
     rng = np.random.default_rng(pw)
     psf = rng.standard_normal((h, w)).astype(np.float32)
     model = np.zeros((h, w), np.float32)
@@ -508,11 +532,14 @@ def test_subminor_loop_bit_exact(sess, orc, w, n_src, threshold_frac, mgain, max
 
 @pytest.mark.parametrize("w,h,pw,ph,rows", [(64, 64, 72, 72, (3, 40)), (200, 150, 224, 168, (0, 1, 77, 149)),
                                             (90, 60, 98, 64, ()), (90, 60, 98, 64, (59,))])
-def test_lds_fft_correction_sparse_rows(sess, w, h, pw, ph, rows):
+@pytest.mark.parametrize("columns", [RDL_CONV_COLUMNS_SINGLE, RDL_CONV_COLUMNS_SPLIT])
+def test_lds_fft_correction_sparse_rows(sess, w, h, pw, ph, rows, columns):
     """The correction with a row mask (empty model rows neither read nor
-    transformed) and a column-major PSF spectrum is bit-identical to the dense
-    row-major sequence: the skipped rows are exact zeros either way."""
-    c = conv_create(sess, pw, ph, True)
+    transformed) and (single-pass columns) a column-major PSF spectrum is
+    bit-identical to the dense row-major sequence: the skipped rows are exact
+    zeros either way."""
+    c = conv_create(sess, pw, ph, True, columns)
+    split = columns == RDL_CONV_COLUMNS_SPLIT
     rng = np.random.default_rng(pw + len(rows))
     psf = rng.standard_normal((h, w)).astype(np.float32)
     model = np.zeros((h, w), np.float32)
@@ -534,18 +561,21 @@ def test_lds_fft_correction_sparse_rows(sess, w, h, pw, ph, rows):
     sess.rdl.rdl_prepare_psf_kernel(sess.h, kplane.vp, pw, ph, dpsf.vp, w, h)
     sess.rdl.rdl_conv_forward(c, kplane.vp, kspec.vp)
     # column-major forward spectrum == the row-major one transposed
-    sess.rdl.rdl_conv_rows_forward(c, kplane.vp, pw, ph, 0, 0, work.vp)
-    sess.rdl.rdl_conv_columns_ex(c, work.vp, kspec_cm.vp, None, 0, C.c_double(1.0), None,
-                                 RDL_CONV_ROW_MAJOR, RDL_CONV_COL_MAJOR)
-    assert np.array_equal(kspec_cm.get(), kspec.get().T)
+    if not split:
+        sess.rdl.rdl_conv_rows_forward(c, kplane.vp, pw, ph, 0, 0, work.vp)
+        sess.rdl.rdl_conv_columns_ex(c, work.vp, kspec_cm.vp, None, 0, C.c_double(1.0), None,
+                                     RDL_CONV_ROW_MAJOR, RDL_CONV_COL_MAJOR)
+        assert np.array_equal(kspec_cm.get(), kspec.get().T)
     norm = C.c_double(1.0 / (pw * ph))
     sess.rdl.rdl_conv_rows_forward(c, dmod.vp, w, h, ox, oy, work.vp)
     sess.rdl.rdl_conv_columns(c, work.vp, work.vp, kspec.vp, 1, norm)
     sess.rdl.rdl_conv_rows_inverse(c, work.vp, dres_a.vp, w, h, ox, oy, 1)
     work.upload(np.full((ph, pw // 2 + 1), np.nan, np.complex128))  # skipped rows stay unread
     sess.rdl.rdl_conv_rows_forward_masked(c, dmod.vp, w, h, ox, oy, work.vp, dmask.vp)
-    sess.rdl.rdl_conv_columns_ex(c, work.vp, work.vp, kspec_cm.vp, 1, norm, dmask.vp,
-                                 RDL_CONV_COL_MAJOR, RDL_CONV_ROW_MAJOR)
+    sess.rdl.rdl_conv_columns_ex(c, work.vp, work.vp, kspec.vp if split else kspec_cm.vp, 1,
+                                 norm, dmask.vp,
+                                 RDL_CONV_ROW_MAJOR if split else RDL_CONV_COL_MAJOR,
+                                 RDL_CONV_ROW_MAJOR)
     sess.rdl.rdl_conv_rows_inverse(c, work.vp, dres_b.vp, w, h, ox, oy, 1)
     a, b = dres_a.get(), dres_b.get()
     assert np.array_equal(a, b)

@@ -38,7 +38,7 @@ def main():
                                          C.POINTER(C.c_uint64), C.POINTER(C.c_double)]
     s.rdl.lib.rdl_conv_spectrum_bytes.restype = C.c_size_t
     reps = 10
-    cases = ((8192, 8192, False), (9072, 9072, True), (4096, 4096, False), (4536, 4536, True))
+    cases = ((8192, 8192, False), (9216, 9216, True), (9072, 9072, True), (4096, 4096, False))
     if len(sys.argv) > 1:  # e.g. "9072,9072,1"
         w, h, f = (int(v) for v in sys.argv[1].split(","))
         cases = ((w, h, bool(f)),)
@@ -71,12 +71,22 @@ def main():
         s.rdl.rdl_session_sync(s.h)
         report(f"rocFFT {w}x{h} {'f64' if f64 else 'f32'} convolve", timings(s), reps)
         s.rdl.rdl_fft_destroy(f)
-        # LDS engine
+        for columns, cname in ((1, "single"), (2, "split")):
+            lds_engine(s, w, h, f64, columns, cname, di, spec, kspec, work, out, reps)
+        for x in (di, spec, kspec, work, out):
+            x.free()
+        if f64:
+            dpl.free()
+
+
+def lds_engine(s, w, h, f64, columns, cname, di, spec, kspec, work, out, reps):
+    if True:
         c = C.c_void_p()
-        rc = s.rdl.lib.rdl_conv_create(s.h, w, h, int(f64), C.byref(c))
+        rc = s.rdl.lib.rdl_conv_create_ex(s.h, w, h, int(f64), columns, C.byref(c))
         if rc != 0:
-            print("LDS engine unsupported", w, h)
-            continue
+            print("LDS engine unsupported", w, h, cname)
+            return
+        s.rdl.lib.rdl_timing_enable(s.h, 1)
         s.rdl.rdl_conv_forward(c, di.vp, kspec.vp)
         s.rdl.rdl_session_sync(s.h)
         timings(s)
@@ -90,7 +100,7 @@ def main():
                 s.rdl.rdl_conv_columns(c, work.vp, work.vp, kspec.vp, 1, C.c_double(1.0 / (w * h)))
                 s.rdl.rdl_conv_rows_inverse(c, work.vp, di.vp, w, h, 0, 0, 0)
         s.rdl.rdl_session_sync(s.h)
-        report(f"LDS {w}x{h} {'f64' if f64 else 'f32'} convolve", timings(s), reps)
+        report(f"LDS[{cname}] {w}x{h} {'f64' if f64 else 'f32'} convolve", timings(s), reps)
         if not f64:
             s.rdl.rdl_conv_forward(c, di.vp, spec.vp)
             timings(s)
@@ -98,13 +108,9 @@ def main():
                 s.rdl.rdl_conv_columns(c, spec.vp, work.vp, kspec.vp, 2, C.c_double(1.0 / (w * h)))
                 s.rdl.rdl_conv_rows_inverse(c, work.vp, out.vp, w, h, 0, 0, 0)
             s.rdl.rdl_session_sync(s.h)
-            report(f"LDS {w}x{h} f32 spectrum->image", timings(s), reps)
+            report(f"LDS[{cname}] {w}x{h} f32 spectrum->image", timings(s), reps)
         s.rdl.lib.rdl_timing_enable(s.h, 0)
         s.rdl.rdl_conv_destroy(c)
-        for x in (di, spec, kspec, work, out):
-            x.free()
-        if f64:
-            dpl.free()
 
 
 if __name__ == "__main__":
