@@ -154,6 +154,51 @@ int rdl_add(rdl_session* s, float* d_dest, const float* d_a, size_t n);
 int rdl_median(rdl_session* s, const float* d_values, size_t n, int use_center,
                float center, float* out);
 
+/* k-th smallest value (of |v - center| when use_center), exact: the
+ * std::nth_element of IuwtDeconvolutionAlgorithm::Mad
+ * (cpp/algorithms/iuwt_deconvolution_algorithm.cc:104-110, k = n/2). */
+int rdl_select_kth(rdl_session* s, const float* d_values, size_t n, int use_center,
+                   float center, size_t k, float* out);
+
+/* ------------------------------------------------ IUWT deconvolution pieces */
+/* IuwtDeconvolutionAlgorithm::GetMaxAbs (iuwt_deconvolution_algorithm.cc:
+ * 112-167): strict '>' from numeric_limits<float>::lowest() over
+ * [xb, W-xb) x [yb, H-yb) (and the mask), first index on ties; value is
+ * |v| when allow_negative. Nothing qualifying: found = 0, x = W, y = H,
+ * value = lowest(). */
+int rdl_max_abs(rdl_session* s, const float* d_data, uint32_t width, uint32_t height,
+                uint32_t x_border, uint32_t y_border, int allow_negative,
+                const uint8_t* d_mask, rdl_peak* out);
+/* image_analysis::SelectStructures (cpp/algorithms/iuwt/image_analysis.cc:
+ * 227-259) as a per-pixel test: the flood fills it starts from every
+ * exceeding pixel only ever reach exceeding pixels of the same box, scale
+ * range and prior mask, so the resulting mask is exactly
+ *   mask[s][p] = ExceedsThreshold(coeffs[s][p], thresholds[s])
+ * for min_scale <= s < end_scale, p in the border box and the prior mask.
+ * d_mask holds end_scale planes of width*height bytes; *area = its count
+ * (the summed flood-fill area sizes). */
+int rdl_iuwt_select(rdl_session* s, const float* d_coeffs, uint32_t width, uint32_t height,
+                    uint32_t min_scale, uint32_t end_scale, const float* h_thresholds,
+                    uint32_t x_border, uint32_t y_border, const uint8_t* d_prior,
+                    uint8_t* d_mask, uint64_t* area);
+/* IuwtDecomposition::ApplyMask for the n_scales coefficient planes
+ * (iuwt_decomposition.h:284-291; the residual plane is not stored here). */
+int rdl_iuwt_apply_mask(rdl_session* s, float* d_coeffs, const uint8_t* d_mask,
+                        uint32_t width, uint32_t height, uint32_t n_scales);
+/* DotProduct (iuwt_deconvolution_algorithm.cc:169-174) with a double sum. */
+int rdl_dot(rdl_session* s, const float* d_a, const float* d_b, size_t n, double* out);
+/* Snr's two sums over the coefficient planes (:308-321), double:
+ * model_sum = sum m^2, noise_sum = sum (m - n)^2 (n = d_noisy, m = d_model). */
+int rdl_iuwt_snr_sums(rdl_session* s, const float* d_noisy, const float* d_model, size_t n,
+                      double* model_sum, double* noise_sum);
+/* BoundingBox's scans (:180-214): with m = max |v| of the image, h_first[y]
+ * and h_last[y] are the first and last x of row y with |v| > m * 0.01
+ * (double compare), -1 for rows without any. */
+int rdl_bbox_rows(rdl_session* s, const float* d_image, uint32_t width, uint32_t height,
+                  int32_t* h_first, int32_t* h_last);
+/* float <-> double planes (to_f64: float src -> double dst). */
+int rdl_convert(rdl_session* s, const void* d_src, void* d_dst, size_t n, int to_f64);
+
 /* ---------------------------------------------------------------- Högbom */
 typedef struct {
   uint32_t width, height;

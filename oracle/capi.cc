@@ -11,6 +11,7 @@
 #include "oracle.h"
 #include "tiling.h"
 #include "iuwt.h"
+#include "iuwt_algorithm.h"
 
 using namespace oracle;
 
@@ -153,6 +154,7 @@ struct OrcAlgo {
   std::vector<double> scale_list;
   size_t iteration_number = 0;
   std::unique_ptr<MultiScale> ms;
+  std::vector<IuwtStep> iuwt_steps;  // type 2: steps of the last execute
 };
 
 static AlgoSettings MakeSettings(const orc_algo_settings* a) {
@@ -190,6 +192,16 @@ void* orc_algo_create(int type, const orc_algo_settings* a) {
 
 void orc_algo_destroy(void* h) { delete static_cast<OrcAlgo*>(h); }
 
+// Steps of the last IUWT (type 2) execute: fills up to cap records, returns
+// the count (IuwtStep layout: i32 succeeded, i32 scale, u32 x, u32 y,
+// i32 end_scale, i32 min_scale, u64 area, f32 max_value, pad to 40 bytes).
+uint64_t orc_iuwt_steps(void* h, IuwtStep* out, uint64_t cap) {
+  auto* algo = static_cast<OrcAlgo*>(h);
+  const size_t n = std::min<size_t>(cap, algo->iuwt_steps.size());
+  for (size_t i = 0; i != n; ++i) out[i] = algo->iuwt_steps[i];
+  return algo->iuwt_steps.size();
+}
+
 // Update the mutable per-call settings (threshold, max iterations, gains).
 void orc_algo_update(void* h, const orc_algo_settings* a) {
   auto* algo = static_cast<OrcAlgo*>(h);
@@ -217,6 +229,20 @@ int orc_algo_execute(void* h, const orc_set_desc* d, float* residual,
     if (algo->type == 0) {
       r = GenericCleanExecute(algo->settings, algo->iteration_number, res, mod,
                               psf_ptrs, &tr);
+    } else if (algo->type == 2) {
+      // IuwtDeconvolution::ExecuteMajorIteration (iuwt_deconvolution.h:22-39)
+      IuwtAlgoSettings is;
+      is.minor_loop_gain = algo->settings.minor_loop_gain;
+      is.major_loop_gain = algo->settings.major_loop_gain;
+      is.clean_border = algo->settings.clean_border_ratio;
+      is.allow_negative = algo->settings.allow_negative;
+      is.mask = algo->settings.clean_mask;
+      is.absolute_threshold = algo->settings.threshold;
+      algo->iuwt_steps.clear();
+      bool another = false;
+      r.final_peak = IuwtExecute(is, algo->iteration_number, algo->settings.max_iterations,
+                                 res, mod, psf_ptrs, another, &algo->iuwt_steps);
+      r.another_iteration_required = another;
     } else {
       algo->ms->iteration_number = algo->iteration_number;
       r = algo->ms->Execute(res, mod, psf_ptrs, &tr);

@@ -90,3 +90,12 @@ extern "C" int rdl_median(rdl_session* s, const float* d_values, size_t n,
   *out = 0.5f * (lo + hi);
   return RDL_OK;
 }
+
+/* k-th smallest of values (or of |values - center|), exact
+ * (std::nth_element at k; IuwtDeconvolutionAlgorithm::Mad selects k = n/2). */
+extern "C" int rdl_select_kth(rdl_session* s, const float* d_values, size_t n,
+                              int use_center, float center, size_t k, float* out) {
+  RDL_ARG_CHECK(s && d_values && out, "NULL argument");
+  RDL_ARG_CHECK(k < n, "k out of range");
+  return rdl::SelectKth(s, d_values, n, use_center, center, k, out);
+}

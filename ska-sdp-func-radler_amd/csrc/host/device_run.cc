@@ -4,6 +4,7 @@
 
 #include "generic_clean.h"
 #include "image_accessors.h"
+#include "iuwt_deconvolution.h"
 #include "multiscale_algorithm.h"
 
 namespace radler {
@@ -67,6 +68,8 @@ DeviceRun::DeviceRun(const Settings& settings, const float* psf,
     algorithm = std::make_unique<algorithms::MultiScaleAlgorithm>(
         settings_.multiscale, beam_size, settings.pixel_scale.x,
         settings.pixel_scale.y, false);
+  else if (settings.algorithm_type == AlgorithmType::kIuwt)
+    algorithm = std::make_unique<algorithms::IuwtDeconvolution>();
   else
     throw std::runtime_error("DeviceRun: unsupported algorithm");
   algorithm->SetMaxIterations(settings.minor_iteration_count);
@@ -125,6 +128,13 @@ const std::vector<uint32_t>& DeviceRun::Trace(size_t index) const {
   if (auto* g = dynamic_cast<const algorithms::GenericClean*>(&a))
     return g->LastTrace();
   return empty;
+}
+
+std::vector<algorithms::IuwtDeconvolution::Step> DeviceRun::IuwtSteps(size_t index) const {
+  const auto* a =
+      dynamic_cast<const algorithms::IuwtDeconvolution*>(&parallel_->Algorithm(index));
+  if (!a) throw std::runtime_error("DeviceRun: not an IUWT run");
+  return a->Steps();
 }
 
 }  // namespace radler

@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "image_set.h"
+#include "iuwt_deconvolution.h"
 #include "parallel_deconvolution.h"
 #include "settings.h"
 #include "work_table.h"
@@ -36,6 +37,8 @@ class DeviceRun {
   std::vector<float> Model() const;
   /// Component trace (x, y, scale triples) of subimage `index`'s algorithm.
   const std::vector<uint32_t>& Trace(size_t index = 0) const;
+  /// Outer-loop steps of the last IUWT major iteration (subimage `index`).
+  std::vector<algorithms::IuwtDeconvolution::Step> IuwtSteps(size_t index = 0) const;
   /// Tiles of the last Execute (empty for a 1x1 grid).
   const std::vector<algorithms::SubImage>& SubImages() const {
     return parallel_->SubImages();

@@ -9,6 +9,7 @@
 #include "image_accessors.h"
 #include "image_set.h"
 #include "logger.h"
+#include "iuwt_deconvolution.h"
 #include "multiscale_algorithm.h"
 #include "parallel_deconvolution.h"
 
@@ -192,7 +193,8 @@ void Radler::InitializeDeconvolutionAlgorithm(
           settings_.save_source_list);
       break;
     case AlgorithmType::kIuwt:
-      Unsupported("The IUWT algorithm");
+      algorithm = std::make_unique<algorithms::IuwtDeconvolution>();
+      break;
     case AlgorithmType::kAdaptiveScalePixel:
       Unsupported("The adaptive scale pixel algorithm");
     case AlgorithmType::kMoreSane:

@@ -413,6 +413,14 @@ void InitGpu(py::module& m) {
         std::copy(t.begin(), t.end(), a.mutable_data());
         return a;
       }, py::arg("index") = 0)
+      .def("iuwt_steps", [](const radler::DeviceRun& self, size_t index) {
+        // (succeeded, scale, x, y, end_scale, min_scale, area, max_value)
+        py::list out;
+        for (const auto& s : self.IuwtSteps(index))
+          out.append(py::make_tuple(s.succeeded, s.scale, s.x, s.y, s.end_scale,
+                                    s.min_scale, s.area, s.max_value));
+        return out;
+      }, py::arg("index") = 0)
       .def("subimages", [](const radler::DeviceRun& self, size_t width, size_t height) {
         // (boxes [n][x, y, w, h], labels [h][w]: subimage index + 1 inside its
         // boundary mask)

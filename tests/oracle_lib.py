@@ -182,7 +182,7 @@ class Oracle:
 
 
 class OracleAlgorithm:
-    """A persistent DeconvolutionAlgorithm (GenericClean=0, MultiScale=1)."""
+    """A persistent DeconvolutionAlgorithm (GenericClean=0, MultiScale=1, IUWT=2)."""
 
     def __init__(self, oracle, kind, **settings):
         self.o = oracle
@@ -206,11 +206,26 @@ class OracleAlgorithm:
             raise RuntimeError(self.o.lib.orc_last_error().decode())
         return r, trace[: min(r.n_trace, trace_cap)].copy()
 
+    def iuwt_steps(self, cap=4096):
+        """Steps of the last IUWT (kind 2) execute (oracle/iuwt_algorithm.h IuwtStep)."""
+        out = np.zeros(cap, IUWT_STEP)
+        L = self.o.lib
+        L.orc_iuwt_steps.restype = C.c_uint64
+        L.orc_iuwt_steps.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
+        n = L.orc_iuwt_steps(self.h, out.ctypes.data, cap)
+        return out[: min(n, cap)].copy()
+
     def __del__(self):
         try:
             self.o.lib.orc_algo_destroy(self.h)
         except Exception:
             pass
+
+
+# oracle/iuwt_algorithm.h IuwtStep (40 bytes)
+IUWT_STEP = np.dtype([("succeeded", np.int32), ("scale", np.int32), ("x", np.uint32),
+                      ("y", np.uint32), ("end_scale", np.int32), ("min_scale", np.int32),
+                      ("area", np.uint64), ("max_value", np.float32), ("pad", np.uint32)])
 
 
 def iuwt_decompose(oracle, image, n_scales, aliased=False, include_largest=True):
