@@ -47,6 +47,7 @@ struct IuwtStep {
   int32_t min_scale;      // curMinScale of the step
   uint64_t area;          // SelectStructures area size (0 if not reached)
   float max_value;        // maxValue after the step (0 if not updated)
+  uint32_t trimmed_width; // width of the trimmed box (0: not trimmed)
 };
 
 // IuwtDeconvolution::ExecuteMajorIteration (cpp/algorithms/iuwt_deconvolution.h:22-39)

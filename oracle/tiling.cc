@@ -16,6 +16,7 @@
 
 #include "oracle.h"
 #include "tiling.h"
+#include "iuwt_algorithm.h"
 
 namespace oracle {
 
@@ -378,6 +379,21 @@ Result TiledAlgorithm::Execute(ImageSet& data, ImageSet& model,
                                std::vector<Component>* trace) {
   if (kind == 0)
     return GenericCleanExecute(settings, iteration_number, data, model, psfs, trace);
+  if (kind == 2) {  // IuwtDeconvolution (iuwt_deconvolution.h:22-39)
+    IuwtAlgoSettings is;
+    is.minor_loop_gain = settings.minor_loop_gain;
+    is.major_loop_gain = settings.major_loop_gain;
+    is.clean_border = settings.clean_border_ratio;
+    is.allow_negative = settings.allow_negative;
+    is.mask = settings.clean_mask;
+    is.absolute_threshold = settings.threshold;
+    Result r;
+    bool another = false;
+    r.final_peak = IuwtExecute(is, iteration_number, settings.max_iterations, data, model,
+                               psfs, another, nullptr);
+    r.another_iteration_required = another;
+    return r;
+  }
   if (!ms) ms = std::make_unique<MultiScale>(settings);
   ms->Settings() = settings;
   if (ms->Settings().beam_size_in_pixels <= 0.0) ms->Settings().beam_size_in_pixels = 1.0;

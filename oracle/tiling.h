@@ -21,7 +21,7 @@ struct SubImage {
 // subimage, parallel_deconvolution.cc:227-242): persistent settings,
 // iteration count and multiscale state.
 struct TiledAlgorithm {
-  int kind = 0;  // 0 GenericClean, 1 MultiScale
+  int kind = 0;  // 0 GenericClean, 1 MultiScale, 2 IUWT
   AlgoSettings settings;
   size_t iteration_number = 0;
   std::unique_ptr<MultiScale> ms;

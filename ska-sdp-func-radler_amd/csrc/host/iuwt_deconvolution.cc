@@ -493,6 +493,7 @@ bool Algorithm::FillAndDeconvolveStructure(
     box_y1_ = y1;
     box_y2_ = y2;
     const size_t nw = x2 - x1, nh = y2 - y1;
+    step.trimmed_width = uint32_t(nw);
     dirty = Trim(s_, dirty.F(), width, x1, y1, x2, y2);
     const Plane small_psf = TrimPsf(s_, psf, nw, nh);
     const std::shared_ptr<Buffer> small_kernel = KernelOf(small_psf);

@@ -34,7 +34,7 @@ class IuwtDeconvolution final : public DeconvolutionAlgorithm {
     int32_t end_scale, min_scale;
     uint64_t area;
     float max_value;
-    uint32_t pad;
+    uint32_t trimmed_width;  // width of the trimmed box (0: not trimmed)
   };
   const std::vector<Step>& Steps() const { return steps_; }
 

@@ -414,11 +414,12 @@ void InitGpu(py::module& m) {
         return a;
       }, py::arg("index") = 0)
       .def("iuwt_steps", [](const radler::DeviceRun& self, size_t index) {
-        // (succeeded, scale, x, y, end_scale, min_scale, area, max_value)
+        // (succeeded, scale, x, y, end_scale, min_scale, area, max_value,
+        //  trimmed_width)
         py::list out;
         for (const auto& s : self.IuwtSteps(index))
           out.append(py::make_tuple(s.succeeded, s.scale, s.x, s.y, s.end_scale,
-                                    s.min_scale, s.area, s.max_value));
+                                    s.min_scale, s.area, s.max_value, s.trimmed_width));
         return out;
       }, py::arg("index") = 0)
       .def("subimages", [](const radler::DeviceRun& self, size_t width, size_t height) {

@@ -225,7 +225,8 @@ class OracleAlgorithm:
 # oracle/iuwt_algorithm.h IuwtStep (40 bytes)
 IUWT_STEP = np.dtype([("succeeded", np.int32), ("scale", np.int32), ("x", np.uint32),
                       ("y", np.uint32), ("end_scale", np.int32), ("min_scale", np.int32),
-                      ("area", np.uint64), ("max_value", np.float32), ("pad", np.uint32)])
+                      ("area", np.uint64), ("max_value", np.float32),
+                      ("trimmed_width", np.uint32)])
 
 
 def iuwt_decompose(oracle, image, n_scales, aliased=False, include_largest=True):

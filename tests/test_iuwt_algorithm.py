@@ -98,3 +98,104 @@ def test_iuwt_gpu_matches_oracle(w, h, points, blobs, seed, iterations, extra):
     tol = 1e-4 * np.abs(dirty).max()
     assert np.abs(run.residual().reshape(h, w) - res_o[0]).max() <= tol
     assert np.abs(run.model().reshape(h, w) - mod_o[0]).max() <= tol
+
+
+JOINED_CASES = [
+    # w, n_channels, weights, seed
+    (128, 2, None, 21),
+    (128, 3, [1.0, 0.5, 2.0], 22),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,n_ch,weights,seed", JOINED_CASES)
+def test_iuwt_joined_channels_matches_oracle(w, n_ch, weights, seed):
+    """Joined channels: the structure is found on the integrated image and
+    refitted per channel (PerformSubImageFitAll / PerformSubImageFitSingle,
+    :608-741: connected components of the structure model, boxed
+    per-component fits, correction factors) with per-channel PSFs."""
+    h = w
+    psf, dirty = problem(w, h, 15, 3, seed=seed)
+    rng = np.random.default_rng(seed)
+    dirties = np.stack([dirty * np.float32(1.0 + 0.25 * k) +
+                        np.float32(1e-3) * rng.standard_normal((h, w)).astype(np.float32)
+                        for k in range(n_ch)]).astype(np.float32)
+    psfs = np.stack([psf * np.float32(1.0 + 0.01 * k) for k in range(n_ch)]).astype(np.float32)
+    psfs[:, h // 2, w // 2] = 1.0
+    wts = np.ones(n_ch) if weights is None else np.asarray(weights, np.float64)
+    iterations = 12
+    orc = get_oracle()
+    orc.set_threads(8)
+    alg = OracleAlgorithm(orc, 2, threshold=1e-3, max_iterations=iterations, border_ratio=0.0,
+                          minor_loop_gain=0.1, major_loop_gain=0.8)
+    res_o, mod_o = dirties.copy(), np.zeros_like(dirties)
+    r_o, _ = alg.execute(res_o, mod_o, psfs.copy(), weights=wts.astype(np.float32))
+    steps_o = alg.iuwt_steps()
+    run = rd.gpu.DeviceRun(_settings(w, h, iterations), psfs, dirties, list(wts), 0.0)
+    r = run.execute()
+    steps = run.iuwt_steps()
+    assert [g[:7] for g in steps] == [
+        (int(o["succeeded"]), int(o["scale"]), int(o["x"]), int(o["y"]), int(o["end_scale"]),
+         int(o["min_scale"]), int(o["area"])) for o in steps_o]
+    assert any(g[0] for g in steps)  # the per-channel refit ran
+    assert r["iterations"] == r_o.iteration_number
+    tol = 1e-4 * np.abs(dirties).max()
+    np.testing.assert_allclose(run.residual().reshape(n_ch, h, w), res_o, atol=tol)
+    np.testing.assert_allclose(run.model().reshape(n_ch, h, w), mod_o, atol=tol)
+
+
+@pytest.mark.gpu
+def test_iuwt_tiled_with_subimage_masks_matches_oracle():
+    """IUWT per subimage of a 2x2 grid (ParallelDeconvolution sets each
+    subimage's boundary mask as the clean mask: GetMaxAbsWithMask and the
+    masked flood fill, image_analysis.cc:150-225). divergence_limit = 0 so
+    the subimage results are kept (the find-peak pass of an IUWT subimage
+    reports a zero peak)."""
+    from oracle_lib import OracleParallel
+    w = h = 256
+    psf, dirty = problem(w, h, 30, 4, seed=31)
+    iterations = 8
+    orc = get_oracle()
+    orc.set_threads(8)
+    par = OracleParallel(orc, 2, 2, 2, threshold=1e-3, max_iterations=iterations,
+                         border_ratio=0.0, minor_loop_gain=0.1, major_loop_gain=0.8,
+                         divergence_limit=0.0)
+    par.set_snapshot(False)
+    res_o, mod_o = dirty[None].copy(), np.zeros((1, h, w), np.float32)
+    r_o, boxes_o, labels_o, _ = par.execute(res_o, mod_o, psf[None], 0.8)
+    s = _settings(w, h, iterations)
+    s.divergence_limit = 0.0
+    s.parallel.grid_width = s.parallel.grid_height = 2
+    s.parallel.max_threads = 1
+    run = rd.gpu.DeviceRun(s, psf, dirty, [], 0.0)
+    r = run.execute()
+    boxes, labels = run.subimages(w, h)
+    assert np.array_equal(boxes, boxes_o) and np.array_equal(labels, labels_o)
+    assert r["iterations"] == r_o.total_iterations
+    assert np.abs(mod_o).sum() > 0
+    tol = 1e-4 * np.abs(dirty).max()
+    assert np.abs(run.residual().reshape(h, w) - res_o[0]).max() <= tol
+    assert np.abs(run.model().reshape(h, w) - mod_o[0]).max() <= tol
+
+
+@pytest.mark.gpu
+def test_iuwt_trimmed_structure_matches_oracle():
+    """A compact structure in a 512^2 field: the bounding box of the selected
+    structure is smaller than the image, so FillAndDeconvolveStructure
+    recurses on the trimmed IUWT, dirty, PSF and model (:520-588)."""
+    w = h = 512
+    psf, dirty = problem(w, h, 4, 0, seed=41)
+    iterations = 6
+    r_o, steps_o, res_o, mod_o = oracle_run(dirty[None], psf[None], iterations=iterations)
+    run = rd.gpu.DeviceRun(_settings(w, h, iterations), psf, dirty, [], 0.0)
+    r = run.execute()
+    steps = run.iuwt_steps()
+    assert [g[:7] for g in steps] == [
+        (int(o["succeeded"]), int(o["scale"]), int(o["x"]), int(o["y"]), int(o["end_scale"]),
+         int(o["min_scale"]), int(o["area"])) for o in steps_o]
+    assert [g[8] for g in steps] == [int(o["trimmed_width"]) for o in steps_o]
+    assert any(0 < g[8] < w for g in steps)  # the trimmed recursion ran
+    assert r["iterations"] == r_o.iteration_number
+    tol = 1e-4 * np.abs(dirty).max()
+    assert np.abs(run.residual().reshape(h, w) - res_o[0]).max() <= tol
+    assert np.abs(run.model().reshape(h, w) - mod_o[0]).max() <= tol
