@@ -151,6 +151,12 @@ def main():
     ap.add_argument("--timing-all", action="store_true",
                     help="count every launch of the process (PMC passes, tools/pmc_traffic.py)")
     ap.add_argument("--dump-families", help="write the per-family launch/byte counts here")
+    ap.add_argument("--workload", choices=["fields", "tiled"], default="fields",
+                    help="fields: one independent field per GPU (weak scaling, the "
+                         "default); tiled: ONE image split into grid x grid subimages "
+                         "(ParallelDeconvolution, SURVEY.md config 5) shared by the "
+                         "ranks over RCCL (strong scaling)")
+    ap.add_argument("--grid", type=int, default=8, help="tiled: subimages per axis")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -168,9 +174,25 @@ def main():
     import radler as rd
 
     threshold = args.sigma * NOISE
-    psf, dirty = make_problem(args.size, SEED + rank, args.points, args.blobs)
+    tiled = args.workload == "tiled"
+    # tiled: every rank holds the same image (one field); fields: one per rank
+    psf, dirty = make_problem(args.size, SEED + (0 if tiled else rank), args.points,
+                              args.blobs)
     s = settings_for(rd, args.size, args.max_iter, args.scales, threshold)
+    if tiled:
+        s.parallel.grid_width = s.parallel.grid_height = args.grid
     run = rd.gpu.DeviceRun(s, psf, dirty, [], BEAM_PX * PIXEL_SCALE)
+    if tiled and dist is not None:
+        # RCCL communicator of the product (rdl_comm_*), id from rank 0
+        import torch
+        idl = torch.zeros(rd.distributed.rccl_id_size(), dtype=torch.uint8, device="cuda")
+        if rank == 0:
+            idl.copy_(torch.frombuffer(bytearray(rd.distributed.rccl_unique_id()),
+                                       dtype=torch.uint8))
+        dist.broadcast(idl, src=0)
+        uid = bytes(idl.cpu().numpy().tobytes())
+        comm = rd.distributed.RcclCommunicator(local_rank, world, rank, uid)
+        run.set_communicator(comm)
     timing = Timing(run.session_handle())
     if args.timing_all:
         timing.enable(True)
@@ -213,7 +235,8 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         c = torch.tensor([comps], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        if not tiled:  # tiled: every rank reports the whole job's components
+            dist.all_reduce(c, op=dist.ReduceOp.SUM)
         max_elapsed, total_comps = float(t.item()), int(c.item())
 
     if rank != 0:
@@ -248,7 +271,7 @@ def main():
               f"results {results}", file=sys.stderr)
 
     cpu = None
-    if args.cpu_sample > 0 and world == 1:
+    if args.cpu_sample > 0 and world == 1 and not tiled:
         cpu = cpu_baseline(psf, dirty, args.scales, threshold, args.cpu_sample,
                            args.cpu_threads)
 
@@ -261,17 +284,20 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 2),
         "wall_clock_to_threshold_s": round(max_elapsed / args.steps, 4),
-        "components_per_step": total_comps // (args.steps * world),
+        "components_per_step": total_comps // (args.steps * (1 if tiled else world)),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if tiled else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (seeded sky: points + Gaussian blobs, analytic PSF, noise)",
-        "config": {"workload": f"multiscale-{args.size}x{args.size}-{args.scales}scales",
+        "config": {"workload": (f"multiscale-{args.size}x{args.size}-{args.scales}scales"
+                                + (f"-tiled{args.grid}x{args.grid}" if tiled else "")),
                    "image": [args.size, args.size], "scales": args.scales,
                    "points": args.points, "blobs": args.blobs, "noise": NOISE,
                    "threshold": threshold, "minor_loop_gain": 0.1, "major_loop_gain": 1.0,
-                   "fields_per_gpu": 1, "parallelism": f"fields{world}"},
+                   "fields_per_gpu": 0 if tiled else 1,
+                   "parallelism": (f"subimages{args.grid * args.grid}/ranks{world}"
+                                   if tiled else f"fields{world}")},
         "roofline": roofline,
         "cpu_baseline": cpu,
     }

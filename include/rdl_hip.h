@@ -481,6 +481,13 @@ int rdl_comm_destroy(rdl_session* s);
  * cpp/algorithms/parallel_deconvolution.cc:592-603). */
 int rdl_comm_allreduce_max(rdl_session* s, float* value);
 int rdl_comm_allreduce_sum_u64(rdl_session* s, uint64_t* value);
+/* In-place broadcast of a device buffer from `root`, stream ordered: the
+ * owner rank's subimage residual/model boxes, which every rank then merges
+ * in subimage order (ImageSet::CopyMasked / AddSubImage,
+ * cpp/algorithms/parallel_deconvolution.cc:458-484). */
+int rdl_comm_broadcast(rdl_session* s, void* d_buf, size_t bytes, int root);
+/* This session's rank and the communicator size. */
+int rdl_comm_rank(rdl_session* s, int* rank, int* n_ranks);
 
 #ifdef __cplusplus
 }

@@ -1,8 +1,11 @@
-// Multi-GPU exchange over RCCL (xGMI): the one global reduction of
-// ParallelDeconvolution::ExecuteParallelRun — the maximum start peak over all
-// subimages (cpp/algorithms/parallel_deconvolution.cc:592-603) — plus a sum
-// of finished/iteration counters (:622-653). 4-8 bytes per call: latency
-// bound, one call per major iteration.
+// Multi-GPU exchange over RCCL (xGMI) for the process-per-GPU split of
+// ParallelDeconvolution::ExecuteParallelRun: the global reduction of the
+// maximum start peak over all subimages (cpp/algorithms/
+// parallel_deconvolution.cc:592-603), a sum of counters (:622-653), and the
+// broadcast of each finished subimage's residual/model boxes from the rank
+// that deconvolved it (the copy-back of :458-484, applied by every rank in
+// subimage order). The reductions are 4-8 bytes (latency bound, once per
+// major iteration); the broadcasts move each box once over xGMI.
 #include <rccl/rccl.h>
 
 #include <cstring>
@@ -74,6 +77,22 @@ int rdl_comm_allreduce_sum_u64(rdl_session* s, uint64_t* value) {
   RDL_HIP_CHECK(hipMemcpyAsync(value, d, sizeof(uint64_t),
                                hipMemcpyDeviceToHost, s->stream));
   RDL_HIP_CHECK(hipStreamSynchronize(s->stream));
+  return RDL_OK;
+}
+
+int rdl_comm_broadcast(rdl_session* s, void* d_buf, size_t bytes, int root) {
+  RDL_ARG_CHECK(s && s->comm, "communicator not initialised");
+  RDL_ARG_CHECK(d_buf || bytes == 0, "NULL buffer");
+  if (bytes == 0) return RDL_OK;
+  RDL_NCCL_CHECK(ncclBroadcast(d_buf, d_buf, bytes, ncclUint8, root,
+                               static_cast<ncclComm_t>(s->comm), s->stream));
+  return RDL_OK;
+}
+
+int rdl_comm_rank(rdl_session* s, int* rank, int* n_ranks) {
+  RDL_ARG_CHECK(s && s->comm && rank && n_ranks, "communicator not initialised");
+  RDL_NCCL_CHECK(ncclCommUserRank(static_cast<ncclComm_t>(s->comm), rank));
+  RDL_NCCL_CHECK(ncclCommCount(static_cast<ncclComm_t>(s->comm), n_ranks));
   return RDL_OK;
 }
 

@@ -44,6 +44,11 @@ class DeviceRun {
     return parallel_->SubImages();
   }
   gpu::Session& Session() { return *session_; }
+  std::shared_ptr<gpu::Session> SharedSession() { return session_; }
+  /// Process-per-GPU split of gridded runs (ParallelDeconvolution).
+  void SetCommunicator(std::shared_ptr<Communicator> comm) {
+    parallel_->SetCommunicator(std::move(comm));
+  }
   void Sync() { session_->Sync(); }
 
  private:

@@ -503,6 +503,106 @@ void ParallelDeconvolution::RunSubImagesConcurrently(
   s.Sync();
 }
 
+double ParallelDeconvolution::RunSubImagesDistributed(
+    ImageSet& data_image, const ImageSet& model_image, ImageSet& result_model,
+    const std::vector<gpu::Planes>& psf_images,
+    const std::vector<size_t>& psf_indices, double major_iteration_threshold,
+    bool find_peak_only) {
+  // The reference's threads (parallel_deconvolution.cc:583-616) become ranks:
+  // subimage i runs on rank SubImageOwner(i). Every owned subimage trims from
+  // the residual as it was when the pass started (the snapshot schedule of
+  // RunSubImagesConcurrently), so the merged result is the same for any
+  // number of ranks, and equal to the one-process pool's.
+  gpu::Session& s = data_image.Session();
+  Communicator& comm = *comm_;
+  const int rank = comm.Rank(), n_ranks = comm.Size();
+  const size_t n_sub = subimages_.size(), n_img = data_image.Size();
+  // per subimage: a 64-byte record, then the residual and model planes
+  struct Record {
+    double peak;
+    uint64_t iteration_number;
+    uint32_t reached_major_threshold;
+    uint32_t converging;
+    uint32_t pad[10];
+  };
+  static_assert(sizeof(Record) == 64, "record layout");
+  constexpr size_t kHeaderFloats = sizeof(Record) / sizeof(float);
+  std::vector<std::unique_ptr<gpu::Buffer>> packs(n_sub);
+  double local_peak = 0.0;
+  for (size_t i = 0; i != n_sub; ++i) {
+    if (SubImageOwner(i, n_ranks) != rank) continue;
+    SubImage& sub = subimages_[i];
+    const size_t sw = sub.width, sh = sub.height, n = sw * sh;
+    const gpu::Planes& psfs = psf_images[psf_indices[i]];
+    gpu::Buffer boundary(s, n);
+    s.H2D(boundary.Ptr(), MaskBytes(sub.boundary_mask).data(), n);
+    ImageSet sub_data(data_image, sw, sh);
+    ImageSet sub_model(model_image, sw, sh);
+    gpu::Planes sub_psfs = gpu::Planes::Make(s, sw, sh, psfs.count);
+    TrimSubImage(s, sub, data_image, model_image, psfs, sub_data.Base(),
+                 sub_model.Base(), sub_psfs.Base(),
+                 static_cast<const uint8_t*>(boundary.Ptr()));
+    std::unique_ptr<ImageSet> initial;
+    if (!find_peak_only) {
+      initial = std::make_unique<ImageSet>(sub_model, sw, sh);
+      initial->CopyFrom(sub_model);
+    }
+    const bool converging = DeconvolveSubImage(sub, sub_data, sub_model, sub_psfs,
+                                               major_iteration_threshold,
+                                               find_peak_only);
+    if (find_peak_only) {
+      if (sub.peak > local_peak) local_peak = sub.peak;  // :592-599, from 0.0
+      continue;
+    }
+    auto pack = std::make_unique<gpu::Buffer>(
+        s, (kHeaderFloats + 2 * n_img * n) * sizeof(float));
+    Record rec{};
+    rec.peak = sub.peak;
+    rec.iteration_number = algorithms_[i]->IterationNumber();
+    rec.reached_major_threshold = sub.reached_major_threshold ? 1u : 0u;
+    rec.converging = converging ? 1u : 0u;
+    s.H2D(pack->Ptr(), &rec, sizeof(rec));
+    float* base = pack->F() + kHeaderFloats;
+    s.D2D(base, sub_data.Base(), n_img * n * sizeof(float));
+    s.D2D(base + n_img * n, (converging ? sub_model : *initial).Base(),
+          n_img * n * sizeof(float));
+    packs[i] = std::move(pack);
+  }
+  s.Sync();
+  if (find_peak_only)  // the RCCL allreduce of the start peak
+    return double(comm.AllreduceMax(s, float(local_peak)));
+
+  // copy-back (:458-484) in subimage order, identical on every rank
+  std::unique_ptr<gpu::Buffer> staging;
+  for (size_t i = 0; i != n_sub; ++i) {
+    SubImage& sub = subimages_[i];
+    const size_t n = sub.width * sub.height;
+    const size_t bytes = (kHeaderFloats + 2 * n_img * n) * sizeof(float);
+    const int owner = SubImageOwner(i, n_ranks);
+    gpu::Buffer* pack = packs[i].get();
+    if (owner != rank) {
+      if (!staging || staging->Bytes() < bytes)
+        staging = std::make_unique<gpu::Buffer>(s, bytes);
+      pack = staging.get();
+    }
+    comm.Broadcast(s, pack->Ptr(), bytes, owner);
+    Record rec{};
+    s.D2H(&rec, pack->Ptr(), sizeof(rec));
+    if (owner != rank) {
+      sub.peak = rec.peak;
+      sub.reached_major_threshold = rec.reached_major_threshold != 0;
+      algorithms_[i]->SetIterationNumber(size_t(rec.iteration_number));
+    }
+    gpu::Buffer boundary(s, n);
+    s.H2D(boundary.Ptr(), MaskBytes(sub.boundary_mask).data(), n);
+    const float* base = pack->F() + kHeaderFloats;
+    MergeSubImage(s, sub, data_image, result_model, base, base + n_img * n,
+                  static_cast<const uint8_t*>(boundary.Ptr()), rec.converging != 0);
+    s.Sync();  // the staging buffer is reused by the next broadcast
+  }
+  return 0.0;
+}
+
 ParallelDeconvolutionResult ParallelDeconvolution::ExecuteParallelRun(
     ImageSet& data_image, ImageSet& model_image,
     const std::vector<gpu::Planes>& psf_images,
@@ -528,22 +628,31 @@ ParallelDeconvolutionResult ParallelDeconvolution::ExecuteParallelRun(
   const size_t n_workers =
       std::min<size_t>(std::max<size_t>(settings_.parallel.max_threads, 1),
                        subimages_.size());
-  const bool concurrent = n_workers > 1;
+  const bool distributed = comm_ != nullptr;
+  const bool concurrent = !distributed && n_workers > 1;
   if (concurrent) EnsureWorkers(s, n_workers);
-  if (concurrent)
-    RunSubImagesConcurrently(data_image, model_image, result_model, psf_images,
-                             psf_indices, 0.0, true);
-  else
-    for (SubImage& sub : subimages_)
-      RunSubImage(sub, data_image, model_image, result_model,
-                  psf_images[psf_indices[sub.index]], 0.0, true);
   double start_peak = 0.0;
-  for (const SubImage& sub : subimages_)
-    if (sub.peak > start_peak) start_peak = sub.peak;
+  if (distributed) {
+    start_peak = RunSubImagesDistributed(data_image, model_image, result_model,
+                                         psf_images, psf_indices, 0.0, true);
+  } else {
+    if (concurrent)
+      RunSubImagesConcurrently(data_image, model_image, result_model, psf_images,
+                               psf_indices, 0.0, true);
+    else
+      for (SubImage& sub : subimages_)
+        RunSubImage(sub, data_image, model_image, result_model,
+                    psf_images[psf_indices[sub.index]], 0.0, true);
+    for (const SubImage& sub : subimages_)
+      if (sub.peak > start_peak) start_peak = sub.peak;
+  }
   const double threshold = start_peak * (1.0 - major_loop_gain);
   log::Info() << "Maximum start peak over " << subimages_.size()
               << " subimages: " << start_peak << '\n';
-  if (concurrent)
+  if (distributed)
+    RunSubImagesDistributed(data_image, model_image, result_model, psf_images,
+                            psf_indices, threshold, false);
+  else if (concurrent)
     RunSubImagesConcurrently(data_image, model_image, result_model, psf_images,
                              psf_indices, threshold, false);
   else

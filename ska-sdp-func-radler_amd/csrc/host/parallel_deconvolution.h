@@ -9,6 +9,7 @@
 #include <optional>
 #include <vector>
 
+#include "communicator.h"
 #include "deconvolution_algorithm.h"
 #include "device.h"
 #include "psf_offset.h"
@@ -63,6 +64,11 @@ class ParallelDeconvolution {
     worker_main_device_ = -1;
     mask_ = nullptr;
   }
+  /// Share the subimages of gridded runs with the other ranks of a
+  /// process-per-GPU job (a size-1 communicator runs them all here, in the
+  /// same snapshot order). Every rank must call Perform with the same inputs.
+  void SetCommunicator(std::shared_ptr<Communicator> comm) { comm_ = std::move(comm); }
+  const std::shared_ptr<Communicator>& GetCommunicator() const { return comm_; }
   /// Worker streams of the concurrent subimage pool (0 until a gridded run
   /// with settings.parallel.max_threads > 1).
   size_t WorkerCount() const { return workers_.size(); }
@@ -90,6 +96,15 @@ class ParallelDeconvolution {
                                 const std::vector<size_t>& psf_indices,
                                 double major_iteration_threshold,
                                 bool find_peak_only);
+  /// Process-per-GPU split: this rank deconvolves the subimages it owns
+  /// (SubImageOwner) from the pass-start residual, then every subimage's
+  /// boxes are broadcast by their owner and merged by all ranks in subimage
+  /// order. Returns the global start peak for the find-peak pass.
+  double RunSubImagesDistributed(ImageSet& data_image, const ImageSet& model_image,
+                                 ImageSet& result_model,
+                                 const std::vector<gpu::Planes>& psf_images,
+                                 const std::vector<size_t>& psf_indices,
+                                 double major_iteration_threshold, bool find_peak_only);
   void EnsureWorkers(gpu::Session& main, size_t n);
   static std::vector<int> PoolDevices(int main_device);
 
@@ -101,6 +116,7 @@ class ParallelDeconvolution {
   std::vector<SubImage> subimages_;
   const Settings& settings_;
   const bool* mask_ = nullptr;
+  std::shared_ptr<Communicator> comm_;
 };
 
 /// Subimage geometry of the grid (parallel_deconvolution.cc:57-166).

@@ -218,6 +218,10 @@ void Radler::FreeDeconvolutionAlgorithms() {
   table_.reset();
 }
 
+void Radler::SetCommunicator(std::shared_ptr<Communicator> comm) {
+  parallel_deconvolution_->SetCommunicator(std::move(comm));
+}
+
 gpu::Session& Radler::DeviceSession() const {
   // The device is opened on first use, so constructing a Radler (argument
   // validation) needs no GPU; Perform() fails loudly without one.

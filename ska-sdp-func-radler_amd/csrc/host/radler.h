@@ -21,6 +21,7 @@ class DeconvolutionAlgorithm;
 namespace gpu {
 class Session;
 }
+class Communicator;
 
 class Radler {
  public:
@@ -48,6 +49,10 @@ class Radler {
   algorithms::ParallelDeconvolution& Parallel() const {
     return *parallel_deconvolution_;
   }
+  /// MI355X build: share the subimages of gridded runs (settings.parallel
+  /// grid > 1x1) with the other ranks of a process-per-GPU job; every rank
+  /// calls Perform with the same inputs and gets the same result.
+  void SetCommunicator(std::shared_ptr<Communicator> comm);
 
  private:
   Radler(const Settings& settings, double beam_size);

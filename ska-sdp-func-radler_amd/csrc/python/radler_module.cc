@@ -9,6 +9,7 @@
 
 #include <sstream>
 
+#include "communicator.h"
 #include "device.h"
 #include "device_run.h"
 #include "image_accessors.h"
@@ -313,6 +314,7 @@ void InitRadler(py::module& m) {  // python/pyradler.cc
              return another;
            },
            py::arg("major_iteration_number"))
+      .def("set_communicator", &radler::Radler::SetCommunicator, py::arg("communicator"))
       .def_property_readonly("iteration_number", &radler::Radler::IterationNumber)
       .def_property_readonly("component_list", &radler::Radler::GetComponentList);
 }
@@ -375,6 +377,65 @@ void InitTiling(py::module& m) {
   }, py::arg("image"), py::arg("grid_width"), py::arg("grid_height"));
 }
 
+void InitDistributed(py::module& m) {
+  py::module d = m.def_submodule(
+      "distributed",
+      "Process-per-GPU split of ParallelDeconvolution (one rank per GPU)");
+  py::class_<radler::Communicator, std::shared_ptr<radler::Communicator>>(d, "Communicator")
+      .def_property_readonly("rank", &radler::Communicator::Rank)
+      .def_property_readonly("size", &radler::Communicator::Size);
+  py::class_<radler::RcclCommunicator, radler::Communicator,
+             std::shared_ptr<radler::RcclCommunicator>>(d, "RcclCommunicator")
+      .def(py::init([](int device, int size, int rank, py::bytes unique_id) {
+             const std::string id = unique_id;
+             if (id.size() != radler::RcclCommunicator::IdSize())
+               throw std::runtime_error("RcclCommunicator: unique id has the wrong size");
+             std::shared_ptr<radler::gpu::Session> session =
+                 radler::gpu::Session::ForDevice(device);
+             py::gil_scoped_release release;  // ncclCommInitRank blocks on the peers
+             return std::make_shared<radler::RcclCommunicator>(session, size, rank,
+                                                               id.data());
+           }),
+           py::arg("device"), py::arg("size"), py::arg("rank"), py::arg("unique_id"));
+  d.def("rccl_id_size", &radler::RcclCommunicator::IdSize);
+  d.def("rccl_unique_id", []() {
+    std::string id(radler::RcclCommunicator::IdSize(), '\0');
+    radler::RcclCommunicator::UniqueId(id.data());
+    return py::bytes(id);
+  });
+  py::class_<radler::HostCommunicator, radler::Communicator,
+             std::shared_ptr<radler::HostCommunicator>>(d, "HostCommunicator")
+      .def(py::init([](int size, int rank, py::function broadcast, py::function max) {
+             // the callbacks run while Perform has released the GIL
+             auto bcast = [broadcast](void* data, size_t bytes, int root) {
+               py::gil_scoped_acquire acquire;
+               py::array_t<uint8_t> view({py::ssize_t(bytes)}, {py::ssize_t(1)},
+                                         static_cast<uint8_t*>(data), py::none());
+               broadcast(view, root);
+             };
+             auto fmax = [max](float v) {
+               py::gil_scoped_acquire acquire;
+               return max(v).cast<float>();
+             };
+             return std::make_shared<radler::HostCommunicator>(size, rank, bcast, fmax);
+           }),
+           py::arg("size"), py::arg("rank"), py::arg("broadcast"),
+           py::arg("allreduce_max"),
+           "Collectives on host memory supplied by the job: broadcast(uint8 array, "
+           "root) fills the array in place on every rank but root; allreduce_max(x) "
+           "returns the maximum over ranks")
+      .def("broadcast_host",
+           [](radler::HostCommunicator& self, py::array_t<uint8_t, py::array::c_style> a,
+              int root) {
+             self.BroadcastHost(a.mutable_data(), size_t(a.size()), root);
+           },
+           py::arg("array"), py::arg("root"))
+      .def("allreduce_max",
+           [](radler::HostCommunicator& self, float v) { return self.AllreduceMaxHost(v); },
+           py::arg("value"));
+  d.def("subimage_owner", &radler::SubImageOwner, py::arg("index"), py::arg("n_ranks"));
+}
+
 void InitGpu(py::module& m) {
   py::module g = m.def_submodule("gpu", "MI355X device helpers (bench/tests)");
   g.def("set_verbosity", &radler::log::SetVerbosity);
@@ -389,6 +450,8 @@ void InitGpu(py::module& m) {
            py::arg("settings"), py::arg("psf"), py::arg("residual"),
            py::arg("weights") = std::vector<double>(), py::arg("beam_size") = 0.0)
       .def("restore", &radler::DeviceRun::Restore)
+      .def("set_communicator", &radler::DeviceRun::SetCommunicator,
+           py::arg("communicator"))
       .def("execute",
            [](radler::DeviceRun& self) {
              radler::algorithms::ParallelDeconvolutionResult r;
@@ -461,4 +524,5 @@ PYBIND11_MODULE(radler, m) {  // python/pywrappers.cc
   InitComponentList(m);
   InitGpu(m);
   InitTiling(m);
+  InitDistributed(m);
 }
