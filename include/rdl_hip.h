@@ -393,6 +393,20 @@ int rdl_conv_columns_ex(rdl_conv* c, const void* d_in, void* d_out,
                         const void* d_kernel, int mode, double scale,
                         const uint8_t* d_row_mask, int kernel_layout,
                         int out_layout);
+/* As rdl_conv_columns_ex with the input layout too (in_layout
+ * RDL_CONV_COL_MAJOR: a mode-2 spectrum stored as columns). Every layout
+ * combination needs the compile-time-planned column kernels
+ * (rdl_conv_fast(c) & RDL_CONV_FAST_COLUMNS); the runtime-plan kernels read
+ * row-major input and write column-major output in mode 0 only. */
+int rdl_conv_columns_layout(rdl_conv* c, const void* d_in, void* d_out,
+                            const void* d_kernel, int mode, double scale,
+                            const uint8_t* d_row_mask, int in_layout,
+                            int kernel_layout, int out_layout);
+/* Which passes of this plan use the compile-time-planned kernels
+ * (csrc/hip/fft_fast.hip): a bitmask of the two flags. */
+#define RDL_CONV_FAST_COLUMNS 1
+#define RDL_CONV_FAST_ROWS 2
+int rdl_conv_fast(const rdl_conv* c);
 
 /* dst = a * b * scale, complex, n_complex elements. */
 int rdl_spectrum_multiply(rdl_session* s, void* d_dst, const void* d_a,

@@ -1,0 +1,545 @@
+// Compile-time-planned FFT kernels for the hot transform sizes of the
+// multiscale path: the float64 padded residual correction
+// (SubMinorLoop::CorrectResidualDirty, cpp/algorithms/subminor_loop.cc:
+// 195-218, sizes utils::GetConvolutionSize(scale, W, 1.1)) and the float32
+// scale convolutions (MultiScaleTransforms::Transform,
+// cpp/algorithms/multiscale/multiscale_transforms.cc:9-21, size W x H).
+// Same data layouts and results (to rounding) as lds_fft.hip's runtime-plan
+// kernels, which remain the path for every other size.
+//
+// Why a second engine: the runtime-plan kernels park their waves ~65 % of
+// the time (rocprofv3 SQ_WAIT_ANY on MI355X): one 145 KiB double column or
+// row pair per CU, the global loads staged through LDS behind a full
+// __syncthreads(), generic index arithmetic and out-of-line passes. Here
+//   * every pass is specialised at compile time (radix, span, butterflies per
+//     thread), fully inlined, twiddles issued before the LDS reads,
+//   * workgroups are persistent (one per CU slot) and keep their global
+//     traffic in flight across LDS-only barriers: the kernel spectrum column
+//     is loaded into registers while the forward column transform runs, the
+//     next row pair's spectrum while the current one is transformed,
+//   * rows outside the output window are never transformed, sparse inputs
+//     (the sub-minor model's occupied rows) are read from a compacted list.
+#include <map>
+#include <mutex>
+#include <tuple>
+
+#include "fft_dft.h"
+#include "fft_fast.h"
+#include "rdl_internal.h"
+
+namespace rdl {
+namespace ff {
+
+// Orders LDS only: __syncthreads() would also drain the prefetch loads.
+__device__ __forceinline__ void LdsSync() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// One Stockham pass (radix R, span NS) over a length-N transform in LDS, in
+// place (inputs read to registers before the barrier). Twiddles W_N^m are
+// tw[m * TWS] (TWS = 2: a half-length transform reads the full-length
+// table). Float twiddles come from the table per power; double builds w^r by
+// recurrence from one load (error ~1e-15, far below the float rounding of
+// the result).
+template <typename T, uint32_t TH, uint32_t N, uint32_t R, uint32_t NS, uint32_t TWS>
+__device__ __forceinline__ void Pass(Cx<T>* buf, const Cx<T>* __restrict__ tw,
+                                     uint32_t tid) {
+  constexpr uint32_t NB = N / R;
+  constexpr uint32_t BPT = (NB + TH - 1) / TH;
+  constexpr uint32_t M = N / (NS * R);
+  constexpr bool kTable = sizeof(T) == 4;
+  constexpr uint32_t NW = NS > 1 ? (kTable ? R - 1 : 1) : 1;
+  Cx<T> v[BPT][R];
+  Cx<T> w[BPT][NW];
+#pragma unroll
+  for (uint32_t i = 0; i < BPT; ++i) {
+    const uint32_t j = tid + i * TH;
+    if (NB % TH == 0 || j < NB) {
+      if constexpr (NS > 1) {
+        const uint32_t k = j % NS;
+#pragma unroll
+        for (uint32_t q = 0; q < NW; ++q) w[i][q] = tw[k * (q + 1) * M * TWS];
+      }
+#pragma unroll
+      for (uint32_t r = 0; r < R; ++r) v[i][r] = buf[j + r * NB];
+    }
+  }
+  LdsSync();
+#pragma unroll
+  for (uint32_t i = 0; i < BPT; ++i) {
+    const uint32_t j = tid + i * TH;
+    if (NB % TH == 0 || j < NB) {
+      const uint32_t k = j % NS;
+      if constexpr (NS > 1) {
+        if constexpr (kTable) {
+#pragma unroll
+          for (uint32_t r = 1; r < R; ++r) v[i][r] = Mul(v[i][r], w[i][r - 1]);
+        } else {
+          Cx<T> wr = w[i][0];
+          v[i][1] = Mul(v[i][1], wr);
+#pragma unroll
+          for (uint32_t r = 2; r < R; ++r) {
+            wr = Mul(wr, w[i][0]);
+            v[i][r] = Mul(v[i][r], wr);
+          }
+        }
+      }
+      Dft<T, int(R)>::Run(v[i]);
+      const uint32_t d = (j / NS) * NS * R + k;
+#pragma unroll
+      for (uint32_t r = 0; r < R; ++r) buf[d + r * NS] = v[i][r];
+    }
+  }
+  LdsSync();
+}
+
+template <typename T, uint32_t TH, uint32_t N, uint32_t TWS, uint32_t NS, uint32_t R,
+          uint32_t... Rest>
+__device__ __forceinline__ void Fft(Cx<T>* buf, const Cx<T>* __restrict__ tw,
+                                    uint32_t tid) {
+  Pass<T, TH, N, R, NS, TWS>(buf, tw, tid);
+  if constexpr (sizeof...(Rest) > 0)
+    Fft<T, TH, N, TWS, NS * R, Rest...>(buf, tw, tid);
+}
+
+template <uint32_t... Rs>
+constexpr uint32_t Product() {
+  return (Rs * ... * 1u);
+}
+
+// ------------------------------------------------------------- columns
+// One spectrum column of length N per workgroup round (persistent grid).
+struct ColArgs {
+  uint32_t n_cols;    // spectrum columns = width / 2 + 1
+  uint32_t ld;        // row stride of row-major buffers (= n_cols)
+  uint32_t mode;      // 0 forward; 1 forward, x K x s, inverse; 2 x K x s, inverse
+  uint32_t in_cm, out_cm, kern_cm;  // column-major layouts (column c at c * N)
+  const uint32_t* rows;    // modes 0/1: the input's non-zero rows, or NULL:
+  const uint32_t* n_rows;  //   rows [row0, row0 + row_n) (their count: device)
+  uint32_t row0, row_n;
+  uint32_t per_xcd;   // columns each XCD takes per round (grid / 8)
+  double scale;
+};
+
+// PF: the kernel column is loaded into registers before the forward
+// transform (in flight meanwhile); otherwise after it.
+template <typename T, uint32_t TH, bool PF, uint32_t... Rs>
+__global__ __launch_bounds__(TH) void Columns(ColArgs a, const Cx<T>* __restrict__ in,
+                                              Cx<T>* out,
+                                              const Cx<T>* __restrict__ kern,
+                                              const Cx<T>* __restrict__ tw) {
+  constexpr uint32_t N = Product<Rs...>();
+  constexpr uint32_t E = (N + TH - 1) / TH;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  Cx<T>* buf = reinterpret_cast<Cx<T>*>(lds_raw);
+  const uint32_t tid = threadIdx.x;
+  const uint32_t b = blockIdx.x, G = gridDim.x;
+  const T s = T(a.scale);
+  // sparse: only some rows are non-zero (a list, or a range short of N);
+  // LDS then holds zeros everywhere else between columns
+  const bool listed = a.rows != nullptr && a.mode != 2;
+  const bool sparse = a.mode != 2 && (listed || a.row_n < N);
+  const uint32_t n_rows = listed ? *a.n_rows : a.row_n;
+  if (sparse) {
+#pragma unroll
+    for (uint32_t i = 0; i < E; ++i) {
+      const uint32_t y = tid + i * TH;
+      if (N % TH == 0 || y < N) buf[y] = Cx<T>{T(0), T(0)};
+    }
+    LdsSync();
+  }
+  for (uint32_t round = 0; round * G < a.n_cols; ++round) {
+    // opaque per round: keeps the (loop-invariant) per-element addresses of
+    // every pass from being hoisted out of the loop into spilled registers
+    uint32_t tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    // XCD-aware: the columns of one round on one XCD are contiguous, so the
+    // row-major lines they share meet in one L2
+    const uint32_t c = round * G + (b & 7u) * a.per_xcd + (b >> 3);
+    const bool active = c < a.n_cols;
+    // uniform column bases (scalar registers) + 32-bit element offsets
+    const uint32_t in_stride = (a.mode == 2 && a.in_cm) ? 1u : a.ld;
+    const Cx<T>* in_c = (a.mode == 2 && a.in_cm) ? in + size_t(c) * N : in + c;
+    const uint32_t k_stride = a.kern_cm ? 1u : a.ld;
+    const Cx<T>* kern_c = a.kern_cm ? kern + size_t(c) * N : kern + c;
+    Cx<T> K[E];
+    auto load_kernel = [&]() {
+#pragma unroll
+      for (uint32_t i = 0; i < E; ++i) {
+        const uint32_t y = tid + i * TH;
+        if (N % TH == 0 || y < N) K[i] = kern_c[y * k_stride];
+      }
+    };
+    if (active) {
+      if (sparse) {
+        for (uint32_t q = tid; q < n_rows; q += TH) {
+          const uint32_t y = listed ? a.rows[q] : a.row0 + q;
+          buf[y] = in_c[y * in_stride];
+        }
+      } else {
+#pragma unroll
+        for (uint32_t i = 0; i < E; ++i) {
+          const uint32_t y = tid + i * TH;
+          if (N % TH == 0 || y < N) buf[y] = in_c[y * in_stride];
+        }
+      }
+      if (PF && a.mode != 0) load_kernel();
+    }
+    LdsSync();
+    if (a.mode != 2) Fft<T, TH, N, 1, 1, Rs...>(buf, tw, tid);
+    if (a.mode != 0) {
+      if (!PF && active) load_kernel();
+      // inverse = conj(forward(conj(X K s)))
+#pragma unroll
+      for (uint32_t i = 0; i < E; ++i) {
+        const uint32_t y = tid + i * TH;
+        if (N % TH == 0 || y < N) buf[y] = Conj(Scale(Mul(buf[y], K[i]), s));
+      }
+      LdsSync();
+      Fft<T, TH, N, 1, 1, Rs...>(buf, tw, tid);
+    }
+    if (active) {
+      const uint32_t o_stride = a.out_cm ? 1u : a.ld;
+      Cx<T>* out_c = a.out_cm ? out + size_t(c) * N : out + c;
+#pragma unroll
+      for (uint32_t i = 0; i < E; ++i) {
+        const uint32_t y = tid + i * TH;
+        if (N % TH == 0 || y < N) {
+          Cx<T> v = buf[y];
+          if (a.mode != 0) v = Conj(v);
+          out_c[y * o_stride] = v;
+          if (sparse) buf[y] = Cx<T>{T(0), T(0)};
+        }
+      }
+    } else if (sparse) {
+#pragma unroll
+      for (uint32_t i = 0; i < E; ++i) {
+        const uint32_t y = tid + i * TH;
+        if (N % TH == 0 || y < N) buf[y] = Cx<T>{T(0), T(0)};
+      }
+    }
+    LdsSync();
+  }
+}
+
+// ----------------------------------------------------------------- rows
+// One real row of length 2H per workgroup, as a half-length complex FFT
+// (z[n] = x[2n] + i x[2n+1]) with the even/odd split folded in: H complex in
+// LDS (72 KiB for H = 4536 double), so two workgroups share a CU and one's
+// loads overlap the other's transform. Twiddles: the length-2H table.
+struct RowArgs {
+  uint32_t height;      // plane rows
+  uint32_t ld;          // spectrum row stride (H + 1)
+  uint32_t img_w, img_h, ox, oy;  // image window inside the plane
+  const uint32_t* rows;    // forward: the non-zero plane rows (NULL: the window rows)
+  const uint32_t* n_rows;  // their count (device)
+  int subtract;         // inverse: 0 write, 1 subtract from out
+};
+
+// spectrum rows (X[0..H]) -> real rows written into / subtracted from the
+// window. Z[k] = (X[k] + conj X[H-k]) + i W^-k (X[k] - conj X[H-k]) gives
+// z = IFFT_H(Z) = N (x_even + i x_odd) (unnormalised, as C2R); the inverse
+// runs as conj(FFT(conj Z)). The imaginary parts of X[0] and X[H] are
+// ignored, as by C2R.
+template <typename T, uint32_t TH, uint32_t... Rs>
+__global__ __launch_bounds__(TH) void RowsInverse(RowArgs a, const Cx<T>* __restrict__ spec,
+                                                  float* __restrict__ out,
+                                                  const Cx<T>* __restrict__ tw) {
+  constexpr uint32_t H = Product<Rs...>();
+  constexpr uint32_t EH = (H + TH - 1) / TH;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  Cx<T>* buf = reinterpret_cast<Cx<T>*>(lds_raw);
+  const uint32_t tid = threadIdx.x;
+  const uint32_t iy = blockIdx.x;  // output row of the window
+  if (iy >= a.img_h) return;
+  const uint32_t y = iy + a.oy;
+  const Cx<T>* X = spec + size_t(y) * a.ld;
+#pragma unroll
+  for (uint32_t i = 0; i < EH; ++i) {
+    const uint32_t k = tid + i * TH;
+    if (H % TH == 0 || k < H) {
+      Cx<T> xk = X[k], xm = X[H - k];
+      if (k == 0) {
+        xk.y = T(0);
+        xm.y = T(0);
+      }
+      const Cx<T> sum = {xk.x + xm.x, xk.y - xm.y};  // X[k] + conj X[H-k]
+      const Cx<T> dif = {xk.x - xm.x, xk.y + xm.y};  // X[k] - conj X[H-k]
+      const Cx<T> wk = Conj(tw[k]);                  // W_N^-k
+      const Cx<T> t = Mul(wk, dif);
+      // Z = sum + i t, stored conjugated
+      buf[k] = {sum.x - t.y, -(sum.y + t.x)};
+    }
+  }
+  LdsSync();
+  Fft<T, TH, H, 2, 1, Rs...>(buf, tw, tid);
+  float* o = out + size_t(iy) * a.img_w;
+#pragma unroll
+  for (uint32_t i = 0; i < EH; ++i) {
+    const uint32_t n = tid + i * TH;
+    if (H % TH != 0 && n >= H) continue;
+    const Cx<T> z = buf[n];  // conj(result): x[2n] = z.x, x[2n+1] = -z.y
+    const uint32_t x0 = 2 * n, x1 = x0 + 1;
+    if (x0 >= a.ox && x0 < a.ox + a.img_w) {
+      float* p = o + (x0 - a.ox);
+      *p = a.subtract ? *p - float(z.x) : float(z.x);
+    }
+    if (x1 >= a.ox && x1 < a.ox + a.img_w) {
+      float* p = o + (x1 - a.ox);
+      *p = a.subtract ? *p - float(-z.y) : float(-z.y);
+    }
+  }
+}
+
+// real plane rows (the window's image rows, zero outside) -> spectrum rows
+// X[0..H]: X[k] = E[k] + W^k O[k], E = (Z[k] + conj Z[H-k]) / 2,
+// O = (Z[k] - conj Z[H-k]) / 2i. Rows not listed are not touched (the
+// column pass reads only listed rows).
+template <typename T, uint32_t TH, uint32_t... Rs>
+__global__ __launch_bounds__(TH) void RowsForward(RowArgs a, const float* __restrict__ in,
+                                                  Cx<T>* __restrict__ spec,
+                                                  const Cx<T>* __restrict__ tw) {
+  constexpr uint32_t H = Product<Rs...>();
+  constexpr uint32_t EH = (H + TH - 1) / TH;
+  constexpr uint32_t EX = (H + 1 + TH - 1) / TH;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  Cx<T>* buf = reinterpret_cast<Cx<T>*>(lds_raw);
+  const uint32_t tid = threadIdx.x;
+  const uint32_t n_rows = a.rows ? *a.n_rows : a.img_h;
+  for (uint32_t r = blockIdx.x; r < n_rows; r += gridDim.x) {
+    uint32_t tid = threadIdx.x;  // opaque per row (see Columns)
+    asm volatile("" : "+v"(tid));
+    const uint32_t y = a.rows ? a.rows[r] : r + a.oy;
+    const int64_t iy = int64_t(y) - a.oy;
+    const bool in_y = iy >= 0 && iy < a.img_h;
+    const float* row = in + (in_y ? size_t(iy) * a.img_w : 0);
+#pragma unroll
+    for (uint32_t i = 0; i < EH; ++i) {
+      const uint32_t n = tid + i * TH;
+      if (H % TH != 0 && n >= H) continue;
+      const uint32_t x0 = 2 * n, x1 = x0 + 1;
+      const T e = in_y && x0 >= a.ox && x0 < a.ox + a.img_w ? T(row[x0 - a.ox]) : T(0);
+      const T od = in_y && x1 >= a.ox && x1 < a.ox + a.img_w ? T(row[x1 - a.ox]) : T(0);
+      buf[n] = {e, od};
+    }
+    LdsSync();
+    Fft<T, TH, H, 2, 1, Rs...>(buf, tw, tid);
+    Cx<T>* X = spec + size_t(y) * a.ld;
+    const T h = T(0.5);
+#pragma unroll
+    for (uint32_t i = 0; i < EX; ++i) {
+      const uint32_t k = tid + i * TH;
+      if (k > H) continue;
+      const Cx<T> zk = buf[k == H ? 0 : k];
+      const Cx<T> zc = Conj(buf[k == 0 ? 0 : H - k]);
+      const Cx<T> ev = {h * (zk.x + zc.x), h * (zk.y + zc.y)};
+      const Cx<T> od = {h * (zk.y - zc.y), -h * (zk.x - zc.x)};  // (zk - zc) / 2i
+      X[k] = Add(ev, Mul(tw[k], od));
+    }
+    LdsSync();
+  }
+}
+
+// row mask (one byte per plane row) -> ascending list of the non-zero rows
+__global__ __launch_bounds__(1024) void CompactRows(const uint8_t* __restrict__ mask,
+                                                    uint32_t n, uint32_t* __restrict__ rows,
+                                                    uint32_t* __restrict__ count) {
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t base;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  if (tid == 0) base = 0;
+  __syncthreads();
+  for (uint32_t off = 0; off < n; off += 1024) {
+    const uint32_t y = off + tid;
+    const bool f = y < n && mask[y] != 0;
+    const uint64_t bal = __ballot(f);
+    const uint32_t before = __popcll(bal & ((uint64_t(1) << lane) - 1));
+    if (lane == 0) wsum[wave] = __popcll(bal);
+    __syncthreads();
+    uint32_t wbase = base;
+    for (uint32_t w = 0; w < wave; ++w) wbase += wsum[w];
+    if (f) rows[wbase + before] = y;
+    __syncthreads();
+    if (tid == 0)
+      for (uint32_t w = 0; w < 16; ++w) base += wsum[w];
+    __syncthreads();
+  }
+  if (tid == 0) *count = base;
+}
+
+}  // namespace ff
+
+// ---------------------------------------------------------------- plans
+// Supported transform lengths: columns (full length N) and rows (half length
+// H = N / 2). Radices in pass order; double stays at radix <= 9 and keeps
+// each pass's butterflies-per-thread x radix small (1024 threads leave 128
+// VGPRs; checked spill-free with -Rpass-analysis=kernel-resource-usage).
+#define RDL_FAST_COLS(T, TH, PF, ...)                                          \
+  FastColumns {                                                                \
+    ff::Product<__VA_ARGS__>(), sizeof(T) == 8, TH,                            \
+        reinterpret_cast<const void*>(&ff::Columns<T, TH, PF, __VA_ARGS__>)    \
+  }
+#define RDL_FAST_ROWS(T, TH, ...)                                              \
+  FastRows {                                                                   \
+    2 * ff::Product<__VA_ARGS__>(), sizeof(T) == 8, TH,                        \
+        reinterpret_cast<const void*>(&ff::RowsInverse<T, TH, __VA_ARGS__>),   \
+        reinterpret_cast<const void*>(&ff::RowsForward<T, TH, __VA_ARGS__>)    \
+  }
+
+const FastColumns* FindFastColumns(uint32_t n, bool f64) {
+  static const FastColumns kPlans[] = {
+      // float64 padded correction sizes of 8192^2 (scales 0..256) and 4096^2
+      RDL_FAST_COLS(double, 1024, true, 4, 4, 9, 9, 7),        // 9072
+      RDL_FAST_COLS(double, 1024, true, 4, 4, 4, 4, 4, 9),     // 9216
+      RDL_FAST_COLS(double, 1024, true, 4, 4, 4, 3, 7, 7),     // 9408
+      RDL_FAST_COLS(double, 1024, true, 2, 3, 3, 3, 5, 5, 7),  // 9450
+      RDL_FAST_COLS(double, 1024, true, 8, 9, 9, 7),           // 4536
+      RDL_FAST_COLS(double, 1024, true, 8, 8, 8, 9),           // 4608
+      RDL_FAST_COLS(double, 1024, true, 8, 4, 3, 7, 7),        // 4704
+      RDL_FAST_COLS(double, 1024, true, 8, 8, 3, 5, 5),        // 4800
+      RDL_FAST_COLS(double, 1024, true, 8, 5, 5, 5, 5),        // 5000
+      // float32 scale convolutions (two workgroups per CU)
+      RDL_FAST_COLS(float, 512, true, 8, 8, 8, 16),            // 8192
+      RDL_FAST_COLS(float, 512, true, 8, 8, 8, 8),             // 4096
+  };
+  for (const FastColumns& p : kPlans)
+    if (p.n == n && p.f64 == f64) return &p;
+  return nullptr;
+}
+
+const FastRows* FindFastRows(uint32_t n, bool f64) {
+  static const FastRows kPlans[] = {
+      RDL_FAST_ROWS(double, 512, 8, 9, 9, 7),      // 9072
+      RDL_FAST_ROWS(double, 512, 8, 8, 8, 9),      // 9216
+      RDL_FAST_ROWS(double, 512, 8, 4, 3, 7, 7),   // 9408
+      RDL_FAST_ROWS(double, 512, 9, 3, 5, 5, 7),   // 9450
+      RDL_FAST_ROWS(double, 256, 4, 9, 9, 7),      // 4536
+      RDL_FAST_ROWS(double, 256, 4, 4, 4, 4, 9),   // 4608
+      RDL_FAST_ROWS(double, 256, 4, 4, 3, 7, 7),   // 4704
+      RDL_FAST_ROWS(double, 256, 8, 4, 3, 5, 5),   // 4800
+      RDL_FAST_ROWS(double, 256, 4, 5, 5, 5, 5),   // 5000
+      RDL_FAST_ROWS(float, 256, 16, 16, 16),       // 8192
+      RDL_FAST_ROWS(float, 256, 16, 16, 8),        // 4096
+  };
+  for (const FastRows& p : kPlans)
+    if (p.n == n && p.f64 == f64) return &p;
+  return nullptr;
+}
+
+#undef RDL_FAST_COLS
+#undef RDL_FAST_ROWS
+
+namespace {
+// workgroups per CU for a kernel at its LDS size (cached), after raising its
+// dynamic LDS limit once per device
+int SlotsPerCu(rdl_session* s, const void* fn, uint32_t threads, size_t lds) {
+  static std::mutex mutex;
+  static std::map<std::tuple<const void*, int, size_t>, int> cache;
+  std::lock_guard<std::mutex> lock(mutex);
+  const auto key = std::make_tuple(fn, s->device, lds);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          int(kFftLdsBytesFast)) != hipSuccess)
+    return -1;
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, int(threads), lds) != hipSuccess)
+    return -1;
+  cache[key] = std::max(n, 1);
+  return cache[key];
+}
+}  // namespace
+
+int FastColumnsLaunch(rdl_session* s, const FastColumns* p, const void* in, void* out,
+                      const void* kern, const void* tw, uint32_t n_cols, uint32_t mode,
+                      int in_cm, int out_cm, int kern_cm, const uint32_t* rows,
+                      const uint32_t* n_rows, uint32_t row0, uint32_t row_n,
+                      double scale) {
+  const size_t lds = size_t(p->n) * (p->f64 ? 16 : 8);
+  const int slots = SlotsPerCu(s, p->kernel, p->threads, lds);
+  if (slots < 0) {
+    SetError("fast FFT columns: occupancy query failed");
+    return RDL_ERR_HIP;
+  }
+  ff::ColArgs a{};
+  a.n_cols = n_cols;
+  a.ld = n_cols;
+  a.mode = mode;
+  a.in_cm = in_cm ? 1u : 0u;
+  a.out_cm = out_cm ? 1u : 0u;
+  a.kern_cm = kern_cm ? 1u : 0u;
+  a.rows = rows;
+  a.n_rows = n_rows;
+  a.row0 = rows ? 0u : row0;
+  a.row_n = rows ? p->n : row_n;
+  a.scale = scale;
+  const uint32_t want = std::min<uint32_t>(n_cols, uint32_t(s->n_cus) * uint32_t(slots));
+  a.per_xcd = std::max<uint32_t>(1, (want + 7) / 8);
+  const uint32_t grid = 8 * a.per_xcd;
+  void* args[] = {&a, (void*)&in, (void*)&out, (void*)&kern,
+                  (void*)&tw};
+  RDL_HIP_CHECK(hipLaunchKernel(p->kernel, dim3(grid), dim3(p->threads), args, lds,
+                                s->stream));
+  return RDL_OK;
+}
+
+int FastRowsInverseLaunch(rdl_session* s, const FastRows* p, const void* spec, float* out,
+                          const void* tw, uint32_t height, uint32_t img_w, uint32_t img_h,
+                          uint32_t ox, uint32_t oy, int subtract) {
+  const size_t lds = size_t(p->n / 2) * (p->f64 ? 16 : 8);
+  if (SlotsPerCu(s, p->inverse, p->threads, lds) < 0) {
+    SetError("fast FFT rows: occupancy query failed");
+    return RDL_ERR_HIP;
+  }
+  if (img_h == 0) return RDL_OK;
+  ff::RowArgs a{};
+  a.height = height;
+  a.ld = p->n / 2 + 1;
+  a.img_w = img_w;
+  a.img_h = img_h;
+  a.ox = ox;
+  a.oy = oy;
+  a.subtract = subtract;
+  void* args[] = {&a, (void*)&spec, (void*)&out, (void*)&tw};
+  RDL_HIP_CHECK(hipLaunchKernel(p->inverse, dim3(img_h), dim3(p->threads), args, lds,
+                                s->stream));
+  return RDL_OK;
+}
+
+int FastRowsForwardLaunch(rdl_session* s, const FastRows* p, const float* in, void* spec,
+                          const void* tw, uint32_t height, uint32_t img_w, uint32_t img_h,
+                          uint32_t ox, uint32_t oy, const uint32_t* rows,
+                          const uint32_t* n_rows) {
+  const size_t lds = size_t(p->n / 2) * (p->f64 ? 16 : 8);
+  const int slots = SlotsPerCu(s, p->forward, p->threads, lds);
+  if (slots < 0) {
+    SetError("fast FFT rows: occupancy query failed");
+    return RDL_ERR_HIP;
+  }
+  ff::RowArgs a{};
+  a.height = height;
+  a.ld = p->n / 2 + 1;
+  a.img_w = img_w;
+  a.img_h = img_h;
+  a.ox = ox;
+  a.oy = oy;
+  a.rows = rows;
+  a.n_rows = n_rows;
+  const uint32_t max_rows = rows ? height : img_h;
+  if (max_rows == 0) return RDL_OK;
+  const uint32_t grid =
+      std::min<uint32_t>(max_rows, uint32_t(s->n_cus) * uint32_t(slots) * 2);
+  void* args[] = {&a, (void*)&in, (void*)&spec, (void*)&tw};
+  RDL_HIP_CHECK(hipLaunchKernel(p->forward, dim3(grid), dim3(p->threads), args, lds,
+                                s->stream));
+  return RDL_OK;
+}
+
+int FastCompactRows(rdl_session* s, const uint8_t* mask, uint32_t n, uint32_t* rows,
+                    uint32_t* count) {
+  ff::CompactRows<<<1, 1024, 0, s->stream>>>(mask, n, rows, count);
+  RDL_HIP_CHECK(hipGetLastError());
+  return RDL_OK;
+}
+
+}  // namespace rdl

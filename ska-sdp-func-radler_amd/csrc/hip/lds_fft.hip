@@ -22,41 +22,14 @@
 // rdl_conv_create returns RDL_ERR_UNSUPPORTED and callers use rocFFT.
 // Twiddles come from a float64 table (rounded to T for float plans).
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
+#include "fft_dft.h"
+#include "fft_fast.h"
 #include "rdl_internal.h"
 
 namespace rdl {
-
-template <typename T>
-struct Cx {
-  T x, y;
-};
-
-template <typename T>
-__device__ __forceinline__ Cx<T> Add(Cx<T> a, Cx<T> b) {
-  return {a.x + b.x, a.y + b.y};
-}
-template <typename T>
-__device__ __forceinline__ Cx<T> Sub(Cx<T> a, Cx<T> b) {
-  return {a.x - b.x, a.y - b.y};
-}
-template <typename T>
-__device__ __forceinline__ Cx<T> Mul(Cx<T> a, Cx<T> b) {
-  return {a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x};
-}
-template <typename T>
-__device__ __forceinline__ Cx<T> MulMinusI(Cx<T> a) {  // a * (-i)
-  return {a.y, -a.x};
-}
-template <typename T>
-__device__ __forceinline__ Cx<T> Conj(Cx<T> a) {
-  return {a.x, -a.y};
-}
-template <typename T>
-__device__ __forceinline__ Cx<T> Scale(Cx<T> a, T s) {
-  return {a.x * s, a.y * s};
-}
 
 #ifndef RDL_FFT_THREADS
 #define RDL_FFT_THREADS 1024
@@ -80,199 +53,7 @@ struct LdsPlan {
   const void* tw;   // n twiddles exp(-2 pi i k / n), Cx<T>
 };
 
-// ---- radix-R DFT (forward, e^{-2 pi i jk/R}) on registers
-template <typename T, int R>
-struct Dft;
 
-template <typename T>
-struct Dft<T, 2> {
-  __device__ __forceinline__ static void Run(Cx<T>* a) {
-    const Cx<T> t = a[1];
-    a[1] = Sub(a[0], t);
-    a[0] = Add(a[0], t);
-  }
-};
-
-template <typename T>
-struct Dft<T, 4> {
-  __device__ __forceinline__ static void Run(Cx<T>* a) {
-    const Cx<T> t0 = Add(a[0], a[2]), t1 = Sub(a[0], a[2]);
-    const Cx<T> t2 = Add(a[1], a[3]), t3 = MulMinusI(Sub(a[1], a[3]));
-    a[0] = Add(t0, t2);
-    a[2] = Sub(t0, t2);
-    a[1] = Add(t1, t3);
-    a[3] = Sub(t1, t3);
-  }
-};
-
-template <typename T>
-struct Dft<T, 8> {
-  __device__ __forceinline__ static void Run(Cx<T>* a) {
-    Cx<T> e[4] = {a[0], a[2], a[4], a[6]};
-    Cx<T> o[4] = {a[1], a[3], a[5], a[7]};
-    Dft<T, 4>::Run(e);
-    Dft<T, 4>::Run(o);
-    const T c = T(0.70710678118654752440084436210485);
-    // o[k] *= W8^k, W8 = (c, -c)
-    o[1] = {c * (o[1].x + o[1].y), c * (o[1].y - o[1].x)};
-    o[2] = MulMinusI(o[2]);
-    o[3] = {c * (o[3].y - o[3].x), -c * (o[3].x + o[3].y)};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      a[k] = Add(e[k], o[k]);
-      a[k + 4] = Sub(e[k], o[k]);
-    }
-  }
-};
-
-// odd radix: pairs (a_j, a_{R-j})
-template <int R>
-struct OddTables;
-template <>
-struct OddTables<3> {
-  static constexpr double c[3] = {1.0, -0.5, -0.5};
-  static constexpr double s[3] = {0.0, 0.86602540378443864676372317075294,
-                                  -0.86602540378443864676372317075294};
-};
-template <>
-struct OddTables<5> {
-  static constexpr double c[5] = {1.0, 0.30901699437494742410229341718282,
-                                  -0.80901699437494742410229341718282,
-                                  -0.80901699437494742410229341718282,
-                                  0.30901699437494742410229341718282};
-  static constexpr double s[5] = {0.0, 0.95105651629515357211643933337938,
-                                  0.58778525229247312916870595463907,
-                                  -0.58778525229247312916870595463907,
-                                  -0.95105651629515357211643933337938};
-};
-template <>
-struct OddTables<7> {
-  static constexpr double c[7] = {1.0,
-                                  0.62348980185873353052500488400424,
-                                  -0.22252093395631440428890256449679,
-                                  -0.90096886790241912623610231950745,
-                                  -0.90096886790241912623610231950745,
-                                  -0.22252093395631440428890256449679,
-                                  0.62348980185873353052500488400424};
-  static constexpr double s[7] = {0.0,
-                                  0.78183148246802980870844452667406,
-                                  0.97492791218182360701813168299393,
-                                  0.43388373911755812047576833284836,
-                                  -0.43388373911755812047576833284836,
-                                  -0.97492791218182360701813168299393,
-                                  -0.78183148246802980870844452667406};
-};
-
-template <typename T, int R>
-struct DftOdd {
-  __device__ __forceinline__ static void Run(Cx<T>* a) {
-    constexpr int H = (R - 1) / 2;
-    Cx<T> sp[H], sm[H];
-#pragma unroll
-    for (int j = 1; j <= H; ++j) {
-      sp[j - 1] = Add(a[j], a[R - j]);
-      sm[j - 1] = Sub(a[j], a[R - j]);
-    }
-    const Cx<T> a0 = a[0];
-    Cx<T> y0 = a0;
-#pragma unroll
-    for (int j = 0; j < H; ++j) y0 = Add(y0, sp[j]);
-#pragma unroll
-    for (int k = 1; k <= H; ++k) {
-      Cx<T> re = a0, im = {T(0), T(0)};
-#pragma unroll
-      for (int j = 1; j <= H; ++j) {
-        const T cj = T(OddTables<R>::c[(j * k) % R]);
-        const T sj = T(OddTables<R>::s[(j * k) % R]);
-        re = {re.x + cj * sp[j - 1].x, re.y + cj * sp[j - 1].y};
-        im = {im.x + sj * sm[j - 1].x, im.y + sj * sm[j - 1].y};
-      }
-      // y_k = re - i im, y_{R-k} = re + i im
-      a[k] = {re.x + im.y, re.y - im.x};
-      a[R - k] = {re.x - im.y, re.y + im.x};
-    }
-    a[0] = y0;
-  }
-};
-template <typename T>
-struct Dft<T, 3> : DftOdd<T, 3> {};
-template <typename T>
-struct Dft<T, 5> : DftOdd<T, 5> {};
-template <typename T>
-struct Dft<T, 7> : DftOdd<T, 7> {};
-
-// composite radices R = P x Q (Cooley-Tukey in registers):
-// X[k2 + Q k3] = sum_k1 W_P^{k1 k3} W_R^{k1 k2} sum_n2 x[k1 + P n2] W_Q^{n2 k2}
-template <typename T, int P, int Q>
-struct DftComposite {
-  __device__ __forceinline__ static void Run(Cx<T>* a, const double (*w)[2]) {
-    constexpr int R = P * Q;
-    Cx<T> t[P][Q];
-#pragma unroll
-    for (int k1 = 0; k1 < P; ++k1) {
-#pragma unroll
-      for (int n2 = 0; n2 < Q; ++n2) t[k1][n2] = a[k1 + P * n2];
-      Dft<T, Q>::Run(t[k1]);
-#pragma unroll
-      for (int k2 = 1; k2 < Q; ++k2)
-        if (k1 > 0) {
-          const int m = (k1 * k2) % R;
-          t[k1][k2] = Mul(t[k1][k2], Cx<T>{T(w[m][0]), T(w[m][1])});
-        }
-    }
-#pragma unroll
-    for (int k2 = 0; k2 < Q; ++k2) {
-      Cx<T> u[P];
-#pragma unroll
-      for (int k1 = 0; k1 < P; ++k1) u[k1] = t[k1][k2];
-      Dft<T, P>::Run(u);
-#pragma unroll
-      for (int k3 = 0; k3 < P; ++k3) a[k2 + Q * k3] = u[k3];
-    }
-  }
-};
-
-// exp(-2 pi i m / 16), exp(-2 pi i m / 9)
-__device__ constexpr double kW16[16][2] = {
-    {1.0, 0.0},
-    {0.92387953251128675612818318939679, -0.38268343236508977172845998403040},
-    {0.70710678118654752440084436210485, -0.70710678118654752440084436210485},
-    {0.38268343236508977172845998403040, -0.92387953251128675612818318939679},
-    {0.0, -1.0},
-    {-0.38268343236508977172845998403040, -0.92387953251128675612818318939679},
-    {-0.70710678118654752440084436210485, -0.70710678118654752440084436210485},
-    {-0.92387953251128675612818318939679, -0.38268343236508977172845998403040},
-    {-1.0, 0.0},
-    {-0.92387953251128675612818318939679, 0.38268343236508977172845998403040},
-    {-0.70710678118654752440084436210485, 0.70710678118654752440084436210485},
-    {-0.38268343236508977172845998403040, 0.92387953251128675612818318939679},
-    {0.0, 1.0},
-    {0.38268343236508977172845998403040, 0.92387953251128675612818318939679},
-    {0.70710678118654752440084436210485, 0.70710678118654752440084436210485},
-    {0.92387953251128675612818318939679, 0.38268343236508977172845998403040}};
-__device__ constexpr double kW9[9][2] = {
-    {1.0, 0.0},
-    {0.76604444311897803520239265055542, -0.64278760968653932632264340990726},
-    {0.17364817766693034885171662676931, -0.98480775301220805936674302458952},
-    {-0.5, -0.86602540378443864676372317075294},
-    {-0.93969262078590838405410927732473, -0.34202014332566873304409961468226},
-    {-0.93969262078590838405410927732473, 0.34202014332566873304409961468226},
-    {-0.5, 0.86602540378443864676372317075294},
-    {0.17364817766693034885171662676931, 0.98480775301220805936674302458952},
-    {0.76604444311897803520239265055542, 0.64278760968653932632264340990726}};
-
-template <typename T>
-struct Dft<T, 16> {
-  __device__ __forceinline__ static void Run(Cx<T>* a) {
-    DftComposite<T, 4, 4>::Run(a, kW16);
-  }
-};
-template <typename T>
-struct Dft<T, 9> {
-  __device__ __forceinline__ static void Run(Cx<T>* a) {
-    DftComposite<T, 3, 3>::Run(a, kW9);
-  }
-};
 
 // ---- one Stockham pass over `count` transforms of length n held in LDS
 // (in place: all butterfly inputs are read to registers before the barrier)
@@ -719,6 +500,11 @@ struct rdl_conv {
   uint32_t split_cols = 0;
   void* scratch = nullptr;  // spectrum-sized, for the out-of-place B passes
   size_t scratch_bytes = 0;
+  // compile-time-planned kernels (fft_fast.hip) where the size has a plan
+  const rdl::FastColumns* fast_cols = nullptr;
+  const rdl::FastRows* fast_rows = nullptr;
+  uint32_t* rows_list = nullptr;            // height words + the count
+  const uint8_t* rows_list_mask = nullptr;  // mask the list was made from
 };
 
 namespace {
@@ -754,9 +540,39 @@ int MakePlan(rdl_conv* c, uint32_t n, bool f64, rdl::LdsPlan* plan, void** tw) {
   return RDL_OK;
 }
 
+// the non-zero rows of `row_mask` as a device list (+ count), made once per
+// rows-forward / columns pair
+int CompactRowsFor(rdl_conv* c, const uint8_t* row_mask, bool reuse) {
+  if (reuse && c->rows_list_mask == row_mask) return RDL_OK;
+  if (!c->rows_list)
+    RDL_HIP_CHECK(hipMalloc(&c->rows_list, (size_t(c->height) + 1) * sizeof(uint32_t)));
+  RDL_TRY(rdl::FastCompactRows(c->s, row_mask, c->height, c->rows_list,
+                               c->rows_list + c->height));
+  c->rows_list_mask = row_mask;
+  return RDL_OK;
+}
+
 template <typename T>
 int LaunchRowsForward(rdl_conv* c, const float* in, uint32_t in_w, uint32_t in_h,
                       uint32_t ox, uint32_t oy, void* spec, const uint8_t* row_mask) {
+  if (c->fast_rows) {
+    const size_t row_bytes = size_t(c->width / 2 + 1) * sizeof(rdl::Cx<T>);
+    if (row_mask) {
+      RDL_TRY(CompactRowsFor(c, row_mask, false));
+      return rdl::FastRowsForwardLaunch(c->s, c->fast_rows, in, spec, c->tw_row,
+                                        c->height, in_w, in_h, ox, oy, c->rows_list,
+                                        c->rows_list + c->height);
+    }
+    // rows outside the window are zero spectra
+    char* base = static_cast<char*>(spec);
+    if (oy > 0) RDL_HIP_CHECK(hipMemsetAsync(base, 0, size_t(oy) * row_bytes, c->s->stream));
+    if (oy + in_h < c->height)
+      RDL_HIP_CHECK(hipMemsetAsync(base + size_t(oy + in_h) * row_bytes, 0,
+                                   size_t(c->height - oy - in_h) * row_bytes,
+                                   c->s->stream));
+    return rdl::FastRowsForwardLaunch(c->s, c->fast_rows, in, spec, c->tw_row, c->height,
+                                      in_w, in_h, ox, oy, nullptr, nullptr);
+  }
   rdl::RowArgs a{};
   a.row_mask = row_mask;
   a.plan = c->row_plan;
@@ -783,6 +599,9 @@ int LaunchRowsForward(rdl_conv* c, const float* in, uint32_t in_w, uint32_t in_h
 template <typename T>
 int LaunchRowsInverse(rdl_conv* c, const void* spec, float* out, uint32_t out_w,
                       uint32_t out_h, uint32_t ox, uint32_t oy, int subtract) {
+  if (c->fast_rows)
+    return rdl::FastRowsInverseLaunch(c->s, c->fast_rows, spec, out, c->tw_row, c->height,
+                                      out_w, out_h, ox, oy, subtract);
   rdl::RowArgs a{};
   a.plan = c->row_plan;
   a.height = c->height;
@@ -808,7 +627,20 @@ int LaunchRowsInverse(rdl_conv* c, const void* spec, float* out, uint32_t out_w,
 template <typename T>
 int LaunchColumns(rdl_conv* c, const void* in, void* out, const void* kern,
                   int mode, double scale, const uint8_t* row_mask, int kern_cm,
-                  int out_cm) {
+                  int out_cm, int in_cm = 0) {
+  if (c->fast_cols) {
+    const uint32_t* rows = nullptr;
+    const uint32_t* n_rows = nullptr;
+    if (row_mask && mode != 2) {
+      RDL_TRY(CompactRowsFor(c, row_mask, true));
+      rows = c->rows_list;
+      n_rows = c->rows_list + c->height;
+      c->rows_list_mask = nullptr;  // the mask's contents may change next time
+    }
+    return rdl::FastColumnsLaunch(c->s, c->fast_cols, in, out, kern, c->tw_col,
+                                  c->width / 2 + 1, uint32_t(mode), in_cm, out_cm, kern_cm,
+                                  rows, n_rows, 0, c->height, scale);
+  }
   rdl::ColArgs a{};
   a.row_mask = row_mask;
   a.kern_cm = kern_cm ? 1u : 0u;
@@ -918,10 +750,10 @@ int LaunchColumnsSplit(rdl_conv* c, const void* in, void* out, const void* kern,
 template <typename T>
 int LaunchColumnsAny(rdl_conv* c, const void* in, void* out, const void* kern,
                      int mode, double scale, const uint8_t* row_mask, int kern_cm,
-                     int out_cm) {
+                     int out_cm, int in_cm = 0) {
   if (c->split)
     return LaunchColumnsSplit<T>(c, in, out, kern, mode, scale, row_mask);
-  return LaunchColumns<T>(c, in, out, kern, mode, scale, row_mask, kern_cm, out_cm);
+  return LaunchColumns<T>(c, in, out, kern, mode, scale, row_mask, kern_cm, out_cm, in_cm);
 }
 
 double SpectrumBytes(const rdl_conv* c) {
@@ -982,6 +814,14 @@ int rdl_conv_create_ex(rdl_session* s, uint32_t width, uint32_t height, int f64,
                   " has no split into two factors >= 4");
     return RDL_ERR_UNSUPPORTED;
   }
+  // compile-time-planned kernels for the sizes that have one
+  // (RDL_FFT_FAST=0 keeps the runtime-plan kernels, for comparison)
+  const char* fast_env = std::getenv("RDL_FFT_FAST");
+  const bool fast_ok = !(fast_env && fast_env[0] == '0') && !want_split;
+  if (fast_ok) {
+    c->fast_cols = rdl::FindFastColumns(height, c->f64);
+    if (width % 2 == 0) c->fast_rows = rdl::FindFastRows(width, c->f64);
+  }
   if (want_split && can_split) {
     c->split = true;
     c->n1 = n1;
@@ -1005,6 +845,7 @@ int rdl_conv_destroy(rdl_conv* c) {
   if (c->tw_n1) (void)hipFree(c->tw_n1);
   if (c->tw_n2) (void)hipFree(c->tw_n2);
   if (c->scratch) (void)hipFree(c->scratch);
+  if (c->rows_list) (void)hipFree(c->rows_list);
   delete c;
   return RDL_OK;
 }
@@ -1083,6 +924,46 @@ int rdl_conv_columns_ex(rdl_conv* c, const void* d_in, void* d_out,
                                            d_row_mask, kcm, ocm)
                 : LaunchColumnsAny<float>(c, d_in, d_out, d_kernel, mode, scale,
                                           d_row_mask, kcm, ocm);
+}
+
+int rdl_conv_columns_layout(rdl_conv* c, const void* d_in, void* d_out,
+                            const void* d_kernel, int mode, double scale,
+                            const uint8_t* d_row_mask, int in_layout,
+                            int kernel_layout, int out_layout) {
+  RDL_ARG_CHECK(c && d_in && d_out, "NULL argument");
+  RDL_ARG_CHECK(mode >= 0 && mode <= 2, "mode must be 0, 1 or 2");
+  RDL_ARG_CHECK(mode == 0 || d_kernel, "kernel spectrum required");
+  for (int l : {in_layout, kernel_layout, out_layout})
+    RDL_ARG_CHECK(l == RDL_CONV_ROW_MAJOR || l == RDL_CONV_COL_MAJOR, "bad layout");
+  RDL_ARG_CHECK(in_layout == RDL_CONV_ROW_MAJOR || mode == 2,
+                "a column-major input is a mode-2 spectrum");
+  RDL_ARG_CHECK(in_layout == out_layout || d_out != d_in,
+                "changing the layout needs a separate output");
+  if (!c->fast_cols) {
+    if (in_layout == RDL_CONV_ROW_MAJOR && (out_layout == RDL_CONV_ROW_MAJOR || mode == 0))
+      return rdl_conv_columns_ex(c, d_in, d_out, d_kernel, mode, scale, d_row_mask,
+                                 kernel_layout, out_layout);
+    rdl::SetError("LDS FFT: this layout needs the compile-time-planned column kernels");
+    return RDL_ERR_UNSUPPORTED;
+  }
+  const double sb = SpectrumBytes(c);
+  const char* fam = d_row_mask ? (c->f64 ? "conv64_cols_sparse" : "conv_cols_sparse")
+                               : (c->f64 ? "conv64_cols" : "conv_cols");
+  const double bytes = d_row_mask ? (mode == 0 ? sb : 2.0 * sb)
+                                  : (mode == 0 ? 2.0 * sb : 3.0 * sb);
+  rdl::ScopedTiming t(c->s, fam, bytes);
+  const int icm = in_layout == RDL_CONV_COL_MAJOR;
+  const int kcm = kernel_layout == RDL_CONV_COL_MAJOR;
+  const int ocm = out_layout == RDL_CONV_COL_MAJOR;
+  return c->f64 ? LaunchColumnsAny<double>(c, d_in, d_out, d_kernel, mode, scale,
+                                           d_row_mask, kcm, ocm, icm)
+                : LaunchColumnsAny<float>(c, d_in, d_out, d_kernel, mode, scale,
+                                          d_row_mask, kcm, ocm, icm);
+}
+
+int rdl_conv_fast(const rdl_conv* c) {
+  if (!c) return 0;
+  return (c->fast_cols ? RDL_CONV_FAST_COLUMNS : 0) | (c->fast_rows ? RDL_CONV_FAST_ROWS : 0);
 }
 
 int rdl_conv_rows_inverse(rdl_conv* c, const void* d_spec, float* d_out,

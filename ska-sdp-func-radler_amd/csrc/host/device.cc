@@ -52,6 +52,9 @@ Fft::Fft(Session& s, size_t width, size_t height, bool f64)
   // (tools/bench_fft.py). RADLER_FFT=rocfft / lds overrides.
   const char* force = std::getenv("RADLER_FFT");
   const std::string mode = force ? force : "";
+  // float: rocFFT (RADLER_FFT=lds selects the LDS engine; at 8192^2 its
+  // compile-time-planned kernels tie with rocFFT, 453 vs 450 ms per bench
+  // step, the strided column access being the limit)
   const bool want_lds = mode == "lds" || (mode != "rocfft" && f64);
   // RADLER_FFT_COLUMNS=single / split overrides the column-pass choice
   const char* cols_env = std::getenv("RADLER_FFT_COLUMNS");
@@ -62,7 +65,12 @@ Fft::Fft(Session& s, size_t width, size_t height, bool f64)
   const bool lds_ok = want_lds &&
                       rdl_conv_create_ex(s.Handle(), uint32_t(width), uint32_t(height),
                                          f64 ? 1 : 0, strategy, &conv_) == RDL_OK;
-  if (lds_ok) {
+  const int fast = lds_ok ? rdl_conv_fast(conv_) : 0;
+  (void)fast;
+  if (conv_) {
+    // the compile-time-planned column kernels read and write any layout:
+    // spectra are then stored column by column (contiguous column reads)
+    cm_ = (rdl_conv_fast(conv_) & RDL_CONV_FAST_COLUMNS) != 0 && !SplitColumns();
     spectrum_bytes_ = rdl_conv_spectrum_bytes(conv_);
   } else {
     conv_ = nullptr;
@@ -83,7 +91,9 @@ Fft::~Fft() {
 }
 
 void Fft::Forward(const float* d_in, void* d_spectrum) {
-  if (conv_)
+  if (conv_ && cm_)
+    ForwardColumnMajor(d_in, d_spectrum);
+  else if (conv_)
     Check(rdl_conv_forward(conv_, d_in, d_spectrum), "rdl_conv_forward");
   else
     Check(rdl_fft_forward(f_, d_in, d_spectrum), "rdl_fft_forward");
@@ -101,9 +111,10 @@ void Fft::Convolve(float* d_image, const void* d_kernel_spectrum) {
     Check(rdl_conv_rows_forward(conv_, d_image, uint32_t(width_), uint32_t(height_),
                                 0, 0, work_.Ptr()),
           "rdl_conv_rows_forward");
-    Check(rdl_conv_columns(conv_, work_.Ptr(), work_.Ptr(), d_kernel_spectrum, 1,
-                           f64_ ? norm : double(float(norm))),
-          "rdl_conv_columns");
+    Check(rdl_conv_columns_layout(conv_, work_.Ptr(), work_.Ptr(), d_kernel_spectrum, 1,
+                                  f64_ ? norm : double(float(norm)), nullptr,
+                                  RDL_CONV_ROW_MAJOR, Layout(), RDL_CONV_ROW_MAJOR),
+          "rdl_conv_columns_layout");
     Check(rdl_conv_rows_inverse(conv_, work_.Ptr(), d_image, uint32_t(width_),
                                 uint32_t(height_), 0, 0, 0),
           "rdl_conv_rows_inverse");
@@ -117,9 +128,10 @@ void Fft::ConvolveSpectrum(const void* d_spectrum, const void* d_kernel_spectrum
                            void* d_work, float* d_out) {
   const double norm = 1.0 / (double(width_) * double(height_));
   if (conv_) {
-    Check(rdl_conv_columns(conv_, d_spectrum, d_work, d_kernel_spectrum, 2,
-                           f64_ ? norm : double(float(norm))),
-          "rdl_conv_columns");
+    Check(rdl_conv_columns_layout(conv_, d_spectrum, d_work, d_kernel_spectrum, 2,
+                                  f64_ ? norm : double(float(norm)), nullptr, Layout(),
+                                  Layout(), RDL_CONV_ROW_MAJOR),
+          "rdl_conv_columns_layout");
     Check(rdl_conv_rows_inverse(conv_, d_work, d_out, uint32_t(width_),
                                 uint32_t(height_), 0, 0, 0),
           "rdl_conv_rows_inverse");

@@ -78,6 +78,10 @@ class Fft {
   /// k * height), the layout the column pass reads contiguously.
   void ForwardColumnMajor(const float* d_in, void* d_spectrum);
   bool UsesLds() const { return conv_ != nullptr; }
+  /// LDS engine with compile-time-planned columns: Forward() stores spectra
+  /// column by column, which Convolve / ConvolveSpectrum then expect.
+  bool ColumnMajorSpectra() const { return cm_; }
+  int Layout() const { return cm_ ? RDL_CONV_COL_MAJOR : RDL_CONV_ROW_MAJOR; }
   /// LDS engine with the split (four-step) column passes: spectra are read
   /// row-major, so ForwardColumnMajor is not used.
   bool SplitColumns() const { return conv_ && rdl_conv_columns_split(conv_); }
@@ -90,6 +94,7 @@ class Fft {
   Session& s_;
   rdl_fft* f_ = nullptr;
   rdl_conv* conv_ = nullptr;
+  bool cm_ = false;  // column-major spectra (see ColumnMajorSpectra)
   size_t width_, height_, spectrum_bytes_;
   bool f64_;
   Buffer work_;

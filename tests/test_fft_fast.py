@@ -1,0 +1,217 @@
+"""The compile-time-planned FFT kernels (csrc/hip/fft_fast.hip) at the sizes
+they cover: the float64 padded residual-correction planes of 4096^2 / 8192^2
+images (utils::GetConvolutionSize(scale, W, 1.1), cpp/utils/
+fft_size_calculations.h:45-50) and the float32 scale-convolution planes.
+
+Reference: numpy's float64 FFT (an independent algorithm). Tolerances:
+float64 |err| <= 1e-12 * scale, float32 |err| <= 2e-6 * scale (written per
+check). Also: the masked (sparse-row) correction sequence equals the dense
+one, rows outside the output window are left untouched, and the fast and the
+runtime-plan kernels (RDL_FFT_FAST=0 in a subprocess) agree.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from rdl_lib import Session
+
+pytestmark = pytest.mark.gpu
+
+RDL_CONV_ROW_MAJOR, RDL_CONV_COL_MAJOR = 0, 1
+RDL_CONV_COLUMNS_SINGLE = 1
+
+
+@pytest.fixture(scope="module")
+def sess():
+    s = Session(0)
+    yield s
+    s.close()
+
+
+def conv(sess, w, h, f64):
+    c = C.c_void_p()
+    sess.rdl.rdl_conv_create_ex(sess.h, w, h, int(f64), RDL_CONV_COLUMNS_SINGLE, C.byref(c))
+    return c
+
+
+# (width, height, f64): rows use the half-length plan of `width`, columns the
+# plan of `height`
+CASES = [(4536, 4608, True), (4800, 5000, True), (4704, 4536, True), (9072, 9216, True),
+         (9450, 9408, True), (8192, 4096, False), (4096, 8192, False)]
+
+
+@pytest.mark.parametrize("w,h,f64", CASES)
+def test_fast_forward_matches_numpy(sess, w, h, f64):
+    rng = np.random.default_rng(w + h)
+    img = rng.standard_normal((h, w)).astype(np.float32)
+    c = conv(sess, w, h, f64)
+    cdt = np.complex128 if f64 else np.complex64
+    di = sess.array(img)
+    spec = sess.array(shape=(h, w // 2 + 1), dtype=cdt)
+    sess.rdl.rdl_conv_forward(c, di.vp, spec.vp)
+    ref = np.fft.rfft2(img.astype(np.float64))
+    err = np.abs(spec.get() - ref).max()
+    scale = np.sqrt(w * h) * np.sqrt(np.log2(w * h))
+    assert err <= (1e-13 if f64 else 2e-6) * scale, err
+    for x in (di, spec):
+        x.free()
+    sess.rdl.rdl_conv_destroy(c)
+
+
+@pytest.mark.parametrize("w,h,f64", CASES[:3] + CASES[5:])
+def test_fast_convolutions_match_numpy(sess, w, h, f64):
+    """In-place (columns mode 1) and shared-spectrum (mode 2) circular
+    convolution with a kernel spectrum in both layouts."""
+    rng = np.random.default_rng(3 * w + h)
+    img = rng.standard_normal((h, w)).astype(np.float32)
+    ker = np.zeros((h, w), np.float32)
+    ker[:7, :9] = rng.standard_normal((7, 9))
+    ker = np.roll(ker, (-3, -4), axis=(0, 1)).copy()
+    ref = np.fft.irfft2(np.fft.rfft2(img.astype(np.float64)) *
+                        np.fft.rfft2(ker.astype(np.float64)), s=(h, w))
+    c = conv(sess, w, h, f64)
+    cdt = np.complex128 if f64 else np.complex64
+    dk, di = sess.array(ker), sess.array(img)
+    kspec = sess.array(shape=(h, w // 2 + 1), dtype=cdt)
+    kspec_cm = sess.array(shape=(w // 2 + 1, h), dtype=cdt)
+    work = sess.array(shape=(h, w // 2 + 1), dtype=cdt)
+    sspec = sess.array(shape=(h, w // 2 + 1), dtype=cdt)
+    out = sess.array(shape=(h, w))
+    sess.rdl.rdl_conv_forward(c, dk.vp, kspec.vp)
+    sess.rdl.rdl_conv_rows_forward(c, dk.vp, w, h, 0, 0, work.vp)
+    sess.rdl.rdl_conv_columns_ex(c, work.vp, kspec_cm.vp, None, 0, C.c_double(1.0), None,
+                                 RDL_CONV_ROW_MAJOR, RDL_CONV_COL_MAJOR)
+    assert np.abs(kspec_cm.get().T - kspec.get()).max() == 0.0
+    norm = 1.0 / (w * h) if f64 else float(np.float32(1.0 / (w * h)))
+
+    def close(got):
+        # float64: the float output is the exact result rounded (half an ulp
+        # of float32, + 1e-12 * scale for the transform); float32: 2e-6 * scale
+        scale = np.abs(ref).max() * np.sqrt(np.log2(w * h))
+        if f64:
+            half_ulp = 0.5 * np.spacing(np.abs(ref).astype(np.float32)).astype(np.float64)
+            return np.all(np.abs(got - ref) <= half_ulp + 1e-12 * scale)
+        return np.abs(got - ref).max() <= 2e-6 * scale
+    for kern, layout in ((kspec, RDL_CONV_ROW_MAJOR), (kspec_cm, RDL_CONV_COL_MAJOR)):
+        di.upload(img)
+        sess.rdl.rdl_conv_rows_forward(c, di.vp, w, h, 0, 0, work.vp)
+        sess.rdl.rdl_conv_columns_ex(c, work.vp, work.vp, kern.vp, 1, C.c_double(norm), None,
+                                     layout, RDL_CONV_ROW_MAJOR)
+        sess.rdl.rdl_conv_rows_inverse(c, work.vp, di.vp, w, h, 0, 0, 0)
+        assert close(di.get())
+    di.upload(img)
+    sess.rdl.rdl_conv_forward(c, di.vp, sspec.vp)
+    sess.rdl.rdl_conv_columns(c, sspec.vp, work.vp, kspec.vp, 2, C.c_double(norm))
+    sess.rdl.rdl_conv_rows_inverse(c, work.vp, out.vp, w, h, 0, 0, 0)
+    assert close(out.get())
+    for x in (dk, di, kspec, kspec_cm, work, sspec, out):
+        x.free()
+    sess.rdl.rdl_conv_destroy(c)
+
+
+@pytest.mark.parametrize("pw,ph,w,h", [(4536, 4536, 4096, 4096), (9216, 9216, 8192, 8192),
+                                       (4800, 4800, 4096, 4096)])
+def test_fast_masked_correction(sess, pw, ph, w, h):
+    """CorrectResidualDirty's sequence: sparse model rows (row mask) placed at
+    the centred offset, x column-major PSF spectrum, trimmed subtraction from
+    the residual window; equals numpy float64 and leaves nothing outside the
+    window touched."""
+    rng = np.random.default_rng(pw)
+    psf = np.zeros((h, w), np.float32)
+    psf[h // 2 - 20:h // 2 + 21, w // 2 - 20:w // 2 + 21] = rng.standard_normal((41, 41))
+    model = np.zeros((h, w), np.float32)
+    idx = rng.choice(w * h, 300, replace=False)
+    model.flat[idx] = rng.standard_normal(300).astype(np.float32)
+    residual = rng.standard_normal((h, w)).astype(np.float32)
+    ox, oy = (pw - w) // 2, (ph - h) // 2
+    # numpy: circular convolution at the padded size
+    kp = np.zeros((ph, pw))
+    kp[oy:oy + h, ox:ox + w] = psf
+    kp = np.roll(kp, (-(ph // 2), -(pw // 2)), axis=(0, 1))
+    mp = np.zeros((ph, pw))
+    mp[oy:oy + h, ox:ox + w] = model
+    conv_ref = np.fft.irfft2(np.fft.rfft2(mp) * np.fft.rfft2(kp), s=(ph, pw))
+    expect = residual - conv_ref[oy:oy + h, ox:ox + w].astype(np.float32)
+
+    c = conv(sess, pw, ph, True)
+    dpsf, dmod = sess.array(psf), sess.array(model)
+    dres = sess.array(shape=(h + 2, w))  # a guard row after the window
+    guard = np.full((h + 2, w), 7.0, np.float32)
+    guard[:h] = residual
+    dres.upload(guard)
+    kplane = sess.array(shape=(ph, pw))
+    kspec = sess.array(shape=(pw // 2 + 1, ph), dtype=np.complex128)
+    work = sess.array(shape=(ph, pw // 2 + 1), dtype=np.complex128)
+    mask = np.zeros(ph, np.uint8)
+    mask[oy + np.unique(idx // w)] = 1
+    dmask = sess.array(mask, dtype=np.uint8)
+    sess.rdl.rdl_prepare_psf_kernel(sess.h, kplane.vp, pw, ph, dpsf.vp, w, h)
+    sess.rdl.rdl_conv_rows_forward(c, kplane.vp, pw, ph, 0, 0, work.vp)
+    sess.rdl.rdl_conv_columns_ex(c, work.vp, kspec.vp, None, 0, C.c_double(1.0), None,
+                                 RDL_CONV_ROW_MAJOR, RDL_CONV_COL_MAJOR)
+    sess.rdl.rdl_conv_rows_forward_masked(c, dmod.vp, w, h, ox, oy, work.vp, dmask.vp)
+    sess.rdl.rdl_conv_columns_ex(c, work.vp, work.vp, kspec.vp, 1,
+                                 C.c_double(1.0 / (pw * ph)), dmask.vp, RDL_CONV_COL_MAJOR,
+                                 RDL_CONV_ROW_MAJOR)
+    sess.rdl.rdl_conv_rows_inverse(c, work.vp, dres.vp, w, h, ox, oy, 1)
+    got = dres.get()
+    assert np.all(got[h:] == 7.0)
+    err = np.abs(got[:h] - expect).max()
+    assert err <= 2.4e-7 * max(np.abs(conv_ref).max(), np.abs(residual).max()), err
+    for x in (dpsf, dmod, dres, kplane, kspec, work, dmask):
+        x.free()
+    sess.rdl.rdl_conv_destroy(c)
+
+
+_PIPELINE = r"""
+import sys, numpy as np
+sys.path.insert(0, {tests!r})
+from radler_import import radler as rd
+from synthetic import problem
+w = 4096
+psf, dirty = problem(w, w, 60, 6, seed=11)
+s = rd.Settings()
+s.algorithm_type = rd.AlgorithmType.multiscale
+s.trimmed_image_width = s.trimmed_image_height = w
+s.pixel_scale.x = s.pixel_scale.y = 1.0 / 3600.0 * np.pi / 180.0
+s.minor_iteration_count = 3000
+s.absolute_threshold = 1e-3
+s.multiscale.max_scales = 5
+run = rd.gpu.DeviceRun(s, psf, dirty, [], 2.0 * s.pixel_scale.x)
+r = run.execute()
+np.savez({out!r}, trace=run.trace(), residual=run.residual(), model=run.model(),
+         iterations=r["iterations"], dirty_max=np.abs(dirty).max())
+"""
+
+
+def test_pipeline_fast_vs_runtime_plan_kernels(tmp_path):
+    """A 4096^2 multiscale major iteration (float64 corrections at 4536..5000,
+    i.e. the fast plans) with the fast kernels and with the runtime-plan
+    kernels (RDL_FFT_FAST=0): both float64, so the component traces agree and
+    the images agree to float rounding."""
+    import os
+    import subprocess
+    import sys
+    tests = os.path.dirname(os.path.abspath(__file__))
+    outs = []
+    for fast in ("1", "0"):
+        out = str(tmp_path / f"fast{fast}.npz")
+        env = dict(os.environ, RDL_FFT_FAST=fast)
+        subprocess.run([sys.executable, "-c", _PIPELINE.format(tests=tests, out=out)],
+                       env=env, check=True, timeout=300)
+        outs.append(np.load(out))
+    a, b = outs
+    assert int(a["iterations"]) == int(b["iterations"]) > 100
+    # the two float64 engines round differently in the last bits: a float
+    # result can differ by one ulp, which eventually flips a near-tie; the
+    # traces agree for most of the run and the images to the multiscale
+    # parity tolerance (2e-5 * max|dirty|, tests/test_multiscale_gpu.py)
+    ta, tb = a["trace"], b["trace"]
+    diff = np.nonzero(np.any(ta != tb, axis=1))[0]
+    first = int(diff[0]) if diff.size else len(ta)
+    print(f"traces agree for {first} of {len(ta)} components")
+    assert first >= len(ta) // 2
+    tol = 2e-5 * float(a["dirty_max"])
+    assert np.abs(a["residual"] - b["residual"]).max() <= tol
+    assert np.abs(a["model"] - b["model"]).max() <= tol
