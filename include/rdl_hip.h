@@ -406,6 +406,11 @@ int rdl_conv_columns_layout(rdl_conv* c, const void* d_in, void* d_out,
  * (csrc/hip/fft_fast.hip): a bitmask of the two flags. */
 #define RDL_CONV_FAST_COLUMNS 1
 #define RDL_CONV_FAST_ROWS 2
+/* float planes with four-step column plans: every spectrum of this plan is
+ * stored in tiles of 16 columns (complex element (y, k) at
+ * ((k / 16) * height + y) * 16 + k % 16; rdl_conv_spectrum_bytes covers the
+ * padded last tile) and the layout arguments do not apply. */
+#define RDL_CONV_FAST_TILED 4
 int rdl_conv_fast(const rdl_conv* c);
 
 /* dst = a * b * scale, complex, n_complex elements. */

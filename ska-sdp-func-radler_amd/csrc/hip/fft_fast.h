@@ -25,7 +25,25 @@ struct FastRows {
   const void* forward;
 };
 
+/* float four-step column passes (column tiles of 16, see ff::TileIndex) */
+struct FastSteps {
+  uint32_t n, n1, n2, ga, gb;
+  uint32_t threads;
+  const void* step_a;
+  const void* step_b;
+};
+
 const FastColumns* FindFastColumns(uint32_t n, bool f64);
+const FastSteps* FindFastSteps(uint32_t n);
+/* One four-step pass over all column tiles (pass_b: B, else A). inverse: A
+ * loads conj(in x kern x scale), B stores conjugated. */
+int FastStepLaunch(rdl_session* s, const FastSteps* p, bool pass_b, const void* in,
+                   void* out, const void* kern, const void* tw, uint32_t n_cols,
+                   int inverse, float scale);
+/* tiled spectrum size in complex elements for a plane of `width` x `height` */
+inline size_t TiledComplexCount(uint32_t width, uint32_t height) {
+  return size_t((width / 2 + 1 + 15) / 16) * 16 * height;
+}
 const FastRows* FindFastRows(uint32_t n, bool f64);
 
 /* mode 0 forward / 1 forward x K x s inverse / 2 x K x s inverse, one
@@ -39,12 +57,12 @@ int FastColumnsLaunch(rdl_session* s, const FastColumns* p, const void* in, void
 /* spectrum rows oy .. oy+img_h-1 -> the img_w x img_h window at (ox, oy) */
 int FastRowsInverseLaunch(rdl_session* s, const FastRows* p, const void* spec, float* out,
                           const void* tw, uint32_t height, uint32_t img_w, uint32_t img_h,
-                          uint32_t ox, uint32_t oy, int subtract);
+                          uint32_t ox, uint32_t oy, int subtract, int tiled = 0);
 /* the window's rows (or the listed plane rows) -> spectrum rows */
 int FastRowsForwardLaunch(rdl_session* s, const FastRows* p, const float* in, void* spec,
                           const void* tw, uint32_t height, uint32_t img_w, uint32_t img_h,
                           uint32_t ox, uint32_t oy, const uint32_t* rows,
-                          const uint32_t* n_rows);
+                          const uint32_t* n_rows, int tiled = 0);
 /* ascending list of the rows whose mask byte is non-zero, and its length */
 int FastCompactRows(rdl_session* s, const uint8_t* mask, uint32_t n, uint32_t* rows,
                     uint32_t* count);

@@ -234,7 +234,17 @@ struct RowArgs {
   const uint32_t* rows;    // forward: the non-zero plane rows (NULL: the window rows)
   const uint32_t* n_rows;  // their count (device)
   int subtract;         // inverse: 0 write, 1 subtract from out
+  int tiled;            // spectrum in column tiles (see TileIndex), else row-major
+  int all_rows;         // forward: every plane row (zero outside the window)
 };
+
+// Tiled spectrum layout of the four-step column passes: 16 adjacent columns
+// (128 B of float complex) of every row side by side, tile after tile, so
+// both the row passes and the column passes move whole cache lines.
+constexpr uint32_t kTile = 16;
+__device__ __forceinline__ size_t TileIndex(uint32_t y, uint32_t k, uint32_t height) {
+  return (size_t(k / kTile) * height + y) * kTile + (k % kTile);
+}
 
 // spectrum rows (X[0..H]) -> real rows written into / subtracted from the
 // window. Z[k] = (X[k] + conj X[H-k]) + i W^-k (X[k] - conj X[H-k]) gives
@@ -258,7 +268,14 @@ __global__ __launch_bounds__(TH) void RowsInverse(RowArgs a, const Cx<T>* __rest
   for (uint32_t i = 0; i < EH; ++i) {
     const uint32_t k = tid + i * TH;
     if (H % TH == 0 || k < H) {
-      Cx<T> xk = X[k], xm = X[H - k];
+      Cx<T> xk, xm;
+      if (a.tiled) {
+        xk = spec[TileIndex(y, k, a.height)];
+        xm = spec[TileIndex(y, H - k, a.height)];
+      } else {
+        xk = X[k];
+        xm = X[H - k];
+      }
       if (k == 0) {
         xk.y = T(0);
         xm.y = T(0);
@@ -305,11 +322,11 @@ __global__ __launch_bounds__(TH) void RowsForward(RowArgs a, const float* __rest
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   Cx<T>* buf = reinterpret_cast<Cx<T>*>(lds_raw);
   const uint32_t tid = threadIdx.x;
-  const uint32_t n_rows = a.rows ? *a.n_rows : a.img_h;
+  const uint32_t n_rows = a.rows ? *a.n_rows : (a.all_rows ? a.height : a.img_h);
   for (uint32_t r = blockIdx.x; r < n_rows; r += gridDim.x) {
     uint32_t tid = threadIdx.x;  // opaque per row (see Columns)
     asm volatile("" : "+v"(tid));
-    const uint32_t y = a.rows ? a.rows[r] : r + a.oy;
+    const uint32_t y = a.rows ? a.rows[r] : (a.all_rows ? r : r + a.oy);
     const int64_t iy = int64_t(y) - a.oy;
     const bool in_y = iy >= 0 && iy < a.img_h;
     const float* row = in + (in_y ? size_t(iy) * a.img_w : 0);
@@ -334,9 +351,165 @@ __global__ __launch_bounds__(TH) void RowsForward(RowArgs a, const float* __rest
       const Cx<T> zc = Conj(buf[k == 0 ? 0 : H - k]);
       const Cx<T> ev = {h * (zk.x + zc.x), h * (zk.y + zc.y)};
       const Cx<T> od = {h * (zk.y - zc.y), -h * (zk.x - zc.x)};  // (zk - zc) / 2i
-      X[k] = Add(ev, Mul(tw[k], od));
+      const Cx<T> v = Add(ev, Mul(tw[k], od));
+      if (a.tiled)
+        spec[TileIndex(y, k, a.height)] = v;
+      else
+        X[k] = v;
     }
     LdsSync();
+  }
+}
+
+// ------------------------------------------- four-step column passes
+// A column transform of length N = N1 * N2 (float, tiled layout) as two
+// passes that each move whole 128-B lines (the one-pass column kernel reads
+// one 8-B element per row, which makes it L2-request bound):
+//   A: for each n2, the N1 rows n2 + N2 n1 of a tile: length-N1 DFTs,
+//      x W_N^(n2 k1), to rows k1 N2 + n2 of the scratch;
+//   B: for each k1, the N2 consecutive scratch rows k1 N2 .. k1 N2 + N2 - 1:
+//      length-N2 DFTs -> X[k1 + N1 k2] at row k1 + N1 k2 (natural order).
+// The inverse convolution runs the same two passes on conj(X K s) (A's load)
+// and conjugates B's store.
+
+// `COUNT` transforms of length N at stride S in LDS (batched Pass).
+template <typename T, uint32_t TH, uint32_t N, uint32_t R, uint32_t NS, uint32_t TWS,
+          uint32_t COUNT, uint32_t S>
+__device__ __forceinline__ void BPass(Cx<T>* buf, const Cx<T>* __restrict__ tw,
+                                      uint32_t tid) {
+  constexpr uint32_t NB = N / R;
+  constexpr uint32_t TOT = COUNT * NB;
+  constexpr uint32_t BPT = (TOT + TH - 1) / TH;
+  constexpr uint32_t M = N / (NS * R);
+  Cx<T> v[BPT][R];
+  Cx<T> w[BPT][NS > 1 ? R - 1 : 1];
+#pragma unroll
+  for (uint32_t i = 0; i < BPT; ++i) {
+    const uint32_t b = tid + i * TH;
+    if (TOT % TH == 0 || b < TOT) {
+      const uint32_t t = b / NB, j = b % NB;
+      if constexpr (NS > 1) {
+        const uint32_t k = j % NS;
+#pragma unroll
+        for (uint32_t q = 0; q + 1 < R; ++q) w[i][q] = tw[k * (q + 1) * M * TWS];
+      }
+#pragma unroll
+      for (uint32_t r = 0; r < R; ++r) v[i][r] = buf[t * S + j + r * NB];
+    }
+  }
+  LdsSync();
+#pragma unroll
+  for (uint32_t i = 0; i < BPT; ++i) {
+    const uint32_t b = tid + i * TH;
+    if (TOT % TH == 0 || b < TOT) {
+      const uint32_t t = b / NB, j = b % NB;
+      const uint32_t k = j % NS;
+      if constexpr (NS > 1) {
+#pragma unroll
+        for (uint32_t r = 1; r < R; ++r) v[i][r] = Mul(v[i][r], w[i][r - 1]);
+      }
+      Dft<T, int(R)>::Run(v[i]);
+      const uint32_t d = (j / NS) * NS * R + k;
+#pragma unroll
+      for (uint32_t r = 0; r < R; ++r) buf[t * S + d + r * NS] = v[i][r];
+    }
+  }
+  LdsSync();
+}
+
+template <typename T, uint32_t TH, uint32_t N, uint32_t TWS, uint32_t COUNT, uint32_t S,
+          uint32_t NS, uint32_t R, uint32_t... Rest>
+__device__ __forceinline__ void BFft(Cx<T>* buf, const Cx<T>* __restrict__ tw,
+                                     uint32_t tid) {
+  BPass<T, TH, N, R, NS, TWS, COUNT, S>(buf, tw, tid);
+  if constexpr (sizeof...(Rest) > 0)
+    BFft<T, TH, N, TWS, COUNT, S, NS * R, Rest...>(buf, tw, tid);
+}
+
+template <uint32_t... Rs>
+struct Radices {};
+
+struct StepArgs {
+  uint32_t n_tiles;  // column tiles
+  int inverse;       // A: load conj(X K s); B: store conj
+  float scale;
+};
+
+// Pass A: workgroup = (tile, GA consecutive n2). tw: the length-N table.
+template <uint32_t TH, uint32_t N1, uint32_t N2, uint32_t GA, uint32_t... R1>
+__global__ __launch_bounds__(TH) void ColStepA(StepArgs a, const Cx<float>* __restrict__ in,
+                                               Cx<float>* __restrict__ out,
+                                               const Cx<float>* __restrict__ kern,
+                                               const Cx<float>* __restrict__ tw) {
+  constexpr uint32_t N = N1 * N2;
+  constexpr uint32_t S = N1 + 1;  // padded stride: columns of one row on distinct banks
+  constexpr uint32_t COUNT = kTile * GA;
+  constexpr uint32_t EL = COUNT * N1;
+  constexpr uint32_t E = (EL + TH - 1) / TH;
+  __shared__ Cx<float> buf[COUNT * S];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t tile = blockIdx.x / (N2 / GA);
+  const uint32_t n2_0 = (blockIdx.x % (N2 / GA)) * GA;
+  const size_t base = size_t(tile) * N * kTile;
+#pragma unroll
+  for (uint32_t i = 0; i < E; ++i) {
+    const uint32_t idx = tid + i * TH;
+    if (EL % TH != 0 && idx >= EL) continue;
+    const uint32_t col = idx % kTile, q = idx / kTile;
+    const uint32_t g = q % GA, n1 = q / GA;  // GA adjacent rows: one contiguous run
+    const size_t off = base + size_t(n2_0 + g + N2 * n1) * kTile + col;
+    Cx<float> v = in[off];
+    if (a.inverse) v = Conj(Scale(Mul(v, kern[off]), a.scale));
+    buf[(g * kTile + col) * S + n1] = v;
+  }
+  LdsSync();
+  BFft<float, TH, N1, N2, COUNT, S, 1, R1...>(buf, tw, tid);
+#pragma unroll
+  for (uint32_t i = 0; i < E; ++i) {
+    const uint32_t idx = tid + i * TH;
+    if (EL % TH != 0 && idx >= EL) continue;
+    const uint32_t col = idx % kTile, q = idx / kTile;
+    const uint32_t g = q % GA, k1 = q / GA;
+    const uint32_t n2 = n2_0 + g;
+    const Cx<float> v = Mul(buf[(g * kTile + col) * S + k1], tw[(n2 * k1) % N]);
+    out[base + size_t(k1 * N2 + n2) * kTile + col] = v;
+  }
+}
+
+// Pass B: workgroup = (tile, GB consecutive k1).
+template <uint32_t TH, uint32_t N1, uint32_t N2, uint32_t GB, uint32_t... R2>
+__global__ __launch_bounds__(TH) void ColStepB(StepArgs a, const Cx<float>* __restrict__ in,
+                                               Cx<float>* __restrict__ out,
+                                               const Cx<float>* __restrict__ tw) {
+  constexpr uint32_t N = N1 * N2;
+  constexpr uint32_t S = N2 + 1;
+  constexpr uint32_t COUNT = kTile * GB;
+  constexpr uint32_t EL = COUNT * N2;
+  constexpr uint32_t E = (EL + TH - 1) / TH;
+  __shared__ Cx<float> buf[COUNT * S];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t tile = blockIdx.x / (N1 / GB);
+  const uint32_t k1_0 = (blockIdx.x % (N1 / GB)) * GB;
+  const size_t base = size_t(tile) * N * kTile;
+#pragma unroll
+  for (uint32_t i = 0; i < E; ++i) {
+    const uint32_t idx = tid + i * TH;
+    if (EL % TH != 0 && idx >= EL) continue;
+    const uint32_t col = idx % kTile, q = idx / kTile;
+    const uint32_t n2 = q % N2, g = q / N2;  // rows k1 N2 .. k1 N2 + N2 - 1: contiguous
+    buf[(g * kTile + col) * S + n2] = in[base + size_t((k1_0 + g) * N2 + n2) * kTile + col];
+  }
+  LdsSync();
+  BFft<float, TH, N2, N1, COUNT, S, 1, R2...>(buf, tw, tid);
+#pragma unroll
+  for (uint32_t i = 0; i < E; ++i) {
+    const uint32_t idx = tid + i * TH;
+    if (EL % TH != 0 && idx >= EL) continue;
+    const uint32_t col = idx % kTile, q = idx / kTile;
+    const uint32_t g = q % GB, k2 = q / GB;  // rows k1 + N1 k2: GB adjacent rows per k2
+    Cx<float> v = buf[(g * kTile + col) * S + k2];
+    if (a.inverse) v = Conj(v);
+    out[base + size_t(k1_0 + g + N1 * k2) * kTile + col] = v;
   }
 }
 
@@ -429,6 +602,27 @@ const FastRows* FindFastRows(uint32_t n, bool f64) {
 #undef RDL_FAST_COLS
 #undef RDL_FAST_ROWS
 
+#define RDL_FAST_STEPS(N1, N2, GA, GB, RA, RB)                                     \
+  FastSteps {                                                                      \
+    N1 * N2, N1, N2, GA, GB, 256,                                                  \
+        reinterpret_cast<const void*>(&ff::ColStepA<256, N1, N2, GA, RA>),         \
+        reinterpret_cast<const void*>(&ff::ColStepB<256, N1, N2, GB, RB>)          \
+  }
+#define RDL_R(...) __VA_ARGS__
+
+const FastSteps* FindFastSteps(uint32_t n) {
+  static const FastSteps kPlans[] = {
+      RDL_FAST_STEPS(64, 128, 4, 2, RDL_R(8, 8), RDL_R(16, 8)),  // 8192
+      RDL_FAST_STEPS(64, 64, 4, 4, RDL_R(8, 8), RDL_R(8, 8)),    // 4096
+  };
+  for (const FastSteps& p : kPlans)
+    if (p.n == n) return &p;
+  return nullptr;
+}
+
+#undef RDL_FAST_STEPS
+#undef RDL_R
+
 namespace {
 // workgroups per CU for a kernel at its LDS size (cached), after raising its
 // dynamic LDS limit once per device
@@ -485,7 +679,7 @@ int FastColumnsLaunch(rdl_session* s, const FastColumns* p, const void* in, void
 
 int FastRowsInverseLaunch(rdl_session* s, const FastRows* p, const void* spec, float* out,
                           const void* tw, uint32_t height, uint32_t img_w, uint32_t img_h,
-                          uint32_t ox, uint32_t oy, int subtract) {
+                          uint32_t ox, uint32_t oy, int subtract, int tiled) {
   const size_t lds = size_t(p->n / 2) * (p->f64 ? 16 : 8);
   if (SlotsPerCu(s, p->inverse, p->threads, lds) < 0) {
     SetError("fast FFT rows: occupancy query failed");
@@ -500,6 +694,7 @@ int FastRowsInverseLaunch(rdl_session* s, const FastRows* p, const void* spec, f
   a.ox = ox;
   a.oy = oy;
   a.subtract = subtract;
+  a.tiled = tiled;
   void* args[] = {&a, (void*)&spec, (void*)&out, (void*)&tw};
   RDL_HIP_CHECK(hipLaunchKernel(p->inverse, dim3(img_h), dim3(p->threads), args, lds,
                                 s->stream));
@@ -509,7 +704,7 @@ int FastRowsInverseLaunch(rdl_session* s, const FastRows* p, const void* spec, f
 int FastRowsForwardLaunch(rdl_session* s, const FastRows* p, const float* in, void* spec,
                           const void* tw, uint32_t height, uint32_t img_w, uint32_t img_h,
                           uint32_t ox, uint32_t oy, const uint32_t* rows,
-                          const uint32_t* n_rows) {
+                          const uint32_t* n_rows, int tiled) {
   const size_t lds = size_t(p->n / 2) * (p->f64 ? 16 : 8);
   const int slots = SlotsPerCu(s, p->forward, p->threads, lds);
   if (slots < 0) {
@@ -525,13 +720,36 @@ int FastRowsForwardLaunch(rdl_session* s, const FastRows* p, const float* in, vo
   a.oy = oy;
   a.rows = rows;
   a.n_rows = n_rows;
-  const uint32_t max_rows = rows ? height : img_h;
+  a.tiled = tiled;
+  a.all_rows = tiled;
+  const uint32_t max_rows = (rows || tiled) ? height : img_h;
   if (max_rows == 0) return RDL_OK;
   const uint32_t grid =
       std::min<uint32_t>(max_rows, uint32_t(s->n_cus) * uint32_t(slots) * 2);
   void* args[] = {&a, (void*)&in, (void*)&spec, (void*)&tw};
   RDL_HIP_CHECK(hipLaunchKernel(p->forward, dim3(grid), dim3(p->threads), args, lds,
                                 s->stream));
+  return RDL_OK;
+}
+
+int FastStepLaunch(rdl_session* s, const FastSteps* p, bool pass_b, const void* in,
+                   void* out, const void* kern, const void* tw, uint32_t n_cols,
+                   int inverse, float scale) {
+  ff::StepArgs a{};
+  a.n_tiles = (n_cols + ff::kTile - 1) / ff::kTile;
+  a.inverse = inverse;
+  a.scale = scale;
+  if (pass_b) {
+    const uint32_t grid = a.n_tiles * (p->n1 / p->gb);
+    void* args[] = {&a, (void*)&in, (void*)&out, (void*)&tw};
+    RDL_HIP_CHECK(hipLaunchKernel(p->step_b, dim3(grid), dim3(p->threads), args, 0,
+                                  s->stream));
+  } else {
+    const uint32_t grid = a.n_tiles * (p->n2 / p->ga);
+    void* args[] = {&a, (void*)&in, (void*)&out, (void*)&kern, (void*)&tw};
+    RDL_HIP_CHECK(hipLaunchKernel(p->step_a, dim3(grid), dim3(p->threads), args, 0,
+                                  s->stream));
+  }
   return RDL_OK;
 }
 

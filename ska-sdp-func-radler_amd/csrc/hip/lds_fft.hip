@@ -505,9 +505,15 @@ struct rdl_conv {
   const rdl::FastRows* fast_rows = nullptr;
   uint32_t* rows_list = nullptr;            // height words + the count
   const uint8_t* rows_list_mask = nullptr;  // mask the list was made from
+  // float planes with four-step column plans: spectra in 16-column tiles
+  const rdl::FastSteps* steps = nullptr;
+  bool tiled = false;
 };
 
 namespace {
+
+double SpectrumBytes(const rdl_conv* c);
+int EnsureSplitScratch(rdl_conv* c, size_t bytes);
 
 int MakePlan(rdl_conv* c, uint32_t n, bool f64, rdl::LdsPlan* plan, void** tw) {
   std::vector<uint8_t> radix;
@@ -555,6 +561,14 @@ int CompactRowsFor(rdl_conv* c, const uint8_t* row_mask, bool reuse) {
 template <typename T>
 int LaunchRowsForward(rdl_conv* c, const float* in, uint32_t in_w, uint32_t in_h,
                       uint32_t ox, uint32_t oy, void* spec, const uint8_t* row_mask) {
+  if (c->tiled) {
+    if (row_mask) {
+      rdl::SetError("LDS FFT: row masks need the row-major (float64) plans");
+      return RDL_ERR_UNSUPPORTED;
+    }
+    return rdl::FastRowsForwardLaunch(c->s, c->fast_rows, in, spec, c->tw_row, c->height,
+                                      in_w, in_h, ox, oy, nullptr, nullptr, 1);
+  }
   if (c->fast_rows) {
     const size_t row_bytes = size_t(c->width / 2 + 1) * sizeof(rdl::Cx<T>);
     if (row_mask) {
@@ -601,7 +615,7 @@ int LaunchRowsInverse(rdl_conv* c, const void* spec, float* out, uint32_t out_w,
                       uint32_t out_h, uint32_t ox, uint32_t oy, int subtract) {
   if (c->fast_rows)
     return rdl::FastRowsInverseLaunch(c->s, c->fast_rows, spec, out, c->tw_row, c->height,
-                                      out_w, out_h, ox, oy, subtract);
+                                      out_w, out_h, ox, oy, subtract, c->tiled ? 1 : 0);
   rdl::RowArgs a{};
   a.plan = c->row_plan;
   a.height = c->height;
@@ -628,6 +642,28 @@ template <typename T>
 int LaunchColumns(rdl_conv* c, const void* in, void* out, const void* kern,
                   int mode, double scale, const uint8_t* row_mask, int kern_cm,
                   int out_cm, int in_cm = 0) {
+  if (c->tiled) {
+    // four-step passes through the conv's scratch (tiled spectra; the
+    // layout flags do not apply)
+    if (row_mask) {
+      rdl::SetError("LDS FFT: row masks need the row-major (float64) plans");
+      return RDL_ERR_UNSUPPORTED;
+    }
+    RDL_TRY(EnsureSplitScratch(c, size_t(SpectrumBytes(c))));
+    const uint32_t nc = c->width / 2 + 1;
+    const float sc = float(scale);
+    auto step = [&](bool b, const void* i, void* o, int inv) {
+      return rdl::FastStepLaunch(c->s, c->steps, b, i, o, kern, c->tw_col, nc, inv, sc);
+    };
+    if (mode != 2) {
+      RDL_TRY(step(false, in, c->scratch, 0));
+      RDL_TRY(step(true, c->scratch, out, 0));
+      if (mode == 0) return RDL_OK;
+      in = out;
+    }
+    RDL_TRY(step(false, in, c->scratch, 1));
+    return step(true, c->scratch, out, 1);
+  }
   if (c->fast_cols) {
     const uint32_t* rows = nullptr;
     const uint32_t* n_rows = nullptr;
@@ -757,6 +793,7 @@ int LaunchColumnsAny(rdl_conv* c, const void* in, void* out, const void* kern,
 }
 
 double SpectrumBytes(const rdl_conv* c) {
+  if (c->tiled) return double(rdl::TiledComplexCount(c->width, c->height)) * 8.0;
   return double(c->width / 2 + 1) * c->height * (c->f64 ? 16.0 : 8.0);
 }
 
@@ -821,6 +858,10 @@ int rdl_conv_create_ex(rdl_session* s, uint32_t width, uint32_t height, int f64,
   if (fast_ok) {
     c->fast_cols = rdl::FindFastColumns(height, c->f64);
     if (width % 2 == 0) c->fast_rows = rdl::FindFastRows(width, c->f64);
+    if (!c->f64 && c->fast_rows) {
+      c->steps = rdl::FindFastSteps(height);
+      c->tiled = c->steps != nullptr;
+    }
   }
   if (want_split && can_split) {
     c->split = true;
@@ -935,11 +976,11 @@ int rdl_conv_columns_layout(rdl_conv* c, const void* d_in, void* d_out,
   RDL_ARG_CHECK(mode == 0 || d_kernel, "kernel spectrum required");
   for (int l : {in_layout, kernel_layout, out_layout})
     RDL_ARG_CHECK(l == RDL_CONV_ROW_MAJOR || l == RDL_CONV_COL_MAJOR, "bad layout");
-  RDL_ARG_CHECK(in_layout == RDL_CONV_ROW_MAJOR || mode == 2,
+  RDL_ARG_CHECK(c->tiled || in_layout == RDL_CONV_ROW_MAJOR || mode == 2,
                 "a column-major input is a mode-2 spectrum");
-  RDL_ARG_CHECK(in_layout == out_layout || d_out != d_in,
+  RDL_ARG_CHECK(c->tiled || in_layout == out_layout || d_out != d_in,
                 "changing the layout needs a separate output");
-  if (!c->fast_cols) {
+  if (!c->fast_cols && !c->tiled) {
     if (in_layout == RDL_CONV_ROW_MAJOR && (out_layout == RDL_CONV_ROW_MAJOR || mode == 0))
       return rdl_conv_columns_ex(c, d_in, d_out, d_kernel, mode, scale, d_row_mask,
                                  kernel_layout, out_layout);
@@ -963,7 +1004,8 @@ int rdl_conv_columns_layout(rdl_conv* c, const void* d_in, void* d_out,
 
 int rdl_conv_fast(const rdl_conv* c) {
   if (!c) return 0;
-  return (c->fast_cols ? RDL_CONV_FAST_COLUMNS : 0) | (c->fast_rows ? RDL_CONV_FAST_ROWS : 0);
+  return (c->fast_cols ? RDL_CONV_FAST_COLUMNS : 0) | (c->fast_rows ? RDL_CONV_FAST_ROWS : 0) |
+         (c->tiled ? RDL_CONV_FAST_TILED : 0);
 }
 
 int rdl_conv_rows_inverse(rdl_conv* c, const void* d_spec, float* d_out,

@@ -52,10 +52,10 @@ Fft::Fft(Session& s, size_t width, size_t height, bool f64)
   // (tools/bench_fft.py). RADLER_FFT=rocfft / lds overrides.
   const char* force = std::getenv("RADLER_FFT");
   const std::string mode = force ? force : "";
-  // float: rocFFT (RADLER_FFT=lds selects the LDS engine; at 8192^2 its
-  // compile-time-planned kernels tie with rocFFT, 453 vs 450 ms per bench
-  // step, the strided column access being the limit)
-  const bool want_lds = mode == "lds" || (mode != "rocfft" && f64);
+  // float: the LDS engine where its four-step tiled plans exist (the 4096 /
+  // 8192 scale-convolution planes), rocFFT elsewhere (RADLER_FFT=lds forces
+  // the LDS engine)
+  const bool want_lds = mode != "rocfft";
   // RADLER_FFT_COLUMNS=single / split overrides the column-pass choice
   const char* cols_env = std::getenv("RADLER_FFT_COLUMNS");
   const std::string cols = cols_env ? cols_env : "";
@@ -66,7 +66,10 @@ Fft::Fft(Session& s, size_t width, size_t height, bool f64)
                       rdl_conv_create_ex(s.Handle(), uint32_t(width), uint32_t(height),
                                          f64 ? 1 : 0, strategy, &conv_) == RDL_OK;
   const int fast = lds_ok ? rdl_conv_fast(conv_) : 0;
-  (void)fast;
+  if (lds_ok && !f64 && mode != "lds" && !(fast & RDL_CONV_FAST_TILED)) {
+    rdl_conv_destroy(conv_);
+    conv_ = nullptr;
+  }
   if (conv_) {
     // the compile-time-planned column kernels read and write any layout:
     // spectra are then stored column by column (contiguous column reads)

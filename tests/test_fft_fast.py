@@ -35,6 +35,27 @@ def conv(sess, w, h, f64):
     return c
 
 
+RDL_CONV_FAST_TILED = 4  # rdl_hip.h
+
+
+def tiled(sess, c):
+    return bool(sess.rdl.lib.rdl_conv_fast(c) & RDL_CONV_FAST_TILED)
+
+
+def spectrum_array(sess, c, w, h, cdt):
+    n = sess.rdl.lib.rdl_conv_spectrum_bytes(c) // np.dtype(cdt).itemsize
+    return sess.array(shape=(n,), dtype=cdt)
+
+
+def natural(sess, c, flat, w, h):
+    """A spectrum buffer's contents as [row][column] (h x w/2+1)."""
+    if not tiled(sess, c):
+        return flat.reshape(h, w // 2 + 1)
+    nt = (w // 2 + 1 + 15) // 16
+    t = flat.reshape(nt, h, 16).transpose(1, 0, 2).reshape(h, nt * 16)
+    return t[:, :w // 2 + 1]
+
+
 # (width, height, f64): rows use the half-length plan of `width`, columns the
 # plan of `height`
 CASES = [(4536, 4608, True), (4800, 5000, True), (4704, 4536, True), (9072, 9216, True),
@@ -48,10 +69,11 @@ def test_fast_forward_matches_numpy(sess, w, h, f64):
     c = conv(sess, w, h, f64)
     cdt = np.complex128 if f64 else np.complex64
     di = sess.array(img)
-    spec = sess.array(shape=(h, w // 2 + 1), dtype=cdt)
+    spec = spectrum_array(sess, c, w, h, cdt)
     sess.rdl.rdl_conv_forward(c, di.vp, spec.vp)
     ref = np.fft.rfft2(img.astype(np.float64))
-    err = np.abs(spec.get() - ref).max()
+    assert tiled(sess, c) == (not f64)
+    err = np.abs(natural(sess, c, spec.get(), w, h) - ref).max()
     scale = np.sqrt(w * h) * np.sqrt(np.log2(w * h))
     assert err <= (1e-13 if f64 else 2e-6) * scale, err
     for x in (di, spec):
@@ -73,16 +95,17 @@ def test_fast_convolutions_match_numpy(sess, w, h, f64):
     c = conv(sess, w, h, f64)
     cdt = np.complex128 if f64 else np.complex64
     dk, di = sess.array(ker), sess.array(img)
-    kspec = sess.array(shape=(h, w // 2 + 1), dtype=cdt)
-    kspec_cm = sess.array(shape=(w // 2 + 1, h), dtype=cdt)
-    work = sess.array(shape=(h, w // 2 + 1), dtype=cdt)
-    sspec = sess.array(shape=(h, w // 2 + 1), dtype=cdt)
+    kspec, kspec_cm, work, sspec = (spectrum_array(sess, c, w, h, cdt) for _ in range(4))
     out = sess.array(shape=(h, w))
     sess.rdl.rdl_conv_forward(c, dk.vp, kspec.vp)
     sess.rdl.rdl_conv_rows_forward(c, dk.vp, w, h, 0, 0, work.vp)
     sess.rdl.rdl_conv_columns_ex(c, work.vp, kspec_cm.vp, None, 0, C.c_double(1.0), None,
                                  RDL_CONV_ROW_MAJOR, RDL_CONV_COL_MAJOR)
-    assert np.abs(kspec_cm.get().T - kspec.get()).max() == 0.0
+    if tiled(sess, c):  # one layout for every spectrum
+        assert np.array_equal(kspec_cm.get(), kspec.get())
+    else:
+        cm = kspec_cm.get()[:(w // 2 + 1) * h].reshape(w // 2 + 1, h)
+        assert np.abs(cm.T - natural(sess, c, kspec.get(), w, h)).max() == 0.0
     norm = 1.0 / (w * h) if f64 else float(np.float32(1.0 / (w * h)))
 
     def close(got):

@@ -86,6 +86,11 @@ def lds_engine(s, w, h, f64, columns, cname, di, spec, kspec, work, out, reps):
         if rc != 0:
             print("LDS engine unsupported", w, h, cname)
             return
+        # spectra of this plan (the tiled float layout pads the last tile)
+        nbytes = s.rdl.lib.rdl_conv_spectrum_bytes(c)
+        cdt = np.complex128 if f64 else np.complex64
+        spec, kspec, work = (s.array(shape=(nbytes // np.dtype(cdt).itemsize,), dtype=cdt)
+                             for _ in range(3))
         s.rdl.lib.rdl_timing_enable(s.h, 1)
         s.rdl.rdl_conv_forward(c, di.vp, kspec.vp)
         s.rdl.rdl_session_sync(s.h)
@@ -111,6 +116,8 @@ def lds_engine(s, w, h, f64, columns, cname, di, spec, kspec, work, out, reps):
             report(f"LDS[{cname}] {w}x{h} f32 spectrum->image", timings(s), reps)
         s.rdl.lib.rdl_timing_enable(s.h, 0)
         s.rdl.rdl_conv_destroy(c)
+        for x in (spec, kspec, work):
+            x.free()
 
 
 if __name__ == "__main__":
