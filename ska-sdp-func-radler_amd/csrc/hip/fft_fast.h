@@ -11,11 +11,22 @@ namespace rdl {
 
 constexpr size_t kFftLdsBytesFast = 160 * 1024;
 
+/* radices of a compile-time plan, in pass order */
+struct RadixList {
+  uint8_t r[8];
+  uint8_t n;
+};
+template <uint32_t... Rs>
+constexpr RadixList MakeRadixList() {
+  return RadixList{{uint8_t(Rs)...}, uint8_t(sizeof...(Rs))};
+}
+
 struct FastColumns {
   uint32_t n;  // column length
   bool f64;
   uint32_t threads;
   const void* kernel;
+  RadixList radix;
 };
 struct FastRows {
   uint32_t n;  // full row length (2 x the half-length transform)
@@ -23,6 +34,7 @@ struct FastRows {
   uint32_t threads;
   const void* inverse;
   const void* forward;
+  RadixList radix;  // of the half-length transform
 };
 
 /* float four-step column passes (column tiles of 16, see ff::TileIndex) */
@@ -31,15 +43,22 @@ struct FastSteps {
   uint32_t threads;
   const void* step_a;
   const void* step_b;
+  RadixList radix_a, radix_b;  // of the length-n1 / length-n2 transforms
 };
+
+/* The pass table of a length-n transform with these radices (ff::Pass):
+ * for pass p (span NS = product of the earlier radices, M = n / (NS R)),
+ * entries W_n^{k (q+1) M} at [offset_p + q NS + k], q < R - 1, k < NS;
+ * float or double complex, computed in long double. hipMalloc'ed. */
+int MakePassTable(uint32_t n, const RadixList& radix, bool f64, void** out);
 
 const FastColumns* FindFastColumns(uint32_t n, bool f64);
 const FastSteps* FindFastSteps(uint32_t n);
 /* One four-step pass over all column tiles (pass_b: B, else A). inverse: A
  * loads conj(in x kern x scale), B stores conjugated. */
 int FastStepLaunch(rdl_session* s, const FastSteps* p, bool pass_b, const void* in,
-                   void* out, const void* kern, const void* tw, uint32_t n_cols,
-                   int inverse, float scale);
+                   void* out, const void* kern, const void* tw, const void* ptw,
+                   uint32_t n_cols, int inverse, float scale);
 /* tiled spectrum size in complex elements for a plane of `width` x `height` */
 inline size_t TiledComplexCount(uint32_t width, uint32_t height) {
   return size_t((width / 2 + 1 + 15) / 16) * 16 * height;
@@ -50,17 +69,17 @@ const FastRows* FindFastRows(uint32_t n, bool f64);
  * spectrum column per workgroup round. Input rows: a device list (rows,
  * n_rows) or the range [row0, row0 + row_n) (other rows zero). */
 int FastColumnsLaunch(rdl_session* s, const FastColumns* p, const void* in, void* out,
-                      const void* kern, const void* tw, uint32_t n_cols, uint32_t mode,
+                      const void* kern, const void* ptw, uint32_t n_cols, uint32_t mode,
                       int in_cm, int out_cm, int kern_cm, const uint32_t* rows,
                       const uint32_t* n_rows, uint32_t row0, uint32_t row_n,
                       double scale);
 /* spectrum rows oy .. oy+img_h-1 -> the img_w x img_h window at (ox, oy) */
 int FastRowsInverseLaunch(rdl_session* s, const FastRows* p, const void* spec, float* out,
-                          const void* tw, uint32_t height, uint32_t img_w, uint32_t img_h,
+                          const void* tw, const void* ptw, uint32_t height, uint32_t img_w, uint32_t img_h,
                           uint32_t ox, uint32_t oy, int subtract, int tiled = 0);
 /* the window's rows (or the listed plane rows) -> spectrum rows */
 int FastRowsForwardLaunch(rdl_session* s, const FastRows* p, const float* in, void* spec,
-                          const void* tw, uint32_t height, uint32_t img_w, uint32_t img_h,
+                          const void* tw, const void* ptw, uint32_t height, uint32_t img_w, uint32_t img_h,
                           uint32_t ox, uint32_t oy, const uint32_t* rows,
                           const uint32_t* n_rows, int tiled = 0);
 /* ascending list of the rows whose mask byte is non-zero, and its length */

@@ -19,9 +19,12 @@
 //     next row pair's spectrum while the current one is transformed,
 //   * rows outside the output window are never transformed, sparse inputs
 //     (the sub-minor model's occupied rows) are read from a compacted list.
+#include <cmath>
+#include <cstring>
 #include <map>
 #include <mutex>
 #include <tuple>
+#include <vector>
 
 #include "fft_dft.h"
 #include "fft_fast.h"
@@ -36,17 +39,16 @@ __device__ __forceinline__ void LdsSync() {
 }
 
 // One Stockham pass (radix R, span NS) over a length-N transform in LDS, in
-// place (inputs read to registers before the barrier). Twiddles W_N^m are
-// tw[m * TWS] (TWS = 2: a half-length transform reads the full-length
-// table). Float twiddles come from the table per power; double builds w^r by
-// recurrence from one load (error ~1e-15, far below the float rounding of
-// the result).
-template <typename T, uint32_t TH, uint32_t N, uint32_t R, uint32_t NS, uint32_t TWS>
-__device__ __forceinline__ void Pass(Cx<T>* buf, const Cx<T>* __restrict__ tw,
+// place (inputs read to registers before the barrier). Twiddles come from the
+// plan's pass table (MakePassTable, host): pass p's W_N^{k (q+1) M} at
+// ptw[OFF + q NS + k], so a wave's load for one q is one contiguous run.
+// Float reads every power; double reads w and builds w^r by recurrence (error
+// ~1e-15, far below the float rounding of the result).
+template <typename T, uint32_t TH, uint32_t N, uint32_t R, uint32_t NS, uint32_t OFF>
+__device__ __forceinline__ void Pass(Cx<T>* buf, const Cx<T>* __restrict__ ptw,
                                      uint32_t tid) {
   constexpr uint32_t NB = N / R;
   constexpr uint32_t BPT = (NB + TH - 1) / TH;
-  constexpr uint32_t M = N / (NS * R);
   constexpr bool kTable = sizeof(T) == 4;
   constexpr uint32_t NW = NS > 1 ? (kTable ? R - 1 : 1) : 1;
   Cx<T> v[BPT][R];
@@ -58,7 +60,7 @@ __device__ __forceinline__ void Pass(Cx<T>* buf, const Cx<T>* __restrict__ tw,
       if constexpr (NS > 1) {
         const uint32_t k = j % NS;
 #pragma unroll
-        for (uint32_t q = 0; q < NW; ++q) w[i][q] = tw[k * (q + 1) * M * TWS];
+        for (uint32_t q = 0; q < NW; ++q) w[i][q] = ptw[OFF + q * NS + k];
       }
 #pragma unroll
       for (uint32_t r = 0; r < R; ++r) v[i][r] = buf[j + r * NB];
@@ -93,13 +95,16 @@ __device__ __forceinline__ void Pass(Cx<T>* buf, const Cx<T>* __restrict__ tw,
   LdsSync();
 }
 
-template <typename T, uint32_t TH, uint32_t N, uint32_t TWS, uint32_t NS, uint32_t R,
+// entries of pass (radix R, span NS) in the pass table
+constexpr uint32_t PassTableSize(uint32_t R, uint32_t NS) { return NS > 1 ? NS * (R - 1) : 0; }
+
+template <typename T, uint32_t TH, uint32_t N, uint32_t OFF, uint32_t NS, uint32_t R,
           uint32_t... Rest>
-__device__ __forceinline__ void Fft(Cx<T>* buf, const Cx<T>* __restrict__ tw,
+__device__ __forceinline__ void Fft(Cx<T>* buf, const Cx<T>* __restrict__ ptw,
                                     uint32_t tid) {
-  Pass<T, TH, N, R, NS, TWS>(buf, tw, tid);
+  Pass<T, TH, N, R, NS, OFF>(buf, ptw, tid);
   if constexpr (sizeof...(Rest) > 0)
-    Fft<T, TH, N, TWS, NS * R, Rest...>(buf, tw, tid);
+    Fft<T, TH, N, OFF + PassTableSize(R, NS), NS * R, Rest...>(buf, ptw, tid);
 }
 
 template <uint32_t... Rs>
@@ -127,7 +132,7 @@ template <typename T, uint32_t TH, bool PF, uint32_t... Rs>
 __global__ __launch_bounds__(TH) void Columns(ColArgs a, const Cx<T>* __restrict__ in,
                                               Cx<T>* out,
                                               const Cx<T>* __restrict__ kern,
-                                              const Cx<T>* __restrict__ tw) {
+                                              const Cx<T>* __restrict__ ptw) {
   constexpr uint32_t N = Product<Rs...>();
   constexpr uint32_t E = (N + TH - 1) / TH;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
@@ -186,7 +191,7 @@ __global__ __launch_bounds__(TH) void Columns(ColArgs a, const Cx<T>* __restrict
       if (PF && a.mode != 0) load_kernel();
     }
     LdsSync();
-    if (a.mode != 2) Fft<T, TH, N, 1, 1, Rs...>(buf, tw, tid);
+    if (a.mode != 2) Fft<T, TH, N, 0, 1, Rs...>(buf, ptw, tid);
     if (a.mode != 0) {
       if (!PF && active) load_kernel();
       // inverse = conj(forward(conj(X K s)))
@@ -196,7 +201,7 @@ __global__ __launch_bounds__(TH) void Columns(ColArgs a, const Cx<T>* __restrict
         if (N % TH == 0 || y < N) buf[y] = Conj(Scale(Mul(buf[y], K[i]), s));
       }
       LdsSync();
-      Fft<T, TH, N, 1, 1, Rs...>(buf, tw, tid);
+      Fft<T, TH, N, 0, 1, Rs...>(buf, ptw, tid);
     }
     if (active) {
       const uint32_t o_stride = a.out_cm ? 1u : a.ld;
@@ -254,7 +259,8 @@ __device__ __forceinline__ size_t TileIndex(uint32_t y, uint32_t k, uint32_t hei
 template <typename T, uint32_t TH, uint32_t... Rs>
 __global__ __launch_bounds__(TH) void RowsInverse(RowArgs a, const Cx<T>* __restrict__ spec,
                                                   float* __restrict__ out,
-                                                  const Cx<T>* __restrict__ tw) {
+                                                  const Cx<T>* __restrict__ tw,
+                                                  const Cx<T>* __restrict__ ptw) {
   constexpr uint32_t H = Product<Rs...>();
   constexpr uint32_t EH = (H + TH - 1) / TH;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
@@ -264,38 +270,59 @@ __global__ __launch_bounds__(TH) void RowsInverse(RowArgs a, const Cx<T>* __rest
   if (iy >= a.img_h) return;
   const uint32_t y = iy + a.oy;
   const Cx<T>* X = spec + size_t(y) * a.ld;
+  auto load = [&](uint32_t k) {
+    return a.tiled ? spec[TileIndex(y, k, a.height)] : X[k];
+  };
+  // conj(Z) for bin k from X[k] = xk and X[H-k] = xm
+  auto zc = [&](Cx<T> xk, Cx<T> xm, uint32_t k) {
+    const Cx<T> sum = {xk.x + xm.x, xk.y - xm.y};  // X[k] + conj X[H-k]
+    const Cx<T> dif = {xk.x - xm.x, xk.y + xm.y};  // X[k] - conj X[H-k]
+    const Cx<T> t = Mul(Conj(tw[k]), dif);         // W_N^-k (...)
+    return Cx<T>{sum.x - t.y, -(sum.y + t.x)};      // Z = sum + i t, conjugated
+  };
+  // bins in pairs (k, H - k): every spectrum element is read once
+  constexpr uint32_t NP = H / 2 + 1;
+  constexpr uint32_t EP = (NP + TH - 1) / TH;
 #pragma unroll
-  for (uint32_t i = 0; i < EH; ++i) {
+  for (uint32_t i = 0; i < EP; ++i) {
     const uint32_t k = tid + i * TH;
-    if (H % TH == 0 || k < H) {
-      Cx<T> xk, xm;
-      if (a.tiled) {
-        xk = spec[TileIndex(y, k, a.height)];
-        xm = spec[TileIndex(y, H - k, a.height)];
-      } else {
-        xk = X[k];
-        xm = X[H - k];
-      }
-      if (k == 0) {
-        xk.y = T(0);
-        xm.y = T(0);
-      }
-      const Cx<T> sum = {xk.x + xm.x, xk.y - xm.y};  // X[k] + conj X[H-k]
-      const Cx<T> dif = {xk.x - xm.x, xk.y + xm.y};  // X[k] - conj X[H-k]
-      const Cx<T> wk = Conj(tw[k]);                  // W_N^-k
-      const Cx<T> t = Mul(wk, dif);
-      // Z = sum + i t, stored conjugated
-      buf[k] = {sum.x - t.y, -(sum.y + t.x)};
+    if (NP % TH != 0 && k >= NP) continue;
+    const uint32_t m = H - k;
+    Cx<T> xk = load(k), xm = load(m);
+    if (k == 0) {  // C2R ignores the imaginary parts of X[0] and X[H]
+      xk.y = T(0);
+      xm.y = T(0);
     }
+    buf[k] = zc(xk, xm, k);
+    if (k != 0 && m != k) buf[m] = zc(xm, xk, m);
   }
   LdsSync();
-  Fft<T, TH, H, 2, 1, Rs...>(buf, tw, tid);
+  Fft<T, TH, H, 0, 1, Rs...>(buf, ptw, tid);
   float* o = out + size_t(iy) * a.img_w;
+  if (((a.ox | a.img_w) & 1u) == 0) {
+    // even window: (x[2n], x[2n+1]) both in or both out, one 8-B access
+#pragma unroll
+    for (uint32_t i = 0; i < EH; ++i) {
+      const uint32_t n = tid + i * TH;
+      if (H % TH != 0 && n >= H) continue;
+      const uint32_t x0 = 2 * n;
+      if (x0 < a.ox || x0 >= a.ox + a.img_w) continue;
+      const Cx<T> z = buf[n];  // conj(result): x[2n] = z.x, x[2n+1] = -z.y
+      float2* p = reinterpret_cast<float2*>(o + (x0 - a.ox));
+      float2 v = {float(z.x), float(-z.y)};
+      if (a.subtract) {
+        const float2 r = *p;
+        v = {r.x - v.x, r.y - v.y};
+      }
+      *p = v;
+    }
+    return;
+  }
 #pragma unroll
   for (uint32_t i = 0; i < EH; ++i) {
     const uint32_t n = tid + i * TH;
     if (H % TH != 0 && n >= H) continue;
-    const Cx<T> z = buf[n];  // conj(result): x[2n] = z.x, x[2n+1] = -z.y
+    const Cx<T> z = buf[n];
     const uint32_t x0 = 2 * n, x1 = x0 + 1;
     if (x0 >= a.ox && x0 < a.ox + a.img_w) {
       float* p = o + (x0 - a.ox);
@@ -315,7 +342,8 @@ __global__ __launch_bounds__(TH) void RowsInverse(RowArgs a, const Cx<T>* __rest
 template <typename T, uint32_t TH, uint32_t... Rs>
 __global__ __launch_bounds__(TH) void RowsForward(RowArgs a, const float* __restrict__ in,
                                                   Cx<T>* __restrict__ spec,
-                                                  const Cx<T>* __restrict__ tw) {
+                                                  const Cx<T>* __restrict__ tw,
+                                                  const Cx<T>* __restrict__ ptw) {
   constexpr uint32_t H = Product<Rs...>();
   constexpr uint32_t EH = (H + TH - 1) / TH;
   constexpr uint32_t EX = (H + 1 + TH - 1) / TH;
@@ -330,17 +358,27 @@ __global__ __launch_bounds__(TH) void RowsForward(RowArgs a, const float* __rest
     const int64_t iy = int64_t(y) - a.oy;
     const bool in_y = iy >= 0 && iy < a.img_h;
     const float* row = in + (in_y ? size_t(iy) * a.img_w : 0);
+    const bool even = ((a.ox | a.img_w) & 1u) == 0;
 #pragma unroll
     for (uint32_t i = 0; i < EH; ++i) {
       const uint32_t n = tid + i * TH;
       if (H % TH != 0 && n >= H) continue;
       const uint32_t x0 = 2 * n, x1 = x0 + 1;
-      const T e = in_y && x0 >= a.ox && x0 < a.ox + a.img_w ? T(row[x0 - a.ox]) : T(0);
-      const T od = in_y && x1 >= a.ox && x1 < a.ox + a.img_w ? T(row[x1 - a.ox]) : T(0);
+      T e = T(0), od = T(0);
+      if (even) {  // (x[2n], x[2n+1]) both in or both out: one 8-B load
+        if (in_y && x0 >= a.ox && x0 < a.ox + a.img_w) {
+          const float2 v = *reinterpret_cast<const float2*>(row + (x0 - a.ox));
+          e = T(v.x);
+          od = T(v.y);
+        }
+      } else {
+        e = in_y && x0 >= a.ox && x0 < a.ox + a.img_w ? T(row[x0 - a.ox]) : T(0);
+        od = in_y && x1 >= a.ox && x1 < a.ox + a.img_w ? T(row[x1 - a.ox]) : T(0);
+      }
       buf[n] = {e, od};
     }
     LdsSync();
-    Fft<T, TH, H, 2, 1, Rs...>(buf, tw, tid);
+    Fft<T, TH, H, 0, 1, Rs...>(buf, ptw, tid);
     Cx<T>* X = spec + size_t(y) * a.ld;
     const T h = T(0.5);
 #pragma unroll
@@ -372,15 +410,15 @@ __global__ __launch_bounds__(TH) void RowsForward(RowArgs a, const float* __rest
 // The inverse convolution runs the same two passes on conj(X K s) (A's load)
 // and conjugates B's store.
 
-// `COUNT` transforms of length N at stride S in LDS (batched Pass).
-template <typename T, uint32_t TH, uint32_t N, uint32_t R, uint32_t NS, uint32_t TWS,
+// `COUNT` transforms of length N at stride S in LDS (batched Pass); the
+// pass tables as for Pass, read once per workgroup into LDS (`wt`, shared by
+// all COUNT transforms).
+template <typename T, uint32_t TH, uint32_t N, uint32_t R, uint32_t NS, uint32_t OFF,
           uint32_t COUNT, uint32_t S>
-__device__ __forceinline__ void BPass(Cx<T>* buf, const Cx<T>* __restrict__ tw,
-                                      uint32_t tid) {
+__device__ __forceinline__ void BPass(Cx<T>* buf, const Cx<T>* wt, uint32_t tid) {
   constexpr uint32_t NB = N / R;
   constexpr uint32_t TOT = COUNT * NB;
   constexpr uint32_t BPT = (TOT + TH - 1) / TH;
-  constexpr uint32_t M = N / (NS * R);
   Cx<T> v[BPT][R];
   Cx<T> w[BPT][NS > 1 ? R - 1 : 1];
 #pragma unroll
@@ -391,7 +429,7 @@ __device__ __forceinline__ void BPass(Cx<T>* buf, const Cx<T>* __restrict__ tw,
       if constexpr (NS > 1) {
         const uint32_t k = j % NS;
 #pragma unroll
-        for (uint32_t q = 0; q + 1 < R; ++q) w[i][q] = tw[k * (q + 1) * M * TWS];
+        for (uint32_t q = 0; q + 1 < R; ++q) w[i][q] = wt[OFF + q * NS + k];
       }
 #pragma unroll
       for (uint32_t r = 0; r < R; ++r) v[i][r] = buf[t * S + j + r * NB];
@@ -417,13 +455,20 @@ __device__ __forceinline__ void BPass(Cx<T>* buf, const Cx<T>* __restrict__ tw,
   LdsSync();
 }
 
-template <typename T, uint32_t TH, uint32_t N, uint32_t TWS, uint32_t COUNT, uint32_t S,
+template <typename T, uint32_t TH, uint32_t N, uint32_t COUNT, uint32_t S, uint32_t OFF,
           uint32_t NS, uint32_t R, uint32_t... Rest>
-__device__ __forceinline__ void BFft(Cx<T>* buf, const Cx<T>* __restrict__ tw,
-                                     uint32_t tid) {
-  BPass<T, TH, N, R, NS, TWS, COUNT, S>(buf, tw, tid);
+__device__ __forceinline__ void BFft(Cx<T>* buf, const Cx<T>* wt, uint32_t tid) {
+  BPass<T, TH, N, R, NS, OFF, COUNT, S>(buf, wt, tid);
   if constexpr (sizeof...(Rest) > 0)
-    BFft<T, TH, N, TWS, COUNT, S, NS * R, Rest...>(buf, tw, tid);
+    BFft<T, TH, N, COUNT, S, OFF + PassTableSize(R, NS), NS * R, Rest...>(buf, wt, tid);
+}
+
+template <uint32_t NS, uint32_t R, uint32_t... Rest>
+constexpr uint32_t TableSize() {
+  if constexpr (sizeof...(Rest) > 0)
+    return PassTableSize(R, NS) + TableSize<NS * R, Rest...>();
+  else
+    return PassTableSize(R, NS);
 }
 
 template <uint32_t... Rs>
@@ -435,22 +480,32 @@ struct StepArgs {
   float scale;
 };
 
-// Pass A: workgroup = (tile, GA consecutive n2). tw: the length-N table.
+// Pass A: workgroup = (tile, GA consecutive n2). tw: the length-N table;
+// ptw: the length-N1 pass table.
 template <uint32_t TH, uint32_t N1, uint32_t N2, uint32_t GA, uint32_t... R1>
 __global__ __launch_bounds__(TH) void ColStepA(StepArgs a, const Cx<float>* __restrict__ in,
                                                Cx<float>* __restrict__ out,
                                                const Cx<float>* __restrict__ kern,
-                                               const Cx<float>* __restrict__ tw) {
+                                               const Cx<float>* __restrict__ tw,
+                                               const Cx<float>* __restrict__ ptw) {
   constexpr uint32_t N = N1 * N2;
   constexpr uint32_t S = N1 + 1;  // padded stride: columns of one row on distinct banks
   constexpr uint32_t COUNT = kTile * GA;
   constexpr uint32_t EL = COUNT * N1;
   constexpr uint32_t E = (EL + TH - 1) / TH;
+  constexpr uint32_t NT = TableSize<1, R1...>();
   __shared__ Cx<float> buf[COUNT * S];
+  __shared__ Cx<float> wt[NT > 0 ? NT : 1];
+  __shared__ Cx<float> wa[GA * N1];  // W_N^{n2 k1} of this workgroup's n2
   const uint32_t tid = threadIdx.x;
   const uint32_t tile = blockIdx.x / (N2 / GA);
   const uint32_t n2_0 = (blockIdx.x % (N2 / GA)) * GA;
   const size_t base = size_t(tile) * N * kTile;
+  for (uint32_t i = tid; i < NT; i += TH) wt[i] = ptw[i];
+  for (uint32_t i = tid; i < GA * N1; i += TH) {
+    const uint32_t g = i / N1, k1 = i % N1;
+    wa[i] = tw[((n2_0 + g) * k1) % N];
+  }
 #pragma unroll
   for (uint32_t i = 0; i < E; ++i) {
     const uint32_t idx = tid + i * TH;
@@ -463,7 +518,7 @@ __global__ __launch_bounds__(TH) void ColStepA(StepArgs a, const Cx<float>* __re
     buf[(g * kTile + col) * S + n1] = v;
   }
   LdsSync();
-  BFft<float, TH, N1, N2, COUNT, S, 1, R1...>(buf, tw, tid);
+  BFft<float, TH, N1, COUNT, S, 0, 1, R1...>(buf, wt, tid);
 #pragma unroll
   for (uint32_t i = 0; i < E; ++i) {
     const uint32_t idx = tid + i * TH;
@@ -471,26 +526,29 @@ __global__ __launch_bounds__(TH) void ColStepA(StepArgs a, const Cx<float>* __re
     const uint32_t col = idx % kTile, q = idx / kTile;
     const uint32_t g = q % GA, k1 = q / GA;
     const uint32_t n2 = n2_0 + g;
-    const Cx<float> v = Mul(buf[(g * kTile + col) * S + k1], tw[(n2 * k1) % N]);
+    const Cx<float> v = Mul(buf[(g * kTile + col) * S + k1], wa[g * N1 + k1]);
     out[base + size_t(k1 * N2 + n2) * kTile + col] = v;
   }
 }
 
-// Pass B: workgroup = (tile, GB consecutive k1).
+// Pass B: workgroup = (tile, GB consecutive k1); ptw: the length-N2 pass table.
 template <uint32_t TH, uint32_t N1, uint32_t N2, uint32_t GB, uint32_t... R2>
 __global__ __launch_bounds__(TH) void ColStepB(StepArgs a, const Cx<float>* __restrict__ in,
                                                Cx<float>* __restrict__ out,
-                                               const Cx<float>* __restrict__ tw) {
-  constexpr uint32_t N = N1 * N2;
+                                               const Cx<float>* __restrict__ ptw) {
   constexpr uint32_t S = N2 + 1;
+  constexpr uint32_t N = N1 * N2;
   constexpr uint32_t COUNT = kTile * GB;
   constexpr uint32_t EL = COUNT * N2;
   constexpr uint32_t E = (EL + TH - 1) / TH;
+  constexpr uint32_t NT = TableSize<1, R2...>();
   __shared__ Cx<float> buf[COUNT * S];
+  __shared__ Cx<float> wt[NT > 0 ? NT : 1];
   const uint32_t tid = threadIdx.x;
   const uint32_t tile = blockIdx.x / (N1 / GB);
   const uint32_t k1_0 = (blockIdx.x % (N1 / GB)) * GB;
   const size_t base = size_t(tile) * N * kTile;
+  for (uint32_t i = tid; i < NT; i += TH) wt[i] = ptw[i];
 #pragma unroll
   for (uint32_t i = 0; i < E; ++i) {
     const uint32_t idx = tid + i * TH;
@@ -500,7 +558,7 @@ __global__ __launch_bounds__(TH) void ColStepB(StepArgs a, const Cx<float>* __re
     buf[(g * kTile + col) * S + n2] = in[base + size_t((k1_0 + g) * N2 + n2) * kTile + col];
   }
   LdsSync();
-  BFft<float, TH, N2, N1, COUNT, S, 1, R2...>(buf, tw, tid);
+  BFft<float, TH, N2, COUNT, S, 0, 1, R2...>(buf, wt, tid);
 #pragma unroll
   for (uint32_t i = 0; i < E; ++i) {
     const uint32_t idx = tid + i * TH;
@@ -550,13 +608,15 @@ __global__ __launch_bounds__(1024) void CompactRows(const uint8_t* __restrict__ 
 #define RDL_FAST_COLS(T, TH, PF, ...)                                          \
   FastColumns {                                                                \
     ff::Product<__VA_ARGS__>(), sizeof(T) == 8, TH,                            \
-        reinterpret_cast<const void*>(&ff::Columns<T, TH, PF, __VA_ARGS__>)    \
+        reinterpret_cast<const void*>(&ff::Columns<T, TH, PF, __VA_ARGS__>),   \
+        MakeRadixList<__VA_ARGS__>()                                           \
   }
 #define RDL_FAST_ROWS(T, TH, ...)                                              \
   FastRows {                                                                   \
     2 * ff::Product<__VA_ARGS__>(), sizeof(T) == 8, TH,                        \
         reinterpret_cast<const void*>(&ff::RowsInverse<T, TH, __VA_ARGS__>),   \
-        reinterpret_cast<const void*>(&ff::RowsForward<T, TH, __VA_ARGS__>)    \
+        reinterpret_cast<const void*>(&ff::RowsForward<T, TH, __VA_ARGS__>),   \
+        MakeRadixList<__VA_ARGS__>()                                           \
   }
 
 const FastColumns* FindFastColumns(uint32_t n, bool f64) {
@@ -606,7 +666,8 @@ const FastRows* FindFastRows(uint32_t n, bool f64) {
   FastSteps {                                                                      \
     N1 * N2, N1, N2, GA, GB, 256,                                                  \
         reinterpret_cast<const void*>(&ff::ColStepA<256, N1, N2, GA, RA>),         \
-        reinterpret_cast<const void*>(&ff::ColStepB<256, N1, N2, GB, RB>)          \
+        reinterpret_cast<const void*>(&ff::ColStepB<256, N1, N2, GB, RB>),         \
+        MakeRadixList<RA>(), MakeRadixList<RB>()                                   \
   }
 #define RDL_R(...) __VA_ARGS__
 
@@ -645,7 +706,7 @@ int SlotsPerCu(rdl_session* s, const void* fn, uint32_t threads, size_t lds) {
 }  // namespace
 
 int FastColumnsLaunch(rdl_session* s, const FastColumns* p, const void* in, void* out,
-                      const void* kern, const void* tw, uint32_t n_cols, uint32_t mode,
+                      const void* kern, const void* ptw, uint32_t n_cols, uint32_t mode,
                       int in_cm, int out_cm, int kern_cm, const uint32_t* rows,
                       const uint32_t* n_rows, uint32_t row0, uint32_t row_n,
                       double scale) {
@@ -670,15 +731,14 @@ int FastColumnsLaunch(rdl_session* s, const FastColumns* p, const void* in, void
   const uint32_t want = std::min<uint32_t>(n_cols, uint32_t(s->n_cus) * uint32_t(slots));
   a.per_xcd = std::max<uint32_t>(1, (want + 7) / 8);
   const uint32_t grid = 8 * a.per_xcd;
-  void* args[] = {&a, (void*)&in, (void*)&out, (void*)&kern,
-                  (void*)&tw};
+  void* args[] = {&a, (void*)&in, (void*)&out, (void*)&kern, (void*)&ptw};
   RDL_HIP_CHECK(hipLaunchKernel(p->kernel, dim3(grid), dim3(p->threads), args, lds,
                                 s->stream));
   return RDL_OK;
 }
 
 int FastRowsInverseLaunch(rdl_session* s, const FastRows* p, const void* spec, float* out,
-                          const void* tw, uint32_t height, uint32_t img_w, uint32_t img_h,
+                          const void* tw, const void* ptw, uint32_t height, uint32_t img_w, uint32_t img_h,
                           uint32_t ox, uint32_t oy, int subtract, int tiled) {
   const size_t lds = size_t(p->n / 2) * (p->f64 ? 16 : 8);
   if (SlotsPerCu(s, p->inverse, p->threads, lds) < 0) {
@@ -695,14 +755,14 @@ int FastRowsInverseLaunch(rdl_session* s, const FastRows* p, const void* spec, f
   a.oy = oy;
   a.subtract = subtract;
   a.tiled = tiled;
-  void* args[] = {&a, (void*)&spec, (void*)&out, (void*)&tw};
+  void* args[] = {&a, (void*)&spec, (void*)&out, (void*)&tw, (void*)&ptw};
   RDL_HIP_CHECK(hipLaunchKernel(p->inverse, dim3(img_h), dim3(p->threads), args, lds,
                                 s->stream));
   return RDL_OK;
 }
 
 int FastRowsForwardLaunch(rdl_session* s, const FastRows* p, const float* in, void* spec,
-                          const void* tw, uint32_t height, uint32_t img_w, uint32_t img_h,
+                          const void* tw, const void* ptw, uint32_t height, uint32_t img_w, uint32_t img_h,
                           uint32_t ox, uint32_t oy, const uint32_t* rows,
                           const uint32_t* n_rows, int tiled) {
   const size_t lds = size_t(p->n / 2) * (p->f64 ? 16 : 8);
@@ -726,30 +786,63 @@ int FastRowsForwardLaunch(rdl_session* s, const FastRows* p, const float* in, vo
   if (max_rows == 0) return RDL_OK;
   const uint32_t grid =
       std::min<uint32_t>(max_rows, uint32_t(s->n_cus) * uint32_t(slots) * 2);
-  void* args[] = {&a, (void*)&in, (void*)&spec, (void*)&tw};
+  void* args[] = {&a, (void*)&in, (void*)&spec, (void*)&tw, (void*)&ptw};
   RDL_HIP_CHECK(hipLaunchKernel(p->forward, dim3(grid), dim3(p->threads), args, lds,
                                 s->stream));
   return RDL_OK;
 }
 
 int FastStepLaunch(rdl_session* s, const FastSteps* p, bool pass_b, const void* in,
-                   void* out, const void* kern, const void* tw, uint32_t n_cols,
-                   int inverse, float scale) {
+                   void* out, const void* kern, const void* tw, const void* ptw,
+                   uint32_t n_cols, int inverse, float scale) {
   ff::StepArgs a{};
   a.n_tiles = (n_cols + ff::kTile - 1) / ff::kTile;
   a.inverse = inverse;
   a.scale = scale;
   if (pass_b) {
     const uint32_t grid = a.n_tiles * (p->n1 / p->gb);
-    void* args[] = {&a, (void*)&in, (void*)&out, (void*)&tw};
+    void* args[] = {&a, (void*)&in, (void*)&out, (void*)&ptw};
     RDL_HIP_CHECK(hipLaunchKernel(p->step_b, dim3(grid), dim3(p->threads), args, 0,
                                   s->stream));
   } else {
     const uint32_t grid = a.n_tiles * (p->n2 / p->ga);
-    void* args[] = {&a, (void*)&in, (void*)&out, (void*)&kern, (void*)&tw};
+    void* args[] = {&a, (void*)&in, (void*)&out, (void*)&kern, (void*)&tw, (void*)&ptw};
     RDL_HIP_CHECK(hipLaunchKernel(p->step_a, dim3(grid), dim3(p->threads), args, 0,
                                   s->stream));
   }
+  return RDL_OK;
+}
+
+int MakePassTable(uint32_t n, const RadixList& radix, bool f64, void** out) {
+  std::vector<double> re, im;
+  uint32_t ns = 1;
+  for (uint32_t p = 0; p < radix.n; ++p) {
+    const uint32_t r = radix.r[p];
+    const uint32_t m = n / (ns * r);
+    if (ns > 1)
+      for (uint32_t q = 0; q + 1 < r; ++q)
+        for (uint32_t k = 0; k < ns; ++k) {
+          const uint64_t e = (uint64_t(k) * (q + 1) * m) % n;
+          const long double ang =
+              -2.0L * 3.14159265358979323846264338327950288L * (long double)e / n;
+          re.push_back(double(std::cos(ang)));
+          im.push_back(double(std::sin(ang)));
+        }
+    ns *= r;
+  }
+  const size_t count = std::max<size_t>(re.size(), 1);
+  std::vector<unsigned char> host(count * (f64 ? 16 : 8), 0);
+  for (size_t i = 0; i < re.size(); ++i) {
+    if (f64) {
+      const double v[2] = {re[i], im[i]};
+      std::memcpy(&host[i * 16], v, 16);
+    } else {
+      const float v[2] = {float(re[i]), float(im[i])};
+      std::memcpy(&host[i * 8], v, 8);
+    }
+  }
+  RDL_HIP_CHECK(hipMalloc(out, host.size()));
+  RDL_HIP_CHECK(hipMemcpy(*out, host.data(), host.size(), hipMemcpyHostToDevice));
   return RDL_OK;
 }
 

@@ -508,6 +508,11 @@ struct rdl_conv {
   // float planes with four-step column plans: spectra in 16-column tiles
   const rdl::FastSteps* steps = nullptr;
   bool tiled = false;
+  // pass tables of the compile-time plans (rdl::MakePassTable)
+  void* ptw_row = nullptr;
+  void* ptw_col = nullptr;
+  void* ptw_a = nullptr;
+  void* ptw_b = nullptr;
 };
 
 namespace {
@@ -566,15 +571,16 @@ int LaunchRowsForward(rdl_conv* c, const float* in, uint32_t in_w, uint32_t in_h
       rdl::SetError("LDS FFT: row masks need the row-major (float64) plans");
       return RDL_ERR_UNSUPPORTED;
     }
-    return rdl::FastRowsForwardLaunch(c->s, c->fast_rows, in, spec, c->tw_row, c->height,
-                                      in_w, in_h, ox, oy, nullptr, nullptr, 1);
+    return rdl::FastRowsForwardLaunch(c->s, c->fast_rows, in, spec, c->tw_row, c->ptw_row,
+                                      c->height, in_w, in_h, ox, oy, nullptr, nullptr, 1);
   }
   if (c->fast_rows) {
     const size_t row_bytes = size_t(c->width / 2 + 1) * sizeof(rdl::Cx<T>);
     if (row_mask) {
       RDL_TRY(CompactRowsFor(c, row_mask, false));
       return rdl::FastRowsForwardLaunch(c->s, c->fast_rows, in, spec, c->tw_row,
-                                        c->height, in_w, in_h, ox, oy, c->rows_list,
+                                        c->ptw_row, c->height, in_w, in_h, ox, oy,
+                                        c->rows_list,
                                         c->rows_list + c->height);
     }
     // rows outside the window are zero spectra
@@ -584,8 +590,8 @@ int LaunchRowsForward(rdl_conv* c, const float* in, uint32_t in_w, uint32_t in_h
       RDL_HIP_CHECK(hipMemsetAsync(base + size_t(oy + in_h) * row_bytes, 0,
                                    size_t(c->height - oy - in_h) * row_bytes,
                                    c->s->stream));
-    return rdl::FastRowsForwardLaunch(c->s, c->fast_rows, in, spec, c->tw_row, c->height,
-                                      in_w, in_h, ox, oy, nullptr, nullptr);
+    return rdl::FastRowsForwardLaunch(c->s, c->fast_rows, in, spec, c->tw_row, c->ptw_row,
+                                      c->height, in_w, in_h, ox, oy, nullptr, nullptr);
   }
   rdl::RowArgs a{};
   a.row_mask = row_mask;
@@ -614,7 +620,8 @@ template <typename T>
 int LaunchRowsInverse(rdl_conv* c, const void* spec, float* out, uint32_t out_w,
                       uint32_t out_h, uint32_t ox, uint32_t oy, int subtract) {
   if (c->fast_rows)
-    return rdl::FastRowsInverseLaunch(c->s, c->fast_rows, spec, out, c->tw_row, c->height,
+    return rdl::FastRowsInverseLaunch(c->s, c->fast_rows, spec, out, c->tw_row, c->ptw_row,
+                                      c->height,
                                       out_w, out_h, ox, oy, subtract, c->tiled ? 1 : 0);
   rdl::RowArgs a{};
   a.plan = c->row_plan;
@@ -653,7 +660,8 @@ int LaunchColumns(rdl_conv* c, const void* in, void* out, const void* kern,
     const uint32_t nc = c->width / 2 + 1;
     const float sc = float(scale);
     auto step = [&](bool b, const void* i, void* o, int inv) {
-      return rdl::FastStepLaunch(c->s, c->steps, b, i, o, kern, c->tw_col, nc, inv, sc);
+      return rdl::FastStepLaunch(c->s, c->steps, b, i, o, kern, c->tw_col,
+                                 b ? c->ptw_b : c->ptw_a, nc, inv, sc);
     };
     if (mode != 2) {
       RDL_TRY(step(false, in, c->scratch, 0));
@@ -673,7 +681,7 @@ int LaunchColumns(rdl_conv* c, const void* in, void* out, const void* kern,
       n_rows = c->rows_list + c->height;
       c->rows_list_mask = nullptr;  // the mask's contents may change next time
     }
-    return rdl::FastColumnsLaunch(c->s, c->fast_cols, in, out, kern, c->tw_col,
+    return rdl::FastColumnsLaunch(c->s, c->fast_cols, in, out, kern, c->ptw_col,
                                   c->width / 2 + 1, uint32_t(mode), in_cm, out_cm, kern_cm,
                                   rows, n_rows, 0, c->height, scale);
   }
@@ -862,6 +870,14 @@ int rdl_conv_create_ex(rdl_session* s, uint32_t width, uint32_t height, int f64,
       c->steps = rdl::FindFastSteps(height);
       c->tiled = c->steps != nullptr;
     }
+    if (c->fast_rows)
+      RDL_TRY(rdl::MakePassTable(width / 2, c->fast_rows->radix, c->f64, &c->ptw_row));
+    if (c->fast_cols)
+      RDL_TRY(rdl::MakePassTable(height, c->fast_cols->radix, c->f64, &c->ptw_col));
+    if (c->steps) {
+      RDL_TRY(rdl::MakePassTable(c->steps->n1, c->steps->radix_a, false, &c->ptw_a));
+      RDL_TRY(rdl::MakePassTable(c->steps->n2, c->steps->radix_b, false, &c->ptw_b));
+    }
   }
   if (want_split && can_split) {
     c->split = true;
@@ -887,6 +903,8 @@ int rdl_conv_destroy(rdl_conv* c) {
   if (c->tw_n2) (void)hipFree(c->tw_n2);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->rows_list) (void)hipFree(c->rows_list);
+  for (void* p : {c->ptw_row, c->ptw_col, c->ptw_a, c->ptw_b})
+    if (p) (void)hipFree(p);
   delete c;
   return RDL_OK;
 }
