@@ -309,6 +309,10 @@ int rdl_subminor_model_f64(rdl_subminor* h, uint32_t image_index,
                            uint32_t ox, uint32_t oy);
 /* Selected positions (packed y<<16|x) and per-image model values of the last
  * run, copied to host (UpdateComponentList / UpdateAutoMask inputs). */
+/* SubMinorLoop::UpdateAutoMask (cpp/algorithms/subminor_loop.cc:220-228):
+ * d_mask[y * width + x] = 1 for every selected pixel of the last run whose
+ * model value is non-zero in any image (a width x height byte mask). */
+int rdl_subminor_update_mask(rdl_subminor* h, uint8_t* d_mask);
 int rdl_subminor_get(rdl_subminor* h, uint32_t* h_positions, float* h_models,
                      uint64_t capacity);
 

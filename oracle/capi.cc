@@ -213,6 +213,24 @@ void orc_algo_update(void* h, const orc_algo_settings* a) {
   }
 }
 
+// MultiScaleAlgorithm::SetAutoMaskMode (multiscale_algorithm.h:41-44)
+void orc_algo_set_automask(void* h, int track, int use) {
+  auto* algo = static_cast<OrcAlgo*>(h);
+  if (!algo->ms) return;
+  algo->ms->track_scale_masks = track != 0;
+  algo->ms->use_scale_masks = use != 0;
+}
+
+// copy of scale mask `index` (0/1 bytes, up to n); returns the mask count
+uint64_t orc_algo_scale_mask(void* h, uint64_t index, uint8_t* out, uint64_t n) {
+  auto* algo = static_cast<OrcAlgo*>(h);
+  if (!algo->ms) return 0;
+  const auto& masks = algo->ms->scale_masks;
+  if (out && index < masks.size())
+    std::copy_n(masks[index].data(), std::min<size_t>(n, masks[index].size()), out);
+  return masks.size();
+}
+
 int orc_algo_execute(void* h, const orc_set_desc* d, float* residual,
                      float* model, const float* psfs, orc_result* out,
                      uint32_t* trace, uint64_t trace_cap) {
@@ -283,6 +301,7 @@ struct OrcParallel {
   double major_loop_gain_unused = 0.0;
   bool snapshot = false;
   std::vector<TiledAlgorithm> algorithms;
+  ParallelMasks masks;
 };
 
 // IUWT: coeffs (n_scales + 1) planes; aliased != 0 runs Decompose(x, x, ..)
@@ -351,6 +370,20 @@ void* orc_parallel_create(int kind, const orc_algo_settings* a, uint64_t grid_w,
 
 void orc_parallel_destroy(void* h) { delete static_cast<OrcParallel*>(h); }
 
+// ParallelDeconvolution::SetAutoMaskMode (parallel_deconvolution.cc:260-268)
+void orc_parallel_set_automask(void* h, int track, int use) {
+  auto* p = static_cast<OrcParallel*>(h);
+  p->masks.track = track != 0;
+  p->masks.use = use != 0;
+}
+
+// SetThreshold / SetMinorLoopGain / ... on every subimage algorithm (their
+// iteration counts and multiscale state are kept)
+void orc_parallel_update(void* h, const orc_algo_settings* a) {
+  auto* p = static_cast<OrcParallel*>(h);
+  for (TiledAlgorithm& t : p->algorithms) t.settings = MakeSettings(a);
+}
+
 // 1: subimages of a pass all trim the residual as it was at the start of the
 // pass (the product's concurrent subimage pool, max_threads > 1)
 void orc_parallel_set_snapshot(void* h, int snapshot) {
@@ -379,7 +412,7 @@ int orc_parallel_execute(void* h, const orc_set_desc* d, float* residual,
     ParallelResult r = ParallelRun(p->algorithms, p->grid_w, p->grid_h, desc, res,
                                    mod, psf_ptrs, major_loop_gain, limit,
                                    reinterpret_cast<const bool*>(user_mask), &subs,
-                                   &traces, p->snapshot);
+                                   &traces, p->snapshot, &p->masks);
     out->another_iteration_required = r.another_iteration_required;
     out->n_subimages = int32_t(subs.size());
     out->start_peak = r.start_peak;

@@ -572,6 +572,13 @@ void SubMinorLoop::GetFullIndividualModel(size_t image_index,
         model_[image_index][p];
 }
 
+void SubMinorLoop::UpdateAutoMask(bool* mask) const {
+  for (size_t i = 0; i != model_.size(); ++i)
+    for (size_t p = 0; p != positions_.size(); ++p)
+      if (model_[i][p] != 0.0f)
+        mask[positions_[p].first + positions_[p].second * width_] = true;
+}
+
 void SubMinorLoop::CorrectResidualDirty(size_t image_index, float* residual,
                                         const float* psf) const {
   // subminor_loop.cc:195-218
@@ -802,7 +809,10 @@ void MultiScale::FindPeakDirect(const float* image, size_t w, size_t h,
   const size_t hb = std::round(w * s_.clean_border_ratio);
   const size_t vb = std::round(h * s_.clean_border_ratio);
   Peak p;
-  if (!s_.clean_mask)
+  if (use_scale_masks)
+    p = FindPeakWithMask(image, w, h, s_.allow_negative, 0, h,
+                         ScaleMask(scale_index), hb, vb);
+  else if (!s_.clean_mask)
     p = FindPeakAvx(image, w, h, s_.allow_negative, 0, h, hb, vb);
   else
     p = FindPeakWithMask(image, w, h, s_.allow_negative, 0, h, s_.clean_mask,
@@ -841,11 +851,14 @@ void MultiScale::FindActiveScaleConvolvedMaxima(const ImageSet& set,
                                          border_scale);
       if (report_rms) e.rms = Rms(copy.data(), w * h);
       Peak p;
-      if (!s_.clean_mask)
+      // threaded_deconvolution_tools.cc:43-44: the scale's mask replaces the
+      // clean mask when scale masks are in use
+      const bool* mask = use_scale_masks ? ScaleMask(si) : s_.clean_mask;
+      if (!mask)
         p = FindPeakAvx(copy.data(), w, h, s_.allow_negative, 0, h, xb, yb);
       else
-        p = FindPeakWithMask(copy.data(), w, h, s_.allow_negative, 0, h,
-                             s_.clean_mask, xb, yb);
+        p = FindPeakWithMask(copy.data(), w, h, s_.allow_negative, 0, h, mask,
+                             xb, yb);
       e.max_normalized_image_value = p.has ? p.value : 0.0f;
       e.max_unnormalized_image_value = p.has ? p.value : 0.0f;
       e.max_image_value_x = p.x;
@@ -875,6 +888,12 @@ Result MultiScale::Execute(ImageSet& data, ImageSet& model,
   if (s_.stop_on_negative) s_.allow_negative = true;
   InitializeScales(scales_, s_.beam_size_in_pixels, std::min(width, height),
                    s_.shape, s_.max_scales, s_.scale_list);
+  if (track_scale_masks) {  // :214-226
+    for (const auto& m : scale_masks)
+      if (m.size() != npx)
+        throw std::runtime_error("Invalid automask size in multiscale algorithm");
+    while (scale_masks.size() < scales_.size()) scale_masks.emplace_back(npx, 0);
+  }
   bool has_hit_threshold_in_sub_loop = false;
   size_t threshold_countdown = std::max(size_t{8}, scales_.size() * 3 / 2);
 
@@ -968,7 +987,7 @@ Result MultiScale::Execute(ImageSet& data, ImageSet& model,
           std::max<size_t>(std::round(width * s_.clean_border_ratio), scale_border);
       sub.vertical_border =
           std::max<size_t>(std::round(height * s_.clean_border_ratio), scale_border);
-      sub.mask = s_.clean_mask;
+      sub.mask = use_scale_masks ? ScaleMask(scale_with_peak) : s_.clean_mask;
       sub.trace = trace;
       sub.trace_scale = uint32_t(scale_with_peak);
       std::vector<const float*> twice_ptrs;
@@ -987,6 +1006,9 @@ Result MultiScale::Execute(ImageSet& data, ImageSet& model,
         const float* psf = convolved_psfs[data.PsfIndex(i)][scale_with_peak].data();
         sub.CorrectResidualDirty(i, data.images[i], psf);
         sub.GetFullIndividualModel(i, scratch.data());
+        if (i == 0 && track_scale_masks)  // :444-445
+          sub.UpdateAutoMask(
+              reinterpret_cast<bool*>(scale_masks[scale_with_peak].data()));
         if (scales_[scale_with_peak].scale != 0.0f) {
           std::vector<float*> l{scratch.data()};
           MsTransform(l, width, height, scales_[scale_with_peak].scale, s_.shape);
@@ -1020,6 +1042,8 @@ Result MultiScale::Execute(ImageSet& data, ImageSet& model,
                               cv[i], s_.shape);
           mi.n_components_cleaned++;
           mi.total_flux_cleaned += cv[i];
+          if (track_scale_masks)  // :695-696
+            scale_masks[scale_with_peak][x + width * y] = 1;
         }
         GetLinearIntegrated(individual_set, integrated.data());
         FindPeakDirect(integrated.data(), width, height, scale_with_peak);

@@ -166,6 +166,9 @@ class SubMinorLoop {
   void CorrectResidualDirty(size_t image_index, float* residual,
                             const float* single_convolved_psf) const;
   void GetFullIndividualModel(size_t image_index, float* dest) const;
+  // subminor_loop.cc:220-228: every selected pixel with a non-zero model
+  // value in any image joins the mask
+  void UpdateAutoMask(bool* mask) const;
   size_t NSelected() const { return positions_.size(); }
 
  private:
@@ -201,6 +204,13 @@ class MultiScale {
   }
   AlgoSettings& Settings() { return s_; }
   size_t iteration_number = 0;
+  // Auto-masking (multiscale_algorithm.h:41-55, .cc:214-226, 403-404,
+  // 444-445, 586-610, 695-696, 716-720): track = grow one mask per scale
+  // from the components; use = clean each scale inside its mask only (the
+  // scale-independent clean mask is then ignored). Masks: one byte (0/1)
+  // per pixel, kept across major iterations.
+  bool track_scale_masks = false, use_scale_masks = false;
+  std::vector<std::vector<uint8_t>> scale_masks;
   Result Execute(ImageSet& data, ImageSet& model,
                  const std::vector<const float*>& psfs,
                  std::vector<Component>* trace);
@@ -213,6 +223,9 @@ class MultiScale {
                                       bool report_rms);
   void FindPeakDirect(const float* image, size_t w, size_t h,
                       size_t scale_index);
+  const bool* ScaleMask(size_t i) const {
+    return reinterpret_cast<const bool*>(scale_masks[i].data());
+  }
   void ActivateScales(size_t scale_with_last_peak);
 };
 

@@ -255,7 +255,7 @@ ParallelResult ParallelRun(std::vector<TiledAlgorithm>& algorithms,
                            double major_loop_gain, double divergence_limit,
                            const bool* user_mask, std::vector<SubImage>* out_subs,
                            std::vector<std::vector<Component>>* traces,
-                           bool snapshot) {
+                           bool snapshot, ParallelMasks* masks) {
   // snapshot == false: subimages run one after another, each trimming the
   // residual left by the ones before (the reference with one thread).
   // snapshot == true: every subimage of a pass trims the residual as it was
@@ -311,6 +311,24 @@ ParallelResult ParallelRun(std::vector<TiledAlgorithm>& algorithms,
       sd.images.push_back(&sub_data[i * n]);
       sm.images.push_back(&sub_model[i * n]);
     }
+    const bool ms_masks = masks && (masks->track || masks->use) && alg.kind == 1;
+    if (ms_masks) {  // :359-390
+      if (!alg.ms) alg.ms = std::make_unique<MultiScale>(alg.settings);
+      alg.ms->track_scale_masks = masks->track;
+      alg.ms->use_scale_masks = masks->use;
+      if (!masks->scale_masks.empty()) {
+        auto& own = alg.ms->scale_masks;
+        own.resize(std::max(own.size(), masks->scale_masks.size()));
+        for (size_t i = 0; i != own.size(); ++i) {
+          own[i].assign(n, 0);
+          if (i >= masks->scale_masks.size()) continue;
+          for (size_t y = 0; y != sh; ++y)
+            for (size_t x = 0; x != sw; ++x)
+              own[i][y * sw + x] =
+                  masks->scale_masks[i][(y + s.y) * width + x + s.x] && s.mask[y * sw + x];
+        }
+      }
+    }
     std::vector<Component> tr;
     Result r = alg.Execute(sd, sm, sub_psfs, &tr);
     if (traces && !find_peak_only) (*traces)[s.index] = tr;
@@ -322,6 +340,17 @@ ParallelResult ParallelRun(std::vector<TiledAlgorithm>& algorithms,
         std::isfinite(s.peak) && !r.is_diverging;
     if (!converging && !find_peak_only) s.reached_major_threshold = false;
     alg.settings.clean_mask = nullptr;
+    if (ms_masks && masks->track && converging && !find_peak_only) {  // :425-462
+      const size_t n_scales = alg.ms->Scales().size();
+      if (masks->scale_masks.empty())
+        masks->scale_masks.assign(n_scales, std::vector<unsigned char>(width * height, 0));
+      for (size_t i = 0; i != n_scales && i != masks->scale_masks.size(); ++i)
+        for (size_t y = 0; y != sh; ++y)
+          for (size_t x = 0; x != sw; ++x)
+            if (s.boundary_mask[y * sw + x])
+              masks->scale_masks[i][(y + s.y) * width + x + s.x] =
+                  alg.ms->scale_masks[i][y * sw + x];
+    }
     if (find_peak_only) {
       alg.settings.max_iterations = max_iter;
       return;

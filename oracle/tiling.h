@@ -30,6 +30,13 @@ struct TiledAlgorithm {
                  std::vector<Component>* trace);
 };
 
+// ParallelDeconvolution's auto-mask state (parallel_deconvolution.cc:
+// 260-268, 359-390, 425-462): full-image masks per scale, 0/1 bytes.
+struct ParallelMasks {
+  bool track = false, use = false;
+  std::vector<std::vector<unsigned char>> scale_masks;
+};
+
 struct ParallelResult {
   bool another_iteration_required = false;
   double start_peak = 0.0, end_peak = 0.0;
@@ -46,6 +53,6 @@ ParallelResult ParallelRun(std::vector<TiledAlgorithm>& algorithms,
                            double major_loop_gain, double divergence_limit,
                            const bool* user_mask, std::vector<SubImage>* out_subs,
                            std::vector<std::vector<Component>>* traces,
-                           bool snapshot = false);
+                           bool snapshot = false, ParallelMasks* masks = nullptr);
 
 }  // namespace oracle

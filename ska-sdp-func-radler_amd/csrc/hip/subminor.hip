@@ -471,6 +471,18 @@ __global__ __launch_bounds__(256) void ScatterModel(const uint32_t* pos,
 }
 
 // rows of the (untrimmed) model plane that hold a non-zero component
+// SubMinorLoop::UpdateAutoMask (subminor_loop.cc:220-228)
+__global__ __launch_bounds__(256) void UpdateMaskKernel(const uint32_t* pos,
+                                                        const float* m, uint64_t n_sel,
+                                                        uint32_t n_img, uint32_t width,
+                                                        uint8_t* mask) {
+  const uint64_t p = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (p >= n_sel) return;
+  bool any = false;
+  for (uint32_t k = 0; k < n_img; ++k) any |= m[size_t(k) * n_sel + p] != 0.0f;
+  if (any) mask[size_t(pos[p] >> 16) * width + (pos[p] & 0xffffu)] = 1;
+}
+
 __global__ __launch_bounds__(256) void MarkModelRows(const uint32_t* pos,
                                                      const float* m, uint64_t n_sel,
                                                      uint8_t* rows, uint32_t oy) {
@@ -1366,6 +1378,16 @@ int rdl_subminor_model_f64(rdl_subminor* h, uint32_t image_index,
   rdl::ScatterModel<double><<<grid, 256, 0, s->stream>>>(
       h->d_pos, h->d_m + size_t(image_index) * h->n_selected, h->n_selected,
       d_dest, dest_w, ox, oy, 0);
+  RDL_HIP_CHECK(hipGetLastError());
+  return RDL_OK;
+}
+
+int rdl_subminor_update_mask(rdl_subminor* h, uint8_t* d_mask) {
+  RDL_ARG_CHECK(h && d_mask, "NULL argument");
+  if (h->n_selected == 0) return RDL_OK;
+  const uint32_t grid = uint32_t((h->n_selected + 255) / 256);
+  rdl::UpdateMaskKernel<<<grid, 256, 0, h->s->stream>>>(h->d_pos, h->d_m, h->n_selected,
+                                                       h->n_images, h->width, d_mask);
   RDL_HIP_CHECK(hipGetLastError());
   return RDL_OK;
 }

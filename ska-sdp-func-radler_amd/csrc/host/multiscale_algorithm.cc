@@ -79,7 +79,31 @@ MultiScaleAlgorithm::MultiScaleAlgorithm(const MultiScaleAlgorithm& o)
       settings_(o.settings_),
       beam_size_in_pixels_(o.beam_size_in_pixels_),
       track_components_(o.track_components_),
-      scale_infos_(o.scale_infos_) {}
+      scale_infos_(o.scale_infos_),
+      track_masks_(o.track_masks_),
+      use_masks_(o.use_masks_),
+      host_masks_(o.host_masks_) {}
+
+void MultiScaleAlgorithm::UploadScaleMasks(gpu::Session& s, size_t n_pixels) {
+  if (!masks_dirty_ && masks_session_ == &s && dev_masks_.size() == host_masks_.size())
+    return;
+  dev_masks_.clear();
+  for (const std::vector<uint8_t>& m : host_masks_) {
+    gpu::Buffer& b = dev_masks_.emplace_back(s, n_pixels);
+    if (m.size() == n_pixels)
+      s.H2D(b.Ptr(), m.data(), n_pixels);
+    else
+      b.Zero();
+  }
+  masks_session_ = &s;
+  masks_dirty_ = false;
+}
+
+void MultiScaleAlgorithm::DownloadScaleMasks() {
+  if (!masks_session_) return;
+  for (size_t i = 0; i != host_masks_.size() && i != dev_masks_.size(); ++i)
+    masks_session_->D2H(host_masks_[i].data(), dev_masks_[i].Ptr(), host_masks_[i].size());
+}
 
 void MultiScaleAlgorithm::FindPeakDirect(const float* d_image,
                                          size_t scale_index) {  // :700-748
@@ -90,7 +114,7 @@ void MultiScaleAlgorithm::FindPeakDirect(const float* d_image,
   rdl_peak p;
   gpu::Check(rdl_find_peak(session_->Handle(), d_image, uint32_t(w), uint32_t(h),
                            0, uint32_t(h), hb, vb, AllowNegativeComponents(),
-                           d_mask_, 1, &p),
+                           MaskFor(scale_index), 1, &p),
              "rdl_find_peak");
   info.max_image_value_x = p.x;
   info.max_image_value_y = p.y;
@@ -148,7 +172,7 @@ void MultiScaleAlgorithm::FindActiveScaleConvolvedMaxima(
     rdl_peak p;
     gpu::Check(rdl_find_peak(s, d_conv, uint32_t(w), uint32_t(h), 0,
                              uint32_t(h), xb, yb, AllowNegativeComponents(),
-                             d_mask_, 1, &p),
+                             MaskFor(si), 1, &p),
                "rdl_find_peak");
     e.max_normalized_image_value = p.found ? p.value : 0.0f;
     e.max_unnormalized_image_value = p.found ? p.value : 0.0f;
@@ -181,6 +205,23 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
   if (StopOnNegativeComponents()) SetAllowNegativeComponents(true);
   InitializeScales(scale_infos_, beam_size_in_pixels_, std::min(width, height),
                    settings_.shape, settings_.max_scales, settings_.scale_list);
+  if (track_masks_) {  // :214-226
+    for (const std::vector<uint8_t>& m : host_masks_)
+      if (m.size() != npx)
+        throw std::runtime_error("Invalid automask size in multiscale algorithm");
+    while (host_masks_.size() < scale_infos_.size()) {
+      host_masks_.emplace_back(npx, 0);
+      masks_dirty_ = true;
+    }
+  }
+  if (track_masks_ || use_masks_) UploadScaleMasks(session, npx);
+  // the tracked masks go back to the host copies on every return
+  struct MaskSync {
+    MultiScaleAlgorithm* a;
+    ~MaskSync() {
+      if (a->track_masks_) a->DownloadScaleMasks();
+    }
+  } mask_sync{this};
   if (ComponentOptimizationAlgorithm() != OptimizationAlgorithm::kClean)
     throw std::runtime_error(
         "Component optimisation is not available in the MI355X build");
@@ -334,7 +375,7 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
                            scale_border),
           std::max<size_t>(size_t(std::round(height * CleanBorderRatio())),
                            scale_border));
-      sub.SetMask(d_mask_);
+      sub.SetMask(MaskFor(scale_with_peak));
       std::vector<uint32_t> xy;
       sub.SetTrace(&xy);
       const SubMinorLoop::RunResult r = sub.Run(individual, twice);
@@ -367,6 +408,8 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
                    .first;
         sub.CorrectResidualDirtyWithSpectrum(i, data_image.Data(i),
                                              pc->second->Ptr());
+        if (i == 0 && track_masks_ && scale_with_peak < dev_masks_.size())  // :444-445
+          sub.UpdateAutoMask(static_cast<uint8_t*>(dev_masks_[scale_with_peak].Ptr()));
         if (info.scale != 0.0f) {
           // the sub-minor model is a few hundred components: stamping the
           // shape kernel costs n_sel * n^2 multiply-adds against two
@@ -427,6 +470,12 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
                      "rdl_add_shape_component");
           info.n_components_cleaned++;
           info.total_flux_cleaned += cv[i];
+          if (track_masks_ && scale_with_peak < dev_masks_.size()) {  // :695-696
+            const uint8_t one = 1;
+            session.H2D(static_cast<uint8_t*>(dev_masks_[scale_with_peak].Ptr()) + x +
+                            width * y,
+                        &one, 1);
+          }
         }
         individual.GetLinearIntegrated(integrated.F());
         FindPeakDirect(integrated.F(), scale_with_peak);

@@ -55,11 +55,39 @@ class MultiScaleAlgorithm final : public DeconvolutionAlgorithm {
   /// x, y, scale index of every component of the last major iteration.
   const std::vector<uint32_t>& LastTrace() const { return trace_; }
 
+  /// Auto-masking (multiscale_algorithm.h:41-55): track = grow one mask per
+  /// scale from the components; use = clean each scale inside its mask only
+  /// (the clean mask is then ignored). Masks persist across major
+  /// iterations: canonical host copies (0/1 bytes, width x height), device
+  /// working copies uploaded when changed.
+  void SetAutoMaskMode(bool track_per_scale_masks, bool use_per_scale_masks) {
+    track_masks_ = track_per_scale_masks;
+    use_masks_ = use_per_scale_masks;
+  }
+  size_t GetScaleMaskCount() const { return host_masks_.size(); }
+  void SetScaleMaskCount(size_t n) {
+    host_masks_.resize(n);
+    masks_dirty_ = true;
+  }
+  /// Mutable access (ParallelDeconvolution fills subimage boxes).
+  std::vector<uint8_t>& GetScaleMask(size_t index) {
+    masks_dirty_ = true;
+    return host_masks_[index];
+  }
+
  private:
   void FindActiveScaleConvolvedMaxima(const ImageSet& image_set,
                                       float* d_integrated, bool report_rms);
   void FindPeakDirect(const float* d_image, size_t scale_index);
   void ActivateScales(size_t scale_with_last_peak);
+  void UploadScaleMasks(gpu::Session& s, size_t n_pixels);
+  void DownloadScaleMasks();
+  /// the mask the peak searches and the sub-minor loop of `scale` use
+  const uint8_t* MaskFor(size_t scale) const {
+    if (use_masks_ && scale < dev_masks_.size())
+      return static_cast<const uint8_t*>(dev_masks_[scale].Ptr());
+    return d_mask_;
+  }
 
   const Settings::Multiscale& settings_;
   double beam_size_in_pixels_;
@@ -81,6 +109,12 @@ class MultiScaleAlgorithm final : public DeconvolutionAlgorithm {
   // per scale and swapped in instead of convolving again.
   std::vector<gpu::Planes> scale_images_;
   std::vector<bool> scale_image_valid_;
+
+  bool track_masks_ = false, use_masks_ = false;
+  std::vector<std::vector<uint8_t>> host_masks_;
+  std::vector<gpu::Buffer> dev_masks_;
+  gpu::Session* masks_session_ = nullptr;
+  bool masks_dirty_ = true;
 };
 
 // multiscale_algorithm.cc:90-151 (free functions in the reference)

@@ -68,6 +68,60 @@ void ParallelDeconvolution::SetMinorLoopGain(double gain) {
   for (auto& a : algorithms_) a->SetMinorLoopGain(gain);
 }
 
+void ParallelDeconvolution::SetAutoMaskMode(bool track_per_scale_masks,
+                                            bool use_per_scale_masks) {
+  track_masks_ = track_per_scale_masks;
+  use_masks_ = use_per_scale_masks;
+  for (auto& a : algorithms_)
+    if (auto* ms = dynamic_cast<MultiScaleAlgorithm*>(a.get()))
+      ms->SetAutoMaskMode(track_per_scale_masks, use_per_scale_masks);
+}
+
+void ParallelDeconvolution::LoadScaleMasks(const SubImage& sub, size_t width) {
+  if (!use_masks_ && !track_masks_) return;
+  auto* ms = dynamic_cast<MultiScaleAlgorithm*>(algorithms_[sub.index].get());
+  if (!ms) return;
+  const std::lock_guard<std::mutex> lock(masks_mutex_);
+  if (scale_masks_.empty()) return;
+  ms->SetScaleMaskCount(std::max(ms->GetScaleMaskCount(), scale_masks_.size()));
+  for (size_t i = 0; i != ms->GetScaleMaskCount(); ++i) {
+    std::vector<uint8_t>& m = ms->GetScaleMask(i);
+    m.assign(sub.width * sub.height, 0);
+    if (i >= scale_masks_.size()) continue;
+    // scale mask box AND the subimage's clean mask (:376-386)
+    for (size_t y = 0; y != sub.height; ++y)
+      for (size_t x = 0; x != sub.width; ++x) {
+        const size_t p = y * sub.width + x;
+        m[p] = (scale_masks_[i][(sub.y + y) * width + sub.x + x] && sub.mask[p]) ? 1 : 0;
+      }
+  }
+}
+
+std::vector<std::vector<uint8_t>> ParallelDeconvolution::SubImageScaleMasks(
+    const SubImage& sub) {
+  std::vector<std::vector<uint8_t>> out;
+  auto* ms = dynamic_cast<MultiScaleAlgorithm*>(algorithms_[sub.index].get());
+  if (!ms) return out;
+  for (size_t i = 0; i != ms->ScaleCount() && i != ms->GetScaleMaskCount(); ++i)
+    out.push_back(ms->GetScaleMask(i));
+  return out;
+}
+
+void ParallelDeconvolution::StoreScaleMasks(
+    const SubImage& sub, size_t width, size_t height,
+    const std::vector<std::vector<uint8_t>>& sub_masks) {
+  const std::lock_guard<std::mutex> lock(masks_mutex_);
+  if (scale_masks_.empty())
+    scale_masks_.assign(sub_masks.size(), std::vector<uint8_t>(width * height, 0));
+  for (size_t i = 0; i != sub_masks.size() && i != scale_masks_.size(); ++i)
+    for (size_t y = 0; y != sub.height; ++y)
+      for (size_t x = 0; x != sub.width; ++x) {
+        const size_t p = y * sub.width + x;
+        if (sub.boundary_mask[p])
+          scale_masks_[i][(sub.y + y) * width + sub.x + x] = sub_masks[i][p];
+      }
+}
+
 void ParallelDeconvolution::SetCleanMask(const bool* mask) {
   if (algorithms_.size() == 1)
     algorithms_.front()->SetCleanMask(mask);
@@ -312,9 +366,12 @@ void ParallelDeconvolution::RunSubImage(SubImage& sub, ImageSet& data_image,
                sub_model.Base(), sub_psfs.Base(), d_boundary);
   ImageSet initial_model(sub_model, sw, sh);
   initial_model.CopyFrom(sub_model);
+  LoadScaleMasks(sub, data_image.Width());
   const bool converging = DeconvolveSubImage(
       sub, sub_data, sub_model, sub_psfs, major_iteration_threshold, find_peak_only);
   if (find_peak_only) return;
+  if (track_masks_ && converging)
+    StoreScaleMasks(sub, data_image.Width(), data_image.Height(), SubImageScaleMasks(sub));
   MergeSubImage(s, sub, data_image, result_model, sub_data.Base(),
                 converging ? sub_model.Base() : initial_model.Base(), d_boundary,
                 converging);
@@ -450,9 +507,14 @@ void ParallelDeconvolution::RunSubImagesConcurrently(
           slot.initial = std::make_unique<ImageSet>(*slot.model, sw, sh);
           slot.initial->CopyFrom(*slot.model);
         }
+        LoadScaleMasks(sub, data_image.Width());
         slot.converging = DeconvolveSubImage(sub, *slot.data, *slot.model,
                                              slot.psfs, major_iteration_threshold,
                                              find_peak_only);
+        // boundary masks are disjoint: merging in any order gives one result
+        if (track_masks_ && slot.converging && !find_peak_only)
+          StoreScaleMasks(sub, data_image.Width(), data_image.Height(),
+                          SubImageScaleMasks(sub));
         if (slot.remote && !find_peak_only) {
           float* base = slot.stage->F();
           const ImageSet& model_out = slot.converging ? *slot.model : *slot.initial;
@@ -523,11 +585,13 @@ double ParallelDeconvolution::RunSubImagesDistributed(
     uint64_t iteration_number;
     uint32_t reached_major_threshold;
     uint32_t converging;
-    uint32_t pad[10];
+    uint32_t n_mask_scales;  // tracked auto-masks that follow (second broadcast)
+    uint32_t pad[9];
   };
   static_assert(sizeof(Record) == 64, "record layout");
   constexpr size_t kHeaderFloats = sizeof(Record) / sizeof(float);
   std::vector<std::unique_ptr<gpu::Buffer>> packs(n_sub);
+  std::vector<std::vector<std::vector<uint8_t>>> mask_sets(n_sub);
   double local_peak = 0.0;
   for (size_t i = 0; i != n_sub; ++i) {
     if (SubImageOwner(i, n_ranks) != rank) continue;
@@ -547,6 +611,7 @@ double ParallelDeconvolution::RunSubImagesDistributed(
       initial = std::make_unique<ImageSet>(sub_model, sw, sh);
       initial->CopyFrom(sub_model);
     }
+    LoadScaleMasks(sub, data_image.Width());
     const bool converging = DeconvolveSubImage(sub, sub_data, sub_model, sub_psfs,
                                                major_iteration_threshold,
                                                find_peak_only);
@@ -561,6 +626,10 @@ double ParallelDeconvolution::RunSubImagesDistributed(
     rec.iteration_number = algorithms_[i]->IterationNumber();
     rec.reached_major_threshold = sub.reached_major_threshold ? 1u : 0u;
     rec.converging = converging ? 1u : 0u;
+    if (track_masks_ && converging) {
+      mask_sets[i] = SubImageScaleMasks(sub);
+      rec.n_mask_scales = uint32_t(mask_sets[i].size());
+    }
     s.H2D(pack->Ptr(), &rec, sizeof(rec));
     float* base = pack->F() + kHeaderFloats;
     s.D2D(base, sub_data.Base(), n_img * n * sizeof(float));
@@ -599,6 +668,18 @@ double ParallelDeconvolution::RunSubImagesDistributed(
     MergeSubImage(s, sub, data_image, result_model, base, base + n_img * n,
                   static_cast<const uint8_t*>(boundary.Ptr()), rec.converging != 0);
     s.Sync();  // the staging buffer is reused by the next broadcast
+    if (rec.n_mask_scales > 0) {  // the owner's tracked scale masks
+      const size_t mb = size_t(rec.n_mask_scales) * n;
+      gpu::Buffer dm(s, mb);
+      if (owner == rank)
+        for (size_t m = 0; m != rec.n_mask_scales; ++m)
+          s.H2D(static_cast<uint8_t*>(dm.Ptr()) + m * n, mask_sets[i][m].data(), n);
+      comm.Broadcast(s, dm.Ptr(), mb, owner);
+      std::vector<std::vector<uint8_t>> masks(rec.n_mask_scales, std::vector<uint8_t>(n));
+      for (size_t m = 0; m != rec.n_mask_scales; ++m)
+        s.D2H(masks[m].data(), static_cast<const uint8_t*>(dm.Ptr()) + m * n, n);
+      StoreScaleMasks(sub, data_image.Width(), data_image.Height(), masks);
+    }
   }
   return 0.0;
 }

@@ -6,6 +6,7 @@
 #pragma once
 
 #include <memory>
+#include <mutex>
 #include <optional>
 #include <vector>
 
@@ -45,6 +46,11 @@ class ParallelDeconvolution {
   void SetThreshold(double threshold);
   void SetMinorLoopGain(double gain);
   void SetCleanMask(const bool* mask);
+  /// Auto-masking (parallel_deconvolution.cc:260-268): passed to the
+  /// multiscale algorithms; gridded runs keep full-image per-scale masks and
+  /// hand each subimage its box (:359-390), merging it back inside the
+  /// boundary mask after a converging run (:425-462).
+  void SetAutoMaskMode(bool track_per_scale_masks, bool use_per_scale_masks);
   bool IsInitialized() const { return !algorithms_.empty(); }
   size_t SubImageCount() const { return algorithms_.size(); }
   DeconvolutionAlgorithm& Algorithm(size_t i) { return *algorithms_[i]; }
@@ -106,6 +112,13 @@ class ParallelDeconvolution {
                                  const std::vector<size_t>& psf_indices,
                                  double major_iteration_threshold, bool find_peak_only);
   void EnsureWorkers(gpu::Session& main, size_t n);
+  /// the subimage's box of the full-image scale masks into its algorithm
+  void LoadScaleMasks(const SubImage& sub, size_t width);
+  /// the algorithm's scale masks of `sub` (subimage-sized, one per scale)
+  std::vector<std::vector<uint8_t>> SubImageScaleMasks(const SubImage& sub);
+  /// merge subimage-sized scale masks into the full-image ones (boundary mask)
+  void StoreScaleMasks(const SubImage& sub, size_t width, size_t height,
+                       const std::vector<std::vector<uint8_t>>& sub_masks);
   static std::vector<int> PoolDevices(int main_device);
 
   // worker sessions (one stream each) outlive the algorithms, whose cached
@@ -117,6 +130,9 @@ class ParallelDeconvolution {
   const Settings& settings_;
   const bool* mask_ = nullptr;
   std::shared_ptr<Communicator> comm_;
+  bool track_masks_ = false, use_masks_ = false;
+  std::vector<std::vector<uint8_t>> scale_masks_;  // full image, per scale
+  std::mutex masks_mutex_;
 };
 
 /// Subimage geometry of the grid (parallel_deconvolution.cc:57-166).

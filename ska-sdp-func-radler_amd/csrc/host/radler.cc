@@ -116,13 +116,17 @@ void Radler::Perform(bool& another_iteration_required,
 
   const bool auto_mask_is_enabled =
       settings_.auto_mask_sigma || settings_.absolute_auto_mask_threshold;
-  if (auto_mask_is_enabled) Unsupported("Auto-masking");
   if (settings_.local_rms.method != LocalRmsMethod::kNone ||
       !settings_.local_rms.image.empty())
     Unsupported("Local-RMS thresholding");
-  parallel_deconvolution_->SetMinorLoopGain(settings_.minor_loop_gain);
+  // :167-183: once the auto-mask is complete a more aggressive gain is used
+  if (auto_mask_is_enabled && auto_mask_is_finished_)
+    parallel_deconvolution_->SetMinorLoopGain(
+        std::min(1.0, settings_.minor_loop_gain * 2.0));
+  else
+    parallel_deconvolution_->SetMinorLoopGain(settings_.minor_loop_gain);
 
-  if (settings_.auto_threshold_sigma) {
+  if (settings_.auto_threshold_sigma || auto_mask_is_enabled) {
     // integrated.MedianAndStdDevFromMAD() (:162-166) on the device
     gpu::Buffer integrated(s, image_width_ * image_height_ * sizeof(float));
     residual_set.GetLinearIntegrated(integrated.F());
@@ -135,10 +139,39 @@ void Radler::Perform(bool& another_iteration_required,
     const double stddev = double(mad) * 1.48260221850560;
     log::Info() << "Estimated standard deviation of background noise: "
                 << stddev << '\n';
+    // :228-243
     const double threshold_bias = settings_.squared_joins ? median : 0.0;
-    parallel_deconvolution_->SetThreshold(
-        std::max(stddev * (*settings_.auto_threshold_sigma) + threshold_bias,
-                 settings_.absolute_threshold));
+    if (auto_mask_is_enabled && !auto_mask_is_finished_) {
+      const double combined_auto_mask_threshold =
+          std::max(stddev * settings_.auto_mask_sigma.value_or(0.0) + threshold_bias,
+                   settings_.absolute_auto_mask_threshold.value_or(0.0));
+      parallel_deconvolution_->SetThreshold(
+          std::max(combined_auto_mask_threshold, settings_.absolute_threshold));
+    } else if (settings_.auto_threshold_sigma) {
+      parallel_deconvolution_->SetThreshold(
+          std::max(stddev * (*settings_.auto_threshold_sigma) + threshold_bias,
+                   settings_.absolute_threshold));
+    }
+  }
+
+  // :249-275: multiscale tracks per-scale masks until the auto-mask
+  // threshold is reached, then cleans inside them; the other algorithms get
+  // the scale-independent mask of the model's non-zero pixels
+  if (settings_.algorithm_type == AlgorithmType::kMultiscale) {
+    if (auto_mask_is_enabled)
+      parallel_deconvolution_->SetAutoMaskMode(!auto_mask_is_finished_,
+                                               auto_mask_is_finished_);
+  } else if (auto_mask_is_enabled && auto_mask_is_finished_) {
+    if (auto_mask_.empty()) {
+      auto_mask_.assign(image_width_ * image_height_, 0);
+      std::vector<float> plane(image_width_ * image_height_);
+      for (size_t i = 0; i != model_set.Size(); ++i) {
+        s.D2H(plane.data(), model_set.Data(i), plane.size() * sizeof(float));
+        for (size_t p = 0; p != plane.size(); ++p)
+          if (std::isfinite(plane[p]) && plane[p] != 0.0f) auto_mask_[p] = 1;
+      }
+    }
+    parallel_deconvolution_->SetCleanMask(reinterpret_cast<const bool*>(auto_mask_.data()));
   }
 
   const std::vector<gpu::Planes> psf_images = residual_set.LoadAndAveragePsfs();
@@ -148,11 +181,27 @@ void Radler::Perform(bool& another_iteration_required,
           settings_.major_loop_gain);
   another_iteration_required = result.another_iteration_required;
 
+  if (!another_iteration_required && auto_mask_is_enabled && !auto_mask_is_finished_) {
+    log::Info() << "Auto-masking threshold reached; continuing next major "
+                   "iteration with deeper threshold and mask.\n";
+    auto_mask_is_finished_ = true;
+    another_iteration_required = true;
+    auto_mask_finishing_iteration_ = major_iteration_number;
+  }
   if (another_iteration_required && settings_.major_iteration_count != 0 &&
       major_iteration_number >= settings_.major_iteration_count) {
     another_iteration_required = false;
     log::Info() << "Maximum number of major iterations was reached: not "
                    "continuing deconvolution.\n";
+  }
+  if (another_iteration_required && auto_mask_is_finished_ &&
+      major_iteration_number - auto_mask_finishing_iteration_ >=
+          settings_.major_auto_mask_iteration_count) {
+    another_iteration_required = false;
+    log::Info() << "Performed "
+                << major_iteration_number - auto_mask_finishing_iteration_
+                << " major iterations after reaching the auto-mask threshold: "
+                   "not continuing deconvolution.\n";
   }
   if (another_iteration_required && settings_.minor_iteration_count != 0 &&
       parallel_deconvolution_->FirstAlgorithm().IterationNumber() >=

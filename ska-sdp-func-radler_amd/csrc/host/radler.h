@@ -67,6 +67,10 @@ class Radler {
   double pixel_scale_x_ = 0.0;
   double pixel_scale_y_ = 0.0;
   double beam_size_ = 0.0;
+  // auto-masking state across major iterations (cpp/radler.h:111-114)
+  bool auto_mask_is_finished_ = false;
+  size_t auto_mask_finishing_iteration_ = 0;
+  std::vector<uint8_t> auto_mask_;  // scale-independent mask (non-multiscale)
 };
 
 }  // namespace radler

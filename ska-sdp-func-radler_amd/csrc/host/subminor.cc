@@ -157,6 +157,10 @@ void SubMinorLoop::AddShapeModel(size_t image_index, const float* d_kernel,
              "rdl_subminor_add_shape_model");
 }
 
+void SubMinorLoop::UpdateAutoMask(uint8_t* d_mask) {
+  gpu::Check(rdl_subminor_update_mask(h_, d_mask), "rdl_subminor_update_mask");
+}
+
 void SubMinorLoop::GetSelection(std::vector<uint32_t>& positions,
                                 std::vector<float>& models) const {
   positions.resize(n_selected_);

@@ -34,6 +34,8 @@ class SubMinorLoop {
     vertical_border_ = v;
   }
   void SetMask(const uint8_t* d_mask) { d_mask_ = d_mask; }
+  /// subminor_loop.cc:220-228 on the device (byte mask, W x H).
+  void UpdateAutoMask(uint8_t* d_mask);
   void SetDivergenceLimit(float v) { divergence_limit_ = v; }
   void SetTrace(std::vector<uint32_t>* trace) { trace_ = trace; }
 

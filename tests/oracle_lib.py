@@ -206,6 +206,24 @@ class OracleAlgorithm:
             raise RuntimeError(self.o.lib.orc_last_error().decode())
         return r, trace[: min(r.n_trace, trace_cap)].copy()
 
+    def set_automask(self, track, use):
+        """MultiScaleAlgorithm::SetAutoMaskMode (multiscale only)."""
+        L = self.o.lib
+        L.orc_algo_set_automask.argtypes = [C.c_void_p, C.c_int, C.c_int]
+        L.orc_algo_set_automask.restype = None
+        L.orc_algo_set_automask(self.h, int(track), int(use))
+
+    def scale_masks(self, w, h):
+        """The per-scale auto-masks as a (n_scales, h, w) uint8 array."""
+        L = self.o.lib
+        L.orc_algo_scale_mask.restype = C.c_uint64
+        L.orc_algo_scale_mask.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64]
+        n = L.orc_algo_scale_mask(self.h, 0, None, 0)
+        out = np.zeros((n, h, w), np.uint8)
+        for i in range(n):
+            L.orc_algo_scale_mask(self.h, i, out[i].ctypes.data, w * h)
+        return out
+
     def iuwt_steps(self, cap=4096):
         """Steps of the last IUWT (kind 2) execute (oracle/iuwt_algorithm.h IuwtStep)."""
         out = np.zeros(cap, IUWT_STEP)
@@ -299,6 +317,17 @@ class OracleParallel:
         """True: every subimage of a pass trims the residual as it was at the
         start of the pass (the product's concurrent pool, max_threads > 1)."""
         self.o.lib.orc_parallel_set_snapshot(self.h, 1 if snapshot else 0)
+
+    def set_automask(self, track, use):
+        L = self.o.lib
+        L.orc_parallel_set_automask.argtypes = [C.c_void_p, C.c_int, C.c_int]
+        L.orc_parallel_set_automask(self.h, int(track), int(use))
+
+    def update(self, **settings):
+        self.settings = algo_settings(**settings)
+        L = self.o.lib
+        L.orc_parallel_update.argtypes = [C.c_void_p, C.POINTER(AlgoSettings)]
+        L.orc_parallel_update(self.h, C.byref(self.settings))
 
     def execute(self, residual, model, psfs, major_loop_gain, user_mask=None,
                 trace_cap=1 << 22):
