@@ -199,6 +199,18 @@ int rdl_bbox_rows(rdl_session* s, const float* d_image, uint32_t width, uint32_t
 /* float <-> double planes (to_f64: float src -> double dst). */
 int rdl_convert(rdl_session* s, const void* d_src, void* d_dst, size_t n, int to_f64);
 
+/* ------------------------------------------------ spectral interpolation */
+/* ImageSet::InterpolateAndStoreModel (cpp/image_set.cc:209-288) for a
+ * polynomial SpectralFitter: out plane g (g < n_out, contiguous, n floats
+ * apart) = sum_c h_coefficients[g * n_in + c] * in plane c, where in plane c
+ * starts at d_in + c * in_stride floats. The coefficients are the fit over
+ * the n_in deconvolution channels evaluated at original channel g's
+ * frequency (a fixed linear map; zero pixels stay zero). n_in, n_out <=
+ * RDL_MAX_IMAGES. */
+int rdl_spectral_interpolate(rdl_session* s, const float* d_in, size_t in_stride,
+                             uint32_t n_in, const float* h_coefficients,
+                             uint32_t n_out, float* d_out, size_t n);
+
 /* ---------------------------------------------------------------- Högbom */
 typedef struct {
   uint32_t width, height;
@@ -217,6 +229,11 @@ typedef struct {
   uint32_t start_x, start_y;
   float start_value;
   int32_t start_found;
+  /* DeconvolutionAlgorithm::PerformSpectralFit (deconvolution_algorithm.cc:
+   * 29-46) as a linear map: n_images x n_images row-major float matrix,
+   * applied to the gathered peak values before the gain (generic_clean.cc:
+   * 186); NULL = no fitting. See rdl_spectral_* below. */
+  const float* d_spectral;
 } rdl_hogbom_params;
 
 typedef struct {
@@ -249,6 +266,10 @@ typedef struct {
   float divergence_limit;
   uint64_t iteration_start, max_iterations;
   const uint8_t* d_mask;   /* may be NULL */
+  /* PerformSpectralFit of each component's gain-scaled values
+   * (subminor_loop.cc:64-76) as an n_images x n_images row-major linear map;
+   * NULL = no fitting */
+  const float* d_spectral;
 } rdl_subminor_params;
 
 typedef struct {

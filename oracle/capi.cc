@@ -22,6 +22,11 @@ struct orc_set_desc {
   const float* weights;
   float pol_factor;
   int32_t squared_joins;
+  // spectral fitting (fit_mode 0 = none, 1 = polynomial over n_channels)
+  int32_t fit_mode;
+  uint32_t fit_terms;
+  const double* fit_frequencies;
+  const float* fit_weights;
 };
 
 struct orc_algo_settings {
@@ -124,6 +129,11 @@ static SetDesc MakeDesc(const orc_set_desc* d) {
   desc.weights.assign(d->weights, d->weights + d->n_channels);
   desc.pol_factor = d->pol_factor;
   desc.squared_joins = d->squared_joins != 0;
+  if (d->fit_mode != 0)
+    desc.fitter = std::make_shared<SpectralFit>(
+        d->fit_mode, d->fit_terms,
+        std::vector<double>(d->fit_frequencies, d->fit_frequencies + d->n_channels),
+        std::vector<float>(d->fit_weights, d->fit_weights + d->n_channels));
   return desc;
 }
 
@@ -451,6 +461,59 @@ int orc_parallel_execute(void* h, const orc_set_desc* d, float* residual,
     g_error = e.what();
     return 1;
   }
+}
+
+}  // extern "C"
+
+extern "C" {
+
+// SpectralFitter::FitAndEvaluate on one spectrum (n channels), and the fit's
+// terms (n_terms floats) when terms != nullptr.
+void orc_spectral_fit(int mode, uint32_t n_terms, const double* frequencies,
+                      const float* weights, uint64_t n, float* values, float* terms) {
+  const SpectralFit fit(mode, n_terms, std::vector<double>(frequencies, frequencies + n),
+                        std::vector<float>(weights, weights + n));
+  if (terms) {
+    std::vector<float> t;
+    fit.Fit(t, values);
+    std::copy(t.begin(), t.end(), terms);
+  }
+  fit.FitAndEvaluate(values);
+}
+
+// ImageSet::InterpolateAndStoreModel (cpp/image_set.cc:209-288) for one
+// polarization: in = n_channels deconvolution planes, out = n_out planes at
+// out_frequencies. Zero pixels are not fitted (their terms are zero).
+void orc_spectral_interpolate(int mode, uint32_t n_terms, const double* frequencies,
+                              const float* weights, uint64_t n_channels,
+                              const float* in, uint64_t n_pixels,
+                              const double* out_frequencies, uint64_t n_out,
+                              float* out) {
+  const SpectralFit fit(mode, n_terms,
+                        std::vector<double>(frequencies, frequencies + n_channels),
+                        std::vector<float>(weights, weights + n_channels));
+  std::vector<float> pixel(n_channels), terms;
+  std::vector<float> terms_image(n_pixels * n_terms);
+  for (uint64_t px = 0; px != n_pixels; ++px) {
+    bool is_zero = true;
+    for (uint64_t c = 0; c != n_channels; ++c) {
+      pixel[c] = in[c * n_pixels + px];
+      is_zero = is_zero && pixel[c] == 0.0f;
+    }
+    float* t = &terms_image[px * n_terms];
+    if (is_zero) {
+      std::fill_n(t, n_terms, 0.0f);
+    } else {
+      fit.Fit(terms, pixel.data());
+      std::copy_n(terms.begin(), n_terms, t);
+    }
+  }
+  for (uint64_t g = 0; g != n_out; ++g)
+    for (uint64_t px = 0; px != n_pixels; ++px) {
+      const std::vector<float> t(&terms_image[px * n_terms],
+                                 &terms_image[px * n_terms] + n_terms);
+      out[g * n_pixels + px] = fit.Evaluate(t, out_frequencies[g]);
+    }
 }
 
 }  // extern "C"

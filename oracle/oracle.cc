@@ -541,7 +541,8 @@ SubMinorLoop::RunResult SubMinorLoop::Run(
     const size_t x = positions_[max_component].first;
     const size_t y = positions_[max_component].second;
     if (trace) trace->push_back({uint32_t(x), uint32_t(y), trace_scale});
-    // PerformSpectralFit: identity for kNoFitting.
+    PerformSpectralFit(convolved_residual.desc->fitter.get(),
+                       convolved_residual.desc->n_pol, component_values.data());
     for (size_t i = 0; i != n_img; ++i)
       model_[i][max_component] += component_values[i];
     for (size_t i = 0; i != n_img; ++i) {
@@ -685,6 +686,8 @@ Result GenericCleanExecute(const AlgoSettings& s_in, size_t& iteration_number,
                           uint32_t(peak_index / width), 0});
       for (size_t i = 0; i != dirty.Size(); ++i)
         peak_values[i] = dirty.images[i][peak_index];
+      PerformSpectralFit(dirty.desc->fitter.get(), dirty.desc->n_pol,
+                         peak_values.data());  // generic_clean.cc:186
       const size_t cx = peak_index % width, cy = peak_index / width;
       for (size_t i = 0; i != dirty.Size(); ++i) {
         peak_values[i] *= s.minor_loop_gain;
@@ -1029,6 +1032,8 @@ Result MultiScale::Execute(ImageSet& data, ImageSet& model,
           cv[i] = individual[i][mi.max_image_value_x + mi.max_image_value_y * width];
         const size_t x = mi.max_image_value_x, y = mi.max_image_value_y;
         if (trace) trace->push_back({uint32_t(x), uint32_t(y), uint32_t(scale_with_peak)});
+        PerformSpectralFit(data.desc->fitter.get(), data.desc->n_pol,
+                           cv.data());  // multiscale_algorithm.cc:477
         for (size_t i = 0; i != data.Size(); ++i) {
           cv[i] = cv[i] * mi.gain;
           const float* psf = convolved_psfs[data.PsfIndex(i)][scale_with_peak].data();

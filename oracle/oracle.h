@@ -14,7 +14,10 @@
 #include <cstdint>
 #include <limits>
 #include <map>
+#include <memory>
 #include <vector>
+
+#include "spectral.h"
 
 namespace oracle {
 
@@ -81,6 +84,9 @@ struct SetDesc {
   std::vector<float> weights;  // per deconvolution channel
   float pol_factor = 1.0f;
   bool squared_joins = false;
+  // the algorithms' SpectralFitter (deconvolution_algorithm.h:148-161);
+  // nullptr = kNoFitting
+  std::shared_ptr<const SpectralFit> fitter;
 };
 
 struct ImageSet {

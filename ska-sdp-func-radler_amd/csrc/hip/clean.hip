@@ -71,6 +71,7 @@ struct HogbomArgs {
   float* models;
   const float* psfs;
   const uint8_t* mask;
+  const float* spectral;  // n_images x n_images spectral-fit map, or nullptr
   HogbomState* state;
   uint64_t* partials;
   uint32_t* trace;
@@ -162,7 +163,14 @@ __device__ void HogbomPrepare(const HogbomArgs& a, HogbomState& st) {
   const uint32_t n = a.width * a.height;
   const uint32_t idx = st.peak_index;
   for (uint32_t i = 0; i < a.n_images; ++i) {
-    const float v = a.residuals[size_t(i) * n + idx] * a.gain;
+    float v = a.residuals[size_t(i) * n + idx];
+    if (a.spectral) {  // PerformSpectralFit before the gain (:186-189)
+      v = 0.0f;
+      for (uint32_t q = 0; q < a.n_images; ++q)
+        v = __builtin_fmaf(a.spectral[i * a.n_images + q],
+                           a.residuals[size_t(q) * n + idx], v);
+    }
+    v *= a.gain;
     st.factors[i] = v;
     a.models[size_t(i) * n + idx] += v;
   }
@@ -238,6 +246,7 @@ int rdl_hogbom_run(rdl_session* s, float* d_residuals, float* d_models,
   a.models = d_models;
   a.psfs = d_psfs;
   a.mask = p->d_mask;
+  a.spectral = p->d_spectral;
   a.width = p->width;
   a.height = p->height;
   a.n_images = p->n_images;

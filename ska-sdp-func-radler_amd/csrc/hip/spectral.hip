@@ -1,0 +1,70 @@
+// Spectral interpolation of the model:
+// ImageSet::InterpolateAndStoreModel (cpp/image_set.cc:209-288) with a
+// polynomial fitter. Per pixel the reference fits terms over the
+// deconvolution channels and evaluates them at every original channel's
+// frequency; with fixed frequencies and weights that is one n_out x n_in
+// linear map, so this is a single HBM pass: read the n_in channel values of
+// a pixel once, write its n_out interpolated values. Bound: HBM,
+// 4 * (n_in + n_out) bytes per pixel.
+#include "rdl_internal.h"
+
+namespace rdl {
+
+template <int NI>
+__global__ __launch_bounds__(256) void InterpolateKernel(
+    const float* in, size_t in_stride, uint32_t n_in, const float* coef,
+    uint32_t n_out, float* out, size_t n) {
+  __shared__ float c[RDL_MAX_IMAGES * NI];
+  for (uint32_t i = threadIdx.x; i < n_out * n_in; i += blockDim.x) {
+    const uint32_t g = i / n_in, k = i % n_in;
+    c[g * NI + k] = coef[i];
+  }
+  __syncthreads();
+  for (size_t px = blockIdx.x * size_t(blockDim.x) + threadIdx.x; px < n;
+       px += size_t(gridDim.x) * blockDim.x) {
+    float v[NI];
+#pragma unroll
+    for (int k = 0; k < NI; ++k)
+      v[k] = k < int(n_in) ? in[size_t(k) * in_stride + px] : 0.0f;
+    for (uint32_t g = 0; g < n_out; ++g) {
+      float acc = 0.0f;
+#pragma unroll
+      for (int k = 0; k < NI; ++k)
+        if (k < int(n_in)) acc = __builtin_fmaf(c[g * NI + k], v[k], acc);
+      out[size_t(g) * n + px] = acc;
+    }
+  }
+}
+
+}  // namespace rdl
+
+extern "C" int rdl_spectral_interpolate(rdl_session* s, const float* d_in,
+                                        size_t in_stride, uint32_t n_in,
+                                        const float* h_coefficients,
+                                        uint32_t n_out, float* d_out, size_t n) {
+  RDL_ARG_CHECK(s && d_in && h_coefficients && d_out, "NULL argument");
+  RDL_ARG_CHECK(n_in >= 1 && n_in <= RDL_MAX_IMAGES && n_out >= 1 &&
+                    n_out <= RDL_MAX_IMAGES,
+                "channel count out of range");
+  RDL_ARG_CHECK(n_in == 1 || in_stride >= n, "input planes overlap");
+  if (n == 0) return RDL_OK;
+  const size_t cbytes = size_t(n_out) * n_in * sizeof(float);
+  RDL_TRY(s->EnsureScratch(s->kernel, cbytes));
+  float* d_c = static_cast<float*>(s->kernel.ptr);
+  RDL_HIP_CHECK(hipMemcpyAsync(d_c, h_coefficients, cbytes,
+                               hipMemcpyHostToDevice, s->stream));
+  const unsigned grid = unsigned(std::min<size_t>((n + 255) / 256, 2048));
+  rdl::ScopedTiming t(s, "spectral_interpolate",
+                      double(n) * 4.0 * double(n_in + n_out));
+  if (n_in <= 4)
+    rdl::InterpolateKernel<4><<<grid, 256, 0, s->stream>>>(d_in, in_stride, n_in, d_c,
+                                                           n_out, d_out, n);
+  else if (n_in <= 16)
+    rdl::InterpolateKernel<16><<<grid, 256, 0, s->stream>>>(d_in, in_stride, n_in, d_c,
+                                                            n_out, d_out, n);
+  else
+    rdl::InterpolateKernel<RDL_MAX_IMAGES><<<grid, 256, 0, s->stream>>>(
+        d_in, in_stride, n_in, d_c, n_out, d_out, n);
+  RDL_HIP_CHECK(hipGetLastError());
+  return RDL_OK;
+}

@@ -156,6 +156,7 @@ struct LoopArgs {
   float* r;               // [n_img][n_sel] (in: gathered residuals)
   float* m;               // [n_img][n_sel] (out: model values)
   const float* psfs;      // twice-convolved PSFs, W*H planes
+  const float* spectral;  // n_img x n_img spectral-fit map, or nullptr
   uint32_t* records;      // [2][G][rec_words] (G > 1)
   uint32_t* counter;      // arrival counter (G > 1), zeroed per launch
   uint32_t* result;       // LoopResult
@@ -412,9 +413,22 @@ __global__ __launch_bounds__(kLoopThreads) void SubminorLoop(LoopArgs a) {
                     (!a.stop_on_negative || m >= 0.0f) && !diverging;
     if (!go) break;
     // next component (subminor_loop.cc:64-89)
+    if (a.spectral) {
+      // PerformSpectralFit of the gain-scaled values (subminor_loop.cc:66-76)
 #pragma unroll
-    for (int k = 0; k < NI; ++k)
-      c[k] = k < int(n_img) ? __uint_as_float(win[4 + k]) * a.gain : 0.0f;
+      for (int k = 0; k < NI; ++k) {
+        float acc = 0.0f;
+        if (k < int(n_img))
+          for (uint32_t q = 0; q < n_img; ++q)
+            acc = __builtin_fmaf(a.spectral[k * n_img + q],
+                                 __uint_as_float(win[4 + q]) * a.gain, acc);
+        c[k] = acc;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < NI; ++k)
+        c[k] = k < int(n_img) ? __uint_as_float(win[4 + k]) * a.gain : 0.0f;
+    }
     flux += m * a.gain;
     cx = int(win[3] & 0xffffu);
     cy = int(win[3] >> 16);
@@ -918,8 +932,21 @@ __global__ __launch_bounds__(kRegThreads) void SubminorLoopReg(LoopArgs a) {
     const bool go = fabsf(m) > a.threshold && iteration < a.max_iterations &&
                     (!a.stop_on_negative || m >= 0.0f) && !diverging;
     if (!go) break;
+    if (a.spectral) {
+      // PerformSpectralFit of the gain-scaled values (subminor_loop.cc:66-76)
 #pragma unroll
-    for (int k = 0; k < NI; ++k) c[k] = k < n_img ? wr[k] * a.gain : 0.0f;
+      for (int k = 0; k < NI; ++k) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int q = 0; q < NI; ++q)
+          if (k < n_img && q < n_img)
+            acc = __builtin_fmaf(a.spectral[k * n_img + q], wr[q] * a.gain, acc);
+        c[k] = acc;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < NI; ++k) c[k] = k < n_img ? wr[k] * a.gain : 0.0f;
+    }
     flux += m * a.gain;
     cx = int(wpos & 0xffffu);
     cy = int(wpos >> 16);
@@ -1191,6 +1218,7 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   la.integ = p->integ;
   la.threshold = p->threshold;
   la.gain = p->gain;
+  la.spectral = p->d_spectral;
   la.divergence_limit = p->divergence_limit;
   la.iteration_start = p->iteration_start;
   la.max_iterations = p->max_iterations;

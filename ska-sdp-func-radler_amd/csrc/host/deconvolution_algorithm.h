@@ -12,6 +12,7 @@
 #include "device.h"
 #include "image_set.h"
 #include "settings.h"
+#include "spectral_fitter.h"
 
 namespace radler::algorithms {
 
@@ -74,14 +75,38 @@ class DeconvolutionAlgorithm {
   size_t IterationNumber() const { return iteration_number_; }
   void SetIterationNumber(size_t n) { iteration_number_ = n; }
 
+  // deconvolution_algorithm.h:148-161
+  void SetSpectralFitter(
+      std::unique_ptr<schaapcommon::fitters::SpectralFitter> fitter,
+      size_t n_polarizations) {
+    spectral_fitter_ = std::move(fitter);
+    n_polarizations_ = n_polarizations;
+    spectral_map_.reset();
+  }
+  const schaapcommon::fitters::SpectralFitter& Fitter() const {
+    return *spectral_fitter_;
+  }
+  bool HasSpectralFitter() const { return spectral_fitter_ != nullptr; }
+
  protected:
   DeconvolutionAlgorithm() = default;
-  // Clones share settings and iteration count, not device scratch.
+  // Clones share settings, fitter and iteration count, not device scratch.
   DeconvolutionAlgorithm(const DeconvolutionAlgorithm& o)
-      : settings_(o.settings_), iteration_number_(o.iteration_number_) {}
+      : settings_(o.settings_),
+        iteration_number_(o.iteration_number_),
+        spectral_fitter_(o.spectral_fitter_),
+        n_polarizations_(o.n_polarizations_) {}
 
   /// Device copy (uint8) of CleanMask() for the current call, or nullptr.
   const uint8_t* DeviceCleanMask(gpu::Session& s, size_t width, size_t height);
+
+  /// PerformSpectralFit (deconvolution_algorithm.cc:29-46) on the host, for
+  /// the loops that gather a component's values on the host.
+  void PerformSpectralFit(float* values, size_t x, size_t y) const;
+  /// The same fit as an n_images x n_images device matrix for the device
+  /// loops (rdl_subminor_params / rdl_hogbom_params d_spectral); nullptr
+  /// when the fit leaves values unchanged.
+  const float* DeviceSpectralMap(gpu::Session& s, size_t n_images);
 
  private:
   struct {
@@ -100,6 +125,11 @@ class DeconvolutionAlgorithm {
   } settings_;
   size_t iteration_number_ = 0;
   std::shared_ptr<gpu::Buffer> mask_buffer_;
+  std::shared_ptr<const schaapcommon::fitters::SpectralFitter> spectral_fitter_;
+  size_t n_polarizations_ = 1;
+  std::shared_ptr<gpu::Buffer> spectral_map_;
+  size_t spectral_map_images_ = 0;
+  bool spectral_map_identity_ = false;
 };
 
 }  // namespace radler::algorithms

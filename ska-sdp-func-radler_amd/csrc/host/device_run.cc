@@ -80,6 +80,23 @@ DeviceRun::DeviceRun(const Settings& settings, const float* psf,
   algorithm->SetDivergenceLimit(settings.divergence_limit);
   algorithm->SetAllowNegativeComponents(settings.allow_negative_components);
   algorithm->SetStopOnNegativeComponents(settings.stop_on_negative_components);
+  {  // Radler::CreateSpectralFitter (radler.cc:318-331); channel c sits at
+     // 100 MHz + c x 10 MHz
+    using schaapcommon::fitters::SpectralFittingMode;
+    const SpectralFittingMode mode = settings.spectral_fitting.mode;
+    if (mode == SpectralFittingMode::kLogPolynomial ||
+        mode == SpectralFittingMode::kForcedTerms)
+      throw std::runtime_error("DeviceRun: only polynomial spectral fitting is available");
+    std::vector<double> frequencies;
+    std::vector<float> channel_weights;
+    if (mode != SpectralFittingMode::kNoFitting)
+      ImageSet::CalculateDeconvolutionFrequencies(*table_, frequencies, channel_weights);
+    algorithm->SetSpectralFitter(
+        std::make_unique<schaapcommon::fitters::SpectralFitter>(
+            mode, settings.spectral_fitting.terms, std::move(frequencies),
+            std::move(channel_weights)),
+        1);
+  }
   parallel_ = std::make_unique<algorithms::ParallelDeconvolution>(settings_);
   parallel_->SetAlgorithm(std::move(algorithm));
   Restore();

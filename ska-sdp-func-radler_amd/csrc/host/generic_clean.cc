@@ -74,6 +74,7 @@ DeconvolutionResult GenericClean::ExecuteMajorIteration(
     sub.SetStopOnNegativeComponent(StopOnNegativeComponents());
     sub.SetDivergenceLimit(DivergenceLimit());
     sub.SetMask(d_mask);
+    sub.SetSpectralMap(DeviceSpectralMap(s, dirty_set.Size()));
     sub.SetCleanBorders(size_t(std::round(width * CleanBorderRatio())),
                         size_t(std::round(height * CleanBorderRatio())));
     sub.SetTrace(&trace_);
@@ -114,6 +115,7 @@ DeconvolutionResult GenericClean::ExecuteMajorIteration(
     p.h_border = uint32_t(std::round(width * CleanBorderRatio()));
     p.v_border = uint32_t(std::round(height * CleanBorderRatio()));
     p.d_mask = d_mask;
+    p.d_spectral = DeviceSpectralMap(s, dirty_set.Size());
     p.start_x = max_value.x;
     p.start_y = max_value.y;
     p.start_value = max_value.value;

@@ -282,13 +282,9 @@ void ImageSet::AssignAndStoreResidual() {  // image_set.cc:290-307
   }
 }
 
-void ImageSet::InterpolateAndStoreModel() {
-  // image_set.cc:209-288. With kNoFitting and one deconvolution channel per
-  // original channel the model images are stored as they are. Fewer
-  // deconvolution channels than original channels need schaapcommon's
-  // SpectralFitter (absent from /root/reference); each original channel then
-  // receives the model of the deconvolution channel it was averaged into
-  // (parity unpinned).
+void ImageSet::InterpolateAndStoreModel(
+    const schaapcommon::fitters::SpectralFitter* fitter) {
+  // image_set.cc:209-288
   std::vector<float> host(PlaneSize());
   if (NDeconvolutionChannels() == NOriginalChannels()) {
     size_t image_index = 0;
@@ -299,12 +295,46 @@ void ImageSet::InterpolateAndStoreModel() {
     }
     return;
   }
-  for (size_t g = 0; g != NOriginalChannels(); ++g) {
-    const size_t ch = (g * NDeconvolutionChannels()) / NOriginalChannels();
-    const WorkTable::Group& group = table_.OriginalGroups()[g];
-    for (size_t p = 0; p != group.size(); ++p) {
-      session_->D2H(host.data(), Data(ch * n_pol_ + p), PlaneSize() * sizeof(float));
-      group[p]->model_accessor->Store(host.data());
+  const SpectralMaps maps = fitter ? MakeSpectralMaps(*fitter) : SpectralMaps{};
+  if (maps.Empty()) {
+    // kNoFitting (schaapcommon's fitter would evaluate nothing here; parity
+    // unpinned): the deconvolution channel's model as it is
+    for (size_t g = 0; g != NOriginalChannels(); ++g) {
+      const size_t ch = (g * NDeconvolutionChannels()) / NOriginalChannels();
+      const WorkTable::Group& group = table_.OriginalGroups()[g];
+      for (size_t p = 0; p != group.size(); ++p) {
+        session_->D2H(host.data(), Data(ch * n_pol_ + p), PlaneSize() * sizeof(float));
+        group[p]->model_accessor->Store(host.data());
+      }
+    }
+    return;
+  }
+  if (maps.n_channels != NDeconvolutionChannels())
+    throw std::runtime_error(
+        "InterpolateAndStoreModel: the fitter's channels do not match the image set");
+  const size_t n_orig = NOriginalChannels();
+  const size_t chunk = std::min<size_t>(n_orig, RDL_MAX_IMAGES);
+  gpu::Buffer out(*session_, chunk * PlaneSize() * sizeof(float));
+  for (size_t p = 0; p != n_pol_; ++p) {
+    for (size_t g0 = 0; g0 < n_orig; g0 += chunk) {
+      const size_t n_out = std::min(chunk, n_orig - g0);
+      std::vector<float> coef;
+      coef.reserve(n_out * maps.n_channels);
+      for (size_t g = g0; g != g0 + n_out; ++g) {
+        const std::vector<double> row =
+            maps.EvaluateAt(table_.OriginalGroups()[g][p]->CentralFrequency());
+        for (double c : row) coef.push_back(float(c));
+      }
+      gpu::Check(rdl_spectral_interpolate(session_->Handle(), Data(p),
+                                          n_pol_ * PlaneSize(),
+                                          uint32_t(maps.n_channels), coef.data(),
+                                          uint32_t(n_out), out.F(), PlaneSize()),
+                 "rdl_spectral_interpolate");
+      for (size_t g = g0; g != g0 + n_out; ++g) {
+        session_->D2H(host.data(), out.F() + (g - g0) * PlaneSize(),
+                      PlaneSize() * sizeof(float));
+        table_.OriginalGroups()[g][p]->model_accessor->Store(host.data());
+      }
     }
   }
 }

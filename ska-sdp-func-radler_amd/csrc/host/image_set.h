@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "device.h"
+#include "spectral_fitter.h"
 #include "rdl_hip.h"
 #include "work_table.h"
 
@@ -36,8 +37,13 @@ class ImageSet {
   std::vector<gpu::Planes> LoadAndAveragePsfs() const;
   /// image_set.cc:290-307
   void AssignAndStoreResidual();
-  /// image_set.cc:209-288 for SpectralFittingMode::kNoFitting.
-  void InterpolateAndStoreModel();
+  /// image_set.cc:209-288. With a polynomial fitter and fewer deconvolution
+  /// than original channels, every original channel receives the fit over
+  /// the deconvolution channels evaluated at its central frequency
+  /// (rdl_spectral_interpolate); without one (kNoFitting), the model of the
+  /// deconvolution channel it was averaged into.
+  void InterpolateAndStoreModel(
+      const schaapcommon::fitters::SpectralFitter* fitter = nullptr);
 
   void GetLinearIntegrated(float* d_dest) const;
   void GetSquareIntegrated(float* d_dest) const;

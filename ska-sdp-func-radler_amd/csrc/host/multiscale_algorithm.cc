@@ -376,6 +376,7 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
           std::max<size_t>(size_t(std::round(height * CleanBorderRatio())),
                            scale_border));
       sub.SetMask(MaskFor(scale_with_peak));
+      sub.SetSpectralMap(DeviceSpectralMap(session, data_image.Size()));
       std::vector<uint32_t> xy;
       sub.SetTrace(&xy);
       const SubMinorLoop::RunResult r = sub.Run(individual, twice);
@@ -446,6 +447,7 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
         const size_t x = info.max_image_value_x, y = info.max_image_value_y;
         for (size_t i = 0; i != data_image.Size(); ++i)
           cv[i] = session.ReadFloat(individual.Data(i) + x + y * width);
+        PerformSpectralFit(cv.data(), x, y);  // :477
         trace_.push_back(uint32_t(x));
         trace_.push_back(uint32_t(y));
         trace_.push_back(uint32_t(scale_with_peak));

@@ -211,7 +211,23 @@ void Radler::Perform(bool& another_iteration_required,
                    "reached: not continuing deconvolution.\n";
   }
   residual_set.AssignAndStoreResidual();
-  model_set.InterpolateAndStoreModel();
+  const algorithms::DeconvolutionAlgorithm& first =
+      parallel_deconvolution_->FirstAlgorithm();
+  model_set.InterpolateAndStoreModel(first.HasSpectralFitter() ? &first.Fitter()
+                                                               : nullptr);
+}
+
+std::unique_ptr<schaapcommon::fitters::SpectralFitter>
+Radler::CreateSpectralFitter() const {  // :318-331
+  std::vector<double> channel_frequencies;
+  std::vector<float> channel_weights;
+  if (settings_.spectral_fitting.mode !=
+      schaapcommon::fitters::SpectralFittingMode::kNoFitting)
+    ImageSet::CalculateDeconvolutionFrequencies(*table_, channel_frequencies,
+                                                channel_weights);
+  return std::make_unique<schaapcommon::fitters::SpectralFitter>(
+      settings_.spectral_fitting.mode, settings_.spectral_fitting.terms,
+      std::move(channel_frequencies), std::move(channel_weights));
 }
 
 void Radler::InitializeDeconvolutionAlgorithm(
@@ -223,9 +239,12 @@ void Radler::InitializeDeconvolutionAlgorithm(
     log::Warn() << "No proper beam size available in deconvolution!\n";
     beam_size_ = 0.0;
   }
-  if (settings_.spectral_fitting.mode !=
-      schaapcommon::fitters::SpectralFittingMode::kNoFitting)
-    Unsupported("Spectral fitting");
+  if (settings_.spectral_fitting.mode ==
+      schaapcommon::fitters::SpectralFittingMode::kLogPolynomial)
+    Unsupported("Logarithmic polynomial spectral fitting");
+  if (settings_.spectral_fitting.mode ==
+      schaapcommon::fitters::SpectralFittingMode::kForcedTerms)
+    Unsupported("Forced-term spectral fitting (a FITS spectral-term cube)");
   if (!settings_.fits_mask.empty() || !settings_.casa_mask.empty() ||
       settings_.horizon_mask_distance)
     Unsupported("Mask files / horizon masks");
@@ -259,6 +278,8 @@ void Radler::InitializeDeconvolutionAlgorithm(
   algorithm->SetDivergenceLimit(settings_.divergence_limit);
   algorithm->SetAllowNegativeComponents(settings_.allow_negative_components);
   algorithm->SetStopOnNegativeComponents(settings_.stop_on_negative_components);
+  algorithm->SetSpectralFitter(CreateSpectralFitter(),
+                               table_->OriginalGroups().front().size());
   parallel_deconvolution_->SetAlgorithm(std::move(algorithm));
 }
 

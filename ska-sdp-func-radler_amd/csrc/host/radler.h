@@ -10,6 +10,7 @@
 #include "aocommon_compat.h"
 #include "component_list.h"
 #include "settings.h"
+#include "spectral_fitter.h"
 #include "work_table.h"
 #include "work_table_entry.h"
 
@@ -40,6 +41,8 @@ class Radler {
   const algorithms::DeconvolutionAlgorithm& MaxScaleCountAlgorithm() const;
   void Perform(bool& another_iteration_required, size_t major_iteration_number);
   void FreeDeconvolutionAlgorithms();
+  std::unique_ptr<schaapcommon::fitters::SpectralFitter> CreateSpectralFitter()
+      const;
   bool IsInitialized() const;
   size_t IterationNumber() const;
 

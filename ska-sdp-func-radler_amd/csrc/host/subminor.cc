@@ -34,6 +34,7 @@ SubMinorLoop::RunResult SubMinorLoop::Run(ImageSet& residual,
   p.iteration_start = current_iteration_;
   p.max_iterations = max_iterations_;
   p.d_mask = d_mask_;
+  p.d_spectral = d_spectral_;
   n_images_ = residual.Size();
   uint64_t cap = 0;
   if (trace_) {

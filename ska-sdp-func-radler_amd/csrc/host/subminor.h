@@ -34,6 +34,9 @@ class SubMinorLoop {
     vertical_border_ = v;
   }
   void SetMask(const uint8_t* d_mask) { d_mask_ = d_mask; }
+  /// _parentAlgorithm->PerformSpectralFit (subminor_loop.cc:76) as a device
+  /// matrix (DeconvolutionAlgorithm::DeviceSpectralMap), nullptr = none.
+  void SetSpectralMap(const float* d_map) { d_spectral_ = d_map; }
   /// subminor_loop.cc:220-228 on the device (byte mask, W x H).
   void UpdateAutoMask(uint8_t* d_mask);
   void SetDivergenceLimit(float v) { divergence_limit_ = v; }
@@ -86,6 +89,7 @@ class SubMinorLoop {
   size_t current_iteration_ = 0, max_iterations_ = 0;
   bool allow_negative_ = true, stop_on_negative_ = false;
   const uint8_t* d_mask_ = nullptr;
+  const float* d_spectral_ = nullptr;
   float flux_cleaned_ = 0.0f;
   size_t n_selected_ = 0, n_images_ = 0;
   std::vector<uint32_t>* trace_ = nullptr;

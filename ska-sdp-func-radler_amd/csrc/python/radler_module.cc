@@ -147,6 +147,51 @@ void InitSettings(py::module& m) {  // python/pysettings.cc
       .value("forced_terms", schaapcommon::fitters::SpectralFittingMode::kForcedTerms);
 }
 
+void InitSpectralFitter(py::module& m) {
+  // schaapcommon::fitters::SpectralFitter (the reference binds fit /
+  // fit_and_evaluate in python_deconvolution.cc:22-82, 153-155)
+  using schaapcommon::fitters::SpectralFitter;
+  using schaapcommon::fitters::SpectralFittingMode;
+  py::class_<SpectralFitter>(m, "SpectralFitter")
+      .def(py::init([](SpectralFittingMode mode, size_t n_terms,
+                       const std::vector<double>& frequencies,
+                       const std::vector<float>& weights) {
+             return std::make_unique<SpectralFitter>(mode, n_terms, frequencies, weights);
+           }),
+           py::arg("mode"), py::arg("n_terms"), py::arg("frequencies"),
+           py::arg("weights"))
+      .def_property_readonly("mode", &SpectralFitter::Mode)
+      .def_property_readonly("n_terms", &SpectralFitter::NTerms)
+      .def_property_readonly("frequencies", &SpectralFitter::Frequencies)
+      .def_property_readonly("weights", &SpectralFitter::Weights)
+      .def_property_readonly("reference_frequency", &SpectralFitter::ReferenceFrequency)
+      .def("fit",
+           [](const SpectralFitter& self, const std::vector<float>& values, size_t x,
+              size_t y) {
+             if (values.size() != self.Frequencies().size())
+               throw std::runtime_error("fit: one value per channel is required");
+             std::vector<float> terms;
+             self.Fit(terms, values.data(), x, y);
+             return terms;
+           },
+           py::arg("values"), py::arg("x") = 0, py::arg("y") = 0)
+      .def("fit_and_evaluate",
+           [](const SpectralFitter& self, std::vector<float> values, size_t x, size_t y) {
+             if (self.Mode() != SpectralFittingMode::kNoFitting &&
+                 values.size() != self.Frequencies().size())
+               throw std::runtime_error(
+                   "fit_and_evaluate: one value per channel is required");
+             std::vector<float> scratch;
+             self.FitAndEvaluate(values.data(), x, y, scratch);
+             return values;
+           },
+           py::arg("values"), py::arg("x") = 0, py::arg("y") = 0)
+      .def("evaluate",
+           [](const SpectralFitter& self, const std::vector<float>& terms,
+              double frequency) { return self.Evaluate(terms, frequency); },
+           py::arg("terms"), py::arg("frequency"));
+}
+
 void InitWorkTable(py::module& m) {  // python/pywork_table.cc
   py::class_<AccessorList>(m, "VectorUniquePtrImageAccessor")
       .def("__len__", [](const AccessorList& self) { return self.size(); })
@@ -520,6 +565,7 @@ PYBIND11_MODULE(radler, m) {  // python/pywrappers.cc
   m.doc() = "MI355X-native Radio Astronomical Deconvolution Library (radler API)";
   InitSettings(m);
   InitWorkTable(m);
+  InitSpectralFitter(m);
   InitRadler(m);
   InitComponentList(m);
   InitGpu(m);

@@ -20,7 +20,9 @@ class SetDesc(C.Structure):
     _fields_ = [("width", C.c_uint64), ("height", C.c_uint64),
                 ("n_channels", C.c_uint64), ("n_pol", C.c_uint64),
                 ("weights", C.c_void_p), ("pol_factor", C.c_float),
-                ("squared_joins", C.c_int32)]
+                ("squared_joins", C.c_int32), ("fit_mode", C.c_int32),
+                ("fit_terms", C.c_uint32), ("fit_frequencies", C.c_void_p),
+                ("fit_weights", C.c_void_p)]
 
 
 class AlgoSettings(C.Structure):
@@ -162,7 +164,9 @@ class Oracle:
 
     @staticmethod
     def set_desc(width, height, n_channels=1, n_pol=1, weights=None, pol_factor=1.0,
-                 squared_joins=False):
+                 squared_joins=False, spectral=None):
+        """spectral: None or (mode, n_terms, frequencies, weights) of the
+        algorithms' SpectralFitter (mode 1 = polynomial)."""
         d = SetDesc()
         w = np.ones(n_channels, np.float32) if weights is None else np.asarray(weights, np.float32)
         d._w = np.ascontiguousarray(w)
@@ -170,7 +174,46 @@ class Oracle:
         d.weights = d._w.ctypes.data
         d.pol_factor = pol_factor
         d.squared_joins = int(squared_joins)
+        if spectral is not None:
+            mode, terms, freqs, fw = spectral
+            d._ff = np.ascontiguousarray(freqs, np.float64)
+            d._fw = np.ascontiguousarray(fw, np.float32)
+            assert d._ff.size == n_channels and d._fw.size == n_channels
+            d.fit_mode, d.fit_terms = int(mode), int(terms)
+            d.fit_frequencies, d.fit_weights = d._ff.ctypes.data, d._fw.ctypes.data
         return d
+
+    def spectral_fit(self, mode, n_terms, frequencies, weights, values):
+        """SpectralFitter FitAndEvaluate -> (evaluated values, terms)."""
+        f = np.ascontiguousarray(frequencies, np.float64)
+        w = np.ascontiguousarray(weights, np.float32)
+        v = np.ascontiguousarray(values, np.float32).copy()
+        t = np.zeros(max(int(n_terms), 1), np.float32)
+        L = self.lib
+        L.orc_spectral_fit.argtypes = [C.c_int, C.c_uint32, C.c_void_p, C.c_void_p,
+                                       C.c_uint64, C.c_void_p, C.c_void_p]
+        L.orc_spectral_fit.restype = None
+        L.orc_spectral_fit(int(mode), int(n_terms), f.ctypes.data, w.ctypes.data, f.size,
+                           v.ctypes.data, t.ctypes.data)
+        return v, t[:n_terms]
+
+    def spectral_interpolate(self, mode, n_terms, frequencies, weights, planes,
+                             out_frequencies):
+        """ImageSet::InterpolateAndStoreModel for one polarization."""
+        f = np.ascontiguousarray(frequencies, np.float64)
+        w = np.ascontiguousarray(weights, np.float32)
+        p = np.ascontiguousarray(planes, np.float32)
+        of = np.ascontiguousarray(out_frequencies, np.float64)
+        out = np.zeros((of.size,) + p.shape[1:], np.float32)
+        L = self.lib
+        L.orc_spectral_interpolate.argtypes = [C.c_int, C.c_uint32, C.c_void_p, C.c_void_p,
+                                               C.c_uint64, C.c_void_p, C.c_uint64,
+                                               C.c_void_p, C.c_uint64, C.c_void_p]
+        L.orc_spectral_interpolate.restype = None
+        L.orc_spectral_interpolate(int(mode), int(n_terms), f.ctypes.data, w.ctypes.data,
+                                   f.size, p.ctypes.data, int(np.prod(p.shape[1:])),
+                                   of.ctypes.data, of.size, out.ctypes.data)
+        return out
 
     def integrate(self, images, weights=None, n_pol=1, pol_factor=1.0, square=False):
         images = np.ascontiguousarray(images, np.float32)
@@ -188,6 +231,11 @@ class OracleAlgorithm:
         self.o = oracle
         self.settings = algo_settings(**settings)
         self.h = oracle.lib.orc_algo_create(kind, C.byref(self.settings))
+        self.spectral = None
+
+    def set_spectral_fitter(self, mode, n_terms, frequencies, weights):
+        """DeconvolutionAlgorithm::SetSpectralFitter (polynomial: mode 1)."""
+        self.spectral = (mode, n_terms, frequencies, weights)
 
     def update(self, **settings):
         self.settings = algo_settings(**settings)
@@ -196,7 +244,8 @@ class OracleAlgorithm:
     def execute(self, residual, model, psfs, weights=None, trace_cap=1 << 22):
         """residual/model: (n_img, h, w) float32 updated in place; psfs (n_ch, h, w)."""
         n, h, w = residual.shape
-        d = Oracle.set_desc(w, h, psfs.shape[0], n // psfs.shape[0], weights)
+        d = Oracle.set_desc(w, h, psfs.shape[0], n // psfs.shape[0], weights,
+                            spectral=self.spectral)
         r = Result()
         trace = np.zeros((trace_cap, 3), np.uint32)
         rc = self.o.lib.orc_algo_execute(self.h, C.byref(d), residual, model,
@@ -332,7 +381,8 @@ class OracleParallel:
     def execute(self, residual, model, psfs, major_loop_gain, user_mask=None,
                 trace_cap=1 << 22):
         n, h, w = residual.shape
-        d = Oracle.set_desc(w, h, psfs.shape[0], n // psfs.shape[0], None)
+        d = Oracle.set_desc(w, h, psfs.shape[0], n // psfs.shape[0], None,
+                            spectral=getattr(self, "spectral", None))
         r = ParallelResult()
         boxes = np.zeros((self.n_sub, 4), np.uint32)
         labels = np.zeros((h, w), np.uint16)

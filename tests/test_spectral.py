@@ -1,0 +1,288 @@
+"""Spectral fitting: schaapcommon's SpectralFitter
+(polynomial mode; the submodule is not vendored, so restated — see
+oracle/spectral.h), DeconvolutionAlgorithm::PerformSpectralFit on every
+component (deconvolution_algorithm.cc:29-46, generic_clean.cc:186,
+subminor_loop.cc:76, multiscale_algorithm.cc:477) and
+ImageSet::InterpolateAndStoreModel (image_set.cc:209-288).
+
+CPU: the oracle against the reference's own known answers
+(cpp/test/test_image_set.cc:622-670: a one-term fit is the weighted channel
+mean; python/test/test_radler.py:474-576: one deconvolution channel, two
+terms -> the same value at every original channel) and against numpy's
+weighted polyfit; the product's host SpectralFitter against the oracle.
+GPU: rdl_spectral_interpolate against the oracle's per-pixel fit; joined-
+channel CLEAN with polynomial fitting (Clark sub-minor, Högbom, multiscale
+fast and non-fast) against the oracle: same component trace, residual and
+model within 2e-5 x max|dirty| (the multiscale parity tolerance); the
+reference's two Radler-level spectral tests restated.
+Tolerances: the fitted values differ from the oracle's by float rounding
+(the device applies the fit as one precomputed linear map in float; the
+oracle solves the normal equations per call) — 2e-6 relative in the
+fitter tests.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from oracle_lib import OracleAlgorithm, get_oracle
+from radler_import import radler as rd
+from synthetic import problem
+
+POLY = 1
+
+
+def test_oracle_one_term_is_weighted_mean():
+    """cpp/test/test_image_set.cc:622-670: frequencies 101, 104, weights 1,
+    one term: every output channel gets the mean of the two channels."""
+    orc = get_oracle()
+    planes = np.zeros((2, 9, 7), np.float32)
+    for pol in range(4):
+        planes[0], planes[1] = pol, pol + 4
+        out = orc.spectral_interpolate(POLY, 1, [101.0, 104.0], [1.0, 1.0], planes,
+                                       [100.0 + c for c in range(6)])
+        np.testing.assert_allclose(out, pol + 2.0, rtol=1e-6)
+    # weighted: the weighted mean
+    v, t = orc.spectral_fit(POLY, 1, [2.5e6, 3.5e6], [0.5, 4.2], [2.5, 4.0])
+    np.testing.assert_allclose(v, (0.5 * 2.5 + 4.2 * 4.0) / 4.7, rtol=1e-6)
+
+
+def test_oracle_one_channel_two_terms_is_constant():
+    """python/test/test_radler.py:474-530: one deconvolution channel, a
+    linear fit -> the channel's value at every original frequency."""
+    orc = get_oracle()
+    planes = np.zeros((1, 8, 8), np.float32)
+    planes[0, 3, 4] = 3.7
+    out = orc.spectral_interpolate(POLY, 2, [3.0e6], [4.7], planes, [2.5e6, 3.5e6])
+    np.testing.assert_allclose(out[0], planes[0], rtol=1e-6)
+    np.testing.assert_allclose(out[1], planes[0], rtol=1e-6)
+
+
+@pytest.mark.parametrize("n,terms,seed", [(4, 2, 0), (6, 3, 1), (8, 4, 2), (3, 5, 3)])
+def test_oracle_matches_weighted_polyfit(n, terms, seed):
+    rng = np.random.default_rng(seed)
+    f = 1.2e8 + 8e6 * np.arange(n) + rng.uniform(0, 1e6, n)
+    w = rng.uniform(0.2, 2.0, n).astype(np.float32)
+    v = rng.standard_normal(n).astype(np.float32)
+    orc = get_oracle()
+    out, _ = orc.spectral_fit(POLY, terms, f, w, v)
+    ref = np.average(f, weights=w.astype(np.float64))
+    x = f / ref - 1.0
+    deg = min(terms, n) - 1
+    coef = np.polyfit(x, v.astype(np.float64), deg, w=np.sqrt(w.astype(np.float64)))
+    np.testing.assert_allclose(out, np.polyval(coef, x), rtol=2e-5, atol=2e-6)
+
+
+def test_oracle_zero_weight_channels_are_evaluated_not_fitted():
+    orc = get_oracle()
+    f = [1e8, 1.1e8, 1.2e8, 1.3e8]
+    w = [1.0, 0.0, 1.0, 1.0]
+    v = np.array([1.0, 100.0, 3.0, 4.0], np.float32)  # channel 1 ignored
+    out, _ = orc.spectral_fit(POLY, 2, f, w, v)
+    fx = np.array(f)[[0, 2, 3]]
+    coef = np.polyfit(fx, v[[0, 2, 3]].astype(np.float64), 1)
+    np.testing.assert_allclose(out, np.polyval(coef, np.array(f)), rtol=1e-5)
+
+
+@pytest.mark.parametrize("n,terms,seed", [(1, 2, 0), (4, 2, 1), (6, 3, 2), (5, 1, 3),
+                                          (8, 4, 4), (2, 4, 5)])
+def test_host_fitter_matches_oracle(n, terms, seed):
+    """radler.SpectralFitter (host C++, the pseudo-inverse map the device
+    uses) against the oracle's normal-equation fit."""
+    rng = np.random.default_rng(seed)
+    f = list(1.0e8 + 1.0e7 * np.arange(n) + rng.uniform(0, 2e6, n))
+    w = list(rng.uniform(0.5, 3.0, n))
+    if n > 3:
+        w[1] = 0.0
+    v = list(rng.standard_normal(n).astype(np.float32))
+    fitter = rd.SpectralFitter(rd.SpectralFittingMode.polynomial, terms, f, w)
+    got = np.array(fitter.fit_and_evaluate(v), np.float32)
+    exp, terms_o = get_oracle().spectral_fit(POLY, terms, f, w, v)
+    scale = max(1.0, float(np.abs(exp).max()))
+    np.testing.assert_allclose(got, exp, atol=2e-6 * scale)
+    np.testing.assert_allclose(np.array(fitter.fit(v), np.float32), terms_o,
+                               atol=2e-6 * max(1.0, float(np.abs(terms_o).max())))
+    assert abs(fitter.reference_frequency - np.average(f, weights=w)) < 1e-6 * f[0]
+
+
+def test_host_fitter_no_fitting_is_identity():
+    fitter = rd.SpectralFitter(rd.SpectralFittingMode.no_fitting, 2, [], [])
+    assert fitter.fit_and_evaluate([1.5, -2.0, 3.0]) == [1.5, -2.0, 3.0]
+
+
+def test_unavailable_modes_are_rejected():
+    s = rd.Settings()
+    s.trimmed_image_width = s.trimmed_image_height = 16
+    s.spectral_fitting.mode = rd.SpectralFittingMode.log_polynomial
+    s.spectral_fitting.terms = 2
+    psf = np.zeros((2, 16, 16), np.float32)
+    res, mod = np.zeros_like(psf), np.zeros_like(psf)
+    with pytest.raises(RuntimeError, match="not available"):
+        rd.Radler(s, psf, res, mod, 0.0, 1, np.array([[1e8, 1e8], [2e8, 2e8]]),
+                  np.ones(2))
+
+
+# ------------------------------------------------------------------- GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_in,n_out,terms,w,h", [(2, 6, 1, 7, 9), (4, 12, 2, 300, 200),
+                                                   (3, 3, 3, 128, 128), (20, 40, 3, 64, 33)])
+def test_interpolate_kernel_matches_oracle(n_in, n_out, terms, w, h):
+    from rdl_lib import Session
+    rng = np.random.default_rng(n_in * 100 + n_out)
+    planes = rng.standard_normal((n_in, h, w)).astype(np.float32)
+    planes[:, rng.random((h, w)) < 0.5] = 0.0  # zero pixels are not fitted
+    f_in = 1.0e8 + 2.0e7 * np.arange(n_in)
+    wts = rng.uniform(0.5, 2.0, n_in)
+    f_out = np.linspace(f_in[0] - 5e6, f_in[-1] + 5e6, n_out)
+    fitter = rd.SpectralFitter(rd.SpectralFittingMode.polynomial, terms, list(f_in), list(wts))
+    # the coefficient rows the product uses (the host fitter's evaluation of
+    # unit spectra), computed the way ImageSet does it on the host
+    coef = np.zeros((n_out, n_in), np.float32)
+    for c in range(n_in):
+        unit = [0.0] * n_in
+        unit[c] = 1.0
+        t = fitter.fit(unit)
+        for g in range(n_out):
+            coef[g, c] = fitter.evaluate(t, f_out[g])
+    sess = Session(0)
+    try:
+        d_in = sess.array(planes)
+        d_out = sess.array(np.zeros((n_out, h, w), np.float32))
+        sess.rdl.rdl_spectral_interpolate(sess.h, d_in.vp, C.c_size_t(h * w), C.c_uint32(n_in),
+                                          coef.ctypes.data_as(C.c_void_p), C.c_uint32(n_out),
+                                          d_out.vp, C.c_size_t(h * w))
+        got = d_out.get()
+        d_in.free()
+        d_out.free()
+    finally:
+        sess.close()
+    exp = get_oracle().spectral_interpolate(POLY, terms, f_in, wts, planes, f_out)
+    np.testing.assert_allclose(got, exp, atol=2e-5 * np.abs(exp).max())
+    assert np.all(got[:, np.all(planes == 0.0, axis=0)] == 0.0)
+
+
+def _joined(w, n_ch, seed):
+    psf, dirty = problem(w, w, 14, 3, seed=seed)
+    rng = np.random.default_rng(seed)
+    # a spectral slope plus channel noise: the fit changes every component
+    dirties = np.stack([dirty * np.float32(1.0 + 0.15 * k) + np.float32(2e-3) *
+                        rng.standard_normal((w, w)).astype(np.float32)
+                        for k in range(n_ch)]).astype(np.float32)
+    return np.stack([psf] * n_ch), dirties
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,variant,n_ch,terms,weights", [
+    (0, "clark", 4, 2, None), (0, "hogbom", 3, 2, [1.0, 2.0, 0.5]),
+    (1, "fast", 4, 2, [1.0, 0.5, 2.0, 1.0]), (1, "fast", 5, 3, None),
+    (1, "slow", 3, 2, None)])
+def test_joined_clean_with_polynomial_fit_matches_oracle(kind, variant, n_ch, terms, weights):
+    w = 128 if kind == 1 else 96
+    psfs, dirties = _joined(w, n_ch, 40 + n_ch + terms)
+    wts = np.ones(n_ch) if weights is None else np.asarray(weights, np.float64)
+    freqs = 1.0e8 + 1.0e7 * np.arange(n_ch)  # DeviceRun's channel frequencies
+    thr, max_iter = 1.2e-2, 400
+    st = dict(threshold=thr, max_iterations=max_iter, border_ratio=0.0)
+    if kind == 1:
+        st.update(max_scales=3, beam_size_in_pixels=2.0, fast_sub_minor_loop=int(variant == "fast"))
+    else:
+        st.update(use_sub_minor=int(variant == "clark"))
+    orc = get_oracle()
+    orc.set_threads(8)
+    alg = OracleAlgorithm(orc, kind, **st)
+    alg.set_spectral_fitter(POLY, terms, freqs, wts)
+    res_o, mod_o = dirties.copy(), np.zeros_like(dirties)
+    r_o, trace_o = alg.execute(res_o, mod_o, psfs, weights=wts.astype(np.float32))
+
+    s = rd.Settings()
+    s.algorithm_type = rd.AlgorithmType.multiscale if kind == 1 else \
+        rd.AlgorithmType.generic_clean
+    s.trimmed_image_width = s.trimmed_image_height = w
+    s.pixel_scale.x = s.pixel_scale.y = 1.0 / 3600.0 * np.pi / 180.0
+    s.minor_iteration_count = max_iter
+    s.absolute_threshold = thr
+    s.border_ratio = 0.0
+    s.spectral_fitting.mode = rd.SpectralFittingMode.polynomial
+    s.spectral_fitting.terms = terms
+    if kind == 1:
+        s.multiscale.max_scales = 3
+        s.multiscale.fast_sub_minor_loop = variant == "fast"
+    else:
+        s.generic.use_sub_minor_optimization = variant == "clark"
+    run = rd.gpu.DeviceRun(s, psfs, dirties, list(wts),
+                           2.0 * s.pixel_scale.x if kind == 1 else 0.0)
+    r_g = run.execute()
+    assert r_g["iterations"] == r_o.iteration_number > 10
+    t_g = run.trace()
+    assert np.array_equal(t_g if kind == 1 else t_g[:, :2], trace_o if kind == 1 else trace_o[:, :2])
+    tol = 2e-5 * np.abs(dirties).max()
+    np.testing.assert_allclose(run.residual().reshape(n_ch, w, w), res_o, atol=tol)
+    model = run.model().reshape(n_ch, w, w)
+    np.testing.assert_allclose(model, mod_o, atol=tol)
+    # every component's channel values lie on a polynomial of terms-1 degree
+    # (scale-0 pixels of the model are sums of such spectra)
+    nz = np.nonzero(np.abs(model).sum(axis=0) > 0)
+    spectra = model[:, nz[0], nz[1]].astype(np.float64)
+    x = freqs / np.average(freqs, weights=wts) - 1.0
+    vander = np.vander(x, terms, increasing=True)
+    resid = spectra - vander @ np.linalg.lstsq(vander, spectra, rcond=None)[0]
+    assert np.abs(resid).max() <= 1e-5 * np.abs(spectra).max()
+
+
+def _reference_spectral_case(algorithm, use_work_table):
+    """python/test/test_radler.py:474-576 restated."""
+    from radler_fixtures import BEAM_SIZE, HEIGHT, WIDTH, get_psf, get_residual, make_settings
+    settings = make_settings()
+    settings.algorithm_type = algorithm
+    settings.spectral_fitting.mode = rd.SpectralFittingMode.polynomial
+    settings.spectral_fitting.terms = 2
+    scales = [2.5, 4.0]
+    shifts = [(0, 0), (-9, 23)]
+    weights = np.asarray([0.5, 4.2])
+    frequencies = np.asarray([[2.0e6, 3.0e6], [3.0e6, 4.0e6]])
+    if use_work_table:
+        psf = get_psf()
+        residuals = [get_residual(scales[i], *shifts[i]) for i in range(2)]
+        models = [np.zeros_like(residuals[0]) for _ in range(2)]
+        t = rd.WorkTable([], 2, 1)
+        for i in range(2):
+            e = rd.WorkTableEntry()
+            e.psfs.append(psf)
+            e.residual = residuals[i]
+            e.model = models[i]
+            e.original_channel_index = i
+            e.band_start_frequency = frequencies[i][0]
+            e.band_end_frequency = frequencies[i][1]
+            e.index = i
+            e.image_weight = weights[i]
+            t.add_entry(e)
+        r = rd.Radler(settings, t, BEAM_SIZE)
+    else:
+        psfs = np.resize(get_psf(), (2, HEIGHT, WIDTH))
+        residuals = np.array([get_residual(scales[i], *shifts[i]) for i in range(2)])
+        models = np.zeros_like(residuals)
+        r = rd.Radler(settings, psfs, residuals, models, BEAM_SIZE, 1, frequencies, weights)
+    assert r.perform(0) is False
+    assert r.iteration_number <= settings.minor_iteration_count
+    for residual in residuals:
+        np.testing.assert_allclose(residual, 0.0, atol=2e-6)
+    np.testing.assert_allclose(models[0], models[1], atol=1e-6)
+    ref = np.zeros((HEIGHT, WIDTH), np.float32)
+    for i, shift in enumerate(shifts):
+        ref[HEIGHT // 2 + shift[1], WIDTH // 2 + shift[0]] = \
+            np.sum(weights * np.diag(scales)[i, :]) / np.sum(weights)
+    np.testing.assert_allclose(models[0], ref, atol=2e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("algorithm", [rd.AlgorithmType.generic_clean,
+                                       rd.AlgorithmType.multiscale])
+def test_reference_ndeconvolution_lt_noriginal(algorithm):
+    _reference_spectral_case(algorithm, True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("algorithm", [rd.AlgorithmType.generic_clean,
+                                       rd.AlgorithmType.multiscale])
+def test_reference_image_cube_joined(algorithm):
+    _reference_spectral_case(algorithm, False)
