@@ -22,6 +22,8 @@
 
 #include <cstdio>
 
+#include <cstdlib>
+
 #include "rdl_internal.h"
 
 struct rdl_subminor {
@@ -38,9 +40,10 @@ struct rdl_subminor {
   uint32_t* d_pos = nullptr;
   float* d_r = nullptr;
   float* d_m = nullptr;
-  int mode = 0;                  // 0 auto, 1 LDS kernel, 2 register kernel
+  int mode = 0;  // 0 auto, 1 LDS kernel, 2 register kernel, 3 single-wave kernel
   uint32_t target_per_block = 1024;  // pixels per workgroup (multi-workgroup)
   uint32_t single_max = 2048;         // largest selection kept on one workgroup
+  uint32_t wave_max = 128;            // largest selection on the single-wave kernel
 };
 
 namespace rdl {
@@ -679,10 +682,14 @@ __device__ __forceinline__ uint64_t LoadGranule(uint64_t* g) {
 
 // FAST: one image whose integration is the identity (ImageSet copy fast path,
 // cpp/image_set.cc:425-430): the integrated value is the residual itself.
-template <int NI, int ITEMS, bool FAST>
-__global__ __launch_bounds__(kRegThreads) void SubminorLoopReg(LoopArgs a) {
+// THREADS = 512 (eight waves, one LDS barrier per iteration) or 64: the
+// single-wave form for small selections, where the winner goes from the
+// wave argmax straight to every lane by readlane (no LDS slot, no barrier).
+template <int NI, int ITEMS, bool FAST, int THREADS = kRegThreads>
+__global__ __launch_bounds__(THREADS) void SubminorLoopReg(LoopArgs a) {
   constexpr int REC = 3 + NI;  // granules per record: key hi, key lo, pos, r[NI]
-  __shared__ RegSlot<NI> slots[2][kRegWaves];
+  constexpr int WAVES = THREADS / 64;
+  __shared__ RegSlot<NI> slots[2][WAVES];
   __shared__ RegSlot<NI> gwin;
   __shared__ uint32_t gflag;
 
@@ -698,7 +705,7 @@ __global__ __launch_bounds__(kRegThreads) void SubminorLoopReg(LoopArgs a) {
   float M[ITEMS][NI];
 #pragma unroll
   for (int i = 0; i < ITEMS; ++i) {
-    const uint32_t j = tid + uint32_t(i) * kRegThreads;
+    const uint32_t j = tid + uint32_t(i) * THREADS;
     const bool valid = j < cnt;
     pos[i] = valid ? a.pos[base + j] : 0u;
 #pragma unroll
@@ -739,7 +746,7 @@ __global__ __launch_bounds__(kRegThreads) void SubminorLoopReg(LoopArgs a) {
       bool in[ITEMS];
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
-        const uint32_t j = tid + uint32_t(i) * kRegThreads;
+        const uint32_t j = tid + uint32_t(i) * THREADS;
         const int px = int(pos[i] & 0xffffu), py = int(pos[i] >> 16);
         const int dx = px - cx + W / 2, dy = py - cy + H / 2;
         in[i] = j < cnt && dx >= 0 && dx < W && dy >= 0 && dy < H;
@@ -760,7 +767,7 @@ __global__ __launch_bounds__(kRegThreads) void SubminorLoopReg(LoopArgs a) {
     int best_i = 0;
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
-      const uint32_t j = tid + uint32_t(i) * kRegThreads;
+      const uint32_t j = tid + uint32_t(i) * THREADS;
       if (j < cnt) {
         const float integ = FAST ? R[i][0] : IntegratePixel(a.integ, [&](uint32_t kk) {
           float r = R[i][0];
@@ -782,6 +789,31 @@ __global__ __launch_bounds__(kRegThreads) void SubminorLoopReg(LoopArgs a) {
     const uint64_t wmax = Max64U64(best);
     const uint32_t par = epoch & 1u;
     const int owner_lane = wmax != 0 ? FirstLane(best == wmax) : 0;
+    uint64_t gkey;
+    uint32_t wpos;
+    float wr[NI];
+    if constexpr (WAVES == 1) {
+      // every lane stages its own candidate; the owner's comes by readlane
+      uint32_t pp = pos[0];
+      float rr[NI];
+#pragma unroll
+      for (int k = 0; k < NI; ++k) rr[k] = R[0][k];
+#pragma unroll
+      for (int i = 1; i < ITEMS; ++i)
+        if (i == best_i && wmax != 0) {
+          pp = pos[i];
+#pragma unroll
+          for (int k = 0; k < NI; ++k) rr[k] = R[i][k];
+        }
+      gkey = wmax;
+      wpos = uint32_t(__builtin_amdgcn_readlane(int(pp), owner_lane));
+#pragma unroll
+      for (int k = 0; k < NI; ++k)
+        wr[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rr[k]), owner_lane));
+      ++epoch;
+      RDL_PHASE(2)
+      RDL_PHASE(3)
+    } else {
     if (int(lane) == owner_lane) {
       RegSlot<NI>& sl = slots[par][wave];
       sl.key = wmax;
@@ -812,7 +844,7 @@ __global__ __launch_bounds__(kRegThreads) void SubminorLoopReg(LoopArgs a) {
     float sr[NI];
 #pragma unroll
     for (int k = 0; k < NI; ++k) sr[k] = 0.0f;
-    if (lane < kRegWaves) {
+    if (lane < uint32_t(WAVES)) {
       const RegSlot<NI>& sl = slots[par][lane];
       sk = sl.key;
       spos = sl.pos;
@@ -820,10 +852,9 @@ __global__ __launch_bounds__(kRegThreads) void SubminorLoopReg(LoopArgs a) {
       for (int k = 0; k < NI; ++k) sr[k] = sl.r[k];
     }
     const uint64_t bkey = Max8U64(sk);
-    const int bw = bkey != 0 ? FirstLane(sk == bkey && lane < kRegWaves) : 0;
-    uint64_t gkey = bkey;
-    uint32_t wpos = uint32_t(__builtin_amdgcn_readlane(int(spos), bw));
-    float wr[NI];
+    const int bw = bkey != 0 ? FirstLane(sk == bkey && lane < uint32_t(WAVES)) : 0;
+    gkey = bkey;
+    wpos = uint32_t(__builtin_amdgcn_readlane(int(spos), bw));
 #pragma unroll
     for (int k = 0; k < NI; ++k)
       wr[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sr[k]), bw));
@@ -910,6 +941,7 @@ __global__ __launch_bounds__(kRegThreads) void SubminorLoopReg(LoopArgs a) {
     } else {
       ++epoch;
     }
+    }  // WAVES > 1
 
     RDL_PHASE(4)
     // ---- identical decisions everywhere (subminor_loop.cc:56-89)
@@ -952,8 +984,8 @@ __global__ __launch_bounds__(kRegThreads) void SubminorLoopReg(LoopArgs a) {
     cy = int(wpos >> 16);
     if (winner_p >= base && winner_p < base + cnt) {
       const uint32_t j = uint32_t(winner_p - base);
-      if (j % kRegThreads == tid) {
-        const int wi = int(j / kRegThreads);
+      if (j % THREADS == tid) {
+        const int wi = int(j / THREADS);
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i)
           if (i == wi)
@@ -980,7 +1012,7 @@ __global__ __launch_bounds__(kRegThreads) void SubminorLoopReg(LoopArgs a) {
 
 #pragma unroll
   for (int i = 0; i < ITEMS; ++i) {
-    const uint32_t j = tid + uint32_t(i) * kRegThreads;
+    const uint32_t j = tid + uint32_t(i) * THREADS;
     if (j < cnt)
 #pragma unroll
       for (int k = 0; k < NI; ++k)
@@ -993,6 +1025,32 @@ __global__ __launch_bounds__(kRegThreads) void SubminorLoopReg(LoopArgs a) {
     r->diverging = diverging ? 1 : 0;
     r->flux = flux;
   }
+}
+
+template <int NI, int ITEMS>
+int LaunchWave(const LoopArgs& a, hipStream_t stream) {
+  auto kernel = (NI == 1 && a.integ.copy_fast_path)
+                    ? SubminorLoopReg<NI, ITEMS, NI == 1, 64>
+                    : SubminorLoopReg<NI, ITEMS, false, 64>;
+  kernel<<<1, 64, 0, stream>>>(a);
+  RDL_HIP_CHECK(hipGetLastError());
+  return RDL_OK;
+}
+
+// Single-wave register budget: ITEMS x N_img residuals + model values +
+// gathers per lane.
+constexpr uint32_t WaveMaxItems(uint32_t ni) {
+  return ni <= 1 ? 16 : ni <= 2 ? 8 : ni <= 4 ? 4 : 2;
+}
+
+template <int NI>
+int LaunchWaveItems(const LoopArgs& a, uint32_t items, hipStream_t stream) {
+  constexpr uint32_t kMax = WaveMaxItems(NI);
+  if (items <= 1) return LaunchWave<NI, 1>(a, stream);
+  if (items <= 2) return LaunchWave<NI, 2>(a, stream);
+  if (items <= 4 || kMax <= 4) return LaunchWave<NI, (kMax >= 4 ? 4 : 2)>(a, stream);
+  if (items <= 8 || kMax <= 8) return LaunchWave<NI, (kMax >= 8 ? 8 : 2)>(a, stream);
+  return LaunchWave<NI, (kMax >= 16 ? 16 : 2)>(a, stream);
 }
 
 template <int NI, int ITEMS>
@@ -1065,6 +1123,9 @@ int rdl_subminor_create(rdl_session* s, rdl_subminor** out) {
   RDL_ARG_CHECK(s && out, "NULL argument");
   auto h = new rdl_subminor();
   h->s = s;
+  // experiments: RDL_SUBMINOR_WAVE_MAX=0 disables the single-wave kernel
+  if (const char* e = std::getenv("RDL_SUBMINOR_WAVE_MAX"))
+    h->wave_max = uint32_t(std::strtoul(e, nullptr, 10));
   *out = h;
   return RDL_OK;
 }
@@ -1176,8 +1237,18 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
       use_reg = per <= reg_cap;
     }
   }
-  if (!use_reg && h->mode == 2) {
+  if (!use_reg && (h->mode == 2 || h->mode == 3)) {
     rdl::SetError("register sub-minor kernel cannot hold this selection");
+    return RDL_ERR_ARG;
+  }
+  // single wave: no barrier and no LDS exchange per iteration
+  const uint64_t wave_cap = 64ull * rdl::WaveMaxItems(ni_t);
+  const bool use_wave =
+      use_reg && g == 1 &&
+      ((h->mode == 0 && n_sel <= std::min<uint64_t>(wave_cap, h->wave_max)) ||
+       (h->mode == 3 && n_sel <= wave_cap));
+  if (h->mode == 3 && !use_wave) {
+    rdl::SetError("single-wave sub-minor kernel cannot hold this selection");
     return RDL_ERR_ARG;
   }
   uint32_t items = 0;
@@ -1248,7 +1319,18 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   }
   {
     rdl::ScopedTiming t(s, "subminor_loop", 0.0);
-    if (use_reg) {
+    if (use_wave) {
+      const uint64_t wi = (n_sel + 63) / 64;
+      const uint32_t witems = wi <= 1 ? 1 : wi <= 2 ? 2 : wi <= 4 ? 4 : wi <= 8 ? 8 : 16;
+      if (ni_t == 1)
+        RDL_TRY(rdl::LaunchWaveItems<1>(la, witems, st));
+      else if (ni_t == 2)
+        RDL_TRY(rdl::LaunchWaveItems<2>(la, witems, st));
+      else if (ni_t == 4)
+        RDL_TRY(rdl::LaunchWaveItems<4>(la, witems, st));
+      else
+        RDL_TRY(rdl::LaunchWaveItems<8>(la, witems, st));
+    } else if (use_reg) {
       if (ni_t == 1)
         RDL_TRY(rdl::LaunchRegItems<1>(la, items, st));
       else if (ni_t == 2)
@@ -1321,7 +1403,7 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
 int rdl_subminor_set_tuning(rdl_subminor* h, int mode,
                             uint32_t target_per_block) {
   RDL_ARG_CHECK(h, "NULL argument");
-  RDL_ARG_CHECK(mode >= 0 && mode <= 2, "mode must be 0, 1 or 2");
+  RDL_ARG_CHECK(mode >= 0 && mode <= 3, "mode must be 0, 1, 2 or 3");
   h->mode = mode;
   if (target_per_block) h->target_per_block = target_per_block;
   return RDL_OK;

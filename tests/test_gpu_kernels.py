@@ -451,6 +451,7 @@ SUBMINOR_CASES = [
     (160, 20, 0.003, 0.9, 600, 5, 0, 0),
     (160, 20, 0.003, 0.9, 600, 8, 2, 600),
     (160, 20, 0.003, 0.9, 600, 5, 1, 0),
+    (128, 10, 0.0, 0.8, 300, 1, 3, 0),        # single-wave kernel forced
 ]
 
 

@@ -22,7 +22,12 @@ def main():
     rng = np.random.default_rng(1)
     sm = C.c_void_p()
     s.rdl.rdl_subminor_create(s.h, C.byref(sm))
-    for n_sel in (256, 1024, 4096, 16384, 65536, 262144):
+    sizes = (256, 1024, 4096, 16384, 65536, 262144)
+    variants = ((1, 0), (2, 512), (2, 1024), (2, 2048), (2, 4096))
+    if os.environ.get("RDL_BENCH_WAVE"):  # single-wave vs eight-wave kernel
+        sizes = (64, 128, 256, 400, 512, 768, 1024)
+        variants = ((2, 0), (3, 0))
+    for n_sel in sizes:
         img = np.zeros((size, size), np.float32)
         n_cl = 24
         cx = rng.uniform(500, size - 500, n_cl)
@@ -33,7 +38,7 @@ def main():
         flat = np.unique(ys * size + xs)[:n_sel]
         img.flat[flat] = rng.uniform(1.0, 2.0, flat.size).astype(np.float32)
         dres = s.array(img)
-        for mode, target in ((1, 0), (2, 512), (2, 1024), (2, 2048), (2, 4096)):
+        for mode, target in variants:
             s.rdl.rdl_subminor_set_tuning(sm, mode, target)
             p = SubminorParams()
             p.width = p.height = size
