@@ -211,6 +211,39 @@ int rdl_spectral_interpolate(rdl_session* s, const float* d_in, size_t in_stride
                              uint32_t n_in, const float* h_coefficients,
                              uint32_t n_out, float* d_out, size_t n);
 
+/* ------------------------------------------------------------ local RMS */
+/* radler::math::rms_image (cpp/math/rms_image.cc:16-125) building blocks.
+ * The Gaussian window convolution itself is an FFT convolution of the
+ * squared image with the placed kernel (host: csrc/host/rms_image.cc). */
+/* Image::Square: dst = src * src. */
+int rdl_square(rdl_session* s, const float* d_src, float* d_dst, size_t n);
+/* dst = a * b (the `scratch[i] = image[i] * rms_factor[i]` of every
+ * RMS-weighted peak search, generic_clean.cc:258-264,
+ * multiscale_algorithm.cc:707-713, threaded_deconvolution_tools.cc:84-87). */
+int rdl_multiply(rdl_session* s, float* d_dst, const float* d_a, const float* d_b,
+                 size_t n);
+/* d = sqrt(d * norm) in double (rms_image.cc:32). */
+int rdl_rms_finish(rdl_session* s, float* d, size_t n, double norm);
+/* schaapcommon::math::RestoreImage's kernel: a box x box Gaussian of peak 1
+ * (sigmas in the units of the pixel scales, major axis at `angle`) placed
+ * with its centre (box/2, box/2) at the origin of a zeroed width x height
+ * plane (PrepareSmallConvolutionKernel placement). */
+int rdl_place_gaussian(rdl_session* s, float* d_dest, uint32_t width, uint32_t height,
+                       uint32_t box, double pixel_scale_l, double pixel_scale_m,
+                       double sigma_major, double sigma_minor, double angle);
+/* rms_image::SlidingMinimum (rms_image.cc:35-68): row then column minimum
+ * over [max(k, window/2) - window/2, min(k, len - window/2) + window/2).
+ * d_scratch: 3 * width * height floats; 2 <= window, window/2 <= both sides. */
+int rdl_sliding_min(rdl_session* s, const float* d_in, float* d_out, float* d_scratch,
+                    uint32_t width, uint32_t height, uint64_t window);
+/* rms = max<float>(rms, |min| * 0.3) (rms_image.cc:88-92). */
+int rdl_rms_negativity_limit(rdl_session* s, float* d_rms, const float* d_min,
+                             size_t n);
+/* rms_image::MakeRmsFactorImage (rms_image.cc:95-125) in place; *lowest_rms
+ * = the image minimum; RDL_ERR_ARG when it is negative. */
+int rdl_rms_factor(rdl_session* s, float* d_rms, size_t n, double strength,
+                   double* lowest_rms);
+
 /* ---------------------------------------------------------------- Högbom */
 typedef struct {
   uint32_t width, height;
@@ -234,6 +267,9 @@ typedef struct {
    * applied to the gathered peak values before the gain (generic_clean.cc:
    * 186); NULL = no fitting. See rdl_spectral_* below. */
   const float* d_spectral;
+  /* DeconvolutionAlgorithm::RmsFactorImage (W x H factors multiplied into
+   * every peak search, generic_clean.cc:255-264); NULL = none */
+  const float* d_rms;
 } rdl_hogbom_params;
 
 typedef struct {
@@ -270,6 +306,10 @@ typedef struct {
    * (subminor_loop.cc:64-76) as an n_images x n_images row-major linear map;
    * NULL = no fitting */
   const float* d_spectral;
+  /* SubMinorLoop::SetRmsFactorImage: W x H factors multiplied into the
+   * selection and the loop's argmax (subminor_loop.cc:13-36, 143-149);
+   * NULL = none */
+  const float* d_rms;
 } rdl_subminor_params;
 
 typedef struct {

@@ -10,6 +10,7 @@
 #include "fft.h"
 #include "oracle.h"
 #include "tiling.h"
+#include "rms_image.h"
 #include "iuwt.h"
 #include "iuwt_algorithm.h"
 
@@ -165,6 +166,7 @@ struct OrcAlgo {
   size_t iteration_number = 0;
   std::unique_ptr<MultiScale> ms;
   std::vector<IuwtStep> iuwt_steps;  // type 2: steps of the last execute
+  std::vector<float> rms_factor;     // SetRmsFactorImage (empty = none)
 };
 
 static AlgoSettings MakeSettings(const orc_algo_settings* a) {
@@ -254,6 +256,8 @@ int orc_algo_execute(void* h, const orc_set_desc* d, float* residual,
       psf_ptrs.push_back(psfs + c * d->width * d->height);
     std::vector<Component> tr;
     Result r;
+    algo->settings.rms_factor = algo->rms_factor.empty() ? nullptr : algo->rms_factor.data();
+    if (algo->ms) algo->ms->Settings().rms_factor = algo->settings.rms_factor;
     if (algo->type == 0) {
       r = GenericCleanExecute(algo->settings, algo->iteration_number, res, mod,
                               psf_ptrs, &tr);
@@ -379,6 +383,55 @@ void* orc_parallel_create(int kind, const orc_algo_settings* a, uint64_t grid_w,
 }
 
 void orc_parallel_destroy(void* h) { delete static_cast<OrcParallel*>(h); }
+
+// DeconvolutionAlgorithm::SetRmsFactorImage (deconvolution_algorithm.h:163-166);
+// factor == nullptr clears it
+void orc_algo_set_rms(void* h, const float* factor, uint64_t n) {
+  auto* algo = static_cast<OrcAlgo*>(h);
+  if (factor)
+    algo->rms_factor.assign(factor, factor + n);
+  else
+    algo->rms_factor.clear();
+}
+
+// ParallelDeconvolution::SetRmsFactorImage (parallel_deconvolution.cc:244-250)
+void orc_parallel_set_rms(void* h, const float* factor, uint64_t n) {
+  auto* p = static_cast<OrcParallel*>(h);
+  if (factor)
+    p->masks.rms_factor.assign(factor, factor + n);
+  else
+    p->masks.rms_factor.clear();
+}
+
+// Radler::Perform's local-RMS step (cpp/radler.cc:196-216): method 1 =
+// kRmsWindow, 2 = kRmsAndMinimumWindow; factor receives the RMS factor image
+// and *lowest_rms the value MakeRmsFactorImage returns. rms (may be NULL)
+// receives the RMS image before the factor conversion.
+int orc_local_rms(const float* integrated, uint64_t width, uint64_t height, int method,
+                  double window, double beam, double pixel_scale_x, double pixel_scale_y,
+                  double strength, float* rms, float* factor, double* lowest_rms) {
+  try {
+    std::vector<float> img(width * height);
+    if (method == 1)
+      RmsImageMake(img.data(), integrated, width, height, window, beam, beam, 0.0L,
+                   pixel_scale_x, pixel_scale_y);
+    else
+      RmsImageMakeWithNegativityLimit(img.data(), integrated, width, height, window,
+                                      beam, beam, 0.0L, pixel_scale_x, pixel_scale_y);
+    if (rms) std::copy(img.begin(), img.end(), rms);
+    *lowest_rms = MakeRmsFactorImage(img.data(), img.size(), strength);
+    std::copy(img.begin(), img.end(), factor);
+    return 0;
+  } catch (const std::exception& e) {
+    g_error = e.what();
+    return 1;
+  }
+}
+
+void orc_sliding_minimum(const float* input, uint64_t width, uint64_t height,
+                         uint64_t window, float* output) {
+  SlidingMinimum(output, input, width, height, window);
+}
 
 // ParallelDeconvolution::SetAutoMaskMode (parallel_deconvolution.cc:260-268)
 void orc_parallel_set_automask(void* h, int track, int use) {

@@ -480,6 +480,8 @@ size_t SubMinorLoop::GetMaxComponent(std::vector<float>& scratch,
   set.height = 1;
   for (const auto& r : residual_) set.images.push_back(const_cast<float*>(r.data()));
   GetLinearIntegrated(set, scratch.data());
+  if (!rms_selected_.empty())
+    for (size_t i = 0; i != positions_.size(); ++i) scratch[i] *= rms_selected_[i];
   size_t max_component = 0;
   max_value = scratch[0];
   for (size_t i = 0; i != positions_.size(); ++i) {
@@ -502,6 +504,8 @@ SubMinorLoop::RunResult SubMinorLoop::Run(
   {
     std::vector<float> integrated(width_ * height_);
     GetLinearIntegrated(convolved_residual, integrated.data());
+    if (rms_factor)  // subminor_loop.cc:147-149
+      for (size_t i = 0; i != width_ * height_; ++i) integrated[i] *= rms_factor[i];
     const size_t xs = horizontal_border;
     const size_t xe = std::max<long>(xs, long(width_) - long(horizontal_border));
     const size_t ys = vertical_border;
@@ -524,6 +528,10 @@ SubMinorLoop::RunResult SubMinorLoop::Run(
       residual_[i][p] =
           convolved_residual.images[i][positions_[p].second * width_ +
                                        positions_[p].first];
+  rms_selected_.clear();
+  if (rms_factor)  // SubMinorModel::MakeRmsFactorImage (subminor_loop.cc:134-141)
+    for (const auto& p : positions_)
+      rms_selected_.push_back(rms_factor[p.second * width_ + p.first]);
   if (positions_.empty()) return {false, false, 0.0f};
 
   std::vector<float> scratch(positions_.size());
@@ -603,6 +611,12 @@ Peak GenericFindPeak(const AlgoSettings& s, const float* image, size_t w,
   // generic_clean.cc:255-277 via peak_finder.h:99-107 (border by round())
   const size_t hb = std::round(w * s.clean_border_ratio);
   const size_t vb = std::round(h * s.clean_border_ratio);
+  std::vector<float> scratch;
+  if (s.rms_factor) {  // generic_clean.cc:258-264
+    scratch.assign(image, image + w * h);
+    for (size_t i = 0; i != w * h; ++i) scratch[i] *= s.rms_factor[i];
+    image = scratch.data();
+  }
   if (!s.clean_mask)
     return FindPeakAvx(image, w, h, s.allow_negative, 0, h, hb, vb);
   return FindPeakWithMask(image, w, h, s.allow_negative, 0, h, s.clean_mask,
@@ -650,6 +664,7 @@ Result GenericCleanExecute(const AlgoSettings& s_in, size_t& iteration_number,
     sub.stop_on_negative = s.stop_on_negative;
     sub.divergence_limit = s.divergence_limit;
     sub.mask = s.clean_mask;
+    sub.rms_factor = s.rms_factor;  // generic_clean.cc:126-128
     sub.horizontal_border = std::round(width * s.clean_border_ratio);
     sub.vertical_border = std::round(height * s.clean_border_ratio);
     sub.trace = trace;
@@ -811,6 +826,12 @@ void MultiScale::FindPeakDirect(const float* image, size_t w, size_t h,
   ScaleInfo& info = scales_[scale_index];  // multiscale_algorithm.cc:700-748
   const size_t hb = std::round(w * s_.clean_border_ratio);
   const size_t vb = std::round(h * s_.clean_border_ratio);
+  std::vector<float> scratch;
+  if (s_.rms_factor) {  // :707-713
+    scratch.assign(image, image + w * h);
+    for (size_t i = 0; i != w * h; ++i) scratch[i] *= s_.rms_factor[i];
+    image = scratch.data();
+  }
   Peak p;
   if (use_scale_masks)
     p = FindPeakWithMask(image, w, h, s_.allow_negative, 0, h,
@@ -824,7 +845,8 @@ void MultiScale::FindPeakDirect(const float* image, size_t w, size_t h,
   info.max_image_value_y = p.y;
   if (p.has) {
     info.max_unnormalized_image_value = p.value;
-    info.max_normalized_image_value = p.value;
+    info.max_normalized_image_value =
+        s_.rms_factor ? p.value / s_.rms_factor[p.x + p.y * w] : p.value;
   } else {
     info.max_unnormalized_image_value = 0.0f;
     info.max_normalized_image_value = 0.0f;
@@ -853,6 +875,8 @@ void MultiScale::FindActiveScaleConvolvedMaxima(const ImageSet& set,
       const size_t yb = std::max<size_t>(std::round(h * s_.clean_border_ratio),
                                          border_scale);
       if (report_rms) e.rms = Rms(copy.data(), w * h);
+      if (s_.rms_factor)  // threaded_deconvolution_tools.cc:84-87
+        for (size_t i = 0; i != w * h; ++i) copy[i] *= s_.rms_factor[i];
       Peak p;
       // threaded_deconvolution_tools.cc:43-44: the scale's mask replaces the
       // clean mask when scale masks are in use
@@ -862,7 +886,9 @@ void MultiScale::FindActiveScaleConvolvedMaxima(const ImageSet& set,
       else
         p = FindPeakWithMask(copy.data(), w, h, s_.allow_negative, 0, h, mask,
                              xb, yb);
-      e.max_normalized_image_value = p.has ? p.value : 0.0f;
+      e.max_normalized_image_value =
+          p.has ? (s_.rms_factor ? p.value / s_.rms_factor[p.x + p.y * w] : p.value)
+                : 0.0f;
       e.max_unnormalized_image_value = p.has ? p.value : 0.0f;
       e.max_image_value_x = p.x;
       e.max_image_value_y = p.y;
@@ -991,6 +1017,7 @@ Result MultiScale::Execute(ImageSet& data, ImageSet& model,
       sub.vertical_border =
           std::max<size_t>(std::round(height * s_.clean_border_ratio), scale_border);
       sub.mask = use_scale_masks ? ScaleMask(scale_with_peak) : s_.clean_mask;
+      sub.rms_factor = s_.rms_factor;  // multiscale_algorithm.cc:401-402
       sub.trace = trace;
       sub.trace_scale = uint32_t(scale_with_peak);
       std::vector<const float*> twice_ptrs;

@@ -116,6 +116,9 @@ struct AlgoSettings {
   bool allow_negative = true;
   bool stop_on_negative = false;
   const bool* clean_mask = nullptr;
+  // DeconvolutionAlgorithm::RmsFactorImage (deconvolution_algorithm.h:163-166):
+  // width x height factors multiplied into every peak search; nullptr = none
+  const float* rms_factor = nullptr;
   // generic clean
   bool use_sub_minor_optimization = true;
   // multiscale (cpp/settings.h:465-524)
@@ -157,6 +160,7 @@ class SubMinorLoop {
   size_t current_iteration = 0, max_iterations = 0;
   bool allow_negative = true, stop_on_negative = false;
   const bool* mask = nullptr;
+  const float* rms_factor = nullptr;  // SetRmsFactorImage (full image)
   float flux_cleaned = 0.0f;
   std::vector<Component>* trace = nullptr;
   uint32_t trace_scale = 0;
@@ -181,6 +185,7 @@ class SubMinorLoop {
   size_t width_, height_, padded_width_, padded_height_;
   std::vector<std::pair<size_t, size_t>> positions_;
   std::vector<std::vector<float>> residual_, model_;
+  std::vector<float> rms_selected_;  // SubMinorModel::MakeRmsFactorImage
   const SetDesc* desc_ = nullptr;
   size_t GetMaxComponent(std::vector<float>& scratch, float& max_value) const;
 };

@@ -296,6 +296,12 @@ ParallelResult ParallelRun(std::vector<TiledAlgorithm>& algorithms,
     }
     std::vector<unsigned char> mask_copy = s.mask;
     alg.settings.clean_mask = reinterpret_cast<const bool*>(mask_copy.data());
+    std::vector<float> sub_rms;
+    if (masks && !masks->rms_factor.empty()) {  // rms_image_.TrimBox (:332-337)
+      sub_rms.resize(n);
+      CopyBox(sub_rms.data(), s.x, s.y, sw, sh, masks->rms_factor.data(), width);
+      alg.settings.rms_factor = sub_rms.data();
+    }
     const size_t max_iter = alg.settings.max_iterations;
     if (find_peak_only)
       alg.settings.max_iterations = 0;
@@ -340,6 +346,7 @@ ParallelResult ParallelRun(std::vector<TiledAlgorithm>& algorithms,
         std::isfinite(s.peak) && !r.is_diverging;
     if (!converging && !find_peak_only) s.reached_major_threshold = false;
     alg.settings.clean_mask = nullptr;
+    alg.settings.rms_factor = nullptr;  // :421-423
     if (ms_masks && masks->track && converging && !find_peak_only) {  // :425-462
       const size_t n_scales = alg.ms->Scales().size();
       if (masks->scale_masks.empty())

@@ -32,9 +32,13 @@ struct TiledAlgorithm {
 
 // ParallelDeconvolution's auto-mask state (parallel_deconvolution.cc:
 // 260-268, 359-390, 425-462): full-image masks per scale, 0/1 bytes.
+// Per-run state ParallelDeconvolution keeps across subimages: the per-scale
+// auto-masks (parallel_deconvolution.cc:359-462) and the full-image RMS
+// factor trimmed to each subimage (:244-250, 332-337, 421-423).
 struct ParallelMasks {
   bool track = false, use = false;
   std::vector<std::vector<unsigned char>> scale_masks;
+  std::vector<float> rms_factor;  // width x height, empty = none
 };
 
 struct ParallelResult {

@@ -72,6 +72,7 @@ struct HogbomArgs {
   const float* psfs;
   const uint8_t* mask;
   const float* spectral;  // n_images x n_images spectral-fit map, or nullptr
+  const float* rms;       // RMS factor image, or nullptr
   HogbomState* state;
   uint64_t* partials;
   uint32_t* trace;
@@ -127,12 +128,13 @@ __global__ __launch_bounds__(256) void HogbomPass(HogbomArgs a) {
         v[i] = r;
       }
       if (in_by && x >= a.bx0 && x < a.bx1 && (!a.mask || a.mask[idx])) {
-        const float integ = IntegratePixel(a.integ, [&](uint32_t k) {
+        float integ = IntegratePixel(a.integ, [&](uint32_t k) {
           float r = v[0];
 #pragma unroll
           for (int j = 1; j < NI; ++j) r = (uint32_t(j) == k) ? v[j] : r;
           return r;
         });
+        if (a.rms) integ *= a.rms[idx];  // GenericClean::FindPeak (:258-264)
         const uint64_t k = PeakKey(integ, a.allow_negative, idx);
         best = k > best ? k : best;
       }
@@ -201,7 +203,10 @@ __global__ __launch_bounds__(1024) void HogbomStep(HogbomArgs a, int init) {
     } else {
       st.found = 0;
     }
-    if (st.found) st.peak_value = IntegratedAt(a, st.peak_index);
+    if (st.found) {
+      st.peak_value = IntegratedAt(a, st.peak_index);
+      if (a.rms) st.peak_value *= a.rms[st.peak_index];
+    }
     if (st.found && a.divergence_limit != 0.0f)
       st.diverging = fabsf(st.peak_value) > a.initial_max * a.divergence_limit;
     st.iteration += 1;
@@ -247,6 +252,7 @@ int rdl_hogbom_run(rdl_session* s, float* d_residuals, float* d_models,
   a.psfs = d_psfs;
   a.mask = p->d_mask;
   a.spectral = p->d_spectral;
+  a.rms = p->d_rms;
   a.width = p->width;
   a.height = p->height;
   a.n_images = p->n_images;

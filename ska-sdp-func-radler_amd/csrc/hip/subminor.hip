@@ -61,6 +61,7 @@ struct SelArgs {
   rdl_integration integ;
   float threshold;
   int32_t allow_negative;
+  const float* rms;  // RMS factor image (W x H) or nullptr
 };
 
 __device__ __forceinline__ bool Selected(const SelArgs& a, uint64_t b,
@@ -70,8 +71,9 @@ __device__ __forceinline__ bool Selected(const SelArgs& a, uint64_t b,
   const uint32_t y = a.ys + uint32_t(b / a.bw);
   idx = y * a.width + x;
   if (a.mask && !a.mask[idx]) return false;
-  const float v = IntegratePixel(
+  float v = IntegratePixel(
       a.integ, [&](uint32_t k) { return a.residuals[size_t(k) * a.n + idx]; });
+  if (a.rms) v *= a.rms[idx];  // integratedScratch *= rms (subminor_loop.cc:147-149)
   const float value = a.allow_negative ? fabsf(v) : v;
   return value >= a.threshold;
 }
@@ -160,6 +162,7 @@ struct LoopArgs {
   float* m;               // [n_img][n_sel] (out: model values)
   const float* psfs;      // twice-convolved PSFs, W*H planes
   const float* spectral;  // n_img x n_img spectral-fit map, or nullptr
+  const float* rms;       // RMS factor image (W x H), or nullptr
   uint32_t* records;      // [2][G][rec_words] (G > 1)
   uint32_t* counter;      // arrival counter (G > 1), zeroed per launch
   uint32_t* result;       // LoopResult
@@ -193,6 +196,13 @@ __device__ __forceinline__ uint64_t MaxKey(float integ, bool allow_negative,
   uint32_t u = __float_as_uint(v);
   u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
   return (uint64_t(u) << 32) | uint64_t(0xffffffffu - uint32_t(p));
+}
+
+// The float MaxKey encoded (|v| when allow_negative).
+__device__ __forceinline__ float KeyValue(uint64_t key) {
+  uint32_t u = uint32_t(key >> 32);
+  u = (u & 0x80000000u) ? (u & 0x7fffffffu) : ~u;
+  return __uint_as_float(u);
 }
 
 __device__ __forceinline__ void StoreSc1(uint32_t* p, uint32_t v) {
@@ -287,12 +297,13 @@ __global__ __launch_bounds__(kLoopThreads) void SubminorLoop(LoopArgs a) {
         for (int k = 0; k < NI; ++k)
           v[k] = k < int(n_img) ? R[k * stride + j] : 0.0f;
       }
-      const float integ = IntegratePixel(a.integ, [&](uint32_t kk) {
+      float integ = IntegratePixel(a.integ, [&](uint32_t kk) {
         float r = v[0];
 #pragma unroll
         for (int q = 1; q < NI; ++q) r = (uint32_t(q) == kk) ? v[q] : r;
         return r;
       });
+      if (a.rms) integ *= a.rms[size_t(py) * a.width + px];  // GetMaxComponent
       uint64_t key = MaxKey(integ, a.allow_negative, base + j);
       if (base + j == 0 && integ != integ) key = ~0ull;  // scratch[0] is NaN
       best = key > best ? key : best;
@@ -323,12 +334,14 @@ __global__ __launch_bounds__(kLoopThreads) void SubminorLoop(LoopArgs a) {
 #pragma unroll
         for (int k = 0; k < NI; ++k)
           vv[k] = k < int(n_img) ? R[k * stride + j] : 0.0f;
-        const float integ = IntegratePixel(a.integ, [&](uint32_t kk) {
+        float integ = IntegratePixel(a.integ, [&](uint32_t kk) {
           float r = vv[0];
 #pragma unroll
           for (int q = 1; q < NI; ++q) r = (uint32_t(q) == kk) ? vv[q] : r;
           return r;
         });
+        if (a.rms)
+          integ *= a.rms[size_t(pos[j] >> 16) * a.width + (pos[j] & 0xffffu)];
         win[2] = __float_as_uint(integ);
         win[3] = pos[j];
         for (uint32_t k = 0; k < n_img; ++k) win[4 + k] = __float_as_uint(vv[k]);
@@ -703,11 +716,15 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopReg(LoopArgs a) {
   uint32_t pos[ITEMS];
   float R[ITEMS][NI];
   float M[ITEMS][NI];
+  float F[ITEMS];  // RMS factor of each pixel (1 without one)
 #pragma unroll
   for (int i = 0; i < ITEMS; ++i) {
     const uint32_t j = tid + uint32_t(i) * THREADS;
     const bool valid = j < cnt;
     pos[i] = valid ? a.pos[base + j] : 0u;
+    F[i] = (valid && a.rms)
+               ? a.rms[size_t(pos[i] >> 16) * a.width + (pos[i] & 0xffffu)]
+               : 1.0f;
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
       R[i][k] = (valid && k < n_img) ? a.r[size_t(k) * a.n_sel + base + j] : 0.0f;
@@ -769,12 +786,13 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopReg(LoopArgs a) {
     for (int i = 0; i < ITEMS; ++i) {
       const uint32_t j = tid + uint32_t(i) * THREADS;
       if (j < cnt) {
-        const float integ = FAST ? R[i][0] : IntegratePixel(a.integ, [&](uint32_t kk) {
+        float integ = FAST ? R[i][0] : IntegratePixel(a.integ, [&](uint32_t kk) {
           float r = R[i][0];
 #pragma unroll
           for (int q = 1; q < NI; ++q) r = (uint32_t(q) == kk) ? R[i][q] : r;
           return r;
         });
+        if (a.rms) integ *= F[i];  // scratch *= rms (subminor_loop.cc:16-18)
         uint64_t key = MaxKey(integ, a.allow_negative, base + j);
         if (base + j == 0 && integ != integ) key = ~0ull;  // scratch[0] is NaN
         if (key > best) {
@@ -954,6 +972,14 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopReg(LoopArgs a) {
       for (int q = 1; q < NI; ++q) r = (uint32_t(q) == kk) ? wr[q] : r;
       return r;
     });
+    if (a.rms) {
+      // the winner's integrated x factor is the value its key was made from
+      // (with its sign from the integrated value, the factor being >= 0)
+      const float kv = KeyValue(gkey);
+      m = (gkey == 0 || gkey == ~0ull) ? __int_as_float(0x7fc00000)
+          : a.allow_negative            ? copysignf(kv, m)
+                                        : kv;
+    }
     if (!have_component) {
       start_abs = fabsf(m);
     } else {
@@ -1177,6 +1203,7 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   sa.integ = p->integ;
   sa.threshold = p->threshold;
   sa.allow_negative = p->allow_negative;
+  sa.rms = p->d_rms;
   const uint32_t n_chunks =
       std::max<uint32_t>(1, rdl::DivUp(sa.box_pixels, rdl::kChunk));
   RDL_TRY(rdl::Grow(&h->counts, &h->counts_bytes,
@@ -1290,6 +1317,7 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   la.threshold = p->threshold;
   la.gain = p->gain;
   la.spectral = p->d_spectral;
+  la.rms = p->d_rms;
   la.divergence_limit = p->divergence_limit;
   la.iteration_start = p->iteration_start;
   la.max_iterations = p->max_iterations;

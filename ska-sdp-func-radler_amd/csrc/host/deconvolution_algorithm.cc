@@ -48,4 +48,28 @@ const float* DeconvolutionAlgorithm::DeviceSpectralMap(gpu::Session& s,
   return spectral_map_identity_ ? nullptr : spectral_map_->F();
 }
 
+const float* DeconvolutionAlgorithm::DeviceRmsFactor(gpu::Session& s, size_t width,
+                                                     size_t height) {
+  if (!rms_factor_) return nullptr;
+  const size_t n = width * height;
+  if (rms_factor_->size() != n)
+    throw std::runtime_error("RMS factor image does not match the image size");
+  if (!rms_device_ || rms_device_session_ != &s) {
+    rms_device_ = std::make_shared<gpu::Buffer>(s, n * sizeof(float));
+    s.H2D(rms_device_->Ptr(), rms_factor_->data(), n * sizeof(float));
+    rms_device_session_ = &s;
+  }
+  return rms_device_->F();
+}
+
+const float* DeconvolutionAlgorithm::RmsWeighted(gpu::Session& s, const float* d_image,
+                                                 float* d_scratch, size_t width,
+                                                 size_t height) {
+  const float* rms = DeviceRmsFactor(s, width, height);
+  if (!rms) return d_image;
+  gpu::Check(rdl_multiply(s.Handle(), d_scratch, d_image, rms, width * height),
+             "rdl_multiply");
+  return d_scratch;
+}
+
 }  // namespace radler::algorithms

@@ -88,6 +88,16 @@ class DeconvolutionAlgorithm {
   }
   bool HasSpectralFitter() const { return spectral_fitter_ != nullptr; }
 
+  // deconvolution_algorithm.h:163-166: width x height factors every peak
+  // search multiplies in (local-RMS thresholding); nullptr clears it
+  void SetRmsFactorImage(std::shared_ptr<const std::vector<float>> image) {
+    rms_factor_ = std::move(image);
+    rms_device_.reset();
+  }
+  const std::shared_ptr<const std::vector<float>>& RmsFactorImage() const {
+    return rms_factor_;
+  }
+
  protected:
   DeconvolutionAlgorithm() = default;
   // Clones share settings, fitter and iteration count, not device scratch.
@@ -95,7 +105,8 @@ class DeconvolutionAlgorithm {
       : settings_(o.settings_),
         iteration_number_(o.iteration_number_),
         spectral_fitter_(o.spectral_fitter_),
-        n_polarizations_(o.n_polarizations_) {}
+        n_polarizations_(o.n_polarizations_),
+        rms_factor_(o.rms_factor_) {}
 
   /// Device copy (uint8) of CleanMask() for the current call, or nullptr.
   const uint8_t* DeviceCleanMask(gpu::Session& s, size_t width, size_t height);
@@ -107,6 +118,12 @@ class DeconvolutionAlgorithm {
   /// loops (rdl_subminor_params / rdl_hogbom_params d_spectral); nullptr
   /// when the fit leaves values unchanged.
   const float* DeviceSpectralMap(gpu::Session& s, size_t n_images);
+  /// Device copy of RmsFactorImage() on session s, or nullptr.
+  const float* DeviceRmsFactor(gpu::Session& s, size_t width, size_t height);
+  /// The peak-search input: d_image itself, or d_image x the RMS factor in
+  /// d_scratch (generic_clean.cc:258-264, multiscale_algorithm.cc:707-713).
+  const float* RmsWeighted(gpu::Session& s, const float* d_image, float* d_scratch,
+                           size_t width, size_t height);
 
  private:
   struct {
@@ -130,6 +147,9 @@ class DeconvolutionAlgorithm {
   std::shared_ptr<gpu::Buffer> spectral_map_;
   size_t spectral_map_images_ = 0;
   bool spectral_map_identity_ = false;
+  std::shared_ptr<const std::vector<float>> rms_factor_;
+  std::shared_ptr<gpu::Buffer> rms_device_;
+  gpu::Session* rms_device_session_ = nullptr;
 };
 
 }  // namespace radler::algorithms

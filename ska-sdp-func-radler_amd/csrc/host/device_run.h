@@ -49,6 +49,13 @@ class DeviceRun {
   void SetCommunicator(std::shared_ptr<Communicator> comm) {
     parallel_->SetCommunicator(std::move(comm));
   }
+  /// ParallelDeconvolution::SetRmsFactorImage (an empty vector clears it).
+  void SetRmsFactorImage(std::vector<float> factor) {
+    parallel_->SetRmsFactorImage(
+        factor.empty() ? nullptr
+                       : std::make_shared<const std::vector<float>>(std::move(factor)),
+        settings_.trimmed_image_width);
+  }
   void Sync() { session_->Sync(); }
 
  private:

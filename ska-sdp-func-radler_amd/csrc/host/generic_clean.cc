@@ -16,8 +16,14 @@ GenericClean::GenericClean(bool use_sub_minor_optimization)
 
 rdl_peak GenericClean::FindPeak(gpu::Session& s, const float* d_image,
                                 size_t width, size_t height,
-                                const uint8_t* d_mask) const {
-  // :255-277 -> peak_finder::Find(border ratio) / FindWithMask
+                                const uint8_t* d_mask) {
+  // :255-277 -> peak_finder::Find(border ratio) / FindWithMask, on the image
+  // times the RMS factor when there is one
+  if (RmsFactorImage()) {
+    if (!rms_scratch_ || rms_scratch_->Bytes() < width * height * sizeof(float))
+      rms_scratch_ = std::make_shared<gpu::Buffer>(s, width * height * sizeof(float));
+    d_image = RmsWeighted(s, d_image, rms_scratch_->F(), width, height);
+  }
   const uint32_t hb = uint32_t(std::round(width * CleanBorderRatio()));
   const uint32_t vb = uint32_t(std::round(height * CleanBorderRatio()));
   rdl_peak p;
@@ -75,6 +81,7 @@ DeconvolutionResult GenericClean::ExecuteMajorIteration(
     sub.SetDivergenceLimit(DivergenceLimit());
     sub.SetMask(d_mask);
     sub.SetSpectralMap(DeviceSpectralMap(s, dirty_set.Size()));
+    sub.SetRmsFactor(DeviceRmsFactor(s, width, height));  // :126-128
     sub.SetCleanBorders(size_t(std::round(width * CleanBorderRatio())),
                         size_t(std::round(height * CleanBorderRatio())));
     sub.SetTrace(&trace_);
@@ -116,6 +123,7 @@ DeconvolutionResult GenericClean::ExecuteMajorIteration(
     p.v_border = uint32_t(std::round(height * CleanBorderRatio()));
     p.d_mask = d_mask;
     p.d_spectral = DeviceSpectralMap(s, dirty_set.Size());
+    p.d_rms = DeviceRmsFactor(s, width, height);
     p.start_x = max_value.x;
     p.start_y = max_value.y;
     p.start_value = max_value.value;

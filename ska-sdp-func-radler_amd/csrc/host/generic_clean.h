@@ -3,6 +3,8 @@
 // sub-minor loop and an FFT residual correction.
 #pragma once
 
+#include <memory>
+
 #include "deconvolution_algorithm.h"
 
 namespace radler::algorithms {
@@ -24,11 +26,12 @@ class GenericClean final : public DeconvolutionAlgorithm {
 
  private:
   rdl_peak FindPeak(gpu::Session& s, const float* d_image, size_t width,
-                    size_t height, const uint8_t* d_mask) const;
+                    size_t height, const uint8_t* d_mask);
 
   const float convolution_padding_;
   bool use_sub_minor_optimization_;
   std::vector<uint32_t> trace_;
+  std::shared_ptr<gpu::Buffer> rms_scratch_;  // image x RMS factor
 };
 
 }  // namespace radler::algorithms

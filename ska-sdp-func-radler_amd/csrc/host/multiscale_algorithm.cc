@@ -105,10 +105,24 @@ void MultiScaleAlgorithm::DownloadScaleMasks() {
     masks_session_->D2H(host_masks_[i].data(), dev_masks_[i].Ptr(), host_masks_[i].size());
 }
 
+const float* MultiScaleAlgorithm::PeakSearchInput(const float* d_image, size_t w,
+                                                 size_t h) {
+  if (!RmsFactorImage()) return d_image;
+  if (!rms_scratch_ || rms_scratch_->Bytes() < w * h * sizeof(float))
+    rms_scratch_ = std::make_shared<gpu::Buffer>(*session_, w * h * sizeof(float));
+  return RmsWeighted(*session_, d_image, rms_scratch_->F(), w, h);
+}
+
+float MultiScaleAlgorithm::Normalized(float value, size_t x, size_t y, size_t w) const {
+  if (!RmsFactorImage()) return value;
+  return value / (*RmsFactorImage())[x + y * w];
+}
+
 void MultiScaleAlgorithm::FindPeakDirect(const float* d_image,
                                          size_t scale_index) {  // :700-748
   ScaleInfo& info = scale_infos_[scale_index];
   const size_t w = transforms_->Width(), h = transforms_->Height();
+  d_image = PeakSearchInput(d_image, w, h);
   const uint32_t hb = uint32_t(std::round(w * CleanBorderRatio()));
   const uint32_t vb = uint32_t(std::round(h * CleanBorderRatio()));
   rdl_peak p;
@@ -119,7 +133,7 @@ void MultiScaleAlgorithm::FindPeakDirect(const float* d_image,
   info.max_image_value_x = p.x;
   info.max_image_value_y = p.y;
   info.max_unnormalized_image_value = p.found ? p.value : 0.0f;
-  info.max_normalized_image_value = p.found ? p.value : 0.0f;
+  info.max_normalized_image_value = p.found ? Normalized(p.value, p.x, p.y, w) : 0.0f;
 }
 
 void MultiScaleAlgorithm::FindActiveScaleConvolvedMaxima(
@@ -170,11 +184,11 @@ void MultiScaleAlgorithm::FindActiveScaleConvolvedMaxima(
     if (report_rms)
       gpu::Check(rdl_rms(s, d_conv, w * h, &e.rms), "rdl_rms");
     rdl_peak p;
-    gpu::Check(rdl_find_peak(s, d_conv, uint32_t(w), uint32_t(h), 0,
+    gpu::Check(rdl_find_peak(s, PeakSearchInput(d_conv, w, h), uint32_t(w), uint32_t(h), 0,
                              uint32_t(h), xb, yb, AllowNegativeComponents(),
                              MaskFor(si), 1, &p),
                "rdl_find_peak");
-    e.max_normalized_image_value = p.found ? p.value : 0.0f;
+    e.max_normalized_image_value = p.found ? Normalized(p.value, p.x, p.y, w) : 0.0f;
     e.max_unnormalized_image_value = p.found ? p.value : 0.0f;
     e.max_image_value_x = p.x;
     e.max_image_value_y = p.y;
@@ -377,6 +391,7 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
                            scale_border));
       sub.SetMask(MaskFor(scale_with_peak));
       sub.SetSpectralMap(DeviceSpectralMap(session, data_image.Size()));
+      sub.SetRmsFactor(DeviceRmsFactor(session, width, height));  // :401-402
       std::vector<uint32_t> xy;
       sub.SetTrace(&xy);
       const SubMinorLoop::RunResult r = sub.Run(individual, twice);

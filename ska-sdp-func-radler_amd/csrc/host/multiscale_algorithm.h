@@ -100,6 +100,11 @@ class MultiScaleAlgorithm final : public DeconvolutionAlgorithm {
   std::unique_ptr<multiscale::MultiScaleTransforms> transforms_;
   const uint8_t* d_mask_ = nullptr;
   std::shared_ptr<gpu::Buffer> scratch_;  // W x H
+  std::shared_ptr<gpu::Buffer> rms_scratch_;  // W x H: image x RMS factor
+  /// d_image, or d_image x the RMS factor (multiscale_algorithm.cc:707-713)
+  const float* PeakSearchInput(const float* d_image, size_t w, size_t h);
+  /// unnormalized / factor at the peak (:736-743), the value itself without
+  float Normalized(float value, size_t x, size_t y, size_t w) const;
   std::shared_ptr<gpu::Buffer> spectrum_, spectrum_work_;
   // One image with the identity integration (ImageSet copy fast path): the
   // integrated image IS the residual, so the scale-convolved images that

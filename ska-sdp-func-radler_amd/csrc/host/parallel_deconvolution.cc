@@ -122,6 +122,16 @@ void ParallelDeconvolution::StoreScaleMasks(
       }
 }
 
+void ParallelDeconvolution::SetRmsFactorImage(
+    std::shared_ptr<const std::vector<float>> image, size_t width) {
+  if (algorithms_.size() == 1) {
+    algorithms_.front()->SetRmsFactorImage(std::move(image));
+  } else {
+    rms_image_ = std::move(image);
+    rms_width_ = width;
+  }
+}
+
 void ParallelDeconvolution::SetCleanMask(const bool* mask) {
   if (algorithms_.size() == 1)
     algorithms_.front()->SetCleanMask(mask);
@@ -320,6 +330,13 @@ bool ParallelDeconvolution::DeconvolveSubImage(SubImage& sub, ImageSet& sub_data
   DeconvolutionAlgorithm& alg = *algorithms_[sub.index];
   std::vector<char> mask_copy(sub.mask.begin(), sub.mask.end());
   alg.SetCleanMask(reinterpret_cast<const bool*>(mask_copy.data()));
+  if (rms_image_) {  // rms_image_.TrimBox (:332-337)
+    auto sub_rms = std::make_shared<std::vector<float>>(sub.width * sub.height);
+    for (size_t y = 0; y != sub.height; ++y)
+      std::copy_n(rms_image_->data() + (sub.y + y) * rms_width_ + sub.x, sub.width,
+                  sub_rms->data() + y * sub.width);
+    alg.SetRmsFactorImage(std::move(sub_rms));
+  }
   const size_t max_n_iter = alg.MaxIterations();
   if (find_peak_only)
     alg.SetMaxIterations(0);
@@ -329,6 +346,7 @@ bool ParallelDeconvolution::DeconvolveSubImage(SubImage& sub, ImageSet& sub_data
   const DeconvolutionResult result =
       alg.ExecuteMajorIteration(sub_data, sub_model, sub_psfs);
   alg.SetCleanMask(nullptr);
+  if (rms_image_) alg.SetRmsFactorImage(nullptr);  // :421-423
   sub.peak = result.final_peak_value;
   sub.reached_major_threshold = result.another_iteration_required;
   const bool converging =

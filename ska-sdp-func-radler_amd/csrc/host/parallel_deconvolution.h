@@ -46,6 +46,10 @@ class ParallelDeconvolution {
   void SetThreshold(double threshold);
   void SetMinorLoopGain(double gain);
   void SetCleanMask(const bool* mask);
+  /// parallel_deconvolution.cc:244-250: the single algorithm takes it as
+  /// is; gridded runs trim each subimage's box (:332-337) and drop it after
+  /// the run (:421-423). nullptr clears it.
+  void SetRmsFactorImage(std::shared_ptr<const std::vector<float>> image, size_t width);
   /// Auto-masking (parallel_deconvolution.cc:260-268): passed to the
   /// multiscale algorithms; gridded runs keep full-image per-scale masks and
   /// hand each subimage its box (:359-390), merging it back inside the
@@ -129,6 +133,8 @@ class ParallelDeconvolution {
   std::vector<SubImage> subimages_;
   const Settings& settings_;
   const bool* mask_ = nullptr;
+  std::shared_ptr<const std::vector<float>> rms_image_;  // full image (gridded)
+  size_t rms_width_ = 0;
   std::shared_ptr<Communicator> comm_;
   bool track_masks_ = false, use_masks_ = false;
   std::vector<std::vector<uint8_t>> scale_masks_;  // full image, per scale

@@ -12,6 +12,7 @@
 #include "iuwt_deconvolution.h"
 #include "multiscale_algorithm.h"
 #include "parallel_deconvolution.h"
+#include "rms_image.h"
 
 namespace radler {
 
@@ -116,42 +117,63 @@ void Radler::Perform(bool& another_iteration_required,
 
   const bool auto_mask_is_enabled =
       settings_.auto_mask_sigma || settings_.absolute_auto_mask_threshold;
-  if (settings_.local_rms.method != LocalRmsMethod::kNone ||
-      !settings_.local_rms.image.empty())
-    Unsupported("Local-RMS thresholding");
-  // :167-183: once the auto-mask is complete a more aggressive gain is used
-  if (auto_mask_is_enabled && auto_mask_is_finished_)
-    parallel_deconvolution_->SetMinorLoopGain(
-        std::min(1.0, settings_.minor_loop_gain * 2.0));
-  else
-    parallel_deconvolution_->SetMinorLoopGain(settings_.minor_loop_gain);
-
-  if (settings_.auto_threshold_sigma || auto_mask_is_enabled) {
+  const bool local_rms = settings_.local_rms.method != LocalRmsMethod::kNone;
+  if (!settings_.local_rms.image.empty())
+    Unsupported("A local-RMS image file (FITS input)");
+  const size_t n_px = image_width_ * image_height_;
+  gpu::Buffer integrated;
+  double median = 0.0, stddev = 0.0;
+  if (settings_.auto_threshold_sigma || auto_mask_is_enabled || local_rms) {
     // integrated.MedianAndStdDevFromMAD() (:162-166) on the device
-    gpu::Buffer integrated(s, image_width_ * image_height_ * sizeof(float));
+    integrated = gpu::Buffer(s, n_px * sizeof(float));
     residual_set.GetLinearIntegrated(integrated.F());
-    const size_t n = image_width_ * image_height_;
-    float median = 0.0f, mad = 0.0f;
-    gpu::Check(rdl_median(s.Handle(), integrated.F(), n, 0, 0.0f, &median),
-               "rdl_median");
-    gpu::Check(rdl_median(s.Handle(), integrated.F(), n, 1, median, &mad),
-               "rdl_median");
-    const double stddev = double(mad) * 1.48260221850560;
+    float med = 0.0f, mad = 0.0f;
+    gpu::Check(rdl_median(s.Handle(), integrated.F(), n_px, 0, 0.0f, &med), "rdl_median");
+    gpu::Check(rdl_median(s.Handle(), integrated.F(), n_px, 1, med, &mad), "rdl_median");
+    median = med;
+    stddev = double(mad) * 1.48260221850560;
     log::Info() << "Estimated standard deviation of background noise: "
                 << stddev << '\n';
-    // :228-243
-    const double threshold_bias = settings_.squared_joins ? median : 0.0;
-    if (auto_mask_is_enabled && !auto_mask_is_finished_) {
-      const double combined_auto_mask_threshold =
-          std::max(stddev * settings_.auto_mask_sigma.value_or(0.0) + threshold_bias,
-                   settings_.absolute_auto_mask_threshold.value_or(0.0));
-      parallel_deconvolution_->SetThreshold(
-          std::max(combined_auto_mask_threshold, settings_.absolute_threshold));
-    } else if (settings_.auto_threshold_sigma) {
-      parallel_deconvolution_->SetThreshold(
-          std::max(stddev * (*settings_.auto_threshold_sigma) + threshold_bias,
-                   settings_.absolute_threshold));
+  }
+  if (auto_mask_is_enabled && auto_mask_is_finished_) {
+    // :172-185: once the auto-mask is complete a more aggressive gain is
+    // used, and the RMS background no longer
+    parallel_deconvolution_->SetMinorLoopGain(
+        std::min(1.0, settings_.minor_loop_gain * 2.0));
+    parallel_deconvolution_->SetRmsFactorImage(nullptr, image_width_);
+  } else {
+    parallel_deconvolution_->SetMinorLoopGain(settings_.minor_loop_gain);
+    if (local_rms) {  // :196-216
+      gpu::Buffer rms(s, n_px * sizeof(float));
+      if (settings_.local_rms.method == LocalRmsMethod::kRmsWindow)
+        math::rms_image::Make(s, rms.F(), integrated.F(), image_width_, image_height_,
+                              settings_.local_rms.window, beam_size_, beam_size_, 0.0,
+                              pixel_scale_x_, pixel_scale_y_);
+      else
+        math::rms_image::MakeWithNegativityLimit(
+            s, rms.F(), integrated.F(), image_width_, image_height_,
+            settings_.local_rms.window, beam_size_, beam_size_, 0.0, pixel_scale_x_,
+            pixel_scale_y_);
+      stddev = math::rms_image::MakeRmsFactorImage(s, rms.F(), n_px,
+                                                   settings_.local_rms.strength);
+      log::Info() << "Lowest RMS in image: " << stddev << '\n';
+      auto factor = std::make_shared<std::vector<float>>(n_px);
+      s.D2H(factor->data(), rms.F(), n_px * sizeof(float));
+      parallel_deconvolution_->SetRmsFactorImage(std::move(factor), image_width_);
     }
+  }
+  // :228-243
+  const double threshold_bias = settings_.squared_joins ? median : 0.0;
+  if (auto_mask_is_enabled && !auto_mask_is_finished_) {
+    const double combined_auto_mask_threshold =
+        std::max(stddev * settings_.auto_mask_sigma.value_or(0.0) + threshold_bias,
+                 settings_.absolute_auto_mask_threshold.value_or(0.0));
+    parallel_deconvolution_->SetThreshold(
+        std::max(combined_auto_mask_threshold, settings_.absolute_threshold));
+  } else if (settings_.auto_threshold_sigma) {
+    parallel_deconvolution_->SetThreshold(
+        std::max(stddev * (*settings_.auto_threshold_sigma) + threshold_bias,
+                 settings_.absolute_threshold));
   }
 
   // :249-275: multiscale tracks per-scale masks until the auto-mask

@@ -15,6 +15,7 @@
 #include "image_accessors.h"
 #include "logger.h"
 #include "radler.h"
+#include "rms_image.h"
 
 namespace py = pybind11;
 using AccessorList = std::vector<std::unique_ptr<aocommon::ImageAccessor>>;
@@ -484,6 +485,55 @@ void InitDistributed(py::module& m) {
 void InitGpu(py::module& m) {
   py::module g = m.def_submodule("gpu", "MI355X device helpers (bench/tests)");
   g.def("set_verbosity", &radler::log::SetVerbosity);
+  g.def(
+      "local_rms",
+      [](FloatArray integrated, int method, double window, double beam,
+         double pixel_scale_x, double pixel_scale_y, double strength) {
+        // Radler::Perform's local-RMS step on the device (cpp/radler.cc:196-216)
+        if (integrated.ndim() != 2) throw std::runtime_error("expected a 2-D image");
+        const size_t h = integrated.shape(0), w = integrated.shape(1), n = w * h;
+        std::shared_ptr<radler::gpu::Session> session =
+            radler::gpu::Session::ForDevice(radler::gpu::Session::DefaultDevice());
+        radler::gpu::Session& s = *session;
+        radler::gpu::Buffer in(s, n * sizeof(float)), rms(s, n * sizeof(float));
+        s.H2D(in.Ptr(), integrated.data(), n * sizeof(float));
+        py::array_t<float> out_rms({h, w}), out_factor({h, w});
+        double lowest = 0.0;
+        {
+          py::gil_scoped_release release;
+          if (method == 1)
+            radler::math::rms_image::Make(s, rms.F(), in.F(), w, h, window, beam, beam,
+                                          0.0, pixel_scale_x, pixel_scale_y);
+          else
+            radler::math::rms_image::MakeWithNegativityLimit(
+                s, rms.F(), in.F(), w, h, window, beam, beam, 0.0, pixel_scale_x,
+                pixel_scale_y);
+          s.D2H(out_rms.mutable_data(), rms.F(), n * sizeof(float));
+          lowest = radler::math::rms_image::MakeRmsFactorImage(s, rms.F(), n, strength);
+          s.D2H(out_factor.mutable_data(), rms.F(), n * sizeof(float));
+        }
+        return py::make_tuple(out_rms, out_factor, lowest);
+      },
+      py::arg("integrated"), py::arg("method"), py::arg("window"), py::arg("beam"),
+      py::arg("pixel_scale_x"), py::arg("pixel_scale_y"), py::arg("strength") = 1.0);
+  g.def(
+      "sliding_minimum",
+      [](FloatArray image, size_t window) {
+        if (image.ndim() != 2) throw std::runtime_error("expected a 2-D image");
+        const size_t h = image.shape(0), w = image.shape(1), n = w * h;
+        std::shared_ptr<radler::gpu::Session> session =
+            radler::gpu::Session::ForDevice(radler::gpu::Session::DefaultDevice());
+        radler::gpu::Session& s = *session;
+        radler::gpu::Buffer in(s, n * sizeof(float)), out(s, n * sizeof(float)),
+            scratch(s, 3 * n * sizeof(float));
+        s.H2D(in.Ptr(), image.data(), n * sizeof(float));
+        radler::math::rms_image::SlidingMinimum(s, out.F(), in.F(), scratch.F(), w, h,
+                                                window);
+        py::array_t<float> result({h, w});
+        s.D2H(result.mutable_data(), out.F(), n * sizeof(float));
+        return result;
+      },
+      py::arg("image"), py::arg("window"));
   py::class_<radler::DeviceRun>(g, "DeviceRun")
       .def(py::init([](const radler::Settings& settings, FloatArray psf,
                        FloatArray residual, std::vector<double> weights,
@@ -497,6 +547,11 @@ void InitGpu(py::module& m) {
       .def("restore", &radler::DeviceRun::Restore)
       .def("set_communicator", &radler::DeviceRun::SetCommunicator,
            py::arg("communicator"))
+      .def("set_rms_factor",
+           [](radler::DeviceRun& self, const std::vector<float>& factor) {
+             self.SetRmsFactorImage(factor);
+           },
+           py::arg("factor"))
       .def("execute",
            [](radler::DeviceRun& self) {
              radler::algorithms::ParallelDeconvolutionResult r;

@@ -183,6 +183,36 @@ class Oracle:
             d.fit_frequencies, d.fit_weights = d._ff.ctypes.data, d._fw.ctypes.data
         return d
 
+    def local_rms(self, integrated, method, window, beam, pixel_scale_x, pixel_scale_y,
+                  strength=1.0):
+        """Radler::Perform's local-RMS step (method 1 = rms_window, 2 =
+        rms_and_minimum_window) -> (rms image, factor image, lowest rms)."""
+        img = np.ascontiguousarray(integrated, np.float32)
+        h, w = img.shape
+        rms = np.zeros_like(img)
+        factor = np.zeros_like(img)
+        lowest = C.c_double()
+        L = self.lib
+        L.orc_local_rms.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_int, C.c_double,
+                                    C.c_double, C.c_double, C.c_double, C.c_double,
+                                    C.c_void_p, C.c_void_p, C.POINTER(C.c_double)]
+        if L.orc_local_rms(img.ctypes.data, w, h, int(method), float(window), float(beam),
+                           float(pixel_scale_x), float(pixel_scale_y), float(strength),
+                           rms.ctypes.data, factor.ctypes.data, C.byref(lowest)) != 0:
+            raise RuntimeError(self.lib.orc_last_error().decode())
+        return rms, factor, lowest.value
+
+    def sliding_minimum(self, image, window):
+        img = np.ascontiguousarray(image, np.float32)
+        h, w = img.shape
+        out = np.zeros_like(img)
+        L = self.lib
+        L.orc_sliding_minimum.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64,
+                                          C.c_void_p]
+        L.orc_sliding_minimum.restype = None
+        L.orc_sliding_minimum(img.ctypes.data, w, h, int(window), out.ctypes.data)
+        return out
+
     def spectral_fit(self, mode, n_terms, frequencies, weights, values):
         """SpectralFitter FitAndEvaluate -> (evaluated values, terms)."""
         f = np.ascontiguousarray(frequencies, np.float64)
@@ -236,6 +266,17 @@ class OracleAlgorithm:
     def set_spectral_fitter(self, mode, n_terms, frequencies, weights):
         """DeconvolutionAlgorithm::SetSpectralFitter (polynomial: mode 1)."""
         self.spectral = (mode, n_terms, frequencies, weights)
+
+    def set_rms(self, factor):
+        """DeconvolutionAlgorithm::SetRmsFactorImage (None clears it)."""
+        L = self.o.lib
+        L.orc_algo_set_rms.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
+        L.orc_algo_set_rms.restype = None
+        if factor is None:
+            L.orc_algo_set_rms(self.h, None, 0)
+        else:
+            f = np.ascontiguousarray(factor, np.float32)
+            L.orc_algo_set_rms(self.h, f.ctypes.data, f.size)
 
     def update(self, **settings):
         self.settings = algo_settings(**settings)
@@ -366,6 +407,17 @@ class OracleParallel:
         """True: every subimage of a pass trims the residual as it was at the
         start of the pass (the product's concurrent pool, max_threads > 1)."""
         self.o.lib.orc_parallel_set_snapshot(self.h, 1 if snapshot else 0)
+
+    def set_rms(self, factor):
+        """ParallelDeconvolution::SetRmsFactorImage (None clears it)."""
+        L = self.o.lib
+        L.orc_parallel_set_rms.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
+        L.orc_parallel_set_rms.restype = None
+        if factor is None:
+            L.orc_parallel_set_rms(self.h, None, 0)
+        else:
+            f = np.ascontiguousarray(factor, np.float32)
+            L.orc_parallel_set_rms(self.h, f.ctypes.data, f.size)
 
     def set_automask(self, track, use):
         L = self.o.lib

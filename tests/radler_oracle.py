@@ -27,7 +27,7 @@ class OraclePerform:
                  absolute_threshold=0.0, auto_mask_sigma=None, auto_threshold_sigma=None,
                  absolute_auto_mask_threshold=None, minor_iteration_count=1000,
                  major_iteration_count=20, major_auto_mask_iteration_count=2,
-                 grid=None, snapshot=False, **algo_settings):
+                 grid=None, snapshot=False, local_rms=None, **algo_settings):
         self.orc, self.kind = orc, kind
         self.psf = psf[None].astype(np.float32)
         self.residual = dirty[None].astype(np.float32).copy()
@@ -45,6 +45,8 @@ class OraclePerform:
         self.finishing_iteration = 0
         self.auto_mask = None
         self.grid = grid
+        # local_rms: None or dict(method=1|2, window, strength, beam, pixel_scale)
+        self.local_rms = local_rms
         if grid is None:
             self.alg = OracleAlgorithm(orc, kind, **self._settings(self.gain, None))
         else:  # ParallelDeconvolution::ExecuteParallelRun (oracle/tiling.cc)
@@ -65,9 +67,19 @@ class OraclePerform:
         """One Perform(major): returns another_iteration_required."""
         enabled = self.am_sigma is not None or self.abs_am is not None
         gain = min(1.0, self.gain * 2.0) if (enabled and self.finished) else self.gain
-        if self.at_sigma is not None or enabled:
+        if self.at_sigma is not None or enabled or self.local_rms:
             med, stddev = median_and_stddev_from_mad(self.residual[0])
             bias = 0.0
+            if enabled and self.finished:  # cpp/radler.cc:172-185
+                if self.local_rms:
+                    self.alg.set_rms(None)
+            elif self.local_rms:  # cpp/radler.cc:196-216
+                lr = self.local_rms
+                _, factor, stddev = self.orc.local_rms(
+                    self.residual[0], lr["method"], lr["window"], lr["beam"],
+                    lr["pixel_scale"], lr["pixel_scale"], lr.get("strength", 1.0))
+                self.alg.set_rms(factor)
+                self.last_rms_factor = factor
             if enabled and not self.finished:
                 am = max(stddev * (self.am_sigma or 0.0) + bias, self.abs_am or 0.0)
                 self.threshold = max(am, self.abs_thr)

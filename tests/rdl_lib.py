@@ -67,7 +67,7 @@ class HogbomParams(C.Structure):
                 ("v_border", C.c_uint32), ("d_mask", C.c_void_p),
                 ("start_x", C.c_uint32), ("start_y", C.c_uint32),
                 ("start_value", C.c_float), ("start_found", C.c_int32),
-                ("d_spectral", C.c_void_p)]
+                ("d_spectral", C.c_void_p), ("d_rms", C.c_void_p)]
 
 
 class HogbomResult(C.Structure):
@@ -82,7 +82,8 @@ class SubminorParams(C.Structure):
                 ("stop_on_negative", C.c_int32), ("threshold", C.c_float),
                 ("gain", C.c_float), ("divergence_limit", C.c_float),
                 ("iteration_start", C.c_uint64), ("max_iterations", C.c_uint64),
-                ("d_mask", C.c_void_p), ("d_spectral", C.c_void_p)]
+                ("d_mask", C.c_void_p), ("d_spectral", C.c_void_p),
+                ("d_rms", C.c_void_p)]
 
 
 class SubminorResult(C.Structure):
