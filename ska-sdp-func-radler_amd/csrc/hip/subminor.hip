@@ -44,6 +44,8 @@ struct rdl_subminor {
   uint32_t target_per_block = 1024;  // pixels per workgroup (multi-workgroup)
   uint32_t single_max = 2048;         // largest selection kept on one workgroup
   uint32_t wave_max = 128;            // largest selection on the single-wave kernel
+  uint32_t big_max = 3584;            // largest selection on one 1024-thread workgroup
+  uint32_t big_target = 0;            // > 0: larger selections on 1024-thread grids
 };
 
 namespace rdl {
@@ -649,6 +651,19 @@ __device__ __forceinline__ uint64_t Max8U64(uint64_t v) {
   v = t > v ? t : v;
   return ReadLaneU64(v, 0);
 }
+// Max over lanes 0..15 (others must hold 0); uniform result.
+__device__ __forceinline__ uint64_t Max16U64(uint64_t v) {
+  uint64_t t;
+  t = DppU64<0xb1>(v);
+  v = t > v ? t : v;
+  t = DppU64<0x4e>(v);
+  v = t > v ? t : v;
+  t = DppU64<0x141>(v);
+  v = t > v ? t : v;
+  t = DppU64<0x140>(v);  // row_mirror
+  v = t > v ? t : v;
+  return ReadLaneU64(v, 0);
+}
 // Max over the 64 lanes; uniform result.
 __device__ __forceinline__ uint64_t Max64U64(uint64_t v) {
   uint64_t t;
@@ -869,7 +884,7 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopReg(LoopArgs a) {
 #pragma unroll
       for (int k = 0; k < NI; ++k) sr[k] = sl.r[k];
     }
-    const uint64_t bkey = Max8U64(sk);
+    const uint64_t bkey = WAVES <= 8 ? Max8U64(sk) : Max16U64(sk);
     const int bw = bkey != 0 ? FirstLane(sk == bkey && lane < uint32_t(WAVES)) : 0;
     gkey = bkey;
     wpos = uint32_t(__builtin_amdgcn_readlane(int(spos), bw));
@@ -1079,6 +1094,34 @@ int LaunchWaveItems(const LoopArgs& a, uint32_t items, hipStream_t stream) {
   return LaunchWave<NI, (kMax >= 16 ? 16 : 2)>(a, stream);
 }
 
+// One 1024-thread workgroup (sixteen waves): selections too large for one
+// 512-thread workgroup's registers that would otherwise pay the
+// cross-workgroup exchange every iteration.
+template <int NI, int ITEMS>
+int LaunchBig(const LoopArgs& a, hipStream_t stream) {
+  auto kernel = (NI == 1 && a.integ.copy_fast_path)
+                    ? SubminorLoopReg<NI, ITEMS, NI == 1, 1024>
+                    : SubminorLoopReg<NI, ITEMS, false, 1024>;
+  if (a.n_blocks > 1) {
+    void* args[] = {const_cast<LoopArgs*>(&a)};
+    RDL_HIP_CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(kernel),
+                                             dim3(a.n_blocks), dim3(1024), args, 0,
+                                             stream));
+  } else {
+    kernel<<<1, 1024, 0, stream>>>(a);
+    RDL_HIP_CHECK(hipGetLastError());
+  }
+  return RDL_OK;
+}
+
+template <int NI>
+int LaunchBigItems(const LoopArgs& a, uint32_t items, hipStream_t stream) {
+  if (items <= 1) return LaunchBig<NI, 1>(a, stream);
+  if (items <= 2) return LaunchBig<NI, 2>(a, stream);
+  if (items <= 4 || NI > 2) return LaunchBig<NI, 4>(a, stream);
+  return LaunchBig<NI, 8>(a, stream);
+}
+
 template <int NI, int ITEMS>
 int LaunchReg(const LoopArgs& a, hipStream_t stream) {
   auto kernel = (NI == 1 && a.integ.copy_fast_path) ? SubminorLoopReg<NI, ITEMS, NI == 1>
@@ -1152,6 +1195,10 @@ int rdl_subminor_create(rdl_session* s, rdl_subminor** out) {
   // experiments: RDL_SUBMINOR_WAVE_MAX=0 disables the single-wave kernel
   if (const char* e = std::getenv("RDL_SUBMINOR_WAVE_MAX"))
     h->wave_max = uint32_t(std::strtoul(e, nullptr, 10));
+  if (const char* e = std::getenv("RDL_SUBMINOR_BIG_MAX"))
+    h->big_max = uint32_t(std::strtoul(e, nullptr, 10));
+  if (const char* e = std::getenv("RDL_SUBMINOR_BIG_TARGET"))
+    h->big_target = uint32_t(std::strtoul(e, nullptr, 10));
   *out = h;
   return RDL_OK;
 }
@@ -1278,6 +1325,40 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
     rdl::SetError("single-wave sub-minor kernel cannot hold this selection");
     return RDL_ERR_ARG;
   }
+  // one sixteen-wave workgroup (mode 4 forces it)
+  const uint64_t big_cap = 1024ull * (ni_t <= 2 ? 8 : 4);
+  bool use_big =
+      !use_wave && ni <= 8 && h->mode != 1 && h->mode != 2 &&
+      ((h->mode == 0 && n_sel <= std::min<uint64_t>(big_cap, h->big_max) &&
+        n_sel > 1024) ||
+       (h->mode == 4 && n_sel <= big_cap));
+  // 1024-thread workgroups on a cooperative grid (mode 5, target pixels per
+  // workgroup from set_tuning; mode 0 when big_target is set)
+  bool use_big_grid = false;
+  if (!use_wave && !use_big && ni <= 8 &&
+      ((h->mode == 5) || (h->mode == 0 && h->big_target > 0 && n_sel > h->big_max))) {
+    const uint64_t target = h->mode == 5 ? std::max<uint32_t>(h->target_per_block, 1024)
+                                         : h->big_target;
+    uint32_t gb = uint32_t(std::min<uint64_t>(max_blocks, (n_sel + target - 1) / target));
+    gb = std::max<uint32_t>(gb, 1);
+    const uint64_t pb = (n_sel + gb - 1) / gb;
+    if (pb <= big_cap) {
+      use_big_grid = true;
+      g = gb;
+      per = pb;
+      use_reg = true;
+    }
+  }
+  if (h->mode == 4 && !use_big) {
+    rdl::SetError("1024-thread sub-minor kernel cannot hold this selection");
+    return RDL_ERR_ARG;
+  }
+  if (use_big) {
+    g = 1;
+    per = n_sel;
+    use_reg = true;
+  }
+  if (use_big_grid) use_big = true;
   uint32_t items = 0;
   bool use_lds = false;
   size_t lds_bytes = 0;
@@ -1347,7 +1428,18 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   }
   {
     rdl::ScopedTiming t(s, "subminor_loop", 0.0);
-    if (use_wave) {
+    if (use_big) {
+      const uint64_t bi = (per + 1023) / 1024;
+      const uint32_t bitems = bi <= 1 ? 1 : bi <= 2 ? 2 : bi <= 4 ? 4 : 8;
+      if (ni_t == 1)
+        RDL_TRY(rdl::LaunchBigItems<1>(la, bitems, st));
+      else if (ni_t == 2)
+        RDL_TRY(rdl::LaunchBigItems<2>(la, bitems, st));
+      else if (ni_t == 4)
+        RDL_TRY(rdl::LaunchBigItems<4>(la, bitems, st));
+      else
+        RDL_TRY(rdl::LaunchBigItems<8>(la, bitems, st));
+    } else if (use_wave) {
       const uint64_t wi = (n_sel + 63) / 64;
       const uint32_t witems = wi <= 1 ? 1 : wi <= 2 ? 2 : wi <= 4 ? 4 : wi <= 8 ? 8 : 16;
       if (ni_t == 1)
@@ -1431,7 +1523,7 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
 int rdl_subminor_set_tuning(rdl_subminor* h, int mode,
                             uint32_t target_per_block) {
   RDL_ARG_CHECK(h, "NULL argument");
-  RDL_ARG_CHECK(mode >= 0 && mode <= 3, "mode must be 0, 1, 2 or 3");
+  RDL_ARG_CHECK(mode >= 0 && mode <= 5, "mode must be 0 to 5");
   h->mode = mode;
   if (target_per_block) h->target_per_block = target_per_block;
   return RDL_OK;

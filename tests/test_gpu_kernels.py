@@ -452,6 +452,9 @@ SUBMINOR_CASES = [
     (160, 20, 0.003, 0.9, 600, 8, 2, 600),
     (160, 20, 0.003, 0.9, 600, 5, 1, 0),
     (128, 10, 0.0, 0.8, 300, 1, 3, 0),        # single-wave kernel forced
+    (128, 10, 0.0, 0.8, 300, 1, 4, 0),        # one 1024-thread workgroup forced
+    (512, 200, 0.002, 1.0, 2000, 1, 5, 2048),  # grid of 1024-thread workgroups
+    (200, 30, 0.002, 0.9, 800, 3, 5, 1024),
 ]
 
 

@@ -27,6 +27,12 @@ def main():
     if os.environ.get("RDL_BENCH_WAVE"):  # single-wave vs eight-wave kernel
         sizes = (64, 128, 256, 400, 512, 768, 1024)
         variants = ((2, 0), (3, 0))
+    if os.environ.get("RDL_BENCH_BIGGRID"):  # grids of 1024- vs 512-thread workgroups
+        sizes = (4096, 6144, 8192, 12288, 16384, 32768)
+        variants = ((0, 1024), (5, 2048), (5, 3072), (5, 4096))
+    if os.environ.get("RDL_BENCH_BIG"):  # one 1024-thread workgroup vs the grid
+        sizes = (1536, 2048, 3072, 4096, 6144, 8192)
+        variants = ((0, 1024), (4, 0))
     for n_sel in sizes:
         img = np.zeros((size, size), np.float32)
         n_cl = 24
