@@ -244,6 +244,18 @@ int rdl_rms_negativity_limit(rdl_session* s, float* d_rms, const float* d_min,
 int rdl_rms_factor(rdl_session* s, float* d_rms, size_t n, double strength,
                    double* lowest_rms);
 
+/* ------------------------------------------------ component optimisation */
+/* math::GradientDescent (cpp/math/component_optimization.cc:100-177,
+ * 265-321) on planes: the components are the model's non-zero pixels.
+ * dst = model != 0 ? sign * src : 0 (CalculateDerivatives' gather). */
+int rdl_masked_copy(rdl_session* s, const float* d_model, const float* d_src, float* d_dst,
+                    size_t n, float sign);
+/* model[i] += values[i] where model[i] != 0 (GradientDescent's update). */
+int rdl_masked_add(rdl_session* s, float* d_model, const float* d_values, size_t n);
+/* *ab = sum a*b, *aa = sum a*a in double (ApplyLineSearch's two sums). */
+int rdl_dot_pair(rdl_session* s, const float* d_a, const float* d_b, size_t n,
+                 double* ab, double* aa);
+
 /* ---------------------------------------------------------------- Högbom */
 typedef struct {
   uint32_t width, height;

@@ -11,6 +11,7 @@
 #include "oracle.h"
 #include "tiling.h"
 #include "rms_image.h"
+#include "component_optimization.h"
 #include "iuwt.h"
 #include "iuwt_algorithm.h"
 
@@ -167,6 +168,7 @@ struct OrcAlgo {
   std::unique_ptr<MultiScale> ms;
   std::vector<IuwtStep> iuwt_steps;  // type 2: steps of the last execute
   std::vector<float> rms_factor;     // SetRmsFactorImage (empty = none)
+  int component_optimization = 0;    // SetComponentOptimizationAlgorithm
 };
 
 static AlgoSettings MakeSettings(const orc_algo_settings* a) {
@@ -257,6 +259,7 @@ int orc_algo_execute(void* h, const orc_set_desc* d, float* residual,
     std::vector<Component> tr;
     Result r;
     algo->settings.rms_factor = algo->rms_factor.empty() ? nullptr : algo->rms_factor.data();
+    algo->settings.component_optimization = algo->component_optimization;
     if (algo->ms) algo->ms->Settings().rms_factor = algo->settings.rms_factor;
     if (algo->type == 0) {
       r = GenericCleanExecute(algo->settings, algo->iteration_number, res, mod,
@@ -394,6 +397,12 @@ void orc_algo_set_rms(void* h, const float* factor, uint64_t n) {
     algo->rms_factor.clear();
 }
 
+// DeconvolutionAlgorithm::SetComponentOptimizationAlgorithm (0 clean, 2 gradient
+// descent; generic clean only)
+void orc_algo_set_component_optimization(void* h, int algorithm) {
+  static_cast<OrcAlgo*>(h)->component_optimization = algorithm;
+}
+
 // ParallelDeconvolution::SetRmsFactorImage (parallel_deconvolution.cc:244-250)
 void orc_parallel_set_rms(void* h, const float* factor, uint64_t n) {
   auto* p = static_cast<OrcParallel*>(h);
@@ -426,6 +435,19 @@ int orc_local_rms(const float* integrated, uint64_t width, uint64_t height, int 
     g_error = e.what();
     return 1;
   }
+}
+
+// GenericClean's RunComponentOptimization with kGradientDescent for one
+// image (generic_clean.cc:26-48): model += GradientDescent(model, residual,
+// psf, 2W x 2H, FFT).
+void orc_gradient_descent(float* model, const float* residual, const float* psf,
+                          uint64_t width, uint64_t height) {
+  GradientDescent(model, residual, psf, width, height, 2 * width, 2 * height);
+}
+
+void orc_padded_convolution(float* image, const float* psf, uint64_t width,
+                            uint64_t height, uint64_t padded_width, uint64_t padded_height) {
+  PaddedConvolution(image, psf, width, height, padded_width, padded_height);
 }
 
 void orc_sliding_minimum(const float* input, uint64_t width, uint64_t height,

@@ -2,6 +2,8 @@
 // CPU restatement of Radler's CLEAN hot path; see oracle.h.
 #include "oracle.h"
 
+#include "component_optimization.h"
+
 #include <algorithm>
 #include <cassert>
 #include <cstdio>
@@ -646,6 +648,20 @@ Result GenericCleanExecute(const AlgoSettings& s_in, size_t& iteration_number,
   result.final_peak = max_value.has ? max_value.value : 0.0f;
   if (!max_value.has) return result;
   if (iteration_number >= s.max_iterations) return result;
+  if (s.component_optimization != 0) {  // generic_clean.cc:89-95
+    for (size_t i = 0; i != dirty.Size(); ++i)  // RunComponentOptimization (:26-48)
+      GradientDescent(model.images[i], dirty.images[i], psfs[dirty.PsfIndex(i)], width,
+                      height, 2 * width, 2 * height);
+    if (dirty.desc->fitter) {  // FitSpectra (:278-297)
+      std::vector<float> values(model.Size());
+      for (size_t p = 0; p != width * height; ++p) {
+        for (size_t i = 0; i != model.Size(); ++i) values[i] = model.images[i][p];
+        PerformSpectralFit(dirty.desc->fitter.get(), dirty.desc->n_pol, values.data());
+        for (size_t i = 0; i != model.Size(); ++i) model.images[i][p] = values[i];
+      }
+    }
+    return result;
+  }
 
   const float initial_max_value = std::fabs(max_value.value);
   float first_threshold = s.threshold;

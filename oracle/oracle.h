@@ -119,6 +119,8 @@ struct AlgoSettings {
   // DeconvolutionAlgorithm::RmsFactorImage (deconvolution_algorithm.h:163-166):
   // width x height factors multiplied into every peak search; nullptr = none
   const float* rms_factor = nullptr;
+  // OptimizationAlgorithm (settings.h): 0 kClean, 2 kGradientDescent
+  int component_optimization = 0;
   // generic clean
   bool use_sub_minor_optimization = true;
   // multiscale (cpp/settings.h:465-524)

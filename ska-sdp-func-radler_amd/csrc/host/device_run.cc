@@ -80,6 +80,7 @@ DeviceRun::DeviceRun(const Settings& settings, const float* psf,
   algorithm->SetDivergenceLimit(settings.divergence_limit);
   algorithm->SetAllowNegativeComponents(settings.allow_negative_components);
   algorithm->SetStopOnNegativeComponents(settings.stop_on_negative_components);
+  algorithm->SetComponentOptimizationAlgorithm(settings.component_optimization_algorithm);
   {  // Radler::CreateSpectralFitter (radler.cc:318-331); channel c sits at
      // 100 MHz + c x 10 MHz
     using schaapcommon::fitters::SpectralFittingMode;

@@ -5,6 +5,7 @@
 #include <cmath>
 #include <stdexcept>
 
+#include "component_optimization.h"
 #include "logger.h"
 #include "subminor.h"
 
@@ -34,6 +35,49 @@ rdl_peak GenericClean::FindPeak(gpu::Session& s, const float* d_image,
   return p;
 }
 
+void GenericClean::RunComponentOptimization(ImageSet& residual_set, ImageSet& model_set,
+                                            const gpu::Planes& psfs) {
+  // :26-48, per image
+  gpu::Session& s = residual_set.Session();
+  const size_t w = residual_set.Width(), h = residual_set.Height();
+  for (size_t i = 0; i != residual_set.Size(); ++i) {
+    switch (ComponentOptimizationAlgorithm()) {
+      case OptimizationAlgorithm::kGradientDescent:
+        math::GradientDescent(s, model_set.Data(i), residual_set.Data(i),
+                              psfs.Plane(residual_set.PsfIndex(i)), w, h, 2 * w, 2 * h);
+        break;
+      case OptimizationAlgorithm::kLinearEquationSolver:
+        throw std::runtime_error(
+            "The linear-equation component solver is not available in the MI355X "
+            "build");
+      case OptimizationAlgorithm::kRegularizedGradientDescent:
+        throw std::runtime_error(
+            "Regularized gradient descent has not yet been implemented");
+      default:
+        throw std::runtime_error(
+            "Unsupported optimization algorithm for generic clean algorithm");
+    }
+  }
+}
+
+void GenericClean::FitSpectra(ImageSet& model_set) {
+  // :278-297: every pixel's spectrum through PerformSpectralFit, which for
+  // the polynomial fitter is one linear map (rdl_spectral_interpolate with
+  // the per-component matrix)
+  gpu::Session& s = model_set.Session();
+  const size_t n_img = model_set.Size(), n = model_set.Width() * model_set.Height();
+  const float* d_map = DeviceSpectralMap(s, n_img);
+  if (!d_map) return;
+  std::vector<float> map(n_img * n_img);
+  s.D2H(map.data(), d_map, map.size() * sizeof(float));
+  gpu::Buffer out(s, n_img * n * sizeof(float));
+  gpu::Check(rdl_spectral_interpolate(s.Handle(), model_set.Data(0), n, uint32_t(n_img),
+                                      map.data(), uint32_t(n_img), out.F(), n),
+             "rdl_spectral_interpolate");
+  for (size_t i = 0; i != n_img; ++i)
+    s.D2D(model_set.Data(i), out.F() + i * n, n * sizeof(float));
+}
+
 DeconvolutionResult GenericClean::ExecuteMajorIteration(
     ImageSet& dirty_set, ImageSet& model_set, const gpu::Planes& psfs) {
   gpu::Session& s = dirty_set.Session();
@@ -42,9 +86,6 @@ DeconvolutionResult GenericClean::ExecuteMajorIteration(
   const size_t iteration_at_start = IterationNumber();
   trace_.clear();
   if (StopOnNegativeComponents()) SetAllowNegativeComponents(true);
-  if (ComponentOptimizationAlgorithm() != OptimizationAlgorithm::kClean)
-    throw std::runtime_error(
-        "Component optimisation is not available in the MI355X build");
   // :63-66
   size_t conv_w = size_t(std::ceil(convolution_padding_ * width));
   size_t conv_h = size_t(std::ceil(convolution_padding_ * height));
@@ -63,6 +104,12 @@ DeconvolutionResult GenericClean::ExecuteMajorIteration(
     return result;
   }
   if (IterationNumber() >= MaxIterations()) return result;
+  if (ComponentOptimizationAlgorithm() != OptimizationAlgorithm::kClean) {  // :89-95
+    log::Info() << "Running optimization algorithm...\n";
+    RunComponentOptimization(dirty_set, model_set, psfs);
+    FitSpectra(model_set);
+    return result;
+  }
 
   const float initial_max_value = std::fabs(max_value.value);
   float first_threshold = Threshold();

@@ -27,6 +27,9 @@ class GenericClean final : public DeconvolutionAlgorithm {
  private:
   rdl_peak FindPeak(gpu::Session& s, const float* d_image, size_t width,
                     size_t height, const uint8_t* d_mask);
+  void RunComponentOptimization(ImageSet& residual_set, ImageSet& model_set,
+                                const gpu::Planes& psfs);
+  void FitSpectra(ImageSet& model_set);
 
   const float convolution_padding_;
   bool use_sub_minor_optimization_;

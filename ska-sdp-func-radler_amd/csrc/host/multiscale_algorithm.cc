@@ -238,7 +238,8 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
   } mask_sync{this};
   if (ComponentOptimizationAlgorithm() != OptimizationAlgorithm::kClean)
     throw std::runtime_error(
-        "Component optimisation is not available in the MI355X build");
+        "Multiscale component optimisation (it fits the multiscale component "
+        "list) is not available in the MI355X build");
 
   bool has_hit_threshold_in_sub_loop = false;
   size_t threshold_countdown = std::max(size_t{8}, scale_infos_.size() * 3 / 2);

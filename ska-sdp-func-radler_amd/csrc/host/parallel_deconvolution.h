@@ -46,6 +46,10 @@ class ParallelDeconvolution {
   void SetThreshold(double threshold);
   void SetMinorLoopGain(double gain);
   void SetCleanMask(const bool* mask);
+  /// parallel_deconvolution.cc:271-276
+  void SetComponentOptimization(OptimizationAlgorithm algorithm) {
+    for (auto& a : algorithms_) a->SetComponentOptimizationAlgorithm(algorithm);
+  }
   /// parallel_deconvolution.cc:244-250: the single algorithm takes it as
   /// is; gridded runs trim each subimage's box (:332-337) and drop it after
   /// the run (:421-423). nullptr clears it.

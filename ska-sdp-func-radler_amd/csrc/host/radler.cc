@@ -141,6 +141,10 @@ void Radler::Perform(bool& another_iteration_required,
     parallel_deconvolution_->SetMinorLoopGain(
         std::min(1.0, settings_.minor_loop_gain * 2.0));
     parallel_deconvolution_->SetRmsFactorImage(nullptr, image_width_);
+    // component optimisation only once the mask is complete (:180-185)
+    if (settings_.component_optimization_algorithm != OptimizationAlgorithm::kClean)
+      parallel_deconvolution_->SetComponentOptimization(
+          settings_.component_optimization_algorithm);
   } else {
     parallel_deconvolution_->SetMinorLoopGain(settings_.minor_loop_gain);
     if (local_rms) {  // :196-216

@@ -16,6 +16,7 @@
 #include "logger.h"
 #include "radler.h"
 #include "rms_image.h"
+#include "component_optimization.h"
 
 namespace py = pybind11;
 using AccessorList = std::vector<std::unique_ptr<aocommon::ImageAccessor>>;
@@ -41,6 +42,12 @@ void InitSettings(py::module& m) {  // python/pysettings.cc
       .value("iuwt", radler::AlgorithmType::kIuwt)
       .value("more_sane", radler::AlgorithmType::kMoreSane)
       .value("python", radler::AlgorithmType::kPython);
+  py::enum_<radler::OptimizationAlgorithm>(m, "OptimizationAlgorithm")
+      .value("clean", radler::OptimizationAlgorithm::kClean)
+      .value("linear_equation_solver", radler::OptimizationAlgorithm::kLinearEquationSolver)
+      .value("gradient_descent", radler::OptimizationAlgorithm::kGradientDescent)
+      .value("regularized_gradient_descent",
+             radler::OptimizationAlgorithm::kRegularizedGradientDescent);
   py::enum_<radler::LocalRmsMethod>(m, "LocalRmsMethod")
       .value("none", radler::LocalRmsMethod::kNone)
       .value("rms_window", radler::LocalRmsMethod::kRmsWindow)
@@ -78,6 +85,8 @@ void InitSettings(py::module& m) {  // python/pysettings.cc
       .def_readwrite("spectral_correction_frequency",
                      &radler::Settings::spectral_correction_frequency)
       .def_readwrite("spectral_correction", &radler::Settings::spectral_correction)
+      .def_readwrite("component_optimization_algorithm",
+                     &radler::Settings::component_optimization_algorithm)
       .def_readwrite("border_ratio", &radler::Settings::border_ratio)
       .def_readwrite("fits_mask", &radler::Settings::fits_mask)
       .def_readwrite("casa_mask", &radler::Settings::casa_mask)
@@ -516,6 +525,28 @@ void InitGpu(py::module& m) {
       },
       py::arg("integrated"), py::arg("method"), py::arg("window"), py::arg("beam"),
       py::arg("pixel_scale_x"), py::arg("pixel_scale_y"), py::arg("strength") = 1.0);
+  g.def(
+      "gradient_descent",
+      [](FloatArray model, FloatArray residual, FloatArray psf) {
+        // GenericClean's RunComponentOptimization for one image (padded 2W x 2H)
+        if (model.ndim() != 2) throw std::runtime_error("expected 2-D images");
+        const size_t h = model.shape(0), w = model.shape(1), n = w * h;
+        if (size_t(residual.size()) != n || size_t(psf.size()) != n)
+          throw std::runtime_error("image sizes differ");
+        std::shared_ptr<radler::gpu::Session> session =
+            radler::gpu::Session::ForDevice(radler::gpu::Session::DefaultDevice());
+        radler::gpu::Session& s = *session;
+        radler::gpu::Buffer dm(s, n * sizeof(float)), dr(s, n * sizeof(float)),
+            dp(s, n * sizeof(float));
+        s.H2D(dm.Ptr(), model.data(), n * sizeof(float));
+        s.H2D(dr.Ptr(), residual.data(), n * sizeof(float));
+        s.H2D(dp.Ptr(), psf.data(), n * sizeof(float));
+        radler::math::GradientDescent(s, dm.F(), dr.F(), dp.F(), w, h, 2 * w, 2 * h);
+        py::array_t<float> out({h, w});
+        s.D2H(out.mutable_data(), dm.F(), n * sizeof(float));
+        return out;
+      },
+      py::arg("model"), py::arg("residual"), py::arg("psf"));
   g.def(
       "sliding_minimum",
       [](FloatArray image, size_t window) {

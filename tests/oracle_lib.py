@@ -202,6 +202,31 @@ class Oracle:
             raise RuntimeError(self.lib.orc_last_error().decode())
         return rms, factor, lowest.value
 
+    def gradient_descent(self, model, residual, psf):
+        """GenericClean's kGradientDescent component optimisation of one
+        image: returns model + the update."""
+        m = np.ascontiguousarray(model, np.float32).copy()
+        r = np.ascontiguousarray(residual, np.float32)
+        p = np.ascontiguousarray(psf, np.float32)
+        h, w = m.shape
+        L = self.lib
+        L.orc_gradient_descent.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
+                                           C.c_uint64]
+        L.orc_gradient_descent.restype = None
+        L.orc_gradient_descent(m.ctypes.data, r.ctypes.data, p.ctypes.data, w, h)
+        return m
+
+    def padded_convolution(self, image, psf, pw, ph):
+        img = np.ascontiguousarray(image, np.float32).copy()
+        p = np.ascontiguousarray(psf, np.float32)
+        h, w = img.shape
+        L = self.lib
+        L.orc_padded_convolution.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64,
+                                             C.c_uint64, C.c_uint64]
+        L.orc_padded_convolution.restype = None
+        L.orc_padded_convolution(img.ctypes.data, p.ctypes.data, w, h, pw, ph)
+        return img
+
     def sliding_minimum(self, image, window):
         img = np.ascontiguousarray(image, np.float32)
         h, w = img.shape
@@ -266,6 +291,13 @@ class OracleAlgorithm:
     def set_spectral_fitter(self, mode, n_terms, frequencies, weights):
         """DeconvolutionAlgorithm::SetSpectralFitter (polynomial: mode 1)."""
         self.spectral = (mode, n_terms, frequencies, weights)
+
+    def set_component_optimization(self, algorithm):
+        """SetComponentOptimizationAlgorithm: 0 clean, 2 gradient descent."""
+        L = self.o.lib
+        L.orc_algo_set_component_optimization.argtypes = [C.c_void_p, C.c_int]
+        L.orc_algo_set_component_optimization.restype = None
+        L.orc_algo_set_component_optimization(self.h, int(algorithm))
 
     def set_rms(self, factor):
         """DeconvolutionAlgorithm::SetRmsFactorImage (None clears it)."""

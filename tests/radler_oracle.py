@@ -27,7 +27,8 @@ class OraclePerform:
                  absolute_threshold=0.0, auto_mask_sigma=None, auto_threshold_sigma=None,
                  absolute_auto_mask_threshold=None, minor_iteration_count=1000,
                  major_iteration_count=20, major_auto_mask_iteration_count=2,
-                 grid=None, snapshot=False, local_rms=None, **algo_settings):
+                 grid=None, snapshot=False, local_rms=None, component_optimization=0,
+                 **algo_settings):
         self.orc, self.kind = orc, kind
         self.psf = psf[None].astype(np.float32)
         self.residual = dirty[None].astype(np.float32).copy()
@@ -47,6 +48,7 @@ class OraclePerform:
         self.grid = grid
         # local_rms: None or dict(method=1|2, window, strength, beam, pixel_scale)
         self.local_rms = local_rms
+        self.component_optimization = component_optimization  # 2: gradient descent
         if grid is None:
             self.alg = OracleAlgorithm(orc, kind, **self._settings(self.gain, None))
         else:  # ParallelDeconvolution::ExecuteParallelRun (oracle/tiling.cc)
@@ -73,6 +75,8 @@ class OraclePerform:
             if enabled and self.finished:  # cpp/radler.cc:172-185
                 if self.local_rms:
                     self.alg.set_rms(None)
+                if self.component_optimization:
+                    self.alg.set_component_optimization(self.component_optimization)
             elif self.local_rms:  # cpp/radler.cc:196-216
                 lr = self.local_rms
                 _, factor, stddev = self.orc.local_rms(
