@@ -85,8 +85,6 @@ void InitSettings(py::module& m) {  // python/pysettings.cc
       .def_readwrite("spectral_correction_frequency",
                      &radler::Settings::spectral_correction_frequency)
       .def_readwrite("spectral_correction", &radler::Settings::spectral_correction)
-      .def_readwrite("component_optimization_algorithm",
-                     &radler::Settings::component_optimization_algorithm)
       .def_readwrite("border_ratio", &radler::Settings::border_ratio)
       .def_readwrite("fits_mask", &radler::Settings::fits_mask)
       .def_readwrite("casa_mask", &radler::Settings::casa_mask)
@@ -525,6 +523,15 @@ void InitGpu(py::module& m) {
       },
       py::arg("integrated"), py::arg("method"), py::arg("window"), py::arg("beam"),
       py::arg("pixel_scale_x"), py::arg("pixel_scale_y"), py::arg("strength") = 1.0);
+  // Settings::component_optimization_algorithm is C++-only in the reference's
+  // bindings (python/pysettings.cc): set it through this helper so the
+  // Settings attribute layout stays the reference's
+  g.def(
+      "set_component_optimization",
+      [](radler::Settings& settings, radler::OptimizationAlgorithm algorithm) {
+        settings.component_optimization_algorithm = algorithm;
+      },
+      py::arg("settings"), py::arg("algorithm"));
   g.def(
       "gradient_descent",
       [](FloatArray model, FloatArray residual, FloatArray psf) {

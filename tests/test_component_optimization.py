@@ -87,7 +87,7 @@ def test_perform_with_gradient_descent_matches_oracle():
     s.minor_loop_gain = 0.1
     s.border_ratio = 0.0
     s.auto_mask_sigma = 6.0
-    s.component_optimization_algorithm = rd.OptimizationAlgorithm.gradient_descent
+    rd.gpu.set_component_optimization(s, rd.OptimizationAlgorithm.gradient_descent)
     residual, model = dirty.copy(), np.zeros_like(dirty)
     r = rd.Radler(s, psf, residual, model, 0.0)
     o = OraclePerform(get_oracle(), 0, psf, dirty, minor_loop_gain=0.1, auto_mask_sigma=6.0,
@@ -116,7 +116,7 @@ def test_unavailable_optimisations_are_rejected():
     s.pixel_scale.x = s.pixel_scale.y = PIXEL_SCALE
     s.minor_iteration_count = 100
     s.absolute_threshold = 1e-3
-    s.component_optimization_algorithm = rd.OptimizationAlgorithm.gradient_descent
+    rd.gpu.set_component_optimization(s, rd.OptimizationAlgorithm.gradient_descent)
     run = rd.gpu.DeviceRun(s, psf, dirty, [], 2.0 * PIXEL_SCALE)
     with pytest.raises(RuntimeError, match="not available"):
         run.execute()
