@@ -79,6 +79,8 @@ MultiScaleAlgorithm::MultiScaleAlgorithm(const MultiScaleAlgorithm& o)
       settings_(o.settings_),
       beam_size_in_pixels_(o.beam_size_in_pixels_),
       track_components_(o.track_components_),
+      component_list_(o.component_list_ ? std::make_unique<ComponentList>(*o.component_list_)
+                                        : nullptr),
       scale_infos_(o.scale_infos_),
       track_masks_(o.track_masks_),
       use_masks_(o.use_masks_),
@@ -219,6 +221,13 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
   if (StopOnNegativeComponents()) SetAllowNegativeComponents(true);
   InitializeScales(scale_infos_, beam_size_in_pixels_, std::min(width, height),
                    settings_.shape, settings_.max_scales, settings_.scale_list);
+  if (track_components_) {  // :228-236
+    if (!component_list_)
+      component_list_ = std::make_unique<ComponentList>(width, height, scale_infos_.size(),
+                                                        data_image.Size());
+    else if (component_list_->Width() != width || component_list_->Height() != height)
+      throw std::runtime_error("Error in component list dimensions!");
+  }
   if (track_masks_) {  // :214-226
     for (const std::vector<uint8_t>& m : host_masks_)
       if (m.size() != npx)
@@ -445,6 +454,8 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
           sub.AddIndividualModel(i, model_image.Data(i));
         }
       }
+      if (track_components_)  // :447-448
+        sub.UpdateComponentList(*component_list_, scale_with_peak);
     } else {  // :463-519
       size_t n_kernel = 0;
       std::vector<float> shape_kernel;
@@ -495,6 +506,8 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
                         &one, 1);
           }
         }
+        if (track_components_)  // :502-504
+          component_list_->Add(x, y, scale_with_peak, cv.data());
         individual.GetLinearIntegrated(integrated.F());
         FindPeakDirect(integrated.F(), scale_with_peak);
         const float abs_peak =

@@ -13,6 +13,7 @@
 #include <optional>
 #include <vector>
 
+#include "component_list.h"
 #include "deconvolution_algorithm.h"
 #include "multiscale_transforms.h"
 
@@ -50,6 +51,11 @@ class MultiScaleAlgorithm final : public DeconvolutionAlgorithm {
   };
 
   size_t ScaleCount() const { return scale_infos_.size(); }
+  /// multiscale_algorithm.h:72-79: the components of the major iterations
+  /// so far (save_source_list), per scale with one value per image.
+  const ComponentList& GetComponentList() const { return *component_list_; }
+  bool HasComponentList() const { return component_list_ != nullptr; }
+  void ClearComponentList() { component_list_.reset(); }
   float ScaleSize(size_t i) const { return scale_infos_[i].scale; }
   const std::vector<ScaleInfo>& ScaleInfos() const { return scale_infos_; }
   /// x, y, scale index of every component of the last major iteration.
@@ -92,6 +98,7 @@ class MultiScaleAlgorithm final : public DeconvolutionAlgorithm {
   const Settings::Multiscale& settings_;
   double beam_size_in_pixels_;
   bool track_components_;
+  std::unique_ptr<ComponentList> component_list_;
   std::vector<ScaleInfo> scale_infos_;
   std::vector<uint32_t> trace_;
 

@@ -361,7 +361,35 @@ bool ParallelDeconvolution::DeconvolveSubImage(SubImage& sub, ImageSet& sub_data
                 << " and deconvolution probably diverged: resetting.\n";
     sub.reached_major_threshold = false;
   }
+  // :464-479: a converging multiscale subimage's components join the
+  // full-image list at the subimage offset
+  if (!find_peak_only && settings_.save_source_list && algorithms_.size() > 1 &&
+      settings_.algorithm_type == AlgorithmType::kMultiscale) {
+    auto& ms = static_cast<MultiScaleAlgorithm&>(alg);
+    if (converging && ms.HasComponentList()) {
+      const std::lock_guard<std::mutex> lock(masks_mutex_);
+      if (!component_list_)
+        component_list_ = std::make_unique<ComponentList>(
+            settings_.trimmed_image_width, settings_.trimmed_image_height,
+            ms.ScaleCount(), sub_data.Size());
+      component_list_->Add(ms.GetComponentList(), int(sub.x), int(sub.y));
+    }
+    ms.ClearComponentList();
+  }
   return converging;
+}
+
+ComponentList ParallelDeconvolution::GetMultiscaleComponentList() const {
+  // :184-196: the single algorithm's list, or the merged subimage lists
+  ComponentList list;
+  if (algorithms_.size() == 1) {
+    const auto& ms = static_cast<const MultiScaleAlgorithm&>(*algorithms_.front());
+    if (ms.HasComponentList()) list = ms.GetComponentList();
+  } else if (component_list_) {
+    list = *component_list_;
+  }
+  list.MergeDuplicates();
+  return list;
 }
 
 void ParallelDeconvolution::RunSubImage(SubImage& sub, ImageSet& data_image,

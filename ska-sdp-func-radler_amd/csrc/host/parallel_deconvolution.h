@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "communicator.h"
+#include "component_list.h"
 #include "deconvolution_algorithm.h"
 #include "device.h"
 #include "psf_offset.h"
@@ -46,6 +47,9 @@ class ParallelDeconvolution {
   void SetThreshold(double threshold);
   void SetMinorLoopGain(double gain);
   void SetCleanMask(const bool* mask);
+  /// GetComponentList for multiscale (parallel_deconvolution.cc:184-196);
+  /// with a process-per-GPU split each rank holds its own subimages'.
+  ComponentList GetMultiscaleComponentList() const;
   /// parallel_deconvolution.cc:271-276
   void SetComponentOptimization(OptimizationAlgorithm algorithm) {
     for (auto& a : algorithms_) a->SetComponentOptimizationAlgorithm(algorithm);
@@ -138,6 +142,7 @@ class ParallelDeconvolution {
   const Settings& settings_;
   const bool* mask_ = nullptr;
   std::shared_ptr<const std::vector<float>> rms_image_;  // full image (gridded)
+  std::unique_ptr<ComponentList> component_list_;        // gridded multiscale
   size_t rms_width_ = 0;
   std::shared_ptr<Communicator> comm_;
   bool track_masks_ = false, use_masks_ = false;

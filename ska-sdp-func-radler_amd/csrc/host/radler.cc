@@ -85,7 +85,7 @@ Radler::~Radler() { FreeDeconvolutionAlgorithms(); }
 ComponentList Radler::GetComponentList() const {
   // ParallelDeconvolution::GetComponentList (parallel_deconvolution.cc:185-210)
   if (settings_.algorithm_type == AlgorithmType::kMultiscale)
-    Unsupported("A multiscale component list (save_source_list)");
+    return parallel_deconvolution_->GetMultiscaleComponentList();
   ImageSet model_set(*table_, settings_.squared_joins,
                      settings_.linked_polarizations, image_width_,
                      image_height_, DeviceSession());
@@ -281,7 +281,6 @@ void Radler::InitializeDeconvolutionAlgorithm(
           settings_.generic.use_sub_minor_optimization);
       break;
     case AlgorithmType::kMultiscale:
-      if (settings_.save_source_list) Unsupported("save_source_list");
       algorithm = std::make_unique<algorithms::MultiScaleAlgorithm>(
           settings_.multiscale, beam_size_, pixel_scale_x_, pixel_scale_y_,
           settings_.save_source_list);

@@ -163,6 +163,24 @@ void SubMinorLoop::UpdateAutoMask(uint8_t* d_mask) {
   gpu::Check(rdl_subminor_update_mask(h_, d_mask), "rdl_subminor_update_mask");
 }
 
+void SubMinorLoop::UpdateComponentList(ComponentList& list,
+                                       size_t scale_index) const {
+  std::vector<uint32_t> positions;
+  std::vector<float> models;
+  GetSelection(positions, models);
+  const size_t n = positions.size();
+  std::vector<float> values(n_images_);
+  for (size_t px = 0; px != n; ++px) {
+    bool non_zero = false;
+    for (size_t i = 0; i != n_images_; ++i) {
+      values[i] = models[i * n + px];
+      non_zero = non_zero || values[i] != 0.0f;
+    }
+    if (non_zero)
+      list.Add(positions[px] & 0xffffu, positions[px] >> 16, scale_index, values.data());
+  }
+}
+
 void SubMinorLoop::GetSelection(std::vector<uint32_t>& positions,
                                 std::vector<float>& models) const {
   positions.resize(n_selected_);

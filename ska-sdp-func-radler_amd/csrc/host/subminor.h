@@ -8,6 +8,7 @@
 #include <map>
 #include <vector>
 
+#include "component_list.h"
 #include "device.h"
 #include "image_set.h"
 
@@ -77,6 +78,9 @@ class SubMinorLoop {
   /// UpdateAutoMask inputs).
   void GetSelection(std::vector<uint32_t>& positions,
                     std::vector<float>& models) const;
+  /// subminor_loop.cc:230-246: every selected pixel with a non-zero model
+  /// value in any image joins `list` at `scale_index`.
+  void UpdateComponentList(ComponentList& list, size_t scale_index) const;
 
   size_t CurrentIteration() const { return current_iteration_; }
   float FluxCleaned() const { return flux_cleaned_; }

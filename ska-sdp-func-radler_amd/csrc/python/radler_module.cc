@@ -386,7 +386,18 @@ void InitComponentList(py::module& m) {  // python/pycomponent_list.cc
         if (s >= self.NScales())
           throw std::out_of_range("Scale index out of range in component count");
         return self.ComponentCount(s);
-      });
+      })
+      .def("get_component",
+           [](const radler::ComponentList& self, size_t s, size_t index) {
+             // (x, y, values): ComponentList::GetComponent (component_list.h)
+             if (s >= self.NScales() || index >= self.ComponentCount(s))
+               throw std::out_of_range("Component index out of range");
+             size_t x = 0, y = 0;
+             std::vector<float> values(self.NFrequencies());
+             self.GetComponent(s, index, x, y, values.data());
+             return py::make_tuple(x, y, values);
+           },
+           py::arg("scale_index"), py::arg("index"));
 }
 
 py::dict ResultDict(const radler::algorithms::ParallelDeconvolutionResult& r,
