@@ -592,3 +592,20 @@ void orc_spectral_interpolate(int mode, uint32_t n_terms, const double* frequenc
 }
 
 }  // extern "C"
+
+extern "C" {
+// MultiScaleAlgorithm::RunFullComponentFitter for one image: positions are
+// (x, y) pairs, counts[s] of them for scale s, in scale order.
+void orc_ms_full_component_fitter(float* residual, float* model, const float* psf,
+                                  uint64_t width, uint64_t height, const float* scales,
+                                  uint64_t n_scales, const uint32_t* positions,
+                                  const uint64_t* counts, double padding, int shape) {
+  std::vector<std::vector<std::pair<size_t, size_t>>> lists(n_scales);
+  size_t k = 0;
+  for (uint64_t s = 0; s != n_scales; ++s)
+    for (uint64_t i = 0; i != counts[s]; ++i, ++k)
+      lists[s].emplace_back(positions[2 * k], positions[2 * k + 1]);
+  RunFullComponentFitter(residual, model, psf, width, height,
+                         std::vector<float>(scales, scales + n_scales), lists, padding, shape);
+}
+}  // extern "C"

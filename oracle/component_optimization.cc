@@ -83,3 +83,91 @@ void GradientDescent(float* model, const float* image, const float* psf,
 }
 
 }  // namespace oracle
+
+namespace oracle {
+
+std::vector<std::vector<float>> GradientDescentWithVariablePsf(
+    const std::vector<std::vector<std::pair<size_t, size_t>>>& components_per_psf,
+    const float* image, const std::vector<std::vector<float>>& psfs, size_t width,
+    size_t height, size_t padded_width, size_t padded_height) {
+  const size_t n = width * height;
+  size_t count = 0;
+  for (const auto& c : components_per_psf) count += c.size();
+  std::vector<float> model_step(count), model_values(count, 0.0f);
+  std::vector<float> derivative_image(n), residual(n), times_psf(n);
+  for (size_t iteration = 0; iteration != 10; ++iteration) {  // :347-386
+    residual.assign(image, image + n);
+    if (iteration != 0) {
+      size_t parameter = 0;
+      for (size_t p = 0; p != psfs.size(); ++p) {
+        ConvolveModel<true>(residual.data(), components_per_psf[p], psfs[p].data(),
+                            &model_values[parameter], width, height, padded_width,
+                            padded_height);
+        parameter += components_per_psf[p].size();
+      }
+    }
+    size_t parameter = 0;
+    std::fill(derivative_image.begin(), derivative_image.end(), 0.0f);
+    for (size_t p = 0; p != psfs.size(); ++p) {
+      const auto& components = components_per_psf[p];
+      times_psf = residual;
+      PaddedConvolution(times_psf.data(), psfs[p].data(), width, height, padded_width,
+                        padded_height);
+      for (size_t i = 0; i != components.size(); ++i)
+        model_step[parameter + i] =
+            times_psf[components[i].first + components[i].second * width];
+      ConvolveModel<false>(derivative_image.data(), components, psfs[p].data(),
+                           &model_step[parameter], width, height, padded_width,
+                           padded_height);
+      parameter += components.size();
+    }
+    float numerator = 0.0f, divisor = 0.0f;  // ApplyLineSearch
+    for (size_t i = 0; i != n; ++i) {
+      numerator += derivative_image[i] * residual[i];
+      divisor += derivative_image[i] * derivative_image[i];
+    }
+    if (divisor != 0.0f) {
+      const float step = numerator / divisor;
+      if (std::isfinite(step))
+        for (size_t i = 0; i != count; ++i) model_values[i] += model_step[i] * step;
+    }
+  }
+  std::vector<std::vector<float>> result(psfs.size(), std::vector<float>(n, 0.0f));
+  size_t parameter = 0;
+  for (size_t p = 0; p != psfs.size(); ++p) {
+    for (size_t i = 0; i != components_per_psf[p].size(); ++i) {
+      const auto& pos = components_per_psf[p][i];
+      result[p][pos.second * width + pos.first] += model_values[parameter + i];
+    }
+    parameter += components_per_psf[p].size();
+  }
+  return result;
+}
+
+void RunFullComponentFitter(float* residual, float* model, const float* psf, size_t width,
+                            size_t height, const std::vector<float>& scales,
+                            const std::vector<std::vector<std::pair<size_t, size_t>>>& lists,
+                            double convolution_padding, int shape) {
+  const size_t n = width * height;
+  std::vector<std::vector<float>> convolved_psfs;
+  for (float scale : scales) {  // :845-853
+    convolved_psfs.emplace_back(psf, psf + n);
+    std::vector<float*> l{convolved_psfs.back().data()};
+    MsTransform(l, width, height, scale, Shape(shape));
+  }
+  const size_t pw = GetConvolutionSize(scales.back(), width, convolution_padding);
+  const size_t ph = GetConvolutionSize(scales.back(), height, convolution_padding);
+  std::vector<std::vector<float>> delta = GradientDescentWithVariablePsf(
+      lists, residual, convolved_psfs, width, height, pw, ph);
+  for (size_t s = 0; s != scales.size(); ++s) {  // :898-904
+    std::vector<float*> l{delta[s].data()};
+    MsTransform(l, width, height, scales[s], Shape(shape));
+    for (size_t i = 0; i != n; ++i) model[i] += delta[s][i];
+  }
+  for (size_t s = 0; s != scales.size(); ++s) {  // :906-911
+    PaddedConvolution(delta[s].data(), psf, width, height, pw, ph);
+    for (size_t i = 0; i != n; ++i) residual[i] -= delta[s][i];
+  }
+}
+
+}  // namespace oracle

@@ -10,6 +10,8 @@
 #pragma once
 
 #include <cstddef>
+#include <utility>
+#include <vector>
 
 namespace oracle {
 
@@ -21,5 +23,25 @@ void PaddedConvolution(float* image, const float* psf, size_t width, size_t heig
 void GradientDescent(float* model, const float* image, const float* psf,
                      size_t width, size_t height, size_t padded_width,
                      size_t padded_height);
+
+}  // namespace oracle
+
+namespace oracle {
+
+// component_optimization.cc:323-402: all scales' components fitted together,
+// each scale with its own (scale-convolved) PSF; returns one delta image of
+// component values per scale.
+std::vector<std::vector<float>> GradientDescentWithVariablePsf(
+    const std::vector<std::vector<std::pair<size_t, size_t>>>& components_per_psf,
+    const float* image, const std::vector<std::vector<float>>& psfs, size_t width,
+    size_t height, size_t padded_width, size_t padded_height);
+
+// MultiScaleAlgorithm::RunFullComponentFitter for one image
+// (multiscale_algorithm.cc:837-914, component-list bookkeeping aside):
+// residual and model updated in place.
+void RunFullComponentFitter(float* residual, float* model, const float* psf, size_t width,
+                            size_t height, const std::vector<float>& scales,
+                            const std::vector<std::vector<std::pair<size_t, size_t>>>& lists,
+                            double convolution_padding, int shape);
 
 }  // namespace oracle

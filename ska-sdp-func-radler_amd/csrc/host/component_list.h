@@ -4,6 +4,7 @@
 #pragma once
 
 #include <cstddef>
+#include <utility>
 #include <vector>
 
 namespace radler {
@@ -41,6 +42,14 @@ class ComponentList {
   }
   void GetComponent(size_t scale_index, size_t index, size_t& x, size_t& y,
                     float* values) const;
+  std::pair<size_t, size_t> GetComponentPosition(size_t scale_index, size_t index) const {
+    const auto& p = list_per_scale_[scale_index].positions[index];
+    return {p.x, p.y};
+  }
+  /// GetSingleValue (component_list.h): value of image `image_index`
+  float& Value(size_t scale_index, size_t index, size_t image_index) {
+    return list_per_scale_[scale_index].values[index * n_frequencies_ + image_index];
+  }
 
  private:
   struct ScaleList {

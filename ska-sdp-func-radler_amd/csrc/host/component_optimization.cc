@@ -2,6 +2,7 @@
 
 #include <cmath>
 
+#include "multiscale_transforms.h"
 #include "subminor.h"
 
 namespace radler::math {
@@ -69,6 +70,76 @@ void GradientDescent(gpu::Session& s, float* d_model, const float* d_image,
     }
   }
   gpu::Check(rdl_masked_add(s.Handle(), d_model, values.F(), n), "rdl_masked_add");
+}
+
+}  // namespace radler::math
+
+namespace radler::math {
+
+void RunFullComponentFitter(gpu::Session& s, float* d_residual, float* d_model,
+                            const float* d_psf, size_t width, size_t height,
+                            const std::vector<float>& scales,
+                            const std::vector<std::vector<std::pair<size_t, size_t>>>& lists,
+                            algorithms::multiscale::MultiScaleTransforms& transforms,
+                            size_t padded_width, size_t padded_height) {
+  const size_t n = width * height, bytes = n * sizeof(float), n_scales = scales.size();
+  std::vector<std::shared_ptr<gpu::Buffer>> spectra;
+  std::vector<gpu::Buffer> mask, values, step;
+  for (size_t sc = 0; sc != n_scales; ++sc) {
+    // the PSF convolved by the scale's shape (:845-853) and its padded spectrum
+    gpu::Buffer convolved(s, bytes);
+    s.D2D(convolved.Ptr(), d_psf, bytes);
+    transforms.Transform(convolved.F(), scales[sc]);
+    spectra.push_back(algorithms::SubMinorLoop::MakePaddedPsfSpectrum(
+        s, convolved.F(), width, height, padded_width, padded_height));
+    // a 1.0 at every component position of the scale
+    std::vector<float> m(n, 0.0f);
+    for (const auto& p : lists[sc]) m[p.second * width + p.first] = 1.0f;
+    mask.emplace_back(s, bytes);
+    s.H2D(mask.back().Ptr(), m.data(), bytes);
+    values.emplace_back(s, bytes);
+    values.back().Zero();
+    step.emplace_back(s, bytes);
+  }
+  gpu::Buffer residual(s, bytes), conv(s, bytes), direction(s, bytes);
+  for (size_t iteration = 0; iteration != 10; ++iteration) {  // :347-386
+    s.D2D(residual.Ptr(), d_residual, bytes);
+    if (iteration != 0)
+      for (size_t sc = 0; sc != n_scales; ++sc)
+        PaddedConvolveSubtract(s, values[sc].F(), residual.F(), width, height,
+                               padded_width, padded_height, spectra[sc]->Ptr());
+    direction.Zero();  // holds -(direction image)
+    for (size_t sc = 0; sc != n_scales; ++sc) {
+      conv.Zero();
+      PaddedConvolveSubtract(s, residual.F(), conv.F(), width, height, padded_width,
+                             padded_height, spectra[sc]->Ptr());
+      gpu::Check(rdl_masked_copy(s.Handle(), mask[sc].F(), conv.F(), step[sc].F(), n, -1.0f),
+                 "rdl_masked_copy");
+      PaddedConvolveSubtract(s, step[sc].F(), direction.F(), width, height, padded_width,
+                             padded_height, spectra[sc]->Ptr());
+    }
+    double neg_numerator = 0.0, divisor = 0.0;
+    gpu::Check(rdl_dot_pair(s.Handle(), direction.F(), residual.F(), n, &neg_numerator,
+                            &divisor),
+               "rdl_dot_pair");
+    if (float(divisor) != 0.0f) {
+      const float lambda = float(-neg_numerator) / float(divisor);
+      if (std::isfinite(lambda))
+        for (size_t sc = 0; sc != n_scales; ++sc)
+          gpu::Check(rdl_axpy(s.Handle(), values[sc].F(), step[sc].F(), n, lambda, 0),
+                     "rdl_axpy");
+    }
+  }
+  const std::shared_ptr<gpu::Buffer> psf_spectrum =
+      algorithms::SubMinorLoop::MakePaddedPsfSpectrum(s, d_psf, width, height,
+                                                       padded_width, padded_height);
+  for (size_t sc = 0; sc != n_scales; ++sc) {  // :898-911
+    transforms.Transform(values[sc].F(), scales[sc]);
+    gpu::Check(rdl_add(s.Handle(), d_model, values[sc].F(), n), "rdl_add");
+  }
+  for (size_t sc = 0; sc != n_scales; ++sc)
+    PaddedConvolveSubtract(s, values[sc].F(), d_residual, width, height, padded_width,
+                           padded_height, psf_spectrum->Ptr());
 }
 
 }  // namespace radler::math

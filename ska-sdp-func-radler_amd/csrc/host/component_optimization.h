@@ -3,6 +3,8 @@
 #pragma once
 
 #include <cstddef>
+#include <utility>
+#include <vector>
 
 #include "device.h"
 
@@ -20,5 +22,26 @@ void PaddedConvolveSubtract(gpu::Session& s, const float* d_src, float* d_dst,
 void GradientDescent(gpu::Session& s, float* d_model, const float* d_image,
                      const float* d_psf, size_t width, size_t height,
                      size_t padded_width, size_t padded_height);
+
+}  // namespace radler::math
+
+namespace radler::algorithms::multiscale {
+class MultiScaleTransforms;
+}
+
+namespace radler::math {
+
+/// MultiScaleAlgorithm::RunFullComponentFitter for one image
+/// (multiscale_algorithm.cc:837-914) with GradientDescentWithVariablePsf
+/// (component_optimization.cc:323-402): lists[s] are the scale-s component
+/// positions; every scale is fitted with the PSF convolved by its shape, the
+/// updates are shape-transformed into the model and convolved out of the
+/// residual (padded to the largest scale's convolution size).
+void RunFullComponentFitter(gpu::Session& s, float* d_residual, float* d_model,
+                            const float* d_psf, size_t width, size_t height,
+                            const std::vector<float>& scales,
+                            const std::vector<std::vector<std::pair<size_t, size_t>>>& lists,
+                            algorithms::multiscale::MultiScaleTransforms& transforms,
+                            size_t padded_width, size_t padded_height);
 
 }  // namespace radler::math

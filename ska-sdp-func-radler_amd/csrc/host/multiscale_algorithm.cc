@@ -8,6 +8,7 @@
 #include <set>
 #include <stdexcept>
 
+#include "component_optimization.h"
 #include "fft_sizes.h"
 #include "logger.h"
 #include "subminor.h"
@@ -105,6 +106,56 @@ void MultiScaleAlgorithm::DownloadScaleMasks() {
   if (!masks_session_) return;
   for (size_t i = 0; i != host_masks_.size() && i != dev_masks_.size(); ++i)
     masks_session_->D2H(host_masks_[i].data(), dev_masks_[i].Ptr(), host_masks_[i].size());
+}
+
+void MultiScaleAlgorithm::RunFullComponentFitter(ImageSet& residual_set,
+                                                 ImageSet& model_set,
+                                                 const gpu::Planes& psfs) {
+  // :916-929 over the images, :837-914 per image
+  if (ComponentOptimizationAlgorithm() != OptimizationAlgorithm::kGradientDescent)
+    throw std::runtime_error(
+        "Unsupported optimization algorithm for multiscale clean algorithm");
+  if (!component_list_)
+    throw std::runtime_error(
+        "Multiscale component optimisation fits the component list: it needs "
+        "save_source_list");
+  gpu::Session& s = residual_set.Session();
+  const size_t width = residual_set.Width(), height = residual_set.Height();
+  if (!transforms_ || transforms_->Width() != width || transforms_->Height() != height)
+    transforms_ = std::make_unique<MultiScaleTransforms>(s, width, height, settings_.shape);
+  std::vector<float> scales;
+  std::vector<std::vector<std::pair<size_t, size_t>>> lists(scale_infos_.size());
+  for (size_t sc = 0; sc != scale_infos_.size(); ++sc) {
+    scales.push_back(scale_infos_[sc].scale);
+    if (sc < component_list_->NScales())
+      for (size_t i = 0; i != component_list_->ComponentCount(sc); ++i)
+        lists[sc].push_back(component_list_->GetComponentPosition(sc, i));
+  }
+  const size_t pw = utils::GetConvolutionSize(scales.back(), width,
+                                              settings_.convolution_padding);
+  const size_t ph = utils::GetConvolutionSize(scales.back(), height,
+                                              settings_.convolution_padding);
+  std::vector<float> model(width * height);
+  for (size_t i = 0; i != residual_set.Size(); ++i) {
+    math::RunFullComponentFitter(s, residual_set.Data(i), model_set.Data(i),
+                                 psfs.Plane(residual_set.PsfIndex(i)), width, height, scales,
+                                 lists, *transforms_, pw, ph);
+    // :887-897: the list values take the (updated) model image's values
+    s.D2H(model.data(), model_set.Data(i), model.size() * sizeof(float));
+    for (size_t sc = 0; sc != lists.size(); ++sc)
+      for (size_t c = 0; c != lists[sc].size(); ++c)
+        component_list_->Value(sc, c, i) +=
+            model[lists[sc][c].second * width + lists[sc][c].first];
+  }
+  // ApplySpectralConstraintsToComponents (deconvolution_algorithm.cc:48-64)
+  std::vector<float> values(component_list_->NFrequencies());
+  for (size_t sc = 0; sc != component_list_->NScales(); ++sc)
+    for (size_t c = 0; c != component_list_->ComponentCount(sc); ++c) {
+      size_t x, y;
+      component_list_->GetComponent(sc, c, x, y, values.data());
+      PerformSpectralFit(values.data(), x, y);
+      for (size_t f = 0; f != values.size(); ++f) component_list_->Value(sc, c, f) = values[f];
+    }
 }
 
 const float* MultiScaleAlgorithm::PeakSearchInput(const float* d_image, size_t w,
@@ -245,10 +296,10 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
       if (a->track_masks_) a->DownloadScaleMasks();
     }
   } mask_sync{this};
-  if (ComponentOptimizationAlgorithm() != OptimizationAlgorithm::kClean)
-    throw std::runtime_error(
-        "Multiscale component optimisation (it fits the multiscale component "
-        "list) is not available in the MI355X build");
+  if (ComponentOptimizationAlgorithm() != OptimizationAlgorithm::kClean) {  // :242-246
+    RunFullComponentFitter(data_image, model_image, psfs);
+    return DeconvolutionResult{};
+  }
 
   bool has_hit_threshold_in_sub_loop = false;
   size_t threshold_countdown = std::max(size_t{8}, scale_infos_.size() * 3 / 2);

@@ -85,6 +85,8 @@ class MultiScaleAlgorithm final : public DeconvolutionAlgorithm {
   void FindActiveScaleConvolvedMaxima(const ImageSet& image_set,
                                       float* d_integrated, bool report_rms);
   void FindPeakDirect(const float* d_image, size_t scale_index);
+  void RunFullComponentFitter(ImageSet& residual_set, ImageSet& model_set,
+                              const gpu::Planes& psfs);
   void ActivateScales(size_t scale_with_last_peak);
   void UploadScaleMasks(gpu::Session& s, size_t n_pixels);
   void DownloadScaleMasks();

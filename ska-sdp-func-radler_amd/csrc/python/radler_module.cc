@@ -17,6 +17,8 @@
 #include "radler.h"
 #include "rms_image.h"
 #include "component_optimization.h"
+#include "fft_sizes.h"
+#include "multiscale_transforms.h"
 
 namespace py = pybind11;
 using AccessorList = std::vector<std::unique_ptr<aocommon::ImageAccessor>>;
@@ -565,6 +567,33 @@ void InitGpu(py::module& m) {
         return out;
       },
       py::arg("model"), py::arg("residual"), py::arg("psf"));
+  g.def(
+      "ms_full_component_fitter",
+      [](FloatArray residual, FloatArray model, FloatArray psf, std::vector<float> scales,
+         std::vector<std::vector<std::pair<size_t, size_t>>> lists, double padding) {
+        // MultiScaleAlgorithm::RunFullComponentFitter for one image
+        const size_t h = residual.shape(0), w = residual.shape(1), n = w * h;
+        std::shared_ptr<radler::gpu::Session> session =
+            radler::gpu::Session::ForDevice(radler::gpu::Session::DefaultDevice());
+        radler::gpu::Session& s = *session;
+        radler::gpu::Buffer dr(s, n * sizeof(float)), dm(s, n * sizeof(float)),
+            dp(s, n * sizeof(float));
+        s.H2D(dr.Ptr(), residual.data(), n * sizeof(float));
+        s.H2D(dm.Ptr(), model.data(), n * sizeof(float));
+        s.H2D(dp.Ptr(), psf.data(), n * sizeof(float));
+        radler::algorithms::multiscale::MultiScaleTransforms transforms(
+            s, w, h, radler::MultiscaleShape::kTaperedQuadraticShape);
+        const size_t pw = radler::utils::GetConvolutionSize(scales.back(), w, padding);
+        const size_t ph = radler::utils::GetConvolutionSize(scales.back(), h, padding);
+        radler::math::RunFullComponentFitter(s, dr.F(), dm.F(), dp.F(), w, h, scales, lists,
+                                             transforms, pw, ph);
+        py::array_t<float> out_r({h, w}), out_m({h, w});
+        s.D2H(out_r.mutable_data(), dr.F(), n * sizeof(float));
+        s.D2H(out_m.mutable_data(), dm.F(), n * sizeof(float));
+        return py::make_tuple(out_r, out_m);
+      },
+      py::arg("residual"), py::arg("model"), py::arg("psf"), py::arg("scales"),
+      py::arg("lists"), py::arg("padding") = 1.1);
   g.def(
       "sliding_minimum",
       [](FloatArray image, size_t window) {

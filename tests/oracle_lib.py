@@ -216,6 +216,25 @@ class Oracle:
         L.orc_gradient_descent(m.ctypes.data, r.ctypes.data, p.ctypes.data, w, h)
         return m
 
+    def ms_full_component_fitter(self, residual, model, psf, scales, lists, padding=1.1,
+                                 shape=0):
+        """RunFullComponentFitter for one image -> (residual, model)."""
+        r = np.ascontiguousarray(residual, np.float32).copy()
+        m = np.ascontiguousarray(model, np.float32).copy()
+        p = np.ascontiguousarray(psf, np.float32)
+        h, w = r.shape
+        sc = np.ascontiguousarray(scales, np.float32)
+        pos = np.ascontiguousarray([c for l in lists for xy in l for c in xy] or [0], np.uint32)
+        counts = np.ascontiguousarray([len(l) for l in lists], np.uint64)
+        L = self.lib
+        L.orc_ms_full_component_fitter.argtypes = [C.c_void_p] * 3 + [C.c_uint64] * 2 + [
+            C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_double, C.c_int]
+        L.orc_ms_full_component_fitter.restype = None
+        L.orc_ms_full_component_fitter(r.ctypes.data, m.ctypes.data, p.ctypes.data, w, h,
+                                       sc.ctypes.data, sc.size, pos.ctypes.data,
+                                       counts.ctypes.data, float(padding), int(shape))
+        return r, m
+
     def padded_convolution(self, image, psf, pw, ph):
         img = np.ascontiguousarray(image, np.float32).copy()
         p = np.ascontiguousarray(psf, np.float32)

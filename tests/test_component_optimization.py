@@ -118,5 +118,30 @@ def test_unavailable_optimisations_are_rejected():
     s.absolute_threshold = 1e-3
     rd.gpu.set_component_optimization(s, rd.OptimizationAlgorithm.gradient_descent)
     run = rd.gpu.DeviceRun(s, psf, dirty, [], 2.0 * PIXEL_SCALE)
-    with pytest.raises(RuntimeError, match="not available"):
+    # multiscale gradient descent fits the component list (save_source_list)
+    with pytest.raises(RuntimeError, match="save_source_list"):
         run.execute()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,scales", [(96, [0.0, 8.0, 16.0]), (128, [0.0, 8.0])])
+def test_ms_full_component_fitter_matches_oracle(w, scales):
+    """MultiScaleAlgorithm::RunFullComponentFitter
+    (multiscale_algorithm.cc:837-914) with GradientDescentWithVariablePsf
+    (component_optimization.cc:323-402): residual and model within 1e-4 x
+    their maxima of the oracle's restatement, residual RMS lowered."""
+    from radler_import import radler as rd
+    psf, dirty = problem(w, w, 20, 3, seed=w, noise=1e-3)
+    rng = np.random.default_rng(w)
+    lists = []
+    model = np.zeros_like(dirty)
+    for sc in scales:
+        pts = {(int(x), int(y)) for x, y in rng.integers(8, w - 8, (12, 2))}
+        lists.append(sorted(pts))
+        for x, y in pts:
+            model[y, x] += 0.01
+    res_g, mod_g = rd.gpu.ms_full_component_fitter(dirty, model, psf, scales, lists)
+    res_o, mod_o = get_oracle().ms_full_component_fitter(dirty, model, psf, scales, lists)
+    np.testing.assert_allclose(res_g, res_o, atol=1e-4 * np.abs(res_o).max())
+    np.testing.assert_allclose(mod_g, mod_o, atol=1e-4 * np.abs(mod_o).max())
+    assert np.sqrt(np.mean(res_o ** 2)) < np.sqrt(np.mean(dirty ** 2))
