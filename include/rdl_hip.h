@@ -527,6 +527,15 @@ int rdl_untrim(rdl_session* s, float* d_dest, uint32_t pw, uint32_t ph,
                const float* d_src, uint32_t width, uint32_t height);
 int rdl_trim(rdl_session* s, float* d_dest, uint32_t width, uint32_t height,
              const float* d_src, uint32_t pw, uint32_t ph);
+/* d_dest (pw x ph) = the w x h image repeated periodically and shifted by
+ * (shift_x, shift_y): dest[y][x] = src[(y - sy) mod h][(x - sx) mod w].
+ * Lets the multiscale transforms (multiscale_transforms.cc:9-21, circular at
+ * W x H) run at an FFT-friendly size: a kernel of radius r <= shift convolved
+ * with this plane and cropped at (shift_x, shift_y) is the circular
+ * convolution at W x H, whatever prime factors W and H have. */
+int rdl_periodic_extend(rdl_session* s, float* d_dest, uint32_t pw, uint32_t ph,
+                        const float* d_src, uint32_t width, uint32_t height,
+                        uint32_t shift_x, uint32_t shift_y);
 
 /* multiscale::MultiScaleTransforms::AddShapeComponent
  * (multiscale_transforms.h:62-89): image += kernel(n x n host) * gain at x,y. */

@@ -169,6 +169,8 @@ struct OrcAlgo {
   std::vector<IuwtStep> iuwt_steps;  // type 2: steps of the last execute
   std::vector<float> rms_factor;     // SetRmsFactorImage (empty = none)
   int component_optimization = 0;    // SetComponentOptimizationAlgorithm
+  std::vector<float> margins;        // decision margins of the last trace (+ end)
+  std::vector<float> values;         // the components' |peak| (+ the last one)
 };
 
 static AlgoSettings MakeSettings(const orc_algo_settings* a) {
@@ -290,6 +292,15 @@ int orc_algo_execute(void* h, const orc_set_desc* d, float* residual,
     out->is_diverging = r.is_diverging;
     out->iteration_number = algo->iteration_number;
     out->n_trace = tr.size();
+    algo->margins.clear();
+    algo->values.clear();
+    for (const Component& c : tr) {
+      algo->margins.push_back(c.margin);
+      algo->values.push_back(c.value);
+    }
+    algo->margins.push_back(algo->ms ? algo->ms->end_margin
+                                     : std::numeric_limits<float>::infinity());
+    algo->values.push_back(tr.empty() ? 1.0f : tr.back().value);
     if (trace) {
       const size_t n = std::min<size_t>(tr.size(), trace_cap);
       for (size_t i = 0; i != n; ++i) {
@@ -313,7 +324,21 @@ struct orc_parallel_result {
   uint64_t n_trace;
 };
 
+// Decision margins of the last execute's trace (oracle.h Component::margin),
+// one per component and then the end-of-run margin; returns the count.
+// `values` (may be NULL) gets each component's |peak| (the margin's scale).
+uint64_t orc_algo_margins(void* h, float* out, float* values, uint64_t cap) {
+  auto* algo = static_cast<OrcAlgo*>(h);
+  const size_t n = std::min<size_t>(cap, algo->margins.size());
+  std::copy_n(algo->margins.data(), n, out);
+  if (values) std::copy_n(algo->values.data(), n, values);
+  return algo->margins.size();
+}
+
 struct OrcParallel {
+  std::vector<float> margins;      // per trace entry, in trace order
+  std::vector<float> values;       // the components' |peak|
+  std::vector<float> end_margins;  // per subimage
   size_t grid_w, grid_h;
   double major_loop_gain_unused = 0.0;
   bool snapshot = false;
@@ -508,6 +533,16 @@ int orc_parallel_execute(void* h, const orc_set_desc* d, float* residual,
       out->total_iterations += t.iteration_number;
     if (labels) std::fill(labels, labels + d->width * d->height, uint16_t(0));
     uint64_t n_trace = 0;
+    p->margins.clear();
+    p->values.clear();
+    p->end_margins.assign(subs.size(), std::numeric_limits<float>::infinity());
+    for (const SubImage& s : subs) {
+      p->end_margins[s.index] = s.end_margin;
+      for (const Component& c : traces[s.index]) {
+        p->margins.push_back(c.margin);
+        p->values.push_back(c.value);
+      }
+    }
     for (const SubImage& s : subs) {
       if (sub_boxes) {
         sub_boxes[4 * s.index] = uint32_t(s.x);
@@ -609,3 +644,19 @@ void orc_ms_full_component_fitter(float* residual, float* model, const float* ps
                          std::vector<float>(scales, scales + n_scales), lists, padding, shape);
 }
 }  // extern "C"
+
+// Margins of the last orc_parallel_execute: n_trace entries in trace order,
+// then one end margin per subimage; returns the total count.
+// `values` (may be NULL): the components' |peak| (end entries: 0).
+extern "C" uint64_t orc_parallel_margins(void* h, float* out, float* values,
+                                         uint64_t cap) {
+  auto* p = static_cast<OrcParallel*>(h);
+  std::vector<float> all = p->margins;
+  all.insert(all.end(), p->end_margins.begin(), p->end_margins.end());
+  std::vector<float> vals = p->values;
+  vals.resize(all.size(), 0.0f);
+  const size_t n = std::min<size_t>(cap, all.size());
+  std::copy_n(all.data(), n, out);
+  if (values) std::copy_n(vals.data(), n, values);
+  return all.size();
+}

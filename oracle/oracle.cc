@@ -497,6 +497,21 @@ size_t SubMinorLoop::GetMaxComponent(std::vector<float>& scratch,
   return max_component;
 }
 
+void SubMinorLoop::NoteArgmaxMargin(const std::vector<float>& scratch,
+                                    size_t chosen) const {
+  const auto value = [&](size_t i) {
+    return allow_negative ? std::fabs(scratch[i]) : scratch[i];
+  };
+  bool any = false;
+  float second = 0.0f;
+  for (size_t i = 0; i != positions_.size(); ++i)
+    if (i != chosen && (!any || value(i) > second)) {
+      second = value(i);
+      any = true;
+    }
+  if (any) margins->Note(value(chosen), second);
+}
+
 SubMinorLoop::RunResult SubMinorLoop::Run(
     ImageSet& convolved_residual,
     const std::vector<const float*>& twice_convolved_psfs) {
@@ -542,15 +557,23 @@ SubMinorLoop::RunResult SubMinorLoop::Run(
   const float max_value_at_start = std::fabs(max_value);
   bool diverging = false;
   std::vector<float> component_values(n_img);
-  while (std::fabs(max_value) > threshold &&
-         current_iteration < max_iterations &&
-         (!stop_on_negative || max_value >= 0.0f) && !diverging) {
+  for (;;) {
+    if (margins) margins->Note(std::fabs(max_value), threshold);
+    if (!(std::fabs(max_value) > threshold &&
+          current_iteration < max_iterations &&
+          (!stop_on_negative || max_value >= 0.0f) && !diverging))
+      break;
+    if (margins) NoteArgmaxMargin(scratch, max_component);
     for (size_t i = 0; i != n_img; ++i)
       component_values[i] = residual_[i][max_component] * gain;
     flux_cleaned += max_value * gain;
     const size_t x = positions_[max_component].first;
     const size_t y = positions_[max_component].second;
-    if (trace) trace->push_back({uint32_t(x), uint32_t(y), trace_scale});
+    if (trace)
+      trace->push_back({uint32_t(x), uint32_t(y), trace_scale,
+                        margins ? margins->Take()
+                                : std::numeric_limits<float>::infinity(),
+                        std::fabs(max_value)});
     PerformSpectralFit(convolved_residual.desc->fitter.get(),
                        convolved_residual.desc->n_pol, component_values.data());
     for (size_t i = 0; i != n_img; ++i)
@@ -912,8 +935,29 @@ void MultiScale::FindActiveScaleConvolvedMaxima(const ImageSet& set,
   }
 }
 
+void MultiScale::NoteScaleSelection() {
+  // SelectMaximumScale's std::map<float, size_t> keys (test margins)
+  float first = -1.0f, second = -1.0f;
+  for (const ScaleInfo& e : scales_) {
+    if (!e.is_active) continue;
+    const float key = std::fabs(e.max_unnormalized_image_value * e.bias_factor);
+    if (key > first) {
+      second = first;
+      first = key;
+    } else if (key > second) {
+      second = key;
+    }
+  }
+  if (second >= 0.0f) margins.Note(first, second);
+}
+
 void MultiScale::ActivateScales(size_t last) {  // .cc:636-656
   for (size_t i = 0; i != scales_.size(); ++i) {
+    if (i != last)
+      margins.Note(std::fabs(scales_[i].max_unnormalized_image_value) *
+                       scales_[i].bias_factor,
+                   std::fabs(scales_[last].max_unnormalized_image_value) *
+                       (1.0 - s_.minor_loop_gain) * scales_[last].bias_factor);
     const bool activate =
         i == last ||
         std::fabs(scales_[i].max_unnormalized_image_value) *
@@ -959,6 +1003,9 @@ Result MultiScale::Execute(ImageSet& data, ImageSet& model,
   FindActiveScaleConvolvedMaxima(data, integrated.data(), true);
   Result result;
   size_t scale_with_peak;
+  margins = MarginTracker();
+  end_margin = std::numeric_limits<float>::infinity();
+  NoteScaleSelection();
   if (!SelectMaximumScale(scales_, scale_with_peak)) {
     result.another_iteration_required = false;
     return result;
@@ -984,12 +1031,17 @@ Result MultiScale::Execute(ImageSet& data, ImageSet& model,
   for (auto& v : individual) individual_set.images.push_back(v.data());
   bool diverging = false;
 
-  while (iteration_number < s_.max_iterations &&
-         std::fabs(scales_[scale_with_peak].max_unnormalized_image_value *
-                   scales_[scale_with_peak].bias_factor) > first_threshold &&
-         (!s_.stop_on_negative ||
-          scales_[scale_with_peak].max_unnormalized_image_value >= 0.0f) &&
-         threshold_countdown > 0 && !diverging) {
+  for (;;) {
+    margins.Note(std::fabs(scales_[scale_with_peak].max_unnormalized_image_value *
+                           scales_[scale_with_peak].bias_factor),
+                 first_threshold);
+    if (!(iteration_number < s_.max_iterations &&
+          std::fabs(scales_[scale_with_peak].max_unnormalized_image_value *
+                    scales_[scale_with_peak].bias_factor) > first_threshold &&
+          (!s_.stop_on_negative ||
+           scales_[scale_with_peak].max_unnormalized_image_value >= 0.0f) &&
+          threshold_countdown > 0 && !diverging))
+      break;
     const ScaleInfo& sinfo = scales_[scale_with_peak];
     std::vector<std::vector<float>> twice(n_psf);
     std::vector<float*> transform_list;
@@ -1008,6 +1060,7 @@ Result MultiScale::Execute(ImageSet& data, ImageSet& model,
         std::fabs(sinfo.max_unnormalized_image_value * sinfo.bias_factor) *
         (1.0 - s_.sub_minor_loop_gain);
     float first_sub_iteration_threshold = sub_iteration_gain_threshold;
+    margins.Note(first_threshold, first_sub_iteration_threshold);
     if (first_threshold > first_sub_iteration_threshold) {
       first_sub_iteration_threshold = first_threshold;
       if (!has_hit_threshold_in_sub_loop) has_hit_threshold_in_sub_loop = true;
@@ -1036,6 +1089,7 @@ Result MultiScale::Execute(ImageSet& data, ImageSet& model,
       sub.rms_factor = s_.rms_factor;  // multiscale_algorithm.cc:401-402
       sub.trace = trace;
       sub.trace_scale = uint32_t(scale_with_peak);
+      sub.margins = &margins;
       std::vector<const float*> twice_ptrs;
       for (auto& t : twice) twice_ptrs.push_back(t.data());
       SubMinorLoop::RunResult r = sub.Run(individual_set, twice_ptrs);
@@ -1074,7 +1128,10 @@ Result MultiScale::Execute(ImageSet& data, ImageSet& model,
         for (size_t i = 0; i != data.Size(); ++i)
           cv[i] = individual[i][mi.max_image_value_x + mi.max_image_value_y * width];
         const size_t x = mi.max_image_value_x, y = mi.max_image_value_y;
-        if (trace) trace->push_back({uint32_t(x), uint32_t(y), uint32_t(scale_with_peak)});
+        if (trace)
+          trace->push_back(
+              {uint32_t(x), uint32_t(y), uint32_t(scale_with_peak), margins.Take(),
+               std::fabs(mi.max_unnormalized_image_value * mi.bias_factor)});
         PerformSpectralFit(data.desc->fitter.get(), data.desc->n_pol,
                            cv.data());  // multiscale_algorithm.cc:477
         for (size_t i = 0; i != data.Size(); ++i) {
@@ -1112,11 +1169,14 @@ Result MultiScale::Execute(ImageSet& data, ImageSet& model,
                      e.max_image_value_x, e.max_image_value_y);
       std::fprintf(stderr, "\n");
     }
+    NoteScaleSelection();
     if (!SelectMaximumScale(scales_, scale_with_peak)) {
       result.another_iteration_required = false;
+      end_margin = margins.Take();
       return result;
     }
   }
+  end_margin = margins.Take();
   const bool max_iter_reached = iteration_number >= s_.max_iterations;
   const bool negative_reached =
       s_.stop_on_negative &&

@@ -144,8 +144,31 @@ struct Result {
 };
 
 // One CLEAN component: Högbom/Clark record pixel components (scale 0).
+// `margin` (test harness, not part of the reference): the smallest gap, in
+// the compared quantity's units, between a comparison's two sides over
+// every decision taken since the previous component up to and including the
+// choice of this one (argmax runner-up, loop-continue thresholds, scale
+// selection and activation). A float engine that differs from this one by
+// less than that gap makes the same decisions (tests/trace_compare.py).
 struct Component {
   uint32_t x, y, scale;
+  float margin = std::numeric_limits<float>::infinity();
+  float value = 0.0f;  // |integrated peak| that chose it (margin scale)
+};
+
+// Decision-margin bookkeeping for the traces above.
+struct MarginTracker {
+  float pending = std::numeric_limits<float>::infinity();
+  // a comparison a > b (or a >= b) was evaluated: record |a - b|
+  void Note(double a, double b) {
+    const float m = float(std::fabs(a - b));
+    if (m < pending) pending = m;
+  }
+  float Take() {
+    const float m = pending;
+    pending = std::numeric_limits<float>::infinity();
+    return m;
+  }
 };
 
 // cpp/algorithms/subminor_loop.{h,cc}
@@ -166,6 +189,7 @@ class SubMinorLoop {
   float flux_cleaned = 0.0f;
   std::vector<Component>* trace = nullptr;
   uint32_t trace_scale = 0;
+  MarginTracker* margins = nullptr;  // decision margins (tests only)
 
   // returns {diverging, has_peak, peak}
   struct RunResult {
@@ -190,6 +214,8 @@ class SubMinorLoop {
   std::vector<float> rms_selected_;  // SubMinorModel::MakeRmsFactorImage
   const SetDesc* desc_ = nullptr;
   size_t GetMaxComponent(std::vector<float>& scratch, float& max_value) const;
+  // gap between the chosen |value| and the runner-up in scratch
+  void NoteArgmaxMargin(const std::vector<float>& scratch, size_t chosen) const;
 };
 
 // cpp/algorithms/generic_clean.cc:56-253
@@ -228,9 +254,14 @@ class MultiScale {
                  const std::vector<const float*>& psfs,
                  std::vector<Component>* trace);
   const std::vector<ScaleInfo>& Scales() const { return scales_; }
+  // decision margins (tests): pending margins after the last component end
+  // up in end_margin (the decisions that stopped the run)
+  MarginTracker margins;
+  float end_margin = std::numeric_limits<float>::infinity();
 
  private:
   AlgoSettings s_;
+  void NoteScaleSelection();
   std::vector<ScaleInfo> scales_;
   void FindActiveScaleConvolvedMaxima(const ImageSet& set, float* integrated,
                                       bool report_rms);

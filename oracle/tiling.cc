@@ -338,6 +338,7 @@ ParallelResult ParallelRun(std::vector<TiledAlgorithm>& algorithms,
     std::vector<Component> tr;
     Result r = alg.Execute(sd, sm, sub_psfs, &tr);
     if (traces && !find_peak_only) (*traces)[s.index] = tr;
+    if (!find_peak_only && alg.ms) s.end_margin = alg.ms->end_margin;
     s.peak = r.final_peak;
     s.reached_major_threshold = r.another_iteration_required;
     const bool converging =

@@ -2,6 +2,7 @@
 // ParallelDeconvolution tiling restatement (see tiling.cc).
 #pragma once
 
+#include <limits>
 #include <memory>
 #include <vector>
 
@@ -15,6 +16,8 @@ struct SubImage {
   std::vector<unsigned char> mask, boundary_mask;  // bool per pixel
   double peak = 0.0;
   bool reached_major_threshold = false;
+  // test harness: decision margin after the last component of the clean pass
+  float end_margin = std::numeric_limits<float>::infinity();
 };
 
 // One subimage's algorithm (the reference clones the first algorithm per

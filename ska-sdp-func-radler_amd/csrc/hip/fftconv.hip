@@ -170,6 +170,22 @@ __global__ __launch_bounds__(256) void UntrimKernel(float* dest, uint32_t pw,
   }
 }
 
+// dest (pw x ph) = the w x h image repeated periodically, shifted by (sx, sy):
+// dest[y][x] = src[(y - sy) mod h][(x - sx) mod w]. A circular convolution at
+// w x h with a kernel of radius r <= sx, sy equals the linear convolution of
+// this plane cropped at (sx, sy) when pw >= w + 2r and ph >= h + 2r.
+__global__ __launch_bounds__(256) void PeriodicExtendKernel(
+    float* __restrict__ dest, uint32_t pw, uint32_t ph, const float* __restrict__ src,
+    uint32_t w, uint32_t h, uint32_t sx, uint32_t sy) {
+  const uint32_t x = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t y = blockIdx.y;
+  if (x >= pw) return;
+  const uint32_t sxr = sx % w, syr = sy % h;
+  const uint32_t ix = (x + w - sxr) % w;
+  const uint32_t iy = (y + h - syr) % h;
+  dest[size_t(y) * pw + x] = src[size_t(iy) * w + ix];
+}
+
 __global__ __launch_bounds__(256) void TrimKernel(float* dest, uint32_t w,
                                                   uint32_t h, const float* src,
                                                   uint32_t pw, uint32_t ph) {
@@ -414,6 +430,19 @@ int rdl_untrim(rdl_session* s, float* d_dest, uint32_t pw, uint32_t ph,
   RDL_ARG_CHECK(pw >= width && ph >= height, "padded size smaller than image");
   rdl::UntrimKernel<<<rdl::Grid(size_t(pw) * ph), 256, 0, s->stream>>>(
       d_dest, pw, ph, d_src, width, height);
+  RDL_HIP_CHECK(hipGetLastError());
+  return RDL_OK;
+}
+
+int rdl_periodic_extend(rdl_session* s, float* d_dest, uint32_t pw, uint32_t ph,
+                        const float* d_src, uint32_t width, uint32_t height,
+                        uint32_t shift_x, uint32_t shift_y) {
+  RDL_ARG_CHECK(s && d_dest && d_src, "NULL argument");
+  RDL_ARG_CHECK(width > 0 && height > 0 && ph < 65536, "bad plane size");
+  rdl::ScopedTiming t(s, "extend", double(pw) * ph * 8.0);
+  const dim3 grid((pw + 255) / 256, ph);
+  rdl::PeriodicExtendKernel<<<grid, 256, 0, s->stream>>>(d_dest, pw, ph, d_src, width,
+                                                        height, shift_x, shift_y);
   RDL_HIP_CHECK(hipGetLastError());
   return RDL_OK;
 }

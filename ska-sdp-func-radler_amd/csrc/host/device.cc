@@ -3,6 +3,8 @@
 #include <cstdlib>
 #include <mutex>
 
+#include "host_profile.h"
+
 namespace radler::gpu {
 
 void Check(int rc, const char* what) {
@@ -13,6 +15,7 @@ void Check(int rc, const char* what) {
 Buffer::Buffer(Session& s, size_t bytes) { Resize(s, bytes); }
 
 Buffer::~Buffer() {
+  prof::Section p("gpu.free");
   if (ptr_) rdl_free(s_->Handle(), ptr_);
 }
 
@@ -30,6 +33,7 @@ Buffer& Buffer::operator=(Buffer&& o) noexcept {
 
 void Buffer::Resize(Session& s, size_t bytes) {
   if (ptr_ && bytes <= bytes_) return;
+  prof::Section p("gpu.malloc");
   if (ptr_) Check(rdl_free(s_->Handle(), ptr_), "rdl_free");
   s_ = &s;
   ptr_ = nullptr;
@@ -204,8 +208,10 @@ Session::~Session() {
 Fft& Session::GetFft(size_t width, size_t height, bool f64) {
   auto key = std::make_tuple(width, height, f64);
   auto it = ffts_.find(key);
-  if (it == ffts_.end())
+  if (it == ffts_.end()) {
+    prof::Section p("gpu.fft_plan");
     it = ffts_.emplace(key, std::make_unique<Fft>(*this, width, height, f64)).first;
+  }
   return *it->second;
 }
 
@@ -219,7 +225,9 @@ rdl_subminor* Session::SharedSubminor() {
   return subminor_;
 }
 
-void Session::Sync() { Check(rdl_session_sync(s_), "rdl_session_sync"); }
+void Session::Sync() {
+  prof::Section p("gpu.sync");
+  Check(rdl_session_sync(s_), "rdl_session_sync"); }
 void Session::Bind() { Check(rdl_session_bind(s_), "rdl_session_bind"); }
 void Session::SetConcurrency(size_t n) {
   Check(rdl_session_set_concurrency(s_, uint32_t(n)), "rdl_session_set_concurrency");
@@ -231,9 +239,11 @@ void Session::Peer(void* d, int dst_device, const void* src, int src_device,
 }
 
 void Session::H2D(void* d, const void* h, size_t bytes) {
+  prof::Section p("gpu.h2d");
   Check(rdl_memcpy_h2d(s_, d, h, bytes), "rdl_memcpy_h2d");
 }
 void Session::D2H(void* h, const void* d, size_t bytes) {
+  prof::Section p("gpu.d2h");
   Check(rdl_memcpy_d2h(s_, h, d, bytes), "rdl_memcpy_d2h");
 }
 void Session::D2D(void* d, const void* src, size_t bytes) {

@@ -5,19 +5,21 @@
 #include <cstdint>
 #include <limits>
 #include <queue>
+#include <stdexcept>
 
 namespace radler::math {
 
 namespace {
 
+// One heap entry: the cost of the path up to the predecessor, the target and
+// the predecessor as (u, v) — u runs along the path, v across the band.
+// 12 bytes (images up to 65535 pixels a side); the heap order depends only
+// on `cost`, like the reference's Visit (dijkstra_splitter.h:24-29), so
+// equal costs pop in the same heap order as the reference's queue.
 struct Node {
   float cost;
-  // target and predecessor as (u, v): u runs along the path, v across the band
-  uint32_t u, v, pu, pv;
+  uint16_t u, v, pu, pv;
 };
-// min-cost first; only the cost takes part in the ordering, like the
-// reference's Visit (dijkstra_splitter.h:24-29), so equal costs pop in the
-// same heap order
 struct LaterFirst {
   bool operator()(const Node& a, const Node& b) const { return a.cost > b.cost; }
 };
@@ -28,14 +30,20 @@ template <bool kVertical>
 void DijkstraSplitter::Divide(const float* image, float* output, size_t lo,
                               size_t hi) const {
   const size_t n_u = kVertical ? height_ : width_;  // path length axis
+  if (width_ >= 65535 || height_ >= 65535)
+    throw std::runtime_error("DijkstraSplitter: image side of 65535 pixels or more");
   const size_t band = hi - lo;
   auto pixel = [&](size_t u, size_t v) -> size_t {
     return kVertical ? u * width_ + v : v * width_ + u;
   };
-  std::priority_queue<Node, std::vector<Node>, LaterFirst> open;
+  std::vector<Node> heap_store;
+  heap_store.reserve(8 * band);
+  std::priority_queue<Node, std::vector<Node>, LaterFirst> open(LaterFirst(),
+                                                                std::move(heap_store));
   for (size_t v = lo; v != hi; ++v)
-    open.push(Node{0.0f, 0, uint32_t(v), 0, uint32_t(v)});
-  std::vector<uint64_t> back(band * n_u);  // predecessor (pu << 32 | pv)
+    open.push(Node{0.0f, 0, uint16_t(v), 0, uint16_t(v)});
+  // predecessor of each settled pixel (pu << 16 | pv), band-local layout
+  std::vector<uint32_t> back(band * n_u);
   for (size_t u = 0; u != n_u; ++u)
     for (size_t v = lo; v != hi; ++v)
       output[pixel(u, v)] = std::numeric_limits<float>::max();
@@ -48,19 +56,17 @@ void DijkstraSplitter::Divide(const float* image, float* output, size_t lo,
     const float cost = cur.cost + std::fabs(image[at]);
     if (!(cost < output[at])) continue;
     output[at] = cost;
-    back[(cur.v - lo) + size_t(cur.u) * band] = (uint64_t(cur.pu) << 32) | cur.pv;
-    const uint32_t u = cur.u, v = cur.v;
-    auto expand = [&](uint32_t nu, uint32_t nv) {
-      open.push(Node{cost, nu, nv, u, v});
-    };
+    back[(cur.v - lo) + size_t(cur.u) * band] = (uint32_t(cur.pu) << 16) | cur.pv;
+    const uint16_t u = cur.u, v = cur.v;
+    const uint16_t u1 = uint16_t(u + 1);
     if (v > lo) {
-      expand(u + 1, v - 1);
-      expand(u, v - 1);
+      open.push(Node{cost, u1, uint16_t(v - 1), u, v});
+      open.push(Node{cost, u, uint16_t(v - 1), u, v});
     }
-    expand(u + 1, v);
-    if (v + 1 < hi) {
-      expand(u + 1, v + 1);
-      expand(u, v + 1);
+    open.push(Node{cost, u1, v, u, v});
+    if (v + 1u < hi) {
+      open.push(Node{cost, u1, uint16_t(v + 1), u, v});
+      open.push(Node{cost, u, uint16_t(v + 1), u, v});
     }
   }
   for (size_t u = 0; u != n_u; ++u)
@@ -68,9 +74,9 @@ void DijkstraSplitter::Divide(const float* image, float* output, size_t lo,
   uint32_t pu = cur.pu, pv = cur.pv;
   for (; pu > 0;) {
     output[pixel(pu, pv)] = 1.0f;
-    const uint64_t p = back[(pv - lo) + size_t(pu) * band];
-    pu = uint32_t(p >> 32);
-    pv = uint32_t(p);
+    const uint32_t p = back[(pv - lo) + size_t(pu) * band];
+    pu = p >> 16;
+    pv = p & 0xffffu;
   }
   output[pixel(0, pv)] = 1.0f;
 }

@@ -2,6 +2,7 @@
 // cpp/algorithms/multiscale_algorithm.cc unless stated.
 #include "multiscale_algorithm.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <map>
@@ -10,6 +11,7 @@
 
 #include "component_optimization.h"
 #include "fft_sizes.h"
+#include "host_profile.h"
 #include "logger.h"
 #include "subminor.h"
 
@@ -173,6 +175,7 @@ float MultiScaleAlgorithm::Normalized(float value, size_t x, size_t y, size_t w)
 
 void MultiScaleAlgorithm::FindPeakDirect(const float* d_image,
                                          size_t scale_index) {  // :700-748
+  prof::Section prof_section("ms.find_peak_direct");
   ScaleInfo& info = scale_infos_[scale_index];
   const size_t w = transforms_->Width(), h = transforms_->Height();
   d_image = PeakSearchInput(d_image, w, h);
@@ -191,6 +194,7 @@ void MultiScaleAlgorithm::FindPeakDirect(const float* d_image,
 
 void MultiScaleAlgorithm::FindActiveScaleConvolvedMaxima(
     const ImageSet& image_set, float* d_integrated, bool report_rms) {
+  prof::Section prof_section("ms.find_maxima");
   // :578-634 with ThreadedDeconvolutionTools::FindMultiScalePeak /
   // FindSingleScalePeak (threaded_deconvolution_tools.cc:30-107): one forward
   // FFT of the integrated image feeds every active scale.
@@ -214,8 +218,7 @@ void MultiScaleAlgorithm::FindActiveScaleConvolvedMaxima(
     }
   }
   if (!need_fft) return;
-  gpu::Fft& fft = transforms_->Fft();
-  fft.Forward(d_integrated, spectrum_->Ptr());
+  transforms_->Forward(d_integrated, spectrum_->Ptr());
   for (size_t si = 0; si != scale_infos_.size(); ++si) {
     ScaleInfo& e = scale_infos_[si];
     if (!e.is_active || e.scale == 0.0f) continue;
@@ -227,8 +230,8 @@ void MultiScaleAlgorithm::FindActiveScaleConvolvedMaxima(
       d_conv = kept.Base();
       scale_image_valid_[si] = true;
     }
-    fft.ConvolveSpectrum(spectrum_->Ptr(), transforms_->KernelSpectrum(e.scale),
-                         spectrum_work_->Ptr(), d_conv);
+    transforms_->ConvolveSpectrum(spectrum_->Ptr(), e.scale, spectrum_work_->Ptr(),
+                                  d_conv);
     const size_t border_scale = size_t(std::ceil(e.scale * 0.5));
     const uint32_t xb = uint32_t(
         std::max<size_t>(size_t(std::round(w * CleanBorderRatio())), border_scale));
@@ -262,6 +265,7 @@ void MultiScaleAlgorithm::ActivateScales(size_t last) {  // :636-656
 
 DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
     ImageSet& data_image, ImageSet& model_image, const gpu::Planes& psfs) {
+  prof::Section prof_section("ms.execute");
   gpu::Session& session = data_image.Session();
   session_ = &session;
   rdl_session* s = session.Handle();
@@ -308,10 +312,15 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
       transforms_->Height() != height)
     transforms_ = std::make_unique<MultiScaleTransforms>(session, width, height,
                                                          settings_.shape);
+  {
+    float max_scale = 0.0f;
+    for (const ScaleInfo& e : scale_infos_) max_scale = std::max(max_scale, e.scale);
+    transforms_->SetMaxScale(max_scale);
+  }
   d_mask_ = DeviceCleanMask(session, width, height);
   scratch_ = std::make_shared<gpu::Buffer>(session, npx * sizeof(float));
   gpu::Buffer integrated(session, npx * sizeof(float));
-  const size_t spectrum_bytes = transforms_->Fft().SpectrumBytes();
+  const size_t spectrum_bytes = transforms_->SpectrumBytes();
   spectrum_ = std::make_shared<gpu::Buffer>(session, spectrum_bytes);
   spectrum_work_ = std::make_shared<gpu::Buffer>(session, spectrum_bytes);
 
@@ -345,11 +354,14 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
       }
     }
   };
-  data_image.GetIntegratedPsf(integrated.F(), psfs);
-  convolve_psfs(convolved[0], integrated.F(), true);
-  if (n_psf > 1)
-    for (size_t i = 0; i != n_psf; ++i)
-      convolve_psfs(convolved[i], psfs.Plane(i), false);
+  {
+    prof::Section prof_psfs("ms.convolve_psfs");
+    data_image.GetIntegratedPsf(integrated.F(), psfs);
+    convolve_psfs(convolved[0], integrated.F(), true);
+    if (n_psf > 1)
+      for (size_t i = 0; i != n_psf; ++i)
+        convolve_psfs(convolved[i], psfs.Plane(i), false);
+  }
 
   FindActiveScaleConvolvedMaxima(data_image, integrated.F(), true);
   DeconvolutionResult result;
@@ -392,6 +404,7 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
     // twice-convolved PSFs for this scale (:331-350), cached per major iteration
     auto tw = twice_cache.find(scale_with_peak);
     if (tw == twice_cache.end()) {
+      prof::Section prof_twice("ms.twice_convolved");
       gpu::Planes t = gpu::Planes::Make(session, width, height, n_psf);
       for (size_t i = 0; i != n_psf; ++i) {
         session.D2D(t.Plane(i), convolved[i].Plane(scale_with_peak),
@@ -455,7 +468,11 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
       sub.SetRmsFactor(DeviceRmsFactor(session, width, height));  // :401-402
       std::vector<uint32_t> xy;
       sub.SetTrace(&xy);
-      const SubMinorLoop::RunResult r = sub.Run(individual, twice);
+      SubMinorLoop::RunResult r;
+      {
+        prof::Section prof_run("ms.subminor_run");
+        r = sub.Run(individual, twice);
+      }
       for (size_t c = 0; c + 1 < xy.size(); c += 2) {
         trace_.push_back(xy[c]);
         trace_.push_back(xy[c + 1]);
@@ -473,6 +490,7 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
       SetIterationNumber(sub.CurrentIteration());
       info.n_components_cleaned += IterationNumber() - sub_start;
       info.total_flux_cleaned += sub.FluxCleaned();
+      prof::Section prof_correct("ms.correct_and_model");
       for (size_t i = 0; i != data_image.Size(); ++i) {
         const size_t psf_index = data_image.PsfIndex(i);
         auto key = std::make_pair(psf_index, scale_with_peak);

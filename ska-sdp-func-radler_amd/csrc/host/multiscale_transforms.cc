@@ -1,6 +1,9 @@
 #include "multiscale_transforms.h"
 
 #include <cmath>
+#include <stdexcept>
+
+#include "fft_sizes.h"
 
 namespace radler::algorithms::multiscale {
 
@@ -98,21 +101,64 @@ MultiScaleTransforms::MultiScaleTransforms(gpu::Session& s, size_t width,
       width_(width),
       height_(height),
       shape_(shape),
-      fft_(s.GetFft(width, height)) {}
+      pw_(width),
+      ph_(height),
+      fft_(&s.GetFft(width, height)) {}
+
+size_t MultiScaleTransforms::KernelRadius(float scale) const {
+  size_t n;
+  MakeShapeFunction(scale, n, std::min(width_, height_), shape_);
+  return n / 2;
+}
+
+void MultiScaleTransforms::Plan(size_t radius) {
+  const bool friendly = utils::CalculateGoodFFTSize(width_) == width_ &&
+                        utils::CalculateGoodFFTSize(height_) == height_;
+  size_t pw = width_, ph = height_;
+  if (!friendly && radius < width_ && radius < height_) {
+    pw = std::max(width_, utils::CalculateGoodFFTSize(width_ + 2 * radius));
+    ph = std::max(height_, utils::CalculateGoodFFTSize(height_ + 2 * radius));
+  }
+  radius_ = radius;
+  if (pw == pw_ && ph == ph_) return;
+  pw_ = pw;
+  ph_ = ph;
+  fft_ = &s_.GetFft(pw_, ph_);
+  spectra_.clear();
+  plane_.reset();
+}
+
+void MultiScaleTransforms::SetMaxScale(float scale) {
+  const size_t r = KernelRadius(scale);
+  if (r > radius_ || pw_ == width_) Plan(r);
+}
+
+float* MultiScaleTransforms::Plane() {
+  if (!plane_) plane_ = std::make_shared<gpu::Buffer>(s_, pw_ * ph_ * sizeof(float));
+  return plane_->F();
+}
+
+void MultiScaleTransforms::Crop(float* d_out) {
+  gpu::Check(rdl_box(s_.Handle(), d_out, uint32_t(width_), 0, 0, Plane(), uint32_t(pw_),
+                     uint32_t(radius_), uint32_t(radius_), uint32_t(width_),
+                     uint32_t(height_), nullptr, RDL_BOX_COPY),
+             "rdl_box");
+}
 
 const void* MultiScaleTransforms::KernelSpectrum(float scale) {
+  if (Extended() && KernelRadius(scale) > radius_) Plan(KernelRadius(scale));
   auto it = spectra_.find(scale);
   if (it != spectra_.end()) return it->second->Ptr();
   size_t n;
   const std::vector<float> k =
       MakeShapeFunction(scale, n, std::min(width_, height_), shape_);
-  gpu::Buffer placed(s_, width_ * height_ * sizeof(float));
+  gpu::Buffer placed(s_, pw_ * ph_ * sizeof(float));
   // schaapcommon::math::PrepareSmallConvolutionKernel
-  gpu::Check(rdl_prepare_small_kernel(s_.Handle(), placed.F(), uint32_t(width_),
-                                      uint32_t(height_), k.data(), uint32_t(n)),
+  gpu::Check(rdl_prepare_small_kernel(s_.Handle(), placed.F(), uint32_t(pw_),
+                                      uint32_t(ph_), k.data(), uint32_t(n)),
              "rdl_prepare_small_kernel");
-  auto spectrum = std::make_shared<gpu::Buffer>(s_, fft_.SpectrumBytes());
-  fft_.Forward(placed.F(), spectrum->Ptr());
+  auto spectrum = std::make_shared<gpu::Buffer>(s_, fft_->SpectrumBytes());
+  fft_->Forward(placed.F(), spectrum->Ptr());
   s_.Sync();
   spectra_[scale] = spectrum;
   return spectrum->Ptr();
@@ -133,7 +179,44 @@ const float* MultiScaleTransforms::ShapeKernel(float scale, size_t& n) {
 }
 
 void MultiScaleTransforms::Transform(float* d_image, float scale) {
-  fft_.Convolve(d_image, KernelSpectrum(scale));
+  const void* spectrum = KernelSpectrum(scale);
+  if (!Extended()) {
+    fft_->Convolve(d_image, spectrum);
+    return;
+  }
+  float* plane = Plane();
+  gpu::Check(rdl_periodic_extend(s_.Handle(), plane, uint32_t(pw_), uint32_t(ph_),
+                                 d_image, uint32_t(width_), uint32_t(height_),
+                                 uint32_t(radius_), uint32_t(radius_)),
+             "rdl_periodic_extend");
+  fft_->Convolve(plane, spectrum);
+  Crop(d_image);
+}
+
+void MultiScaleTransforms::Forward(const float* d_image, void* d_spectrum) {
+  if (!Extended()) {
+    fft_->Forward(d_image, d_spectrum);
+    return;
+  }
+  float* plane = Plane();
+  gpu::Check(rdl_periodic_extend(s_.Handle(), plane, uint32_t(pw_), uint32_t(ph_),
+                                 d_image, uint32_t(width_), uint32_t(height_),
+                                 uint32_t(radius_), uint32_t(radius_)),
+             "rdl_periodic_extend");
+  fft_->Forward(plane, d_spectrum);
+}
+
+void MultiScaleTransforms::ConvolveSpectrum(const void* d_spectrum, float scale,
+                                            void* d_work, float* d_out) {
+  if (Extended() && KernelRadius(scale) > radius_)
+    throw std::logic_error("ConvolveSpectrum: scale larger than the planned margin");
+  const void* kernel = KernelSpectrum(scale);
+  if (!Extended()) {
+    fft_->ConvolveSpectrum(d_spectrum, kernel, d_work, d_out);
+    return;
+  }
+  fft_->ConvolveSpectrum(d_spectrum, kernel, d_work, Plane());
+  Crop(d_out);
 }
 
 }  // namespace radler::algorithms::multiscale

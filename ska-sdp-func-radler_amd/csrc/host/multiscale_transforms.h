@@ -22,9 +22,20 @@ class MultiScaleTransforms {
 
   size_t Width() const { return width_; }
   size_t Height() const { return height_; }
-  gpu::Fft& Fft() { return fft_; }
 
-  /// Spectrum of the scale kernel placed at the origin (cached).
+  /// The largest scale the next transforms use. Images whose sides are not
+  /// FFT-friendly (even and 7-smooth, utils::CalculateGoodFFTSize) are then
+  /// convolved in a periodically extended plane of a friendly size that
+  /// holds the largest kernel's radius on every side; the cropped result is
+  /// the same circular W x H convolution (rounding aside). Bluestein
+  /// transforms of arbitrary subimage sizes cost 3-4x more.
+  void SetMaxScale(float scale);
+  /// FFT plane size (W x H, or the extended plane).
+  size_t PlaneWidth() const { return pw_; }
+  size_t PlaneHeight() const { return ph_; }
+  size_t SpectrumBytes() const { return fft_->SpectrumBytes(); }
+
+  /// Spectrum of the scale kernel placed at the origin of the plane (cached).
   const void* KernelSpectrum(float scale);
   /// The scale's n x n shape kernel on the device (cached), for direct
   /// stamping of sparse models.
@@ -32,6 +43,11 @@ class MultiScaleTransforms {
   /// In-place convolution of one W x H plane with the scale kernel
   /// (multiscale_transforms.cc:9-21).
   void Transform(float* d_image, float scale);
+  /// Forward spectrum of a W x H image (shared by several ConvolveSpectrum).
+  void Forward(const float* d_image, void* d_spectrum);
+  /// d_out (W x H) = image of d_spectrum convolved with the scale kernel;
+  /// d_spectrum is preserved, d_work is spectrum-sized scratch.
+  void ConvolveSpectrum(const void* d_spectrum, float scale, void* d_work, float* d_out);
 
   // multiscale_transforms.h:41-195
   static std::vector<float> MakeShapeFunction(float scale, size_t& n,
@@ -40,10 +56,18 @@ class MultiScaleTransforms {
   static float GaussianSigma(float scale) { return scale * (3.0 / 16.0); }
 
  private:
+  bool Extended() const { return pw_ != width_ || ph_ != height_; }
+  size_t KernelRadius(float scale) const;
+  void Plan(size_t radius);
+  float* Plane();
+  void Crop(float* d_out);
+
   gpu::Session& s_;
   size_t width_, height_;
   Shape shape_;
-  gpu::Fft& fft_;
+  size_t pw_, ph_, radius_ = 0;  // FFT plane and the margin it holds
+  gpu::Fft* fft_;
+  std::shared_ptr<gpu::Buffer> plane_;
   std::map<float, std::shared_ptr<gpu::Buffer>> spectra_;
   std::map<float, std::pair<std::shared_ptr<gpu::Buffer>, size_t>> shapes_;
 };

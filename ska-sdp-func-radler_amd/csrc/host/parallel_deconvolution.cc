@@ -3,6 +3,8 @@
 #include "parallel_deconvolution.h"
 
 #include <algorithm>
+#include <atomic>
+#include <cstdint>
 #include <cmath>
 #include <cstdlib>
 #include <exception>
@@ -12,6 +14,7 @@
 #include <thread>
 
 #include "dijkstra_splitter.h"
+#include "host_profile.h"
 #include "logger.h"
 #include "multiscale_algorithm.h"
 
@@ -185,10 +188,52 @@ ParallelDeconvolutionResult ParallelDeconvolution::ExecuteSingleThreadedRun(
   return global;
 }
 
+namespace {
+
+// Run f(0..n-1) on up to `threads` host threads (work items claimed in order).
+template <typename F>
+void ParallelFor(size_t n, size_t threads, F&& f) {
+  threads = std::max<size_t>(1, std::min(threads, n));
+  if (threads == 1) {
+    for (size_t i = 0; i != n; ++i) f(i);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  std::vector<std::exception_ptr> errors(threads);
+  std::vector<std::thread> pool;
+  for (size_t t = 0; t != threads; ++t)
+    pool.emplace_back([&, t] {
+      try {
+        for (size_t i = next++; i < n; i = next++) f(i);
+      } catch (...) {
+        errors[t] = std::current_exception();
+      }
+    });
+  for (std::thread& th : pool) th.join();
+  for (std::exception_ptr& e : errors)
+    if (e) std::rethrow_exception(e);
+}
+
+size_t HostThreads() {
+  const size_t hw = std::thread::hardware_concurrency();
+  return std::max<size_t>(1, std::min<size_t>(hw ? hw : 1, 16));
+}
+
+}  // namespace
+
 // MakeSubImages (parallel_deconvolution.cc:57-166): Dijkstra dividers through
 // the integrated image, then per grid cell the overlap of its vertical and
 // horizontal areas; the subimage mask is that overlap, ANDed with the user
 // clean mask when there is one.
+//
+// Same result as DijkstraSplitter's FloodVerticalArea / FloodHorizontalArea /
+// GetBoundingMask sequence (the reference's), computed as intervals: every
+// row of a vertical area is one run [left, right) of columns (the flood walks
+// outwards from the area's centre column over zeros, plus the divider pixels
+// on its left), and every column of a horizontal area one run [top, bottom)
+// of rows, so the overlap of a cell needs no full-image masks. The dividers
+// are independent searches in disjoint bands (each writes only its band) and
+// run concurrently, as do the cells.
 std::vector<SubImage> MakeSubImages(const std::vector<float>& image, size_t width,
                                     size_t height, const bool* user_mask,
                                     const std::vector<PsfOffset>& psf_offsets,
@@ -197,65 +242,132 @@ std::vector<SubImage> MakeSubImages(const std::vector<float>& image, size_t widt
   const size_t gw = settings.parallel.grid_width, gh = settings.parallel.grid_height;
   const size_t avg_w = width / gw, avg_h = height / gh;
   math::DijkstraSplitter splitter(width, height);
-  std::vector<float> dividing(width * height, 0.0f);
-  std::vector<char> scratch_store(width * height);
-  bool* scratch = reinterpret_cast<bool*>(scratch_store.data());
-  for (size_t d = 1; d < gw; ++d) {
-    const size_t mid = width * d / gw;
-    splitter.DivideVertically(image.data(), dividing.data(), mid - avg_w / 4,
-                              mid + avg_w / 4);
+  std::vector<float> dividing_v(width * height, 0.0f), dividing_h(width * height, 0.0f);
+  {
+    prof::Section p("split.divide");
+    const size_t n_div = (gw - 1) + (gh - 1);
+    ParallelFor(n_div, HostThreads(), [&](size_t k) {
+      if (k + 1 < gw) {
+        const size_t mid = width * (k + 1) / gw;
+        splitter.DivideVertically(image.data(), dividing_v.data(), mid - avg_w / 4,
+                                  mid + avg_w / 4);
+      } else {
+        const size_t mid = height * (k + 2 - gw) / gh;
+        splitter.DivideHorizontally(image.data(), dividing_h.data(), mid - avg_h / 4,
+                                    mid + avg_h / 4);
+      }
+    });
   }
-  struct Column {
-    std::vector<char> mask;
-    size_t x = 0, width = 0;
+  prof::Section p_masks("split.masks");
+  // FloodVerticalArea per grid column: [left, right) per row
+  struct Runs {
+    std::vector<uint32_t> lo, hi;
+    size_t start = 0, extent = 0;  // x, width (or y, height) of the area
   };
-  std::vector<Column> columns(gw);
-  for (size_t d = 0; d != gw; ++d) {
-    Column& c = columns[d];
-    splitter.FloodVerticalArea(dividing.data(), d * width / gw + avg_w / 2, scratch,
-                               c.x, c.width);
-    c.mask.resize(c.width * height);
-    for (size_t y = 0; y != height; ++y)
-      std::copy_n(scratch_store.data() + y * width + c.x, c.width,
-                  c.mask.data() + y * c.width);
-  }
-  std::fill(dividing.begin(), dividing.end(), 0.0f);
-  for (size_t d = 1; d < gh; ++d) {
-    const size_t mid = height * d / gh;
-    splitter.DivideHorizontally(image.data(), dividing.data(), mid - avg_h / 4,
-                                mid + avg_h / 4);
-  }
-  std::vector<char> bounding_store(width * height, 0);
-  bool* bounding = reinterpret_cast<bool*>(bounding_store.data());
-  std::vector<SubImage> subs;
-  for (size_t gy = 0; gy != gh; ++gy) {
-    size_t area_y, area_h;
-    splitter.FloodHorizontalArea(dividing.data(), gy * height / gh + avg_h / 2,
-                                 scratch, area_y, area_h);
-    for (size_t gx = 0; gx != gw; ++gx) {
-      SubImage sub;
-      sub.index = subs.size();
-      const Column& c = columns[gx];
-      splitter.GetBoundingMask(reinterpret_cast<const bool*>(c.mask.data()), c.x,
-                               c.width, scratch, bounding, sub.x, sub.y, sub.width,
-                               sub.height);
-      sub.mask.resize(sub.width * sub.height);
-      for (size_t y = 0; y != sub.height; ++y)
-        for (size_t x = 0; x != sub.width; ++x)
-          sub.mask[y * sub.width + x] =
-              bounding_store[(y + sub.y) * width + x + sub.x] != 0;
-      sub.boundary_mask = sub.mask;
-      if (user_mask)
-        for (size_t y = 0; y != sub.height; ++y)
-          for (size_t x = 0; x != sub.width; ++x)
-            sub.mask[y * sub.width + x] =
-                sub.mask[y * sub.width + x] &&
-                user_mask[(y + sub.y) * width + x + sub.x];
-      psf_indices.push_back(NearestPsfIndex(psf_offsets, sub.x + sub.width / 2,
-                                            sub.y + sub.height / 2));
-      subs.push_back(std::move(sub));
+  std::vector<Runs> columns(gw), rows(gh);
+  ParallelFor(gw + gh, HostThreads(), [&](size_t k) {
+    const bool vertical = k < gw;
+    const size_t d = vertical ? k : k - gw;
+    const size_t n = vertical ? height : width;        // runs
+    const size_t len = vertical ? width : height;      // along a run
+    const size_t stride = vertical ? 1 : width;        // step along a run
+    const size_t across = vertical ? width : 1;        // step between runs
+    const float* div = vertical ? dividing_v.data() : dividing_h.data();
+    const size_t centre = vertical ? d * width / gw + avg_w / 2
+                                   : d * height / gh + avg_h / 2;
+    Runs& r = vertical ? columns[d] : rows[d];
+    r.lo.resize(n);
+    r.hi.resize(n);
+    size_t first = len, last = 0;
+    for (size_t j = 0; j != n; ++j) {
+      const float* line = div + j * across;
+      int64_t i = int64_t(centre);
+      for (; i >= 0 && line[i * stride] == 0.0f; --i) {
+      }
+      for (; i >= 0 && line[i * stride] != 0.0f; --i) {
+      }
+      const size_t lo = size_t(i + 1);
+      size_t hi = centre + 1;
+      for (; hi < len && line[hi * stride] == 0.0f; ++hi) {
+      }
+      r.lo[j] = uint32_t(lo);
+      r.hi[j] = uint32_t(hi);
+      first = std::min(first, lo);
+      last = std::max(last, hi);
     }
-  }
+    r.start = first;
+    r.extent = last < first ? 0 : last - first;
+  });
+  dividing_v = std::vector<float>();
+  dividing_h = std::vector<float>();
+
+  // GetBoundingMask per cell: inside(x, y) = x in column run of row y and
+  // y in row-area run of column x
+  std::vector<SubImage> subs(gw * gh);
+  ParallelFor(gw * gh, HostThreads(), [&](size_t index) {
+    const size_t gy = index / gw, gx = index % gw;
+    const Runs& col = columns[gx];
+    const Runs& row = rows[gy];
+    auto inside = [&](size_t x, size_t y) {
+      return x >= col.lo[y] && x < col.hi[y] && y >= row.lo[x] && y < row.hi[x];
+    };
+    // rows that can hold the cell: the row area's extent over the column's x range
+    size_t y_from = height, y_to = 0;
+    for (size_t x = col.start; x < col.start + col.extent; ++x) {
+      y_from = std::min<size_t>(y_from, row.lo[x]);
+      y_to = std::max<size_t>(y_to, row.hi[x]);
+    }
+    size_t x_lo = col.extent + col.start, y_lo = height, x_hi = 0, y_hi = 0;
+    for (size_t y = y_from; y < y_to; ++y)
+      for (size_t x = col.lo[y]; x < col.hi[y]; ++x)
+        if (y >= row.lo[x] && y < row.hi[x]) {
+          x_lo = std::min(x_lo, x);
+          x_hi = std::max(x_hi, x);
+          y_lo = std::min(y_lo, y);
+          y_hi = y;
+        }
+    SubImage& sub = subs[index];
+    sub.index = index;
+    size_t sw = 0, sh = 0;
+    if (x_hi >= x_lo) {
+      sw = x_hi + 1 - x_lo;
+      sh = y_hi + 1 - y_lo;
+    }
+    // even images keep even subimages: one more column/row (to the left/top
+    // when the right/bottom edge would leave the image), masked out
+    // (dijkstra_splitter.cc GetBoundingMask)
+    size_t ext_col = SIZE_MAX, ext_row = SIZE_MAX;
+    if (width % 2 == 0 && sw % 2 != 0) {
+      ++sw;
+      ext_col = sw + x_lo >= width ? --x_lo : x_lo + sw - 1;
+    }
+    if (height % 2 == 0 && sh % 2 != 0) {
+      ++sh;
+      ext_row = sh + y_lo >= height ? --y_lo : y_lo + sh - 1;
+    }
+    sub.x = x_lo;
+    sub.y = y_lo;
+    sub.width = sw;
+    sub.height = sh;
+    sub.mask.assign(sw * sh, false);
+    for (size_t y = 0; y != sh; ++y) {
+      const size_t gy_ = y + y_lo;
+      if (gy_ == ext_row) continue;
+      const size_t from = std::max<size_t>(col.lo[gy_], x_lo);
+      const size_t to = std::min<size_t>(col.hi[gy_], x_lo + sw);
+      for (size_t gx_ = from; gx_ < to; ++gx_)
+        if (gx_ != ext_col && inside(gx_, gy_)) sub.mask[y * sw + gx_ - x_lo] = true;
+    }
+    sub.boundary_mask = sub.mask;
+    if (user_mask)
+      for (size_t y = 0; y != sh; ++y)
+        for (size_t x = 0; x != sw; ++x)
+          sub.mask[y * sw + x] =
+              sub.mask[y * sw + x] && user_mask[(y + sub.y) * width + x + sub.x];
+  });
+  for (const SubImage& sub : subs)
+    psf_indices.push_back(NearestPsfIndex(psf_offsets, sub.x + sub.width / 2,
+                                          sub.y + sub.height / 2));
   return subs;
 }
 
@@ -274,6 +386,7 @@ void TrimSubImage(gpu::Session& ops, const SubImage& sub, const ImageSet& data_i
                   const ImageSet& model_image, const gpu::Planes& psfs,
                   float* d_data, float* d_model, float* d_psfs,
                   const uint8_t* d_boundary) {
+  prof::Section prof_section("par.trim");
   const size_t W = data_image.Width();
   const uint32_t uw = uint32_t(sub.width), uh = uint32_t(sub.height);
   const size_t n = sub.width * sub.height;
@@ -303,6 +416,7 @@ void MergeSubImage(gpu::Session& ops, const SubImage& sub, ImageSet& data_image,
                    ImageSet& result_model, const float* d_data,
                    const float* d_model, const uint8_t* d_boundary,
                    bool converging) {
+  prof::Section prof_section("par.merge");
   const size_t W = data_image.Width();
   const uint32_t uw = uint32_t(sub.width), uh = uint32_t(sub.height);
   const size_t n = sub.width * sub.height;
@@ -400,6 +514,8 @@ void ParallelDeconvolution::RunSubImage(SubImage& sub, ImageSet& data_image,
                                         bool find_peak_only) {
   // parallel_deconvolution.cc:300-484 on the device: the subimage's planes
   // are box copies of the full image set's planes
+  prof::Section prof_section(find_peak_only ? "par.run_subimage_findpeak"
+                                             : "par.run_subimage_clean");
   gpu::Session& s = data_image.Session();
   const size_t sw = sub.width, sh = sub.height, n = sw * sh;
   gpu::Buffer boundary(s, n);
@@ -748,8 +864,11 @@ ParallelDeconvolutionResult ParallelDeconvolution::ExecuteParallelRun(
     s.D2H(image.data(), integrated.Ptr(), image.size() * sizeof(float));
   }
   std::vector<size_t> psf_indices;
-  subimages_ = MakeSubImages(image, width, height, mask_, psf_offsets, settings_,
-                             psf_indices);
+  {
+    prof::Section prof_split("par.split");
+    subimages_ = MakeSubImages(image, width, height, mask_, psf_offsets, settings_,
+                               psf_indices);
+  }
   ImageSet result_model(model_image, width, height);
   result_model.Fill(0.0f);
   const size_t n_workers =

@@ -18,6 +18,7 @@
 #include "rms_image.h"
 #include "component_optimization.h"
 #include "fft_sizes.h"
+#include "host_profile.h"
 #include "multiscale_transforms.h"
 
 namespace py = pybind11;
@@ -505,6 +506,14 @@ void InitDistributed(py::module& m) {
 void InitGpu(py::module& m) {
   py::module g = m.def_submodule("gpu", "MI355X device helpers (bench/tests)");
   g.def("set_verbosity", &radler::log::SetVerbosity);
+  // RADLER_HOST_PROFILE=1 sections: {name: (count, total seconds)}
+  g.def("host_profile", []() {
+    py::dict out;
+    for (const radler::prof::Entry& e : radler::prof::Snapshot())
+      out[py::str(e.name)] = py::make_tuple(e.count, e.ns * 1e-9);
+    return out;
+  });
+  g.def("host_profile_reset", &radler::prof::Reset);
   g.def(
       "local_rms",
       [](FloatArray integrated, int method, double window, double beam,
@@ -594,6 +603,30 @@ void InitGpu(py::module& m) {
       },
       py::arg("residual"), py::arg("model"), py::arg("psf"), py::arg("scales"),
       py::arg("lists"), py::arg("padding") = 1.1);
+  g.def(
+      "ms_transform",
+      [](FloatArray image, std::vector<float> scales, float max_scale, int shape) {
+        // MultiScaleTransforms::Transform of one image per scale (the
+        // transforms the multiscale algorithm runs, periodically extended
+        // when the size is not FFT-friendly)
+        if (image.ndim() != 2) throw std::runtime_error("expected a 2-D image");
+        const size_t h = image.shape(0), w = image.shape(1), n = w * h;
+        std::shared_ptr<radler::gpu::Session> session =
+            radler::gpu::Session::ForDevice(radler::gpu::Session::DefaultDevice());
+        radler::gpu::Session& s = *session;
+        radler::algorithms::multiscale::MultiScaleTransforms transforms(
+            s, w, h, radler::MultiscaleShape(shape));
+        transforms.SetMaxScale(max_scale);
+        radler::gpu::Buffer d(s, n * sizeof(float));
+        py::array_t<float> out({py::ssize_t(scales.size()), py::ssize_t(h), py::ssize_t(w)});
+        for (size_t i = 0; i != scales.size(); ++i) {
+          s.H2D(d.Ptr(), image.data(), n * sizeof(float));
+          transforms.Transform(d.F(), scales[i]);
+          s.D2H(out.mutable_data(py::ssize_t(i)), d.F(), n * sizeof(float));
+        }
+        return py::make_tuple(out, transforms.PlaneWidth(), transforms.PlaneHeight());
+      },
+      py::arg("image"), py::arg("scales"), py::arg("max_scale"), py::arg("shape") = 0);
   g.def(
       "sliding_minimum",
       [](FloatArray image, size_t window) {

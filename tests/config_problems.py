@@ -1,0 +1,82 @@
+"""The five BASELINE.json configurations as
+deterministic synthetic problems: inputs are regenerated from seeds on any
+machine (numpy only) and checked against the SHA-256 stored in the committed
+fixtures (tests/golden/config_*.npz), so the GPU box and the development
+container clean bit-identical images.
+
+    C1  Högbom generic_clean, 1024^2, 1 channel, 1000 iterations
+    C2  multiscale, 4096^2, 6 scales, sub-minor loop
+    C3  joined-channel multiscale, 8 channels x 4096^2
+    C4  IUWT, 4096^2
+    C5  parallel-deconvolution tiling, 16384^2 multiscale, 8x8 subimages
+"""
+import hashlib
+
+import numpy as np
+
+from synthetic import make_dirty, make_psf_uv, make_sky
+
+SEED = 20251015
+NOISE = 1e-4
+PIXEL_SCALE = 1.0 / 3600.0 * np.pi / 180.0  # 1 arcsec
+BEAM_PX = 4.0
+
+
+def sha256(*arrays):
+    h = hashlib.sha256()
+    for a in arrays:
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
+def single_field(size, n_points, n_blobs, seed=SEED):
+    """PSF and dirty image of one Stokes-I field (bench.py's generator)."""
+    psf = make_psf_uv(size, size, fwhm=BEAM_PX)
+    sky = make_sky(size, size, n_points, n_blobs, seed, flux_range=(1e-3, 1.0),
+                   blob_sigma=(2.0, 40.0))
+    return psf, make_dirty(psf, sky, NOISE, seed)
+
+
+# C3: 100-170 MHz in 10 MHz bands, spectral index -0.7,
+# PSF core FWHM proportional to 1/nu, weights 1
+C3_FREQUENCIES = [100e6 + 10e6 * i for i in range(8)]
+C3_SPECTRAL_INDEX = -0.7
+
+
+def joined_channels(size, n_points, n_blobs, seed=SEED, frequencies=C3_FREQUENCIES):
+    """(psfs [n_ch, h, w], dirty [n_ch, h, w]): one sky whose fluxes scale as
+    (nu / nu_0)^-0.7, each channel convolved with its own PSF."""
+    nu0 = frequencies[0]
+    sky0 = make_sky(size, size, n_points, n_blobs, seed, flux_range=(1e-3, 1.0),
+                    blob_sigma=(2.0, 40.0))
+    psfs, dirty = [], []
+    for c, nu in enumerate(frequencies):
+        psf = make_psf_uv(size, size, fwhm=BEAM_PX * nu0 / nu)
+        psfs.append(psf)
+        dirty.append(make_dirty(psf, sky0 * (nu / nu0) ** C3_SPECTRAL_INDEX, NOISE,
+                                seed + 7 * c))
+    return np.stack(psfs), np.stack(dirty)
+
+
+# Problem sizes and the settings each configuration runs with. `cap` is the
+# component (or IUWT step) budget of the committed oracle fixture.
+CONFIGS = {
+    "c1": dict(kind="hogbom", size=1024, points=200, blobs=20, threshold=0.0,
+               max_iterations=1000),
+    "c2": dict(kind="multiscale", size=4096, points=1000, blobs=100, threshold=5 * NOISE,
+               max_scales=6, cap=20000),
+    "c3": dict(kind="joined", size=4096, points=1000, blobs=100, threshold=5 * NOISE,
+               max_scales=6, cap=3000),
+    "c4": dict(kind="iuwt", size=4096, points=1000, blobs=100, threshold=5 * NOISE,
+               cap=6),
+    "c5": dict(kind="tiled", size=16384, points=2000, blobs=200, threshold=5 * NOISE,
+               max_scales=6, grid=8, cap=200),
+}
+
+
+def problem(name):
+    c = CONFIGS[name]
+    if c["kind"] == "joined":
+        return joined_channels(c["size"], c["points"], c["blobs"])
+    psf, dirty = single_field(c["size"], c["points"], c["blobs"])
+    return psf[None], dirty[None]

@@ -1,0 +1,102 @@
+"""Oracle fixtures for the five BASELINE.json configurations at their stated
+sizes (tests/config_problems.py), for tests/test_configs_gpu.py:
+
+    make -C oracle && python tests/golden/make_config_golden.py [c1 c2 ...]
+
+Each tests/golden/config_<name>.npz holds the SHA-256 of the regenerated
+inputs, the oracle's component trace (or IUWT step records) with the
+decision margins of every component (tests/trace_compare.py), and checksums
+plus a fixed random sample of the oracle's residual and model. The inputs
+themselves are not stored: both machines regenerate them from seeds.
+"""
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+
+import config_problems as cp  # noqa: E402
+from oracle_lib import OracleAlgorithm, OracleParallel, get_oracle  # noqa: E402
+
+SAMPLE = 65536
+
+
+def sample_index(n_pixels, seed=1):
+    return np.sort(np.random.default_rng(seed).choice(n_pixels, SAMPLE, replace=False))
+
+
+def image_summary(prefix, planes):
+    planes = np.ascontiguousarray(planes, np.float32)
+    n = planes.shape[-1] * planes.shape[-2]
+    idx = sample_index(n)
+    flat = planes.reshape(-1, n)
+    return {f"{prefix}_sha256": cp.sha256(planes),
+            f"{prefix}_sample": flat[:, idx],
+            f"{prefix}_absmax": np.abs(flat).max(axis=1),
+            f"{prefix}_rms": np.sqrt(np.mean(flat.astype(np.float64) ** 2, axis=1))}
+
+
+def settings(c):
+    st = dict(threshold=c["threshold"], border_ratio=0.0, minor_loop_gain=0.1,
+              major_loop_gain=1.0, allow_negative=1)
+    if c["kind"] == "hogbom":
+        st.update(max_iterations=c["max_iterations"], use_sub_minor=0)
+    elif c["kind"] == "iuwt":
+        st.update(max_iterations=c["cap"])
+    else:
+        st.update(max_iterations=c["cap"], max_scales=c["max_scales"],
+                  beam_size_in_pixels=cp.BEAM_PX)
+    return st
+
+
+def make(name):
+    c = cp.CONFIGS[name]
+    t0 = time.time()
+    psfs, dirty = cp.problem(name)
+    out = {"psf_sha256": cp.sha256(psfs), "dirty_sha256": cp.sha256(dirty),
+           "dirty_absmax": np.float32(np.abs(dirty).max())}
+    print(f"{name}: inputs {dirty.shape} in {time.time() - t0:.1f} s", flush=True)
+    orc = get_oracle()
+    orc.set_threads(os.cpu_count() or 8)
+    res, mod = dirty.copy(), np.zeros_like(dirty)
+    t0 = time.time()
+    if c["kind"] == "tiled":
+        par = OracleParallel(orc, 1, c["grid"], c["grid"], **settings(c))
+        par.set_snapshot(False)
+        r, boxes, labels, trace = par.execute(res, mod, psfs, 1.0)
+        m, v = par.margins()
+        out.update(boxes=boxes, labels_sha256=cp.sha256(labels), trace=trace,
+                   margins=m, values=v, start_peak=r.start_peak, end_peak=r.end_peak,
+                   total_iterations=r.total_iterations,
+                   first_iteration_number=r.first_iteration_number,
+                   another_iteration_required=r.another_iteration_required)
+    else:
+        kind = {"hogbom": 0, "multiscale": 1, "joined": 1, "iuwt": 2}[c["kind"]]
+        alg = OracleAlgorithm(orc, kind, **settings(c))
+        r, trace = alg.execute(res, mod, psfs)
+        out.update(trace=trace, iteration_number=r.iteration_number,
+                   final_peak=r.final_peak,
+                   another_iteration_required=r.another_iteration_required)
+        if kind == 1:
+            m, v = alg.margins()
+            out.update(margins=m, values=v)
+        if kind == 2:
+            steps = alg.iuwt_steps()
+            out.update(steps=steps.view(np.uint8).reshape(len(steps), -1),
+                       n_steps=len(steps))
+    print(f"{name}: oracle {time.time() - t0:.1f} s, trace {len(out['trace'])}",
+          flush=True)
+    out.update(image_summary("residual", res))
+    out.update(image_summary("model", mod))
+    if c["kind"] == "hogbom":  # sparse model, exact
+        nz = np.flatnonzero(mod.reshape(-1))
+        out.update(model_index=nz.astype(np.int64), model_value=mod.reshape(-1)[nz])
+    np.savez_compressed(os.path.join(HERE, f"config_{name}.npz"), **out)
+
+
+if __name__ == "__main__":
+    for name in sys.argv[1:] or list(cp.CONFIGS):
+        make(name)

@@ -347,6 +347,18 @@ class OracleAlgorithm:
             raise RuntimeError(self.o.lib.orc_last_error().decode())
         return r, trace[: min(r.n_trace, trace_cap)].copy()
 
+    def margins(self):
+        """Decision margins of the last execute (oracle.h Component::margin):
+        (margins [n_trace + 1], values [n_trace + 1]); the last entry is the
+        end-of-run margin and the last component's |peak|."""
+        L = self.o.lib
+        L.orc_algo_margins.restype = C.c_uint64
+        L.orc_algo_margins.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]
+        n = L.orc_algo_margins(self.h, None, None, 0)
+        m, v = np.zeros(n, np.float32), np.zeros(n, np.float32)
+        L.orc_algo_margins(self.h, m.ctypes.data, v.ctypes.data, n)
+        return m, v
+
     def set_automask(self, track, use):
         """MultiScaleAlgorithm::SetAutoMaskMode (multiscale only)."""
         L = self.o.lib
@@ -498,6 +510,18 @@ class OracleParallel:
         if rc != 0:
             raise RuntimeError(self.o.lib.orc_last_error().decode())
         return r, boxes, labels, trace[: min(r.n_trace, trace_cap)].copy()
+
+    def margins(self):
+        """Decision margins of the last execute: (margins, values) of the
+        trace entries in trace order, then one end margin per subimage
+        (values 0 there)."""
+        L = self.o.lib
+        L.orc_parallel_margins.restype = C.c_uint64
+        L.orc_parallel_margins.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]
+        n = L.orc_parallel_margins(self.h, None, None, 0)
+        m, v = np.zeros(n, np.float32), np.zeros(n, np.float32)
+        L.orc_parallel_margins(self.h, m.ctypes.data, v.ctypes.data, n)
+        return m, v
 
     def __del__(self):
         try:

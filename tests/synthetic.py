@@ -56,7 +56,7 @@ def make_sky(w, h, n_points, n_blobs, seed, margin=16, flux_range=(1e-3, 1.0),
     fl = np.exp(rng.uniform(np.log(flux_range[0]), np.log(flux_range[1]), n_points))
     np.add.at(sky, (ys, xs), fl)
     if n_blobs:
-        yy, xx = np.mgrid[0:h, 0:w]
+        yy, xx = np.ogrid[0:h, 0:w]  # broadcast views: same values as mgrid
         for _ in range(n_blobs):
             cx, cy = rng.uniform(margin, w - margin), rng.uniform(margin, h - margin)
             sg = np.exp(rng.uniform(np.log(blob_sigma[0]), np.log(blob_sigma[1])))
@@ -64,7 +64,7 @@ def make_sky(w, h, n_points, n_blobs, seed, margin=16, flux_range=(1e-3, 1.0),
             x0, x1 = int(max(0, cx - 5 * sg)), int(min(w, cx + 5 * sg + 1))
             y0, y1 = int(max(0, cy - 5 * sg)), int(min(h, cy + 5 * sg + 1))
             sky[y0:y1, x0:x1] += amp * np.exp(
-                -0.5 * ((xx[y0:y1, x0:x1] - cx) ** 2 + (yy[y0:y1, x0:x1] - cy) ** 2) / (sg * sg))
+                -0.5 * ((xx[:, x0:x1] - cx) ** 2 + (yy[y0:y1, :] - cy) ** 2) / (sg * sg))
     return sky
 
 

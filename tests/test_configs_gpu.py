@@ -1,0 +1,203 @@
+"""The five BASELINE.json configurations at their stated sizes
+(tests/config_problems.py) on the MI355X against committed oracle fixtures
+(tests/golden/config_*.npz, made by tests/golden/make_config_golden.py).
+
+* C1 Högbom 1024^2, 1000 iterations: bit-exact trace, residual (SHA-256) and
+  model — no FFT on this path.
+* C2 multiscale 4096^2 (6 scales) and C3 joined 8 x 4096^2: the component
+  traces (position and scale) are compared tie-aware (tests/trace_compare.py):
+  identical up to the first divergence, and a divergence is accepted only
+  where the oracle's decision margin is below RTOL x |peak| — the GPU runs the
+  scale convolutions in float32 (the reference: FFTW float), the oracle in
+  float64. Identical traces also get their residual/model samples checked.
+* C4 IUWT 4096^2: the outer-loop step records (success, scale, pixel, scale
+  window, area) for the fixture's steps.
+* C5 tiling 16384^2 8 x 8: subimage geometry bit-exact, then every
+  subimage's trace tie-aware (one worker: the reference's max_threads = 1
+  order), each subimage capped at the fixture's component budget.
+
+The inputs are regenerated from seeds and checked against the fixture's
+SHA-256 before anything runs.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import config_problems as cp
+from trace_compare import assert_tie_aware
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+# float32 vs float64 scale convolutions: measured differences are ~1e-7 of the
+# image peak (test_scale_convolution_error_4096); a decision whose two sides
+# differ by less than RTOL x |peak| may go either way
+RTOL = 1e-5
+# residual / model agreement when the traces are identical (FFT rounding)
+IMG_TOL = 2e-5
+
+
+def fixture(name):
+    path = os.path.join(GOLDEN, f"config_{name}.npz")
+    if not os.path.exists(path):
+        pytest.skip(f"fixture {path} not generated")
+    return np.load(path)
+
+
+def inputs(name, fx):
+    psfs, dirty = cp.problem(name)
+    assert cp.sha256(psfs) == str(fx["psf_sha256"]), "regenerated PSF differs from fixture"
+    assert cp.sha256(dirty) == str(fx["dirty_sha256"]), "regenerated dirty differs"
+    return psfs, dirty
+
+
+def settings(rd, name):
+    c = cp.CONFIGS[name]
+    s = rd.Settings()
+    s.algorithm_type = {"hogbom": rd.AlgorithmType.generic_clean,
+                        "iuwt": rd.AlgorithmType.iuwt}.get(c["kind"],
+                                                          rd.AlgorithmType.multiscale)
+    s.trimmed_image_width = s.trimmed_image_height = c["size"]
+    s.pixel_scale.x = s.pixel_scale.y = cp.PIXEL_SCALE
+    s.absolute_threshold = c["threshold"]
+    s.minor_loop_gain = 0.1
+    s.major_loop_gain = 1.0
+    s.allow_negative_components = True
+    s.border_ratio = 0.0
+    if c["kind"] == "hogbom":
+        s.minor_iteration_count = c["max_iterations"]
+        s.generic.use_sub_minor_optimization = False
+    else:
+        s.minor_iteration_count = c["cap"]
+    if "max_scales" in c:
+        s.multiscale.max_scales = c["max_scales"]
+    if c["kind"] == "tiled":
+        s.parallel.grid_width = s.parallel.grid_height = c["grid"]
+        s.parallel.max_threads = 1
+    return s
+
+
+def sample_index(n_pixels, seed=1):
+    return np.sort(np.random.default_rng(seed).choice(n_pixels, 65536, replace=False))
+
+
+def check_samples(fx, residual, model, tol):
+    idx = sample_index(residual.shape[-1] * residual.shape[-2])
+    r = residual.reshape(len(fx["residual_sample"]), -1)[:, idx]
+    m = model.reshape(len(fx["model_sample"]), -1)[:, idx]
+    assert np.abs(r - fx["residual_sample"]).max() <= tol
+    assert np.abs(m - fx["model_sample"]).max() <= tol
+
+
+@pytest.mark.gpu
+def test_c1_hogbom_1024_bit_exact():
+    from radler_import import radler as rd
+    fx = fixture("c1")
+    psfs, dirty = inputs("c1", fx)
+    run = rd.gpu.DeviceRun(settings(rd, "c1"), psfs[0], dirty[0], [], 0.0)
+    r = run.execute()
+    assert r["iterations"] == int(fx["iteration_number"]) == 1000
+    assert np.array_equal(run.trace()[:, :2], fx["trace"][:, :2])
+    res = run.residual().reshape(dirty.shape)
+    mod = run.model().reshape(dirty.shape)
+    assert cp.sha256(res) == str(fx["residual_sha256"])
+    assert cp.sha256(mod) == str(fx["model_sha256"])
+    nz = np.flatnonzero(mod.reshape(-1))
+    assert np.array_equal(nz, fx["model_index"])
+    assert np.array_equal(mod.reshape(-1)[nz], fx["model_value"])
+
+
+@pytest.mark.gpu
+def test_c1_hogbom_1024_through_perform():
+    """The same run through the drop-in API (Radler.perform)."""
+    from radler_import import radler as rd
+    fx = fixture("c1")
+    psfs, dirty = inputs("c1", fx)
+    residual = dirty[0].copy()
+    model = np.zeros_like(residual)
+    radler = rd.Radler(settings(rd, "c1"), psfs[0].copy(), residual, model, 0.0)
+    radler.perform(0)
+    assert radler.iteration_number == 1000
+    assert cp.sha256(residual[None]) == str(fx["residual_sha256"])
+    assert cp.sha256(model[None]) == str(fx["model_sha256"])
+
+
+def _multiscale(name):
+    from radler_import import radler as rd
+    fx = fixture(name)
+    psfs, dirty = inputs(name, fx)
+    n = len(dirty)
+    run = rd.gpu.DeviceRun(settings(rd, name), psfs if n > 1 else psfs[0],
+                           dirty if n > 1 else dirty[0], [] if n == 1 else [1.0] * n,
+                           cp.BEAM_PX * cp.PIXEL_SCALE)
+    r = run.execute()
+    c = assert_tie_aware(run.trace(), fx["trace"], fx["margins"], fx["values"], RTOL)
+    print(f"{name}: {c}")
+    if c.identical:
+        assert r["iterations"] == int(fx["iteration_number"])
+        tol = IMG_TOL * float(fx["dirty_absmax"])
+        check_samples(fx, run.residual().reshape(dirty.shape),
+                      run.model().reshape(dirty.shape), tol)
+    return c
+
+
+@pytest.mark.gpu
+def test_c2_multiscale_4096_trace():
+    c = _multiscale("c2")
+    # the fixture's budget is 20000 components; report how far the traces agree
+    assert c.matched > 0
+
+
+@pytest.mark.gpu
+def test_c3_joined_8x4096_trace():
+    c = _multiscale("c3")
+    assert c.matched > 0
+
+
+@pytest.mark.gpu
+def test_c4_iuwt_4096_steps():
+    from radler_import import radler as rd
+    fx = fixture("c4")
+    psfs, dirty = inputs("c4", fx)
+    run = rd.gpu.DeviceRun(settings(rd, "c4"), psfs[0], dirty[0], [], 0.0)
+    run.execute()
+    from oracle_lib import IUWT_STEP
+    steps_o = np.frombuffer(fx["steps"].tobytes(), IUWT_STEP)
+    steps_g = run.iuwt_steps()
+    assert len(steps_g) == len(steps_o)
+    for g, o in zip(steps_g, steps_o):
+        assert (bool(g[0]), g[1], g[2], g[3], g[4], g[5], g[6]) == (
+            bool(o["succeeded"]), o["scale"], o["x"], o["y"], o["end_scale"],
+            o["min_scale"], o["area"]), (g, o)
+    tol = 1e-4 * float(fx["dirty_absmax"])
+    check_samples(fx, run.residual().reshape(dirty.shape),
+                  run.model().reshape(dirty.shape), tol)
+
+
+@pytest.mark.gpu
+def test_c5_tiled_16384_8x8():
+    from radler_import import radler as rd
+    fx = fixture("c5")
+    psfs, dirty = inputs("c5", fx)
+    size = dirty.shape[-1]
+    run = rd.gpu.DeviceRun(settings(rd, "c5"), psfs[0], dirty[0], [],
+                           cp.BEAM_PX * cp.PIXEL_SCALE)
+    r = run.execute()
+    boxes, labels = run.subimages(size, size)
+    assert np.array_equal(boxes, fx["boxes"])
+    assert cp.sha256(labels) == str(fx["labels_sha256"])
+    del labels
+    trace, margins, values = fx["trace"], fx["margins"], fx["values"]
+    n_sub = len(boxes)
+    end_margins = margins[len(trace):]
+    summary = []
+    for i in range(n_sub):
+        sel = trace[:, 0] == i
+        m = np.append(margins[:len(trace)][sel], end_margins[i])
+        v = np.append(values[:len(trace)][sel], values[:len(trace)][sel][-1:] if sel.any()
+                      else [1.0])
+        c = assert_tie_aware(run.trace(i), trace[sel][:, 1:], m, v, RTOL)
+        summary.append(c)
+    identical = sum(c.identical for c in summary)
+    print(f"c5: {identical}/{n_sub} subimage traces identical; "
+          f"{sum(c.matched for c in summary)} of {len(trace)} components matched")
+    assert r["iterations"] > 0

@@ -588,3 +588,23 @@ def test_lds_fft_correction_sparse_rows(sess, w, h, pw, ph, rows, columns):
     for x in (dpsf, dmod, dres_a, dres_b, dmask, kplane, kspec, kspec_cm, work):
         x.free()
     sess.rdl.rdl_conv_destroy(c)
+
+
+@pytest.mark.parametrize("w,h", [(256, 256), (301, 257), (262, 222), (498, 350)])
+@pytest.mark.parametrize("shape", [0, 1])
+def test_ms_transform_any_size(orc, w, h, shape):
+    """MultiScaleTransforms::Transform (circular at W x H): sizes that are not
+    even 7-smooth run in a periodically extended plane of a friendly size
+    (rdl_periodic_extend + crop); the result is the oracle's float64
+    circular convolution within float32 FFT rounding."""
+    from radler_import import radler as rd
+    rng = np.random.default_rng(w * h)
+    img = rng.standard_normal((h, w)).astype(np.float32)
+    scales = [8.0, 16.0, 32.0, 64.0]
+    out, pw, ph = rd.gpu.ms_transform(img, scales, max(scales), shape)
+    friendly = orc.good_fft_size(w) == w and orc.good_fft_size(h) == h
+    assert (pw, ph) == (w, h) if friendly else (pw > w and ph > h)
+    for i, sc in enumerate(scales):
+        expect = orc.ms_transform(img.copy(), sc, shape)
+        err = np.abs(out[i] - expect).max()
+        assert err <= 2e-6 * np.abs(img).max() * np.sqrt(np.log2(pw * ph)), (sc, err)

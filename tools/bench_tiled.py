@@ -31,7 +31,9 @@ def main():
         run = rd.gpu.DeviceRun(s, psf, dirty, [], bench.BEAM_PX * bench.PIXEL_SCALE)
         run.execute()  # warm-up: plans, scale kernels, worker streams
         times, comps = [], 0
-        for _ in range(2):
+        rd.gpu.host_profile_reset()
+        runs = int(os.environ.get("BENCH_TILED_RUNS", "2"))
+        for _ in range(runs):
             run.restore()
             run.sync()
             t0 = time.perf_counter()
@@ -42,6 +44,10 @@ def main():
         best = min(times)
         print(f"size={size} grid={grid}x{grid} max_threads={k}: {best:.3f} s, "
               f"{comps} components, {comps / best:.0f} components/s", flush=True)
+        prof = rd.gpu.host_profile()
+        for name, (count, sec) in sorted(prof.items(), key=lambda kv: -kv[1][1]):
+            print(f"  [host] {name:30s} {count:9d} {sec / runs:9.3f} s/run "
+                  f"{1e6 * sec / max(count, 1):9.1f} us", flush=True)
         del run
 
 
