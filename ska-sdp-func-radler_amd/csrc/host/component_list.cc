@@ -54,7 +54,12 @@ void ComponentList::MergeDuplicates() {
 }
 
 void ComponentList::MergeDuplicates(size_t scale_index) {
-  // component_list.h:222-263: sort by position, sum values of duplicates
+  // component_list.h:222-263: the reference accumulates the values into one
+  // image per frequency (in list order), then emits, frequency by frequency,
+  // every raster position whose value in that frequency is non-zero (with
+  // all its frequencies, which are then cleared). Positions whose summed
+  // values are zero in every frequency disappear. Here a stable raster sort
+  // sums duplicates in the same order; the emission passes follow.
   ScaleList& l = list_per_scale_[scale_index];
   std::vector<size_t> order(l.positions.size());
   std::iota(order.begin(), order.end(), 0);
@@ -78,7 +83,29 @@ void ComponentList::MergeDuplicates(size_t scale_index) {
                            l.values.begin() + (idx + 1) * n_frequencies_);
     }
   }
-  l = std::move(merged);
+  ScaleList out;
+  std::vector<char> emitted(merged.positions.size(), 0);
+  for (size_t f = 0; f != n_frequencies_; ++f)
+    for (size_t i = 0; i != merged.positions.size(); ++i) {
+      if (emitted[i] || merged.values[i * n_frequencies_ + f] == 0.0f) continue;
+      emitted[i] = 1;
+      out.positions.push_back(merged.positions[i]);
+      out.values.insert(out.values.end(), merged.values.begin() + i * n_frequencies_,
+                        merged.values.begin() + (i + 1) * n_frequencies_);
+    }
+  l = std::move(out);
+}
+
+void ComponentList::MultiplyScaleComponent(size_t scale_index, size_t position_index,
+                                           size_t channel, double correction_factor) {
+  float& value =
+      list_per_scale_[scale_index].values[channel + position_index * n_frequencies_];
+  value *= correction_factor;  // component_list.h:178-186 (float *= double)
+}
+
+void ComponentList::SetValues(size_t scale_index, size_t index, const float* values) {
+  std::copy_n(values, n_frequencies_,
+              &list_per_scale_[scale_index].values[index * n_frequencies_]);
 }
 
 void ComponentList::Clear() {

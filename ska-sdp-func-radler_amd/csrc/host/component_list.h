@@ -50,6 +50,15 @@ class ComponentList {
   float& Value(size_t scale_index, size_t index, size_t image_index) {
     return list_per_scale_[scale_index].values[index * n_frequencies_ + image_index];
   }
+  /// component_list.h:157-164
+  void SetValues(size_t scale_index, size_t index, const float* values);
+  /// component_list.h:178-186 (primary-beam correction factors)
+  void MultiplyScaleComponent(size_t scale_index, size_t position_index,
+                              size_t channel, double correction_factor);
+  /// component_list.h:191-194
+  const std::vector<Position>& GetPositions(size_t scale_index) const {
+    return list_per_scale_[scale_index].positions;
+  }
 
  private:
   struct ScaleList {

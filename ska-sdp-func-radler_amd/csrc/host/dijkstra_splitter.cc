@@ -81,6 +81,19 @@ void DijkstraSplitter::Divide(const float* image, float* output, size_t lo,
   output[pixel(0, pv)] = 1.0f;
 }
 
+void DijkstraSplitter::AddVerticalDivider(const float* image, float* scratch,
+                                          float* output, size_t x1, size_t x2) const {
+  DivideVertically(image, scratch, x1, x2);
+  for (size_t y = 0; y != height_; ++y)
+    for (size_t i = y * width_ + x1; i != y * width_ + x2; ++i) output[i] += scratch[i];
+}
+
+void DijkstraSplitter::AddHorizontalDivider(const float* image, float* scratch,
+                                            float* output, size_t y1, size_t y2) const {
+  DivideHorizontally(image, scratch, y1, y2);
+  for (size_t i = y1 * width_; i != y2 * width_; ++i) output[i] += scratch[i];
+}
+
 void DijkstraSplitter::DivideVertically(const float* image, float* output,
                                         size_t x1, size_t x2) const {
   Divide<true>(image, output, x1, x2);

@@ -18,6 +18,13 @@ class DijkstraSplitter {
   /// band, untouched outside it (dijkstra_splitter.cc:32-84).
   void DivideVertically(const float* image, float* output, size_t x1,
                         size_t x2) const;
+  /// DivideVertically into `scratch`, then output += scratch over the band
+  /// (dijkstra_splitter.cc:14-23).
+  void AddVerticalDivider(const float* image, float* scratch, float* output,
+                          size_t x1, size_t x2) const;
+  /// The same for a horizontal divider (dijkstra_splitter.cc:25-32).
+  void AddHorizontalDivider(const float* image, float* scratch, float* output,
+                            size_t y1, size_t y2) const;
   /// Left-to-right path inside rows [y1, y2) (dijkstra_splitter.cc:86-136).
   void DivideHorizontally(const float* image, float* output, size_t y1,
                           size_t y2) const;

@@ -139,15 +139,17 @@ void MultiScaleAlgorithm::RunFullComponentFitter(ImageSet& residual_set,
                                               settings_.convolution_padding);
   std::vector<float> model(width * height);
   for (size_t i = 0; i != residual_set.Size(); ++i) {
-    math::RunFullComponentFitter(s, residual_set.Data(i), model_set.Data(i),
-                                 psfs.Plane(residual_set.PsfIndex(i)), width, height, scales,
-                                 lists, *transforms_, pw, ph);
-    // :887-897: the list values take the (updated) model image's values
+    // :885-897 ("Updating component list") runs before :898-905 ("Updating
+    // model"): the list values take the model image's values from before
+    // this fit's deltas are added
     s.D2H(model.data(), model_set.Data(i), model.size() * sizeof(float));
     for (size_t sc = 0; sc != lists.size(); ++sc)
       for (size_t c = 0; c != lists[sc].size(); ++c)
         component_list_->Value(sc, c, i) +=
             model[lists[sc][c].second * width + lists[sc][c].first];
+    math::RunFullComponentFitter(s, residual_set.Data(i), model_set.Data(i),
+                                 psfs.Plane(residual_set.PsfIndex(i)), width, height, scales,
+                                 lists, *transforms_, pw, ph);
   }
   // ApplySpectralConstraintsToComponents (deconvolution_algorithm.cc:48-64)
   std::vector<float> values(component_list_->NFrequencies());

@@ -12,6 +12,7 @@
 #include "communicator.h"
 #include "device.h"
 #include "device_run.h"
+#include "dijkstra_splitter.h"
 #include "image_accessors.h"
 #include "logger.h"
 #include "radler.h"
@@ -400,7 +401,26 @@ void InitComponentList(py::module& m) {  // python/pycomponent_list.cc
              self.GetComponent(s, index, x, y, values.data());
              return py::make_tuple(x, y, values);
            },
-           py::arg("scale_index"), py::arg("index"));
+           py::arg("scale_index"), py::arg("index"))
+      // C++ API members exposed for the restated cpp/test/test_component_list.cc
+      .def("add",
+           [](radler::ComponentList& self, size_t x, size_t y, size_t s,
+              std::vector<float> values) {
+             if (s >= self.NScales() || values.size() != self.NFrequencies())
+               throw std::out_of_range("scale index or value count out of range");
+             self.Add(x, y, s, values.data());
+           },
+           py::arg("x"), py::arg("y"), py::arg("scale_index"), py::arg("values"))
+      .def("merge_duplicates", [](radler::ComponentList& self) { self.MergeDuplicates(); })
+      .def("multiply_scale_component", &radler::ComponentList::MultiplyScaleComponent,
+           py::arg("scale_index"), py::arg("position_index"), py::arg("channel"),
+           py::arg("correction_factor"))
+      .def("get_positions", [](const radler::ComponentList& self, size_t s) {
+        if (s >= self.NScales()) throw std::out_of_range("Scale index out of range");
+        py::list out;
+        for (const auto& p : self.GetPositions(s)) out.append(py::make_tuple(p.x, p.y));
+        return out;
+      });
 }
 
 py::dict ResultDict(const radler::algorithms::ParallelDeconvolutionResult& r,
@@ -442,6 +462,54 @@ void InitTiling(py::module& m) {
     }
     return py::make_tuple(boxes, labels);
   }, py::arg("image"), py::arg("grid_width"), py::arg("grid_height"));
+
+  // math::DijkstraSplitter (cpp/math/dijkstra_splitter.h) member by member,
+  // for the restated cpp/math/test/test_dijkstra_splitter.cc. Images are
+  // C-contiguous float32 (h, w); outputs are modified in place.
+  using F32 = py::array_t<float, py::array::c_style>;
+  using B8 = py::array_t<bool, py::array::c_style>;
+  auto splitter = [](const F32& image) {
+    if (image.ndim() != 2) throw std::runtime_error("image must be 2-D");
+    return radler::math::DijkstraSplitter(image.shape(1), image.shape(0));
+  };
+  t.def("divide_vertically", [splitter](const F32& image, F32& output, size_t x1,
+                                        size_t x2) {
+    splitter(image).DivideVertically(image.data(), output.mutable_data(), x1, x2);
+  });
+  t.def("divide_horizontally", [splitter](const F32& image, F32& output, size_t y1,
+                                          size_t y2) {
+    splitter(image).DivideHorizontally(image.data(), output.mutable_data(), y1, y2);
+  });
+  t.def("add_vertical_divider", [splitter](const F32& image, F32& scratch, F32& output,
+                                           size_t x1, size_t x2) {
+    splitter(image).AddVerticalDivider(image.data(), scratch.mutable_data(),
+                                       output.mutable_data(), x1, x2);
+  });
+  t.def("add_horizontal_divider", [splitter](const F32& image, F32& scratch, F32& output,
+                                             size_t y1, size_t y2) {
+    splitter(image).AddHorizontalDivider(image.data(), scratch.mutable_data(),
+                                         output.mutable_data(), y1, y2);
+  });
+  t.def("flood_vertical_area", [splitter](const F32& division, size_t x, B8& mask) {
+    size_t sx = 0, sw = 0;
+    splitter(division).FloodVerticalArea(division.data(), x, mask.mutable_data(), sx, sw);
+    return py::make_tuple(sx, sw);
+  });
+  t.def("flood_horizontal_area", [splitter](const F32& division, size_t y, B8& mask) {
+    size_t sy = 0, sh = 0;
+    splitter(division).FloodHorizontalArea(division.data(), y, mask.mutable_data(), sy,
+                                           sh);
+    return py::make_tuple(sy, sh);
+  });
+  t.def("get_bounding_mask", [](size_t width, size_t height, const B8& vertical_mask,
+                                size_t vx, size_t vwidth, const B8& horizontal_mask,
+                                B8& output) {
+    size_t x = 0, y = 0, w = 0, h = 0;
+    radler::math::DijkstraSplitter(width, height)
+        .GetBoundingMask(vertical_mask.data(), vx, vwidth, horizontal_mask.data(),
+                         output.mutable_data(), x, y, w, h);
+    return py::make_tuple(x, y, w, h);
+  });
 }
 
 void InitDistributed(py::module& m) {

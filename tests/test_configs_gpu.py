@@ -112,9 +112,11 @@ def test_c1_hogbom_1024_through_perform():
     from radler_import import radler as rd
     fx = fixture("c1")
     psfs, dirty = inputs("c1", fx)
+    # the accessors borrow the arrays (cpp/radler.h:38-40): keep them alive
+    psf = psfs[0].copy()
     residual = dirty[0].copy()
     model = np.zeros_like(residual)
-    radler = rd.Radler(settings(rd, "c1"), psfs[0].copy(), residual, model, 0.0)
+    radler = rd.Radler(settings(rd, "c1"), psf, residual, model, 0.0)
     radler.perform(0)
     assert radler.iteration_number == 1000
     assert cp.sha256(residual[None]) == str(fx["residual_sha256"])
