@@ -3,25 +3,41 @@
 multiscale CLEAN on an 8192^2 synthetic sky (BASELINE.json metric), on the
 MI355X-native engine.
 
-One step = one major iteration to threshold (Radler::Perform's hot path,
-ParallelDeconvolution -> MultiScaleAlgorithm) on the device-resident image set,
-restored to the same dirty image before every step (a 256 MiB device copy,
-inside the timed region). Inputs are resident in HBM when timing starts.
+One step = one `Radler.perform` (the drop-in API): load and
+average the residual/model/PSF through the work-table accessors (host ->
+HBM), one major iteration of ParallelDeconvolution -> MultiScaleAlgorithm to
+the 5-sigma threshold (major_loop_gain 1), and the residual/model stores
+(HBM -> host). Every step gets its own Radler over its own copy of the dirty
+image, built before the timed region (construction does not touch the GPU).
+`device_resident` additionally reports the same major iteration on an image
+set already resident in HBM (radler.gpu.DeviceRun: restore + execute, no
+host transfers).
 
-Multi-GPU (weak scaling): one process per GPU (torch.distributed, RCCL); each
-rank deconvolves its own 8192^2 field of the mosaic (independent subimages, as
-ParallelDeconvolution does with one subimage per GPU); barrier + sync bracket
-the timed region and the slowest rank's time is used. value = components of
-all ranks / that time.
+Workloads (--workload):
+  fields  one independent 8192^2 field per GPU (weak scaling; N = 1 default)
+  tiled   ONE image split into grid x grid subimages (ParallelDeconvolution,
+          SURVEY.md C5) shared by the ranks: find-peak pass, one RCCL
+          allreduce(max) of the start peak, owner broadcasts of the subimage
+          results (strong scaling; N > 1 default, 8192^2 8 x 8)
 
-Also reported: `roofline` of the dominant kernel family (HIP-event device
-time, algorithmic bytes per SURVEY.md §8(d)) and `cpu_baseline` = the oracle
-(C++ restatement, std::thread) on a bounded sample of the same workload.
+Multi-GPU: one process per GPU. `--gpus N` without a launcher re-launches
+itself under torch.distributed.run (before anything touches the GPU); under a
+launcher WORLD_SIZE must equal N. Barrier + device sync bracket the timed
+region and the slowest rank's time is used; value = components of all ranks /
+that time.
+
+Also reported: `roofline` of the dominant kernel family (HIP events on the
+stream of every session of the process, algorithmic bytes per SURVEY.md
+§8(d)) and `cpu_baseline` = the oracle (C++ restatement, std::thread, float64
+FFT) on a bounded sample of the same workload: its cleaning rate after setup,
+with all affinity cores and with one, and the setup time separately.
 """
 import argparse
 import ctypes as C
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -47,7 +63,7 @@ def make_problem(size, seed, n_points, n_blobs, fwhm=4.0):
     return psf, dirty
 
 
-def settings_for(rd, size, max_iter, max_scales, threshold):
+def settings_for(rd, size, max_iter, max_scales, threshold, grid, threads):
     s = rd.Settings()
     s.algorithm_type = rd.AlgorithmType.multiscale
     s.trimmed_image_width = s.trimmed_image_height = size
@@ -59,6 +75,8 @@ def settings_for(rd, size, max_iter, max_scales, threshold):
     s.allow_negative_components = True
     s.border_ratio = 0.0
     s.multiscale.max_scales = max_scales
+    s.parallel.grid_width = s.parallel.grid_height = grid
+    s.parallel.max_threads = threads
     return s
 
 
@@ -71,23 +89,25 @@ FAMILIES = ["conv_rows", "conv_cols", "conv64_rows", "conv64_cols", "conv_rows_s
 
 
 class Timing:
-    def __init__(self, session_handle):
+    """Kernel-family timing over every session of the process
+    (rdl_timing_*_all: the main session and a subimage pool's workers)."""
+
+    def __init__(self):
         self.lib = C.CDLL(os.path.join(ROOT, "ska-sdp-func-radler_amd", "lib", "librdl_hip.so"))
-        self.h = C.c_void_p(session_handle)
-        self.lib.rdl_timing_get.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.c_double),
-                                            C.POINTER(C.c_uint64), C.POINTER(C.c_double)]
+        self.lib.rdl_timing_get_all.argtypes = [C.c_char_p, C.POINTER(C.c_double),
+                                                C.POINTER(C.c_uint64), C.POINTER(C.c_double)]
 
     def enable(self, on):
-        self.lib.rdl_timing_enable(self.h, int(on))
+        self.lib.rdl_timing_enable_all(int(on))
 
     def reset(self):
-        self.lib.rdl_timing_reset(self.h)
+        self.lib.rdl_timing_reset_all()
 
     def get(self):
         out = {}
         for fam in FAMILIES:
             ms, n, b = C.c_double(), C.c_uint64(), C.c_double()
-            self.lib.rdl_timing_get(self.h, fam.encode(), C.byref(ms), C.byref(n), C.byref(b))
+            self.lib.rdl_timing_get_all(fam.encode(), C.byref(ms), C.byref(n), C.byref(b))
             if n.value:
                 out[fam] = {"ms": ms.value, "launches": n.value, "bytes": b.value}
         return out
@@ -112,25 +132,71 @@ def measured_traffic(family, bytes_per_launch):
             os.path.relpath(files[-1], ROOT))
 
 
-def cpu_baseline(psf, dirty, max_scales, threshold, sample_components, threads):
-    """The oracle (tests/oracle_lib -> oracle/build/liboracle.so) on the first
-    `sample_components` components of the same workload (same inputs)."""
+def affinity_cores():
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(psf, dirty, max_scales, threshold, sample_components, thread_counts):
+    """The oracle (tests/oracle_lib -> oracle/build/liboracle.so, float64
+    FFT where the reference uses FFTW float) on the first `sample_components`
+    components of the same workload (same inputs). The rate counts the
+    cleaning after setup; the setup (scale-convolved PSFs, first peak
+    search) is reported on its own."""
     from oracle_lib import OracleAlgorithm, get_oracle
     orc = get_oracle()
-    orc.set_threads(threads)
     size = dirty.shape[0]
-    res, mod = dirty[None].copy(), np.zeros_like(dirty)[None]
-    alg = OracleAlgorithm(orc, 1, threshold=threshold, max_iterations=sample_components,
-                          border_ratio=0.0, max_scales=max_scales, beam_size_in_pixels=BEAM_PX,
-                          minor_loop_gain=0.1, major_loop_gain=1.0)
-    t0 = time.perf_counter()
-    r, _ = alg.execute(res, mod, psf[None], trace_cap=1)
-    dt = time.perf_counter() - t0
-    return {"value": r.iteration_number / dt, "unit": "components/s", "cores": threads,
-            "kind": "port",
-            "sample": (f"oracle MultiScale (C++ restatement, float64 FFT) on the same "
-                       f"{size}x{size} {max_scales}-scale sky, first {r.iteration_number} "
-                       f"components incl. PSF/scale setup, {dt:.1f} s")}
+    runs = []
+    for threads in thread_counts:
+        orc.set_threads(threads)
+        res, mod = dirty[None].copy(), np.zeros_like(dirty)[None]
+        alg = OracleAlgorithm(orc, 1, threshold=threshold, max_iterations=sample_components,
+                              border_ratio=0.0, max_scales=max_scales,
+                              beam_size_in_pixels=BEAM_PX, minor_loop_gain=0.1,
+                              major_loop_gain=1.0)
+        t0 = time.perf_counter()
+        r, _ = alg.execute(res, mod, psf[None], trace_cap=1)
+        total = time.perf_counter() - t0
+        setup = alg.setup_seconds()
+        runs.append({"threads": threads, "components": int(r.iteration_number),
+                     "setup_s": round(setup, 2), "clean_s": round(total - setup, 2),
+                     "value": round(r.iteration_number / max(total - setup, 1e-9), 2)})
+    best = runs[0]
+    return {"value": best["value"], "unit": "components/s", "cores": best["threads"],
+            "kind": "port", "cpu_model": cpu_model(), "affinity_cores": affinity_cores(),
+            "runs": runs,
+            "sample": (f"oracle MultiScale (C++ restatement of the reference, std::thread, "
+                       f"float64 FFT; the reference uses FFTW float) on the same "
+                       f"{size}x{size} {max_scales}-scale sky: the first "
+                       f"{best['components']} components after setup; setup "
+                       f"{best['setup_s']} s reported separately")}
+
+
+def relaunch(args):
+    """--gpus N without a launcher: run this script under
+    torch.distributed.run as a child (nothing here has touched the GPU) and
+    exit with its status."""
+    with socket.socket() as sock:
+        sock.bind(("127.0.0.1", 0))
+        port = sock.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.run(cmd, env=env).returncode
 
 
 def main():
@@ -138,30 +204,40 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", choices=["fields", "tiled"], default=None,
+                    help="default: fields at N = 1, tiled at N > 1")
     ap.add_argument("--size", type=int, default=8192)
+    ap.add_argument("--grid", type=int, default=8, help="tiled: subimages per axis")
+    ap.add_argument("--pool", type=int, default=8,
+                    help="tiled: subimages in flight per GPU (settings.parallel.max_threads)")
     ap.add_argument("--scales", type=int, default=6)
     ap.add_argument("--points", type=int, default=2000)
     ap.add_argument("--blobs", type=int, default=200)
-    ap.add_argument("--max-iter", type=int, default=1000000)
+    ap.add_argument("--max-iter", type=int, default=10 ** 9)
     ap.add_argument("--sigma", type=float, default=5.0)
-    ap.add_argument("--cpu-sample", type=int, default=2000,
+    ap.add_argument("--device-resident", type=int, default=1,
+                    help="also time the HBM-resident major iteration (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=1000,
                     help="components in the CPU-baseline sample (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads of the all-cores CPU run (0: the affinity core count)")
+    ap.add_argument("--cpu-single-thread", type=int, default=1,
+                    help="also run the CPU baseline on one thread")
     ap.add_argument("--breakdown", action="store_true", help="per-kernel times to stderr")
     ap.add_argument("--timing-all", action="store_true",
                     help="count every launch of the process (PMC passes, tools/pmc_traffic.py)")
     ap.add_argument("--dump-families", help="write the per-family launch/byte counts here")
-    ap.add_argument("--workload", choices=["fields", "tiled"], default="fields",
-                    help="fields: one independent field per GPU (weak scaling, the "
-                         "default); tiled: ONE image split into grid x grid subimages "
-                         "(ParallelDeconvolution, SURVEY.md config 5) shared by the "
-                         "ranks over RCCL (strong scaling)")
-    ap.add_argument("--grid", type=int, default=8, help="tiled: subimages per axis")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(relaunch(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    workload = args.workload or ("fields" if world == 1 else "tiled")
+    tiled = workload == "tiled"
     dist = None
     if world > 1:
         import torch
@@ -174,14 +250,12 @@ def main():
     import radler as rd
 
     threshold = args.sigma * NOISE
-    tiled = args.workload == "tiled"
     # tiled: every rank holds the same image (one field); fields: one per rank
     psf, dirty = make_problem(args.size, SEED + (0 if tiled else rank), args.points,
                               args.blobs)
-    s = settings_for(rd, args.size, args.max_iter, args.scales, threshold)
-    if tiled:
-        s.parallel.grid_width = s.parallel.grid_height = args.grid
-    run = rd.gpu.DeviceRun(s, psf, dirty, [], BEAM_PX * PIXEL_SCALE)
+    s = settings_for(rd, args.size, args.max_iter, args.scales, threshold,
+                     args.grid if tiled else 1, args.pool if tiled else 1)
+    comm = None
     if tiled and dist is not None:
         # RCCL communicator of the product (rdl_comm_*), id from rank 0
         import torch
@@ -192,15 +266,14 @@ def main():
         dist.broadcast(idl, src=0)
         uid = bytes(idl.cpu().numpy().tobytes())
         comm = rd.distributed.RcclCommunicator(local_rank, world, rank, uid)
-        run.set_communicator(comm)
-    timing = Timing(run.session_handle())
-    if args.timing_all:
-        timing.enable(True)
 
-    for _ in range(args.warmup):
-        run.restore()
-        run.execute()
-    run.sync()
+    def make_radler():
+        # the accessors borrow these arrays (cpp/radler.h:38-40)
+        arrays = (psf, dirty.copy(), np.zeros_like(dirty))
+        r = rd.Radler(s, *arrays, BEAM_PX * PIXEL_SCALE)
+        if comm is not None:
+            r.set_communicator(comm)
+        return r, arrays
 
     def barrier():
         if dist is not None:
@@ -208,39 +281,72 @@ def main():
             dist.barrier()
             torch.cuda.synchronize()
 
+    timing = Timing()
+    if args.timing_all:
+        timing.enable(True)
+    for _ in range(args.warmup):
+        r, arrays = make_radler()
+        r.perform(0)
+        del r, arrays
+    steps = [make_radler() for _ in range(args.steps)]
+
     if not args.timing_all:
         timing.reset()
     timing.enable(True)
     barrier()
-    run.sync()
     t0 = time.perf_counter()
-    comps, results = 0, []
-    for _ in range(args.steps):
-        run.restore()
-        r = run.execute()
-        comps += r["iterations"]
-        results.append(r)
-    run.sync()
+    comps = 0
+    for r, _ in steps:
+        r.perform(0)  # Perform returns after the residual/model stores (D2H)
+        comps += rd.gpu.total_iteration_number(r)
     barrier()
     elapsed = time.perf_counter() - t0
-    timing.enable(False)
+    if not args.timing_all:
+        timing.enable(False)
     fams = timing.get()
     if args.dump_families and rank == 0:
         with open(args.dump_families, "w") as f:
             json.dump(fams, f, indent=1)
+    del steps
+
+    # the same major iteration on an HBM-resident image set (no host transfers)
+    resident = None
+    if args.device_resident and not tiled:
+        run = rd.gpu.DeviceRun(s, psf, dirty, [], BEAM_PX * PIXEL_SCALE)
+        run.restore()
+        run.execute()  # warm-up
+        run.sync()
+        barrier()
+        t1 = time.perf_counter()
+        rcomps = 0
+        for _ in range(args.steps):
+            run.restore()
+            rcomps += run.execute()["iterations"]
+        run.sync()
+        barrier()
+        relapsed = time.perf_counter() - t1
+        resident = {"ms_per_step": round(1e3 * relapsed / args.steps, 2),
+                    "components_per_step": rcomps // args.steps, "elapsed": relapsed,
+                    "components": rcomps}
+        del run
 
     total_comps, max_elapsed = comps, elapsed
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        c = torch.tensor([comps], dtype=torch.float64, device="cuda")
+        vals = [elapsed, comps] + ([resident["elapsed"], resident["components"]]
+                                   if resident else [0.0, 0.0])
+        t = torch.tensor([vals[0], vals[2]], dtype=torch.float64, device="cuda")
+        c = torch.tensor([vals[1], vals[3]], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         if not tiled:  # tiled: every rank reports the whole job's components
             dist.all_reduce(c, op=dist.ReduceOp.SUM)
-        max_elapsed, total_comps = float(t.item()), int(c.item())
+        max_elapsed, total_comps = float(t[0].item()), int(c[0].item())
+        if resident:
+            resident["elapsed"], resident["components"] = float(t[1].item()), int(c[1].item())
+    if resident:
+        resident["value"] = round(resident.pop("components") / resident.pop("elapsed"), 2)
 
     if rank != 0:
-        del run, timing
         if dist is not None:
             dist.destroy_process_group()
         return
@@ -267,14 +373,16 @@ def main():
             gbs = v["bytes"] / (v["ms"] * 1e-3) / 1e9 if v["ms"] else 0.0
             print(f"[breakdown] {k:18s} {v['ms']:10.2f} ms {v['launches']:8d} launches "
                   f"{gbs:8.1f} GB/s", file=sys.stderr)
-        print(f"[breakdown] device {device_ms:.1f} ms of {1e3 * elapsed:.1f} ms wall; "
-              f"results {results}", file=sys.stderr)
+        print(f"[breakdown] device {device_ms:.1f} ms (all streams) of "
+              f"{1e3 * elapsed:.1f} ms wall", file=sys.stderr)
 
     cpu = None
     if args.cpu_sample > 0 and world == 1 and not tiled:
-        cpu = cpu_baseline(psf, dirty, args.scales, threshold, args.cpu_sample,
-                           args.cpu_threads)
+        threads = args.cpu_threads or affinity_cores()
+        counts = [threads] + ([1] if args.cpu_single_thread and threads > 1 else [])
+        cpu = cpu_baseline(psf, dirty, args.scales, threshold, args.cpu_sample, counts)
 
+    grid = f"-tiled{args.grid}x{args.grid}" if tiled else ""
     line = {
         "metric": "CLEAN components/sec (multiscale, to 5-sigma threshold)",
         "value": round(total_comps / max_elapsed, 2),
@@ -290,19 +398,19 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (seeded sky: points + Gaussian blobs, analytic PSF, noise)",
-        "config": {"workload": (f"multiscale-{args.size}x{args.size}-{args.scales}scales"
-                                + (f"-tiled{args.grid}x{args.grid}" if tiled else "")),
+        "config": {"workload": f"multiscale-{args.size}x{args.size}-{args.scales}scales{grid}",
+                   "step": "Radler.perform (accessor load + major iteration + store)",
                    "image": [args.size, args.size], "scales": args.scales,
                    "points": args.points, "blobs": args.blobs, "noise": NOISE,
                    "threshold": threshold, "minor_loop_gain": 0.1, "major_loop_gain": 1.0,
                    "fields_per_gpu": 0 if tiled else 1,
                    "parallelism": (f"subimages{args.grid * args.grid}/ranks{world}"
-                                   if tiled else f"fields{world}")},
+                                   f"/pool{args.pool}" if tiled else f"fields{world}")},
+        "device_resident": resident,
         "roofline": roofline,
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)
-    del run, timing
     import gc
     gc.collect()  # release device buffers while the runtime is fully alive
     if dist is not None:

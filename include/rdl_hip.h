@@ -77,6 +77,14 @@ int rdl_timing_enable(rdl_session* s, int enable);
 int rdl_timing_get(rdl_session* s, const char* family, double* ms,
                    uint64_t* launches, double* bytes);
 int rdl_timing_reset(rdl_session* s);
+/* The same over EVERY session of the process (the main session, the worker
+ * sessions of a subimage pool, sessions already destroyed since the last
+ * reset): what one Radler::Perform launched, wherever it ran. Call get/reset
+ * only while no other thread launches work. */
+int rdl_timing_enable_all(int enable);
+int rdl_timing_get_all(const char* family, double* ms, uint64_t* launches,
+                       double* bytes);
+int rdl_timing_reset_all(void);
 
 /* ------------------------------------------------------------ peak finder */
 typedef struct {

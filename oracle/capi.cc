@@ -316,6 +316,12 @@ int orc_algo_execute(void* h, const orc_set_desc* d, float* residual,
   }
 }
 
+// Setup seconds of the last multiscale execute (MultiScale::setup_seconds)
+double orc_algo_setup_seconds(void* h) {
+  auto* algo = static_cast<OrcAlgo*>(h);
+  return algo->ms ? algo->ms->setup_seconds : 0.0;
+}
+
 struct orc_parallel_result {
   int32_t another_iteration_required;
   int32_t n_subimages;

@@ -1,5 +1,6 @@
 // ORACLE / TEST INFRASTRUCTURE ONLY — never linked into the product.
 // CPU restatement of Radler's CLEAN hot path; see oracle.h.
+#include <chrono>
 #include "oracle.h"
 
 #include "component_optimization.h"
@@ -972,6 +973,7 @@ Result MultiScale::Execute(ImageSet& data, ImageSet& model,
                            const std::vector<const float*>& psfs,
                            std::vector<Component>* trace) {
   // multiscale_algorithm.cc:183-576
+  const auto setup_start = std::chrono::steady_clock::now();
   const size_t width = data.width, height = data.height;
   const size_t npx = width * height;
   if (s_.stop_on_negative) s_.allow_negative = true;
@@ -1001,6 +1003,8 @@ Result MultiScale::Execute(ImageSet& data, ImageSet& model,
   }
 
   FindActiveScaleConvolvedMaxima(data, integrated.data(), true);
+  setup_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() -
+                                                setup_start).count();
   Result result;
   size_t scale_with_peak;
   margins = MarginTracker();

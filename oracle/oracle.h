@@ -258,6 +258,10 @@ class MultiScale {
   // up in end_margin (the decisions that stopped the run)
   MarginTracker margins;
   float end_margin = std::numeric_limits<float>::infinity();
+  // wall seconds of the last Execute's setup (scale PSFs + first peak
+  // search), before the outer loop: bench.py's cpu_baseline reports the
+  // cleaning rate after setup and the setup separately
+  double setup_seconds = 0.0;
 
  private:
   AlgoSettings s_;

@@ -86,11 +86,17 @@ struct rdl_session {
 };
 
 namespace rdl {
+// rdl_timing_enable_all: time every session of the process
+extern std::atomic<bool> g_timing_all;
+inline bool TimingOn(const rdl_session* s) {
+  return s->timing || g_timing_all.load(std::memory_order_relaxed);
+}
+
 // RAII-less helper used by launchers: records start/end events when timing.
 // Adds algorithmic bytes to a family after the fact (e.g. the sub-minor loop,
 // whose iteration count is known only when it returns).
 inline void AddTimingBytes(rdl_session* s, const char* family, double bytes) {
-  if (s->timing) s->timings[family].bytes += bytes;
+  if (TimingOn(s)) s->timings[family].bytes += bytes;
 }
 
 struct ScopedTiming {
@@ -100,10 +106,10 @@ struct ScopedTiming {
   hipEvent_t start = nullptr;
   ScopedTiming(rdl_session* s_, const char* f, double b)
       : s(s_), family(f), bytes(b) {
-    if (s->timing) s->BeginTiming(family, &start);
+    if (TimingOn(s)) s->BeginTiming(family, &start);
   }
   ~ScopedTiming() {
-    if (s->timing && start) s->EndTiming(family, start, bytes);
+    if (start) s->EndTiming(family, start, bytes);
   }
 };
 

@@ -8,7 +8,24 @@
 namespace rdl {
 namespace {
 thread_local std::string g_last_error;
+
+// Process-wide timing (rdl_timing_*_all): every live session, plus the
+// collected totals of sessions destroyed since the last reset.
+std::mutex g_registry_mutex;
+std::vector<rdl_session*> g_sessions;
+std::map<std::string, TimingEntry> g_retired;
+
+void Fold(std::map<std::string, TimingEntry>& into,
+          const std::map<std::string, TimingEntry>& from) {
+  for (const auto& [name, t] : from) {
+    TimingEntry& e = into[name];
+    e.ms += t.ms;
+    e.launches += t.launches;
+    e.bytes += t.bytes;
+  }
 }
+}  // namespace
+std::atomic<bool> g_timing_all{false};
 void SetError(const std::string& msg) { g_last_error = msg; }
 }  // namespace rdl
 
@@ -107,6 +124,10 @@ int rdl_session_create(int device, rdl_session** out) {
   s->trace_subminor = trace && trace[0] == '1';
   RDL_HIP_CHECK(hipMalloc(&s->d_small, 1 << 16));
   RDL_HIP_CHECK(hipHostMalloc(&s->h_small, 1 << 16, hipHostMallocDefault));
+  {
+    const std::lock_guard<std::mutex> lock(rdl::g_registry_mutex);
+    rdl::g_sessions.push_back(s.get());
+  }
   *out = s.release();
   return RDL_OK;
 }
@@ -115,6 +136,12 @@ int rdl_session_destroy(rdl_session* s) {
   if (!s) return RDL_OK;
   (void)hipSetDevice(s->device);
   (void)hipStreamSynchronize(s->stream);
+  {
+    const std::lock_guard<std::mutex> lock(rdl::g_registry_mutex);
+    auto& v = rdl::g_sessions;
+    v.erase(std::remove(v.begin(), v.end(), s), v.end());
+    if (s->CollectTimings() == RDL_OK) rdl::Fold(rdl::g_retired, s->timings);
+  }
   for (auto& [name, t] : s->timings)
     for (auto& [a, b] : t.pending) {
       (void)hipEventDestroy(a);
@@ -256,6 +283,39 @@ int rdl_timing_reset(rdl_session* s) {
   RDL_ARG_CHECK(s, "NULL session");
   RDL_TRY(s->CollectTimings());
   s->timings.clear();
+  return RDL_OK;
+}
+
+int rdl_timing_enable_all(int enable) {
+  rdl::g_timing_all.store(enable != 0, std::memory_order_relaxed);
+  return RDL_OK;
+}
+
+int rdl_timing_get_all(const char* family, double* ms, uint64_t* launches,
+                       double* bytes) {
+  RDL_ARG_CHECK(family, "NULL family");
+  const std::lock_guard<std::mutex> lock(rdl::g_registry_mutex);
+  std::map<std::string, rdl::TimingEntry> total;
+  rdl::Fold(total, rdl::g_retired);
+  for (rdl_session* s : rdl::g_sessions) {
+    RDL_TRY(s->CollectTimings());
+    rdl::Fold(total, s->timings);
+  }
+  const auto it = total.find(family);
+  const bool found = it != total.end();
+  if (ms) *ms = found ? it->second.ms : 0.0;
+  if (launches) *launches = found ? it->second.launches : 0;
+  if (bytes) *bytes = found ? it->second.bytes : 0.0;
+  return RDL_OK;
+}
+
+int rdl_timing_reset_all(void) {
+  const std::lock_guard<std::mutex> lock(rdl::g_registry_mutex);
+  rdl::g_retired.clear();
+  for (rdl_session* s : rdl::g_sessions) {
+    RDL_TRY(s->CollectTimings());
+    s->timings.clear();
+  }
   return RDL_OK;
 }
 

@@ -713,6 +713,20 @@ void InitGpu(py::module& m) {
         return result;
       },
       py::arg("image"), py::arg("window"));
+  // Radler::IterationNumber reports the first subimage's algorithm only
+  // (cpp/radler.cc:406-408); bench.py counts the components of every
+  // subimage of a gridded Perform
+  g.def(
+      "total_iteration_number",
+      [](const radler::Radler& r) {
+        if (!r.IsInitialized()) return size_t(0);
+        const radler::algorithms::ParallelDeconvolution& p = r.Parallel();
+        size_t total = 0;
+        for (size_t i = 0; i != p.SubImageCount(); ++i)
+          total += p.Algorithm(i).IterationNumber();
+        return total;
+      },
+      py::arg("radler"));
   py::class_<radler::DeviceRun>(g, "DeviceRun")
       .def(py::init([](const radler::Settings& settings, FloatArray psf,
                        FloatArray residual, std::vector<double> weights,

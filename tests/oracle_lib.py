@@ -359,6 +359,14 @@ class OracleAlgorithm:
         L.orc_algo_margins(self.h, m.ctypes.data, v.ctypes.data, n)
         return m, v
 
+    def setup_seconds(self):
+        """Wall seconds of the last multiscale execute's setup (scale-convolved
+        PSFs and the first peak search, before the outer loop)."""
+        L = self.o.lib
+        L.orc_algo_setup_seconds.restype = C.c_double
+        L.orc_algo_setup_seconds.argtypes = [C.c_void_p]
+        return float(L.orc_algo_setup_seconds(self.h))
+
     def set_automask(self, track, use):
         """MultiScaleAlgorithm::SetAutoMaskMode (multiscale only)."""
         L = self.o.lib
