@@ -316,6 +316,23 @@ int orc_algo_execute(void* h, const orc_set_desc* d, float* residual,
   }
 }
 
+// After `after` multiscale outer iterations switch the pool to `n` threads
+// (0 = never), and stop after `stop` outer iterations (0 = never);
+// orc_algo_switch_info reports when the switch happened.
+void orc_algo_set_clean_threads(void* h, uint64_t n, uint64_t after, uint64_t stop) {
+  auto* algo = static_cast<OrcAlgo*>(h);
+  if (!algo->ms) return;
+  algo->ms->clean_threads = n;
+  algo->ms->switch_after = after;
+  algo->ms->stop_after_outer = stop;
+}
+
+void orc_algo_switch_info(void* h, double* seconds, uint64_t* components) {
+  auto* algo = static_cast<OrcAlgo*>(h);
+  *seconds = algo->ms ? algo->ms->switch_seconds : 0.0;
+  *components = algo->ms ? algo->ms->switch_components : 0;
+}
+
 // Setup seconds of the last multiscale execute (MultiScale::setup_seconds)
 double orc_algo_setup_seconds(void* h) {
   auto* algo = static_cast<OrcAlgo*>(h);
@@ -474,6 +491,35 @@ int orc_local_rms(const float* integrated, uint64_t width, uint64_t height, int 
 void orc_gradient_descent(float* model, const float* residual, const float* psf,
                           uint64_t width, uint64_t height) {
   GradientDescent(model, residual, psf, width, height, 2 * width, 2 * height);
+}
+
+void orc_linear_component_solve(float* model, const float* image, const float* psf,
+                                uint64_t width, uint64_t height) {
+  LinearComponentSolve(model, image, psf, width, height);
+}
+
+// GradientDescentWithVariablePsf: n_psfs lists (counts[p] positions each, x,y
+// pairs concatenated), psfs [n_psfs][h][w]; deltas [n_psfs][h][w]
+void orc_gradient_descent_variable_psf(const uint32_t* positions, const uint64_t* counts,
+                                       uint64_t n_psfs, const float* image,
+                                       const float* psfs, uint64_t width, uint64_t height,
+                                       uint64_t padded_width, uint64_t padded_height,
+                                       float* deltas) {
+  std::vector<std::vector<std::pair<size_t, size_t>>> lists(n_psfs);
+  std::vector<std::vector<float>> psf_images;
+  const size_t n = width * height;
+  for (uint64_t p = 0; p != n_psfs; ++p) {
+    for (uint64_t i = 0; i != counts[p]; ++i, positions += 2)
+      lists[p].emplace_back(positions[0], positions[1]);
+    psf_images.emplace_back(psfs + p * n, psfs + (p + 1) * n);
+  }
+  const std::vector<std::vector<float>> d = GradientDescentWithVariablePsf(
+      lists, image, psf_images, width, height, padded_width, padded_height);
+  for (uint64_t p = 0; p != n_psfs; ++p) std::copy(d[p].begin(), d[p].end(), deltas + p * n);
+}
+
+double orc_make_rms_factor_image(float* rms, uint64_t n, double strength) {
+  return MakeRmsFactorImage(rms, n, strength);
 }
 
 void orc_padded_convolution(float* image, const float* psf, uint64_t width,

@@ -170,4 +170,72 @@ void RunFullComponentFitter(float* residual, float* model, const float* psf, siz
   }
 }
 
+void LinearComponentSolve(float* model, const float* image, const float* psf,
+                          size_t width, size_t height) {
+  Positions active;  // GetActivePositions (:20-32)
+  for (size_t y = 0; y != height; ++y)
+    for (size_t x = 0; x != width; ++x)
+      if (model[y * width + x] != 0.0) active.emplace_back(x, y);
+  const size_t n = active.size();
+  if (n == 0) return;
+  // X (n x n) and y (:203-227)
+  std::vector<long double> a(n * n), v(n * n, 0.0L), rhs(n);
+  for (size_t i = 0; i != n; ++i) rhs[i] = image[active[i].first + active[i].second * height];
+  const size_t mid_x = width + width / 2, mid_y = height + height / 2;
+  for (size_t i = 0; i != n; ++i)
+    for (size_t j = 0; j != n; ++j) {
+      const size_t psf_x = (active[i].first + mid_x - active[j].first) % width;
+      const size_t psf_y = (active[i].second + mid_y - active[j].second) % height;
+      a[i * n + j] = psf[psf_x + psf_y * width];
+    }
+  // one-sided Jacobi SVD: A V = U S
+  for (size_t j = 0; j != n; ++j) v[j * n + j] = 1.0L;
+  for (int sweep = 0; sweep != 100; ++sweep) {
+    bool rotated = false;
+    for (size_t j = 0; j + 1 < n; ++j)
+      for (size_t k = j + 1; k != n; ++k) {
+        long double alpha = 0, beta = 0, gamma = 0;
+        for (size_t i = 0; i != n; ++i) {
+          alpha += a[i * n + j] * a[i * n + j];
+          beta += a[i * n + k] * a[i * n + k];
+          gamma += a[i * n + j] * a[i * n + k];
+        }
+        if (gamma == 0 || std::fabs(gamma) <= 1e-19L * std::sqrt(alpha * beta)) continue;
+        rotated = true;
+        const long double zeta = (beta - alpha) / (2 * gamma);
+        const long double t =
+            (zeta >= 0 ? 1.0L : -1.0L) / (std::fabs(zeta) + std::sqrt(1 + zeta * zeta));
+        const long double c = 1 / std::sqrt(1 + t * t), s = c * t;
+        for (size_t i = 0; i != n; ++i) {
+          const long double x = a[i * n + j], y = a[i * n + k];
+          a[i * n + j] = c * x - s * y;
+          a[i * n + k] = s * x + c * y;
+          const long double p = v[i * n + j], q = v[i * n + k];
+          v[i * n + j] = c * p - s * q;
+          v[i * n + k] = s * p + c * q;
+        }
+      }
+    if (!rotated) break;
+  }
+  std::vector<long double> sigma(n);
+  long double sigma_max = 0;
+  for (size_t k = 0; k != n; ++k) {
+    long double n2 = 0;
+    for (size_t i = 0; i != n; ++i) n2 += a[i * n + k] * a[i * n + k];
+    sigma[k] = std::sqrt(n2);
+    sigma_max = std::max(sigma_max, sigma[k]);
+  }
+  // c = V S^-1 U^T y, with U_k = A_k / sigma_k
+  std::vector<long double> c(n, 0.0L);
+  for (size_t k = 0; k != n; ++k) {
+    if (!(sigma[k] > 2.220446049250313e-16L * sigma_max)) continue;
+    long double uty = 0;
+    for (size_t i = 0; i != n; ++i) uty += a[i * n + k] * rhs[i];
+    uty /= sigma[k] * sigma[k];
+    for (size_t j = 0; j != n; ++j) c[j] += v[j * n + k] * uty;
+  }
+  for (size_t p = 0; p != n; ++p)  // model += LinearComponentSolve(...) (:262)
+    model[active[p].first + active[p].second * width] += float(double(c[p]));
+}
+
 }  // namespace oracle

@@ -28,6 +28,14 @@ void GradientDescent(float* model, const float* image, const float* psf,
 
 namespace oracle {
 
+// component_optimization.cc:181-263: model += the least-squares solution of
+// the n_active x n_active system (one equation per component pixel; the
+// reference's gsl_multifit_linear, restated as an SVD pseudo-inverse in long
+// double with singular values below DBL_EPSILON * max dropped). The
+// reference's image index `x + y * height` (:206) is kept.
+void LinearComponentSolve(float* model, const float* image, const float* psf,
+                          size_t width, size_t height);
+
 // component_optimization.cc:323-402: all scales' components fitted together,
 // each scale with its own (scale-convolved) PSF; returns one delta image of
 // component values per scale.

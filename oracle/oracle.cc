@@ -1005,6 +1005,11 @@ Result MultiScale::Execute(ImageSet& data, ImageSet& model,
   FindActiveScaleConvolvedMaxima(data, integrated.data(), true);
   setup_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() -
                                                 setup_start).count();
+  const size_t setup_iteration = iteration_number;
+  const auto clean_start = std::chrono::steady_clock::now();
+  switch_seconds = 0.0;
+  switch_components = 0;
+  bool switched = clean_threads == 0;
   Result result;
   size_t scale_with_peak;
   margins = MarginTracker();
@@ -1035,7 +1040,18 @@ Result MultiScale::Execute(ImageSet& data, ImageSet& model,
   for (auto& v : individual) individual_set.images.push_back(v.data());
   bool diverging = false;
 
+  size_t outer_iteration = 0;
   for (;;) {
+    if (stop_after_outer && outer_iteration == stop_after_outer) break;
+    ++outer_iteration;
+    if (!switched && outer_iteration > switch_after) {
+      // bench.py's cpu_baseline: the rest of the run on clean_threads
+      switch_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() -
+                                                     clean_start).count();
+      switch_components = iteration_number - setup_iteration;
+      SetNThreads(clean_threads);
+      switched = true;
+    }
     margins.Note(std::fabs(scales_[scale_with_peak].max_unnormalized_image_value *
                            scales_[scale_with_peak].bias_factor),
                  first_threshold);

@@ -262,6 +262,14 @@ class MultiScale {
   // search), before the outer loop: bench.py's cpu_baseline reports the
   // cleaning rate after setup and the setup separately
   double setup_seconds = 0.0;
+  // bench.py's cpu_baseline: when clean_threads is non-zero, the pool
+  // switches to clean_threads after switch_after outer iterations;
+  // switch_seconds / switch_components record when (seconds since the setup
+  // ended) and after how many components. stop_after_outer (non-zero) ends
+  // the run after that many outer iterations.
+  size_t clean_threads = 0, switch_after = 0, stop_after_outer = 0;
+  double switch_seconds = 0.0;
+  size_t switch_components = 0;
 
  private:
   AlgoSettings s_;

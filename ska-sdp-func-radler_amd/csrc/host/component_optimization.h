@@ -3,6 +3,7 @@
 #pragma once
 
 #include <cstddef>
+#include <memory>
 #include <utility>
 #include <vector>
 
@@ -30,6 +31,21 @@ class MultiScaleTransforms;
 }
 
 namespace radler::math {
+
+/// component_optimization.cc:323-402 (FFT convolutions): every list's
+/// components fitted together, list p with the PSF whose padded spectrum is
+/// psf_spectra[p] (SubMinorLoop::MakePaddedPsfSpectrum); returns one plane
+/// of component values per list (the deltas).
+std::vector<gpu::Buffer> GradientDescentWithVariablePsf(
+    gpu::Session& s, const std::vector<std::vector<std::pair<size_t, size_t>>>& lists,
+    const float* d_image, const std::vector<std::shared_ptr<gpu::Buffer>>& psf_spectra,
+    size_t width, size_t height, size_t padded_width, size_t padded_height);
+
+/// component_optimization.cc:181-263 (LinearComponentSolve(model, image,
+/// psf)): d_model += the least-squares fit of its non-zero components to
+/// d_image, one equation per component pixel.
+void LinearComponentSolve(gpu::Session& s, float* d_model, const float* d_image,
+                          const float* d_psf, size_t width, size_t height);
 
 /// MultiScaleAlgorithm::RunFullComponentFitter for one image
 /// (multiscale_algorithm.cc:837-914) with GradientDescentWithVariablePsf

@@ -47,9 +47,9 @@ void GenericClean::RunComponentOptimization(ImageSet& residual_set, ImageSet& mo
                               psfs.Plane(residual_set.PsfIndex(i)), w, h, 2 * w, 2 * h);
         break;
       case OptimizationAlgorithm::kLinearEquationSolver:
-        throw std::runtime_error(
-            "The linear-equation component solver is not available in the MI355X "
-            "build");
+        math::LinearComponentSolve(s, model_set.Data(i), residual_set.Data(i),
+                                   psfs.Plane(residual_set.PsfIndex(i)), w, h);
+        break;
       case OptimizationAlgorithm::kRegularizedGradientDescent:
         throw std::runtime_error(
             "Regularized gradient descent has not yet been implemented");

@@ -206,8 +206,15 @@ void ImageSet::LoadAndAverage(bool use_residual_images) {
     for (const size_t original_index : group) {
       image_index = start;
       for (const WorkTableEntry* e : table_.OriginalGroups()[original_index]) {
-        const aocommon::ImageAccessor& acc =
-            use_residual_images ? *e->residual_accessor : *e->model_accessor;
+        const std::unique_ptr<aocommon::ImageAccessor>& acc_ptr =
+            use_residual_images ? e->residual_accessor : e->model_accessor;
+        // the reference's test accessor throws std::logic_error on use
+        // (cpp/test/imageaccessor.h, test_image_set.cc:478)
+        if (!acc_ptr)
+          throw std::logic_error(use_residual_images
+                                     ? "ImageSet: entry has no residual accessor"
+                                     : "ImageSet: entry has no model accessor");
+        const aocommon::ImageAccessor& acc = *acc_ptr;
         if (acc.Width() != width_ || acc.Height() != height_)
           throw std::runtime_error("ImageSet: accessor size mismatch");
         acc.Load(host.data());

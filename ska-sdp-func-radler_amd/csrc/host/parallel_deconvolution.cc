@@ -390,8 +390,6 @@ void TrimSubImage(gpu::Session& ops, const SubImage& sub, const ImageSet& data_i
   const size_t W = data_image.Width();
   const uint32_t uw = uint32_t(sub.width), uh = uint32_t(sub.height);
   const size_t n = sub.width * sub.height;
-  if (psfs.width < sub.width || psfs.height < sub.height)
-    throw std::runtime_error("PSF smaller than a subimage");
   for (size_t i = 0; i != data_image.Size(); ++i) {
     gpu::Check(rdl_box(ops.Handle(), d_data + i * n, uw, 0, 0, data_image.Data(i),
                        uint32_t(W), uint32_t(sub.x), uint32_t(sub.y), uw, uh,
@@ -402,11 +400,16 @@ void TrimSubImage(gpu::Session& ops, const SubImage& sub, const ImageSet& data_i
                        d_boundary, RDL_BOX_COPY_ZERO),
                "rdl_box");  // ImageSet::TrimMasked
   }
+  // Image::Resize (:323-330), centred per axis: a PSF larger than the
+  // subimage is cropped, a smaller one (a fine DD-PSF grid) zero-padded
+  const size_t cw = std::min(psfs.width, sub.width), ch = std::min(psfs.height, sub.height);
+  const size_t src_x = (psfs.width - cw) / 2, src_y = (psfs.height - ch) / 2;
+  const size_t dst_x = (sub.width - cw) / 2, dst_y = (sub.height - ch) / 2;
+  if (cw != sub.width || ch != sub.height) ops.Zero(d_psfs, psfs.count * n * sizeof(float));
   for (size_t i = 0; i != psfs.count; ++i)
-    gpu::Check(rdl_box(ops.Handle(), d_psfs + i * n, uw, 0, 0, psfs.Plane(i),
-                       uint32_t(psfs.width), uint32_t((psfs.width - sub.width) / 2),
-                       uint32_t((psfs.height - sub.height) / 2), uw, uh, nullptr,
-                       RDL_BOX_COPY),
+    gpu::Check(rdl_box(ops.Handle(), d_psfs + i * n, uw, uint32_t(dst_x), uint32_t(dst_y),
+                       psfs.Plane(i), uint32_t(psfs.width), uint32_t(src_x),
+                       uint32_t(src_y), uint32_t(cw), uint32_t(ch), nullptr, RDL_BOX_COPY),
                "rdl_box");
 }
 

@@ -1,6 +1,8 @@
 // Line references are to the reference's cpp/radler.cc.
 #include "radler.h"
 
+#include "host_profile.h"
+
 #include <cmath>
 #include <stdexcept>
 
@@ -103,6 +105,7 @@ const algorithms::DeconvolutionAlgorithm& Radler::MaxScaleCountAlgorithm()
 void Radler::Perform(bool& another_iteration_required,
                      size_t major_iteration_number) {  // :130-316
   if (!table_) throw std::runtime_error("Radler: not initialized");
+  prof::Section prof_total("perform.total");
   table_->ValidatePsfs();
   log::Info() << " == Deconvolving (" << major_iteration_number << ") ==\n";
   gpu::Session& s = DeviceSession();
@@ -112,8 +115,11 @@ void Radler::Perform(bool& another_iteration_required,
   ImageSet model_set(*table_, settings_.squared_joins,
                      settings_.linked_polarizations, image_width_,
                      image_height_, s);
-  residual_set.LoadAndAverage(true);
-  model_set.LoadAndAverage(false);
+  {
+    prof::Section p("perform.load");
+    residual_set.LoadAndAverage(true);
+    model_set.LoadAndAverage(false);
+  }
 
   const bool auto_mask_is_enabled =
       settings_.auto_mask_sigma || settings_.absolute_auto_mask_threshold;
@@ -200,11 +206,18 @@ void Radler::Perform(bool& another_iteration_required,
     parallel_deconvolution_->SetCleanMask(reinterpret_cast<const bool*>(auto_mask_.data()));
   }
 
-  const std::vector<gpu::Planes> psf_images = residual_set.LoadAndAveragePsfs();
-  const algorithms::ParallelDeconvolutionResult result =
-      parallel_deconvolution_->ExecuteMajorIteration(
-          residual_set, model_set, psf_images, table_->PsfOffsets(),
-          settings_.major_loop_gain);
+  std::vector<gpu::Planes> psf_images;
+  {
+    prof::Section p("perform.load_psfs");
+    psf_images = residual_set.LoadAndAveragePsfs();
+  }
+  algorithms::ParallelDeconvolutionResult result;
+  {
+    prof::Section p("perform.execute");
+    result = parallel_deconvolution_->ExecuteMajorIteration(
+        residual_set, model_set, psf_images, table_->PsfOffsets(),
+        settings_.major_loop_gain);
+  }
   another_iteration_required = result.another_iteration_required;
 
   if (!another_iteration_required && auto_mask_is_enabled && !auto_mask_is_finished_) {
@@ -236,6 +249,7 @@ void Radler::Perform(bool& another_iteration_required,
     log::Info() << "Maximum number of minor deconvolution iterations was "
                    "reached: not continuing deconvolution.\n";
   }
+  prof::Section prof_store("perform.store");
   residual_set.AssignAndStoreResidual();
   const algorithms::DeconvolutionAlgorithm& first =
       parallel_deconvolution_->FirstAlgorithm();

@@ -21,8 +21,8 @@ double ReferenceOf(const std::vector<double>& frequencies,
   return frequencies.empty() ? 0.0 : plain / double(frequencies.size());
 }
 
-// Pseudo-inverse of the m x p matrix a (row-major, m >= 1, p >= 1) by a
-// one-sided Jacobi SVD; returns p x m (row-major).
+}  // namespace
+
 std::vector<double> PseudoInverse(std::vector<double> a, size_t m, size_t p) {
   std::vector<double> v(p * p, 0.0);
   for (size_t j = 0; j != p; ++j) v[j * p + j] = 1.0;
@@ -78,7 +78,6 @@ std::vector<double> PseudoInverse(std::vector<double> a, size_t m, size_t p) {
   return pinv;
 }
 
-}  // namespace
 
 SpectralMaps MakeSpectralMaps(const schaapcommon::fitters::SpectralFitter& f) {
   SpectralMaps maps;

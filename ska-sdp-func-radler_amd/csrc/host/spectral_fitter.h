@@ -87,6 +87,11 @@ struct SpectralMaps {
 /// values below DBL_EPSILON of the largest are dropped).
 SpectralMaps MakeSpectralMaps(const schaapcommon::fitters::SpectralFitter& f);
 
+/// Pseudo-inverse of the m x p matrix a (row-major, m >= 1, p >= 1) by a
+/// one-sided Jacobi SVD, singular values below DBL_EPSILON of the largest
+/// dropped; returns p x m (row-major).
+std::vector<double> PseudoInverse(std::vector<double> a, size_t m, size_t p);
+
 /// The per-component map of DeconvolutionAlgorithm::PerformSpectralFit
 /// (deconvolution_algorithm.cc:29-46) over an image set of n_images =
 /// n_channels * n_pol images (index ch * n_pol + p): block-diagonal per

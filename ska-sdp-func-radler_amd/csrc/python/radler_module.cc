@@ -21,6 +21,7 @@
 #include "fft_sizes.h"
 #include "host_profile.h"
 #include "multiscale_transforms.h"
+#include "subminor.h"
 
 namespace py = pybind11;
 using AccessorList = std::vector<std::unique_ptr<aocommon::ImageAccessor>>;
@@ -572,6 +573,12 @@ void InitDistributed(py::module& m) {
 }
 
 void InitGpu(py::module& m) {
+  // utils::CalculateGoodFFTSize / GetConvolutionSize (fft_size_calculations.h:15-50)
+  py::module u = m.def_submodule("utils", "FFT size helpers (host)");
+  u.def("calculate_good_fft_size", &radler::utils::CalculateGoodFFTSize,
+        py::arg("minimum_size"));
+  u.def("get_convolution_size", &radler::utils::GetConvolutionSize, py::arg("scale"),
+        py::arg("original_size"), py::arg("padding"));
   py::module g = m.def_submodule("gpu", "MI355X device helpers (bench/tests)");
   g.def("set_verbosity", &radler::log::SetVerbosity);
   // RADLER_HOST_PROFILE=1 sections: {name: (count, total seconds)}
@@ -644,6 +651,79 @@ void InitGpu(py::module& m) {
         return out;
       },
       py::arg("model"), py::arg("residual"), py::arg("psf"));
+  g.def(
+      "linear_component_solve",
+      [](FloatArray model, FloatArray residual, FloatArray psf) {
+        // math::LinearComponentSolve(model, image, psf) (component_optimization.cc:258-263)
+        if (model.ndim() != 2) throw std::runtime_error("expected 2-D images");
+        const size_t h = model.shape(0), w = model.shape(1), n = w * h;
+        if (size_t(residual.size()) != n || size_t(psf.size()) != n)
+          throw std::runtime_error("image sizes differ");
+        std::shared_ptr<radler::gpu::Session> session =
+            radler::gpu::Session::ForDevice(radler::gpu::Session::DefaultDevice());
+        radler::gpu::Session& s = *session;
+        radler::gpu::Buffer dm(s, n * sizeof(float)), dr(s, n * sizeof(float)),
+            dp(s, n * sizeof(float));
+        s.H2D(dm.Ptr(), model.data(), n * sizeof(float));
+        s.H2D(dr.Ptr(), residual.data(), n * sizeof(float));
+        s.H2D(dp.Ptr(), psf.data(), n * sizeof(float));
+        radler::math::LinearComponentSolve(s, dm.F(), dr.F(), dp.F(), w, h);
+        py::array_t<float> out({h, w});
+        s.D2H(out.mutable_data(), dm.F(), n * sizeof(float));
+        return out;
+      },
+      py::arg("model"), py::arg("residual"), py::arg("psf"));
+  g.def(
+      "gradient_descent_with_variable_psf",
+      [](std::vector<std::vector<std::pair<size_t, size_t>>> components, FloatArray image,
+         std::vector<FloatArray> psfs, size_t padded_width, size_t padded_height) {
+        // math::GradientDescentWithVariablePsf (component_optimization.cc:323-402)
+        if (image.ndim() != 2) throw std::runtime_error("expected a 2-D image");
+        const size_t h = image.shape(0), w = image.shape(1), n = w * h;
+        if (psfs.size() != components.size())
+          throw std::runtime_error("one PSF per component list is required");
+        std::shared_ptr<radler::gpu::Session> session =
+            radler::gpu::Session::ForDevice(radler::gpu::Session::DefaultDevice());
+        radler::gpu::Session& s = *session;
+        if (!padded_width) padded_width = 2 * w;
+        if (!padded_height) padded_height = 2 * h;
+        radler::gpu::Buffer di(s, n * sizeof(float)), dp(s, n * sizeof(float));
+        s.H2D(di.Ptr(), image.data(), n * sizeof(float));
+        std::vector<std::shared_ptr<radler::gpu::Buffer>> spectra;
+        for (const FloatArray& p : psfs) {
+          if (size_t(p.size()) != n) throw std::runtime_error("image sizes differ");
+          s.H2D(dp.Ptr(), p.data(), n * sizeof(float));
+          spectra.push_back(radler::algorithms::SubMinorLoop::MakePaddedPsfSpectrum(
+              s, dp.F(), w, h, padded_width, padded_height));
+        }
+        std::vector<radler::gpu::Buffer> deltas = radler::math::GradientDescentWithVariablePsf(
+            s, components, di.F(), spectra, w, h, padded_width, padded_height);
+        py::list out;
+        for (const radler::gpu::Buffer& d : deltas) {
+          py::array_t<float> a({h, w});
+          s.D2H(a.mutable_data(), d.F(), n * sizeof(float));
+          out.append(a);
+        }
+        return out;
+      },
+      py::arg("components"), py::arg("image"), py::arg("psfs"), py::arg("padded_width") = 0,
+      py::arg("padded_height") = 0);
+  g.def(
+      "make_rms_factor_image",
+      [](FloatArray rms, double strength) {
+        // math::rms_image::MakeRmsFactorImage (rms_image.cc:95-125)
+        const size_t n = rms.size();
+        std::shared_ptr<radler::gpu::Session> session =
+            radler::gpu::Session::ForDevice(radler::gpu::Session::DefaultDevice());
+        radler::gpu::Session& s = *session;
+        radler::gpu::Buffer d(s, std::max<size_t>(n, 1) * sizeof(float));
+        s.H2D(d.Ptr(), rms.data(), n * sizeof(float));
+        const double lowest = radler::math::rms_image::MakeRmsFactorImage(s, d.F(), n, strength);
+        py::array_t<float> out(n);
+        s.D2H(out.mutable_data(), d.F(), n * sizeof(float));
+        return py::make_tuple(out, lowest);
+      },
+      py::arg("rms"), py::arg("strength"));
   g.def(
       "ms_full_component_fitter",
       [](FloatArray residual, FloatArray model, FloatArray psf, std::vector<float> scales,
@@ -727,6 +807,84 @@ void InitGpu(py::module& m) {
         return total;
       },
       py::arg("radler"));
+  // The device-resident ImageSet (cpp/image_set.h) for the restated
+  // cpp/test/test_image_set.cc: planes set/read through host copies, the
+  // integrations and averaging run on the device.
+  struct PyImageSet {
+    std::shared_ptr<radler::gpu::Session> session;
+    std::unique_ptr<radler::ImageSet> set;
+    py::array_t<float> Plane(const float* d) const {
+      py::array_t<float> out({py::ssize_t(set->Height()), py::ssize_t(set->Width())});
+      session->D2H(out.mutable_data(), d, set->PlaneSize() * sizeof(float));
+      return out;
+    }
+  };
+  py::class_<PyImageSet>(g, "ImageSet")
+      .def(py::init([](const radler::WorkTable& table, bool squared_joins,
+                       const std::set<aocommon::PolarizationEnum>& linked, size_t width,
+                       size_t height) {
+             auto p = std::make_unique<PyImageSet>();
+             p->session = radler::gpu::Session::ForDevice(radler::gpu::Session::DefaultDevice());
+             p->set = std::make_unique<radler::ImageSet>(table, squared_joins, linked, width,
+                                                         height, *p->session);
+             return p;
+           }),
+           py::arg("work_table"), py::arg("squared_joins"), py::arg("linked_polarizations"),
+           py::arg("width"), py::arg("height"), py::keep_alive<1, 2>())
+      .def_property_readonly("n_original_channels",
+                             [](const PyImageSet& s) { return s.set->NOriginalChannels(); })
+      .def_property_readonly("n_deconvolution_channels",
+                             [](const PyImageSet& s) { return s.set->NDeconvolutionChannels(); })
+      .def_property_readonly("psf_count", [](const PyImageSet& s) { return s.set->PsfCount(); })
+      .def_property_readonly("square_joined_channels",
+                             [](const PyImageSet& s) { return s.set->SquareJoinedChannels(); })
+      .def("__len__", [](const PyImageSet& s) { return s.set->Size(); })
+      .def("psf_index", [](const PyImageSet& s, size_t i) { return s.set->PsfIndex(i); })
+      .def("fill_zero", [](PyImageSet& s) { s.set->Fill(0.0f); })
+      .def("set_image",
+           [](PyImageSet& s, size_t i, FloatArray image) {
+             if (i >= s.set->Size() || size_t(image.size()) != s.set->PlaneSize())
+               throw std::out_of_range("set_image: index or size out of range");
+             s.session->H2D(s.set->Data(i), image.data(), s.set->PlaneSize() * sizeof(float));
+           })
+      .def("image", [](const PyImageSet& s, size_t i) {
+        if (i >= s.set->Size()) throw std::out_of_range("image index out of range");
+        return s.Plane(s.set->Data(i));
+      })
+      .def("linear_integrated", [](const PyImageSet& s) {
+        radler::gpu::Buffer d(*s.session, s.set->PlaneSize() * sizeof(float));
+        s.set->GetLinearIntegrated(d.F());
+        return s.Plane(d.F());
+      })
+      .def("square_integrated", [](const PyImageSet& s) {
+        radler::gpu::Buffer d(*s.session, s.set->PlaneSize() * sizeof(float));
+        s.set->GetSquareIntegrated(d.F());
+        return s.Plane(d.F());
+      })
+      .def("load_and_average", [](PyImageSet& s, bool use_residual_images) {
+        s.set->LoadAndAverage(use_residual_images);
+      }, py::arg("use_residual_images"))
+      .def("load_and_average_psfs", [](const PyImageSet& s) {
+        // [psf index][deconvolution channel] -> 2-D arrays
+        py::list out;
+        for (const radler::gpu::Planes& planes : s.set->LoadAndAveragePsfs()) {
+          py::list channels;
+          for (size_t ch = 0; ch != planes.count; ++ch) {
+            py::array_t<float> a({py::ssize_t(planes.height), py::ssize_t(planes.width)});
+            s.session->D2H(a.mutable_data(), planes.Plane(ch),
+                           planes.PlaneSize() * sizeof(float));
+            channels.append(a);
+          }
+          out.append(channels);
+        }
+        return out;
+      })
+      .def("interpolate_and_store_model",
+           [](PyImageSet& s, const schaapcommon::fitters::SpectralFitter* fitter) {
+             s.set->InterpolateAndStoreModel(fitter);
+           },
+           py::arg("fitter") = nullptr)
+      .def("assign_and_store_residual", [](PyImageSet& s) { s.set->AssignAndStoreResidual(); });
   py::class_<radler::DeviceRun>(g, "DeviceRun")
       .def(py::init([](const radler::Settings& settings, FloatArray psf,
                        FloatArray residual, std::vector<double> weights,

@@ -235,6 +235,46 @@ class Oracle:
                                        counts.ctypes.data, float(padding), int(shape))
         return r, m
 
+    def linear_component_solve(self, model, image, psf):
+        """math::LinearComponentSolve(model, image, psf): returns the new model."""
+        m = np.ascontiguousarray(model, np.float32).copy()
+        i = np.ascontiguousarray(image, np.float32)
+        p = np.ascontiguousarray(psf, np.float32)
+        h, w = m.shape
+        L = self.lib
+        L.orc_linear_component_solve.argtypes = [C.c_void_p] * 3 + [C.c_uint64] * 2
+        L.orc_linear_component_solve.restype = None
+        L.orc_linear_component_solve(m.ctypes.data, i.ctypes.data, p.ctypes.data, w, h)
+        return m
+
+    def gradient_descent_variable_psf(self, components, image, psfs, pw=0, ph=0):
+        """math::GradientDescentWithVariablePsf (FFT convolutions) -> deltas."""
+        img = np.ascontiguousarray(image, np.float32)
+        h, w = img.shape
+        ps = np.ascontiguousarray(np.stack(psfs), np.float32)
+        pos = np.ascontiguousarray([c for l in components for xy in l for c in xy] or [0],
+                                   np.uint32)
+        counts = np.ascontiguousarray([len(l) for l in components], np.uint64)
+        out = np.zeros((len(psfs), h, w), np.float32)
+        L = self.lib
+        L.orc_gradient_descent_variable_psf.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64,
+                                                        C.c_void_p, C.c_void_p] + \
+            [C.c_uint64] * 4 + [C.c_void_p]
+        L.orc_gradient_descent_variable_psf.restype = None
+        L.orc_gradient_descent_variable_psf(pos.ctypes.data, counts.ctypes.data, len(psfs),
+                                            img.ctypes.data, ps.ctypes.data, w, h,
+                                            pw or 2 * w, ph or 2 * h, out.ctypes.data)
+        return list(out)
+
+    def make_rms_factor_image(self, rms, strength):
+        """math::rms_image::MakeRmsFactorImage -> (factor image, lowest rms)."""
+        r = np.ascontiguousarray(rms, np.float32).copy()
+        L = self.lib
+        L.orc_make_rms_factor_image.argtypes = [C.c_void_p, C.c_uint64, C.c_double]
+        L.orc_make_rms_factor_image.restype = C.c_double
+        lowest = L.orc_make_rms_factor_image(r.ctypes.data, r.size, float(strength))
+        return r, lowest
+
     def padded_convolution(self, image, psf, pw, ph):
         img = np.ascontiguousarray(image, np.float32).copy()
         p = np.ascontiguousarray(psf, np.float32)
@@ -289,10 +329,11 @@ class Oracle:
                                    of.ctypes.data, of.size, out.ctypes.data)
         return out
 
-    def integrate(self, images, weights=None, n_pol=1, pol_factor=1.0, square=False):
+    def integrate(self, images, weights=None, n_pol=1, pol_factor=1.0, square=False,
+                  squared_joins=False):
         images = np.ascontiguousarray(images, np.float32)
         n, h, w = images.shape
-        d = self.set_desc(w, h, n // n_pol, n_pol, weights, pol_factor)
+        d = self.set_desc(w, h, n // n_pol, n_pol, weights, pol_factor, squared_joins)
         out = np.zeros((h, w), np.float32)
         self.lib.orc_integrate(C.byref(d), images, out, int(square))
         return out
@@ -358,6 +399,24 @@ class OracleAlgorithm:
         m, v = np.zeros(n, np.float32), np.zeros(n, np.float32)
         L.orc_algo_margins(self.h, m.ctypes.data, v.ctypes.data, n)
         return m, v
+
+    def set_clean_threads(self, n, after, stop=0):
+        """Switch the multiscale outer loop to n threads after `after` outer
+        iterations (n = 0: never) and stop after `stop` (0: never)."""
+        L = self.o.lib
+        L.orc_algo_set_clean_threads.restype = None
+        L.orc_algo_set_clean_threads.argtypes = [C.c_void_p] + [C.c_uint64] * 3
+        L.orc_algo_set_clean_threads(self.h, int(n), int(after), int(stop))
+
+    def switch_info(self):
+        """(seconds after the setup, components cleaned) at the thread switch."""
+        L = self.o.lib
+        L.orc_algo_switch_info.restype = None
+        L.orc_algo_switch_info.argtypes = [C.c_void_p, C.POINTER(C.c_double),
+                                           C.POINTER(C.c_uint64)]
+        s, n = C.c_double(), C.c_uint64()
+        L.orc_algo_switch_info(self.h, C.byref(s), C.byref(n))
+        return s.value, int(n.value)
 
     def setup_seconds(self):
         """Wall seconds of the last multiscale execute's setup (scale-convolved
