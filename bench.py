@@ -139,6 +139,17 @@ def affinity_cores():
         return os.cpu_count() or 1
 
 
+def cpu_share():
+    """Threads for the CPU baseline: the job's CPU share (OMP_NUM_THREADS, 16
+    per GPU on the pool's boxes, where the affinity mask shows the whole
+    machine), else the affinity core count."""
+    try:
+        n = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        n = 0
+    return min(n, affinity_cores()) if n > 0 else affinity_cores()
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -236,9 +247,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=["fields", "tiled"], default=None,
+    ap.add_argument("--workload", choices=["fields", "tiled", "joined"], default=None,
                     help="default: fields at N = 1, tiled at N > 1")
-    ap.add_argument("--size", type=int, default=8192)
+    ap.add_argument("--size", type=int, default=None,
+                    help="image side (default 8192; joined: 4096, SURVEY.md C3)")
+    ap.add_argument("--channels", type=int, default=8, help="joined: channels")
     ap.add_argument("--grid", type=int, default=8, help="tiled: subimages per axis")
     ap.add_argument("--pool", type=int, default=8,
                     help="tiled: subimages in flight per GPU (settings.parallel.max_threads)")
@@ -253,10 +266,12 @@ def main():
                     help="multiscale outer iterations of the CPU baseline on all threads "
                          "(0 = skip the CPU baseline)")
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="threads of the all-cores CPU run (0: the affinity core count)")
-    ap.add_argument("--cpu-single-thread", type=int, default=1,
+                    help="threads of the all-cores CPU run (0: OMP_NUM_THREADS, else the "
+                         "affinity core count)")
+    ap.add_argument("--cpu-single-thread", type=int, default=0,
                     help="outer iterations of the CPU baseline on one thread after the "
-                         "all-threads ones (0 = skip)")
+                         "all-threads ones (0 = skip; one 8192^2 outer iteration on one "
+                         "thread takes minutes, so it is a separate measurement)")
     ap.add_argument("--breakdown", action="store_true", help="per-kernel times to stderr")
     ap.add_argument("--timing-all", action="store_true",
                     help="count every launch of the process (PMC passes, tools/pmc_traffic.py)")
@@ -272,6 +287,12 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     workload = args.workload or ("fields" if world == 1 else "tiled")
     tiled = workload == "tiled"
+    joined = workload == "joined"
+    if args.size is None:
+        args.size = 4096 if joined else 8192
+    # joined over N > 1 ranks: the image set (all channels) split into
+    # grid x grid subimages owned by the ranks, as tiled
+    split = tiled or (joined and world > 1)
     dist = None
     if world > 1:
         import torch
@@ -284,13 +305,24 @@ def main():
     import radler as rd
 
     threshold = args.sigma * NOISE
-    # tiled: every rank holds the same image (one field); fields: one per rank
-    psf, dirty = make_problem(args.size, SEED + (0 if tiled else rank), args.points,
-                              args.blobs)
+    extra = {}
+    if joined:
+        # one sky over 100-170 MHz (spectral index -0.7), one
+        # PSF per channel (FWHM ~ 1/nu), weights 1, 8 deconvolution channels
+        from config_problems import joined_channels
+        freqs = [100e6 + 10e6 * i for i in range(args.channels)]
+        psf, dirty = joined_channels(args.size, args.points, args.blobs, SEED, freqs)
+        extra = dict(n_deconvolution_groups=args.channels,
+                     frequencies=np.array([[f, f] for f in freqs], np.float64),
+                     weights=np.ones(args.channels, np.float64))
+    else:
+        # tiled: every rank holds the same image (one field); fields: one per rank
+        psf, dirty = make_problem(args.size, SEED + (0 if tiled else rank), args.points,
+                                  args.blobs)
     s = settings_for(rd, args.size, args.max_iter, args.scales, threshold,
-                     args.grid if tiled else 1, args.pool if tiled else 1)
+                     args.grid if split else 1, args.pool if split else 1)
     comm = None
-    if tiled and dist is not None:
+    if split and dist is not None:
         # RCCL communicator of the product (rdl_comm_*), id from rank 0
         import torch
         idl = torch.zeros(rd.distributed.rccl_id_size(), dtype=torch.uint8, device="cuda")
@@ -304,7 +336,7 @@ def main():
     def make_radler():
         # the accessors borrow these arrays (cpp/radler.h:38-40)
         arrays = (psf, dirty.copy(), np.zeros_like(dirty))
-        r = rd.Radler(s, *arrays, BEAM_PX * PIXEL_SCALE)
+        r = rd.Radler(s, *arrays, BEAM_PX * PIXEL_SCALE, **extra)
         if comm is not None:
             r.set_communicator(comm)
         return r, arrays
@@ -345,8 +377,9 @@ def main():
 
     # the same major iteration on an HBM-resident image set (no host transfers)
     resident = None
-    if args.device_resident and not tiled:
-        run = rd.gpu.DeviceRun(s, psf, dirty, [], BEAM_PX * PIXEL_SCALE)
+    if args.device_resident and not split:
+        run = rd.gpu.DeviceRun(s, psf, dirty, [1.0] * args.channels if joined else [],
+                               BEAM_PX * PIXEL_SCALE)
         run.restore()
         run.execute()  # warm-up
         run.sync()
@@ -372,7 +405,7 @@ def main():
         t = torch.tensor([vals[0], vals[2]], dtype=torch.float64, device="cuda")
         c = torch.tensor([vals[1], vals[3]], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        if not tiled:  # tiled: every rank reports the whole job's components
+        if not split:  # split: every rank reports the whole job's components
             dist.all_reduce(c, op=dist.ReduceOp.SUM)
         max_elapsed, total_comps = float(t[0].item()), int(c[0].item())
         if resident:
@@ -411,12 +444,13 @@ def main():
               f"{1e3 * elapsed:.1f} ms wall", file=sys.stderr)
 
     cpu = None
-    if args.cpu_outer > 0 and world == 1 and not tiled:
-        threads = args.cpu_threads or affinity_cores()
+    if args.cpu_outer > 0 and world == 1 and workload == "fields":
+        threads = args.cpu_threads or cpu_share()
         cpu = cpu_baseline(psf, dirty, args.scales, threshold, threads, args.cpu_outer,
                            args.cpu_single_thread if threads > 1 else 0)
 
-    grid = f"-tiled{args.grid}x{args.grid}" if tiled else ""
+    grid = f"-tiled{args.grid}x{args.grid}" if split else ""
+    chans = f"joined{args.channels}ch-" if joined else ""
     line = {
         "metric": "CLEAN components/sec (multiscale, to 5-sigma threshold)",
         "value": round(total_comps / max_elapsed, 2),
@@ -426,20 +460,22 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 2),
         "wall_clock_to_threshold_s": round(max_elapsed / args.steps, 4),
-        "components_per_step": total_comps // (args.steps * (1 if tiled else world)),
+        "components_per_step": total_comps // (args.steps * (1 if split else world)),
         "higher_is_better": True,
-        "scaling": "strong" if tiled else "weak",
+        "scaling": "strong" if split else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (seeded sky: points + Gaussian blobs, analytic PSF, noise)",
-        "config": {"workload": f"multiscale-{args.size}x{args.size}-{args.scales}scales{grid}",
+        "config": {"workload": (f"{chans}multiscale-{args.size}x{args.size}-"
+                                f"{args.scales}scales{grid}"),
                    "step": "Radler.perform (accessor load + major iteration + store)",
                    "image": [args.size, args.size], "scales": args.scales,
                    "points": args.points, "blobs": args.blobs, "noise": NOISE,
                    "threshold": threshold, "minor_loop_gain": 0.1, "major_loop_gain": 1.0,
-                   "fields_per_gpu": 0 if tiled else 1,
+                   "channels": args.channels if joined else 1,
+                   "fields_per_gpu": 0 if split else 1,
                    "parallelism": (f"subimages{args.grid * args.grid}/ranks{world}"
-                                   f"/pool{args.pool}" if tiled else f"fields{world}")},
+                                   f"/pool{args.pool}" if split else f"fields{world}")},
         "device_resident": resident,
         "roofline": roofline,
         "cpu_baseline": cpu,

@@ -64,6 +64,12 @@ int rdl_memcpy_h2d(rdl_session* s, void* d_dst, const void* h_src, size_t bytes)
 int rdl_memcpy_d2h(rdl_session* s, void* h_dst, const void* d_src, size_t bytes);
 int rdl_memcpy_d2d(rdl_session* s, void* d_dst, const void* d_src, size_t bytes);
 int rdl_memset_zero(rdl_session* s, void* d_dst, size_t bytes);
+/* Page-locked host memory (hipHostMalloc) for the accessor staging of
+ * ImageSet::LoadAndAverage / Store (cpp/image_set.cc:105-140, 290-307):
+ * copies from it run at the link rate instead of through pageable bounce
+ * buffers. */
+int rdl_host_alloc(size_t bytes, void** h_out);
+int rdl_host_free(void* h_ptr);
 /* Device-to-device copy between GPUs (xGMI peer copy when the devices
  * differ), ordered on the session's stream. */
 int rdl_memcpy_peer(rdl_session* s, void* d_dst, int dst_device,

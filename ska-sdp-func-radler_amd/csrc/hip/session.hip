@@ -227,6 +227,18 @@ int rdl_memcpy_d2h(rdl_session* s, void* h_dst, const void* d_src,
   return RDL_OK;
 }
 
+int rdl_host_alloc(size_t bytes, void** h_out) {
+  RDL_ARG_CHECK(h_out, "NULL argument");
+  *h_out = nullptr;
+  RDL_HIP_CHECK(hipHostMalloc(h_out, std::max<size_t>(bytes, 64), hipHostMallocDefault));
+  return RDL_OK;
+}
+
+int rdl_host_free(void* h_ptr) {
+  if (h_ptr) RDL_HIP_CHECK(hipHostFree(h_ptr));
+  return RDL_OK;
+}
+
 int rdl_memcpy_d2d(rdl_session* s, void* d_dst, const void* d_src,
                    size_t bytes) {
   RDL_ARG_CHECK(s, "NULL session");

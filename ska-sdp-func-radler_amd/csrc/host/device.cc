@@ -202,6 +202,7 @@ Session::~Session() {
   ffts_.clear();
   for (Buffer& b : scratch_) b = Buffer();
   if (subminor_) rdl_subminor_destroy(subminor_);
+  if (pinned_) rdl_host_free(pinned_);
   rdl_session_destroy(s_);
 }
 
@@ -218,6 +219,18 @@ Fft& Session::GetFft(size_t width, size_t height, bool f64) {
 Buffer& Session::Scratch(ScratchSlot slot, size_t bytes) {
   scratch_[slot].Resize(*this, bytes);
   return scratch_[slot];
+}
+
+void* Session::PinnedStaging(size_t bytes) {
+  if (bytes > pinned_bytes_) {
+    prof::Section p("gpu.host_alloc");
+    if (pinned_) Check(rdl_host_free(pinned_), "rdl_host_free");
+    pinned_ = nullptr;
+    pinned_bytes_ = 0;
+    Check(rdl_host_alloc(bytes, &pinned_), "rdl_host_alloc");
+    pinned_bytes_ = bytes;
+  }
+  return pinned_;
 }
 
 rdl_subminor* Session::SharedSubminor() {
@@ -259,15 +272,28 @@ float Session::ReadFloat(const float* d) {
 }
 
 std::shared_ptr<Session> Session::ForDevice(int device) {
+  // One session per GPU for the life of the process: its FFT plans, kernel
+  // spectra scratch and sub-minor state outlive the Radler objects, so
+  // consecutive Perform calls (WSClean creates a Radler per run) do not
+  // re-plan or re-allocate. Intentionally never destroyed: the HIP runtime
+  // releases the device at exit, after static destructors would have run.
   static std::mutex mutex;
-  static std::map<int, std::weak_ptr<Session>> sessions;
+  static auto* sessions = new std::map<int, std::shared_ptr<Session>>();
   std::lock_guard<std::mutex> lock(mutex);
-  auto it = sessions.find(device);
-  if (it != sessions.end())
-    if (auto s = it->second.lock()) return s;
+  auto it = sessions->find(device);
+  if (it != sessions->end()) return it->second;
   auto s = std::make_shared<Session>(device);
-  sessions[device] = s;
+  (*sessions)[device] = s;
   return s;
+}
+
+std::shared_ptr<Session> Session::Worker(int device, size_t index) {
+  static std::mutex mutex;
+  static auto* workers = new std::map<std::pair<int, size_t>, std::shared_ptr<Session>>();
+  std::lock_guard<std::mutex> lock(mutex);
+  auto& w = (*workers)[{device, index}];
+  if (!w) w = std::make_shared<Session>(device);
+  return w;
 }
 
 int Session::DefaultDevice() {

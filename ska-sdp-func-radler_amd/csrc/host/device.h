@@ -130,9 +130,13 @@ class Session {
     kCorrectionModel = 0,
     kCorrectionSpectrum,
     kCorrectionRows,
+    kStaging,  // device side of the accessor staging (ImageSet loads)
     kNumScratch
   };
   Buffer& Scratch(ScratchSlot slot, size_t bytes);
+  /// Grow-only page-locked host buffer for accessor loads/stores (one per
+  /// session: the loads and stores of a Perform are sequential).
+  void* PinnedStaging(size_t bytes);
   /// The session's sub-minor loop state (selection, model values), reused by
   /// consecutive SubMinorLoop objects.
   rdl_subminor* SharedSubminor();
@@ -140,6 +144,9 @@ class Session {
   /// Process-wide session for a device (one per GPU, shared by the Radler
   /// objects of this process).
   static std::shared_ptr<Session> ForDevice(int device);
+  /// Process-wide worker session `index` on a device (a subimage pool's
+  /// streams), kept with its FFT plans across Radler objects.
+  static std::shared_ptr<Session> Worker(int device, size_t index);
   /// The device a Radler instance uses when Settings::gpu_device == -1.
   static int DefaultDevice();
 
@@ -149,6 +156,8 @@ class Session {
   std::map<std::tuple<size_t, size_t, bool>, std::unique_ptr<Fft>> ffts_;
   Buffer scratch_[kNumScratch];
   rdl_subminor* subminor_ = nullptr;
+  void* pinned_ = nullptr;
+  size_t pinned_bytes_ = 0;
 };
 
 /// A stack of `count` planes of width x height floats, contiguous.

@@ -192,13 +192,13 @@ void ImageSet::GetIntegratedPsf(float* d_dest, const gpu::Planes& psfs) const {
 
 void ImageSet::LoadAndAverage(bool use_residual_images) {
   // image_set.cc:105-140: sum of weight*image per deconvolution channel and
-  // polarization, then *= 1/sum(weights). Accessor loads go through one
-  // host staging buffer; the arithmetic runs on the device.
+  // polarization, then *= 1/sum(weights). Accessor loads go through the
+  // session's page-locked staging buffer; the arithmetic runs on the device.
   rdl_session* s = session_->Handle();
   planes_.buffer->Zero();
   const size_t n = PlaneSize();
-  std::vector<float> host(n);
-  gpu::Buffer staging(*session_, n * sizeof(float));
+  float* host = static_cast<float*>(session_->PinnedStaging(n * sizeof(float)));
+  gpu::Buffer& staging = session_->Scratch(gpu::Session::kStaging, n * sizeof(float));
   std::vector<double> averaged_weights(n_images_, 0.0);
   size_t image_index = 0;
   for (const std::vector<size_t>& group : table_.DeconvolutionGroups()) {
@@ -217,9 +217,9 @@ void ImageSet::LoadAndAverage(bool use_residual_images) {
         const aocommon::ImageAccessor& acc = *acc_ptr;
         if (acc.Width() != width_ || acc.Height() != height_)
           throw std::runtime_error("ImageSet: accessor size mismatch");
-        acc.Load(host.data());
+        acc.Load(host);
         if (e->image_weight != 0.0) {
-          session_->H2D(staging.Ptr(), host.data(), n * sizeof(float));
+          session_->H2D(staging.Ptr(), host, n * sizeof(float));
           // AddWithFactor into a zeroed plane
           gpu::Check(rdl_axpy(s, Data(image_index), staging.F(), n,
                               float(e->image_weight), 0),
@@ -248,15 +248,15 @@ std::vector<gpu::Planes> ImageSet::LoadAndAveragePsfs() const {
     gpu::Planes planes =
         gpu::Planes::Make(*session_, pw, ph, NDeconvolutionChannels());
     planes.buffer->Zero();
-    std::vector<float> host(n);
-    gpu::Buffer staging(*session_, n * sizeof(float));
+    float* host = static_cast<float*>(session_->PinnedStaging(n * sizeof(float)));
+    gpu::Buffer& staging = session_->Scratch(gpu::Session::kStaging, n * sizeof(float));
     std::vector<double> averaged(NDeconvolutionChannels(), 0.0);
     for (size_t g = 0; g != NOriginalChannels(); ++g) {
       const size_t ch = (g * NDeconvolutionChannels()) / NOriginalChannels();
       const WorkTableEntry& e = *table_.OriginalGroups()[g].front();
       const aocommon::ImageAccessor& acc = *e.psf_accessors[psf_index];
-      acc.Load(host.data());
-      session_->H2D(staging.Ptr(), host.data(), n * sizeof(float));
+      acc.Load(host);
+      session_->H2D(staging.Ptr(), host, n * sizeof(float));
       gpu::Check(rdl_axpy_f64(s, planes.Plane(ch), staging.F(), n,
                               e.image_weight, 0),
                  "rdl_axpy_f64");
@@ -274,15 +274,15 @@ std::vector<gpu::Planes> ImageSet::LoadAndAveragePsfs() const {
 }
 
 void ImageSet::AssignAndStoreResidual() {  // image_set.cc:290-307
-  std::vector<float> host(PlaneSize());
+  float* host = static_cast<float*>(session_->PinnedStaging(PlaneSize() * sizeof(float)));
   size_t image_index = 0;
   for (const std::vector<size_t>& group : table_.DeconvolutionGroups()) {
     const size_t start = image_index;
     for (const size_t original_index : group) {
       image_index = start;
       for (const WorkTableEntry* e : table_.OriginalGroups()[original_index]) {
-        session_->D2H(host.data(), Data(image_index), PlaneSize() * sizeof(float));
-        e->residual_accessor->Store(host.data());
+        session_->D2H(host, Data(image_index), PlaneSize() * sizeof(float));
+        e->residual_accessor->Store(host);
         ++image_index;
       }
     }
@@ -292,12 +292,12 @@ void ImageSet::AssignAndStoreResidual() {  // image_set.cc:290-307
 void ImageSet::InterpolateAndStoreModel(
     const schaapcommon::fitters::SpectralFitter* fitter) {
   // image_set.cc:209-288
-  std::vector<float> host(PlaneSize());
+  float* host = static_cast<float*>(session_->PinnedStaging(PlaneSize() * sizeof(float)));
   if (NDeconvolutionChannels() == NOriginalChannels()) {
     size_t image_index = 0;
     for (const WorkTableEntry& e : table_) {
-      session_->D2H(host.data(), Data(image_index), PlaneSize() * sizeof(float));
-      e.model_accessor->Store(host.data());
+      session_->D2H(host, Data(image_index), PlaneSize() * sizeof(float));
+      e.model_accessor->Store(host);
       ++image_index;
     }
     return;
@@ -310,8 +310,8 @@ void ImageSet::InterpolateAndStoreModel(
       const size_t ch = (g * NDeconvolutionChannels()) / NOriginalChannels();
       const WorkTable::Group& group = table_.OriginalGroups()[g];
       for (size_t p = 0; p != group.size(); ++p) {
-        session_->D2H(host.data(), Data(ch * n_pol_ + p), PlaneSize() * sizeof(float));
-        group[p]->model_accessor->Store(host.data());
+        session_->D2H(host, Data(ch * n_pol_ + p), PlaneSize() * sizeof(float));
+        group[p]->model_accessor->Store(host);
       }
     }
     return;
@@ -338,9 +338,9 @@ void ImageSet::InterpolateAndStoreModel(
                                           uint32_t(n_out), out.F(), PlaneSize()),
                  "rdl_spectral_interpolate");
       for (size_t g = g0; g != g0 + n_out; ++g) {
-        session_->D2H(host.data(), out.F() + (g - g0) * PlaneSize(),
+        session_->D2H(host, out.F() + (g - g0) * PlaneSize(),
                       PlaneSize() * sizeof(float));
-        table_.OriginalGroups()[g][p]->model_accessor->Store(host.data());
+        table_.OriginalGroups()[g][p]->model_accessor->Store(host);
       }
     }
   }

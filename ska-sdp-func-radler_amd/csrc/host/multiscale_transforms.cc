@@ -103,7 +103,24 @@ MultiScaleTransforms::MultiScaleTransforms(gpu::Session& s, size_t width,
       shape_(shape),
       pw_(width),
       ph_(height),
-      fft_(&s.GetFft(width, height)) {}
+      fft_(nullptr) {}
+
+namespace {
+// A coarse ladder of FFT-friendly plane sides for the periodically extended
+// transforms: subimages of slightly different sizes (Dijkstra boundaries)
+// then share a few FFT plans instead of planning one per subimage.
+size_t CanonicalFftSize(size_t n) {
+  const size_t step = n > 2048 ? 512 : n > 1024 ? 256 : n > 256 ? 64 : 2;
+  size_t m = (n + step - 1) / step * step;
+  while (utils::CalculateGoodFFTSize(m) != m) m += step;
+  return m;
+}
+}  // namespace
+
+gpu::Fft& MultiScaleTransforms::TheFft() {
+  if (!fft_) Plan(radius_);
+  return *fft_;
+}
 
 size_t MultiScaleTransforms::KernelRadius(float scale) const {
   size_t n;
@@ -116,11 +133,11 @@ void MultiScaleTransforms::Plan(size_t radius) {
                         utils::CalculateGoodFFTSize(height_) == height_;
   size_t pw = width_, ph = height_;
   if (!friendly && radius < width_ && radius < height_) {
-    pw = std::max(width_, utils::CalculateGoodFFTSize(width_ + 2 * radius));
-    ph = std::max(height_, utils::CalculateGoodFFTSize(height_ + 2 * radius));
+    pw = std::max(width_, CanonicalFftSize(width_ + 2 * radius));
+    ph = std::max(height_, CanonicalFftSize(height_ + 2 * radius));
   }
   radius_ = radius;
-  if (pw == pw_ && ph == ph_) return;
+  if (fft_ && pw == pw_ && ph == ph_) return;
   pw_ = pw;
   ph_ = ph;
   fft_ = &s_.GetFft(pw_, ph_);
@@ -130,7 +147,7 @@ void MultiScaleTransforms::Plan(size_t radius) {
 
 void MultiScaleTransforms::SetMaxScale(float scale) {
   const size_t r = KernelRadius(scale);
-  if (r > radius_ || pw_ == width_) Plan(r);
+  if (!fft_ || r > radius_ || pw_ == width_) Plan(r);
 }
 
 float* MultiScaleTransforms::Plane() {
@@ -146,6 +163,7 @@ void MultiScaleTransforms::Crop(float* d_out) {
 }
 
 const void* MultiScaleTransforms::KernelSpectrum(float scale) {
+  TheFft();
   if (Extended() && KernelRadius(scale) > radius_) Plan(KernelRadius(scale));
   auto it = spectra_.find(scale);
   if (it != spectra_.end()) return it->second->Ptr();
@@ -194,6 +212,7 @@ void MultiScaleTransforms::Transform(float* d_image, float scale) {
 }
 
 void MultiScaleTransforms::Forward(const float* d_image, void* d_spectrum) {
+  TheFft();
   if (!Extended()) {
     fft_->Forward(d_image, d_spectrum);
     return;

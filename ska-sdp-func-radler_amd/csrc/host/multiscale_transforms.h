@@ -33,7 +33,7 @@ class MultiScaleTransforms {
   /// FFT plane size (W x H, or the extended plane).
   size_t PlaneWidth() const { return pw_; }
   size_t PlaneHeight() const { return ph_; }
-  size_t SpectrumBytes() const { return fft_->SpectrumBytes(); }
+  size_t SpectrumBytes() { return TheFft().SpectrumBytes(); }
 
   /// Spectrum of the scale kernel placed at the origin of the plane (cached).
   const void* KernelSpectrum(float scale);
@@ -57,6 +57,9 @@ class MultiScaleTransforms {
 
  private:
   bool Extended() const { return pw_ != width_ || ph_ != height_; }
+  /// The plane's FFT, planned on first use (an unfriendly W x H is never
+  /// planned itself: its transforms run in the extended plane).
+  gpu::Fft& TheFft();
   size_t KernelRadius(float scale) const;
   void Plan(size_t radius);
   float* Plane();

@@ -580,7 +580,7 @@ void ParallelDeconvolution::EnsureWorkers(gpu::Session& main, size_t n) {
   std::map<int, size_t> per_device;
   for (size_t w = 0; w != n; ++w) {
     const int d = devices[w % devices.size()];
-    workers_.push_back(std::make_unique<gpu::Session>(d));
+    workers_.push_back(gpu::Session::Worker(d, per_device[d]));
     ++per_device[d];
   }
   for (auto& w : workers_) w->SetConcurrency(per_device[w->Device()]);

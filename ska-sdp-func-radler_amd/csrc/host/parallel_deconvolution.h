@@ -135,7 +135,7 @@ class ParallelDeconvolution {
 
   // worker sessions (one stream each) outlive the algorithms, whose cached
   // transforms and scratch live on them
-  std::vector<std::unique_ptr<gpu::Session>> workers_;
+  std::vector<std::shared_ptr<gpu::Session>> workers_;
   int worker_main_device_ = -1;
   std::vector<std::unique_ptr<DeconvolutionAlgorithm>> algorithms_;
   std::vector<SubImage> subimages_;

@@ -42,7 +42,11 @@ SubMinorLoop::RunResult SubMinorLoop::Run(ImageSet& residual,
     cap = max_iterations_ > current_iteration_ ? max_iterations_ - current_iteration_ : 0;
     cap = std::min<uint64_t>(cap, uint64_t(1) << 22);
   }
-  std::vector<uint32_t> tr(2 * cap);
+  // grow-only per-thread trace buffer: a fresh (zeroed, page-faulting) 32 MB
+  // vector per outer iteration cost milliseconds of host time while the GPU
+  // idled; the device writes only the components it cleans
+  thread_local std::vector<uint32_t> tr;
+  if (tr.size() < 2 * cap) tr.resize(2 * cap);
   rdl_subminor_result r;
   gpu::Check(rdl_subminor_run(h_, residual.Base(), psfs.Base(), &p, &r,
                               cap ? tr.data() : nullptr, cap),
@@ -51,7 +55,7 @@ SubMinorLoop::RunResult SubMinorLoop::Run(ImageSet& residual,
   const size_t done = r.iteration - current_iteration_;
   current_iteration_ = r.iteration;
   flux_cleaned_ += r.flux_cleaned;
-  if (trace_)
+  if (trace_ && cap)
     trace_->insert(trace_->end(), tr.begin(),
                    tr.begin() + 2 * std::min<uint64_t>(done, cap));
   return {r.diverging != 0, r.has_peak != 0, r.peak};

@@ -64,6 +64,36 @@ def main():
         span = max(e for _, e in iv) - iv[0][0]
         print(f"\n# GPU busy {busy * 1e-9:.3f} s of {span * 1e-9:.3f} s span "
               f"({100.0 * busy / span:.1f} %), {len(iv)} intervals", file=out)
+        # idle gaps and the host API calls overlapping them: what the host was
+        # doing while the GPU had nothing to run
+        gaps = []
+        cur_e = iv[0][1]
+        for s_, e_ in iv[1:]:
+            if s_ > cur_e:
+                gaps.append((cur_e, s_))
+            cur_e = max(cur_e, e_)
+        total_gap = sum(b - a for a, b in gaps)
+        big = [g for g in gaps if g[1] - g[0] > 20000]
+        print(f"# idle gaps: {len(gaps)} totalling {total_gap * 1e-9:.3f} s; "
+              f"{len(big)} longer than 20 us totalling "
+              f"{sum(b - a for a, b in big) * 1e-9:.3f} s", file=out)
+        if "regions" in cols:
+            regs = sorted(c.execute("select name, start, end from regions").fetchall(),
+                          key=lambda r: r[1])
+            import bisect
+            starts = [r[1] for r in regs]
+            blame = defaultdict(int)
+            for a_, b_ in big:
+                i = max(0, bisect.bisect_left(starts, a_) - 2000)
+                while i < len(regs) and regs[i][1] < b_:
+                    n, rs, re_ = regs[i]
+                    ov = min(re_, b_) - max(rs, a_)
+                    if ov > 0:
+                        blame[n] += ov
+                    i += 1
+            print("# host API time overlapping the >20 us idle gaps", file=out)
+            for n, t in sorted(blame.items(), key=lambda kv: -kv[1])[:25]:
+                print(f"{n[:60]:60s} {t * 1e-6:11.2f} ms", file=out)
 
 
 if __name__ == "__main__":
