@@ -355,6 +355,8 @@ def main():
         r.perform(0)
         del r, arrays
     steps = [make_radler() for _ in range(args.steps)]
+    if os.environ.get("RADLER_HOST_PROFILE") == "1":
+        rd.gpu.host_profile_reset()  # the printed host profile covers the timed steps
 
     if not args.timing_all:
         timing.reset()

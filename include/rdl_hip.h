@@ -600,6 +600,10 @@ int rdl_comm_destroy(rdl_session* s);
  * cpp/algorithms/parallel_deconvolution.cc:592-603). */
 int rdl_comm_allreduce_max(rdl_session* s, float* value);
 int rdl_comm_allreduce_sum_u64(rdl_session* s, uint64_t* value);
+/* Element-wise max of n host floats over the ranks, in place (the
+ * per-subimage peaks of the find-peak pass, which every rank needs for the
+ * cost-ordered ownership of the cleaning pass). */
+int rdl_comm_allreduce_max_n(rdl_session* s, float* values, size_t n);
 /* In-place broadcast of a device buffer from `root`, stream ordered: the
  * owner rank's subimage residual/model boxes, which every rank then merges
  * in subimage order (ImageSet::CopyMasked / AddSubImage,

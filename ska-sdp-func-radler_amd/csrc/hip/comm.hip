@@ -67,6 +67,21 @@ int rdl_comm_allreduce_max(rdl_session* s, float* value) {
   return RDL_OK;
 }
 
+int rdl_comm_allreduce_max_n(rdl_session* s, float* values, size_t n) {
+  RDL_ARG_CHECK(s && values && s->comm, "communicator not initialised");
+  RDL_ARG_CHECK(n * sizeof(float) <= (1u << 16), "too many values");
+  if (n == 0) return RDL_OK;
+  float* d = static_cast<float*>(s->d_small);
+  RDL_HIP_CHECK(hipMemcpyAsync(d, values, n * sizeof(float), hipMemcpyHostToDevice,
+                               s->stream));
+  RDL_NCCL_CHECK(ncclAllReduce(d, d, n, ncclFloat32, ncclMax,
+                               static_cast<ncclComm_t>(s->comm), s->stream));
+  RDL_HIP_CHECK(hipMemcpyAsync(values, d, n * sizeof(float), hipMemcpyDeviceToHost,
+                               s->stream));
+  RDL_HIP_CHECK(hipStreamSynchronize(s->stream));
+  return RDL_OK;
+}
+
 int rdl_comm_allreduce_sum_u64(rdl_session* s, uint64_t* value) {
   RDL_ARG_CHECK(s && value && s->comm, "communicator not initialised");
   uint64_t* d = static_cast<uint64_t*>(s->d_small);

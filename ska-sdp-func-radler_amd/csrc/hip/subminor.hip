@@ -1302,9 +1302,14 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   uint64_t per = n_sel;
   bool use_reg = ni <= 8 && h->mode != 1;
   const uint64_t reg_cap = uint64_t(rdl::kRegThreads) * rdl::RegMaxItems(ni_t);
+  // the size limits count PSF gathers per iteration (pixels x images): with
+  // joined channels one workgroup's memory pipe, not the exchange, bounds an
+  // iteration (8 channels x 3000 pixels on one CU: 26 us per component)
+  const uint64_t work = n_sel * ni;
   if (use_reg) {
-    if (n_sel > std::min<uint64_t>(reg_cap, h->single_max)) {
-      const uint64_t target = std::max<uint32_t>(h->target_per_block, 512);
+    if (n_sel > reg_cap || work > h->single_max) {
+      const uint64_t target = std::max<uint64_t>(
+          std::max<uint32_t>(h->target_per_block, 512) / ni, 64);
       g = uint32_t(std::min<uint64_t>(max_blocks, (n_sel + target - 1) / target));
       g = std::max<uint32_t>(g, std::min<uint32_t>(2, max_blocks));
       per = (n_sel + g - 1) / g;
@@ -1319,7 +1324,7 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   const uint64_t wave_cap = 64ull * rdl::WaveMaxItems(ni_t);
   const bool use_wave =
       use_reg && g == 1 &&
-      ((h->mode == 0 && n_sel <= std::min<uint64_t>(wave_cap, h->wave_max)) ||
+      ((h->mode == 0 && n_sel <= wave_cap && work <= h->wave_max) ||
        (h->mode == 3 && n_sel <= wave_cap));
   if (h->mode == 3 && !use_wave) {
     rdl::SetError("single-wave sub-minor kernel cannot hold this selection");
@@ -1329,8 +1334,7 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   const uint64_t big_cap = 1024ull * (ni_t <= 2 ? 8 : 4);
   bool use_big =
       !use_wave && ni <= 8 && h->mode != 1 && h->mode != 2 &&
-      ((h->mode == 0 && n_sel <= std::min<uint64_t>(big_cap, h->big_max) &&
-        n_sel > 1024) ||
+      ((h->mode == 0 && n_sel <= big_cap && work <= h->big_max && work > 1024) ||
        (h->mode == 4 && n_sel <= big_cap));
   // 1024-thread workgroups on a cooperative grid (mode 5, target pixels per
   // workgroup from set_tuning; mode 0 when big_target is set)

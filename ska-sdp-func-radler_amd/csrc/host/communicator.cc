@@ -1,5 +1,6 @@
 #include "communicator.h"
 
+#include <algorithm>
 #include <stdexcept>
 #include <utility>
 #include <vector>
@@ -35,6 +36,12 @@ float RcclCommunicator::AllreduceMax(gpu::Session& s, float value) {
   return value;
 }
 
+void RcclCommunicator::AllreduceMax(gpu::Session& s, float* values, std::size_t n) {
+  if (&s != session_.get())
+    throw std::runtime_error("RcclCommunicator: collective on a foreign session");
+  gpu::Check(rdl_comm_allreduce_max_n(s.Handle(), values, n), "rdl_comm_allreduce_max_n");
+}
+
 void RcclCommunicator::Broadcast(gpu::Session& s, void* d_buffer, size_t bytes,
                                  int root) {
   if (&s != session_.get())
@@ -63,6 +70,24 @@ void HostCommunicator::Broadcast(gpu::Session& s, void* d_buffer, size_t bytes,
   if (rank_ == root) s.D2H(host.data(), d_buffer, bytes);  // synchronous
   broadcast_(host.data(), bytes, root);
   if (rank_ != root) s.H2D(d_buffer, host.data(), bytes);
+}
+
+std::vector<int> LptOwners(const std::vector<double>& costs, int n_ranks) {
+  std::vector<int> owners(costs.size(), 0);
+  if (n_ranks <= 1) return owners;
+  std::vector<std::size_t> order(costs.size());
+  for (std::size_t i = 0; i != order.size(); ++i) order[i] = i;
+  std::stable_sort(order.begin(), order.end(),
+                   [&](std::size_t a, std::size_t b) { return costs[a] > costs[b]; });
+  std::vector<double> load(std::size_t(n_ranks), 0.0);
+  for (std::size_t i : order) {
+    int best = 0;
+    for (int r = 1; r != n_ranks; ++r)
+      if (load[std::size_t(r)] < load[std::size_t(best)]) best = r;
+    owners[i] = best;
+    load[std::size_t(best)] += costs[i];
+  }
+  return owners;
 }
 
 }  // namespace radler

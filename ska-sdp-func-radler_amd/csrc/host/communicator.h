@@ -11,6 +11,7 @@
 #include <cstddef>
 #include <functional>
 #include <memory>
+#include <vector>
 
 namespace radler {
 namespace gpu {
@@ -24,6 +25,11 @@ class Communicator {
   virtual int Size() const = 0;
   /// Maximum of one float over all ranks (every rank gets the result).
   virtual float AllreduceMax(gpu::Session& s, float value) = 0;
+  /// Element-wise maximum of n floats over all ranks, in place (a rank
+  /// gathers the others' entries by leaving its unknown ones at lowest()).
+  virtual void AllreduceMax(gpu::Session& s, float* values, std::size_t n) {
+    for (std::size_t i = 0; i != n; ++i) values[i] = AllreduceMax(s, values[i]);
+  }
   /// In-place broadcast of `bytes` of device memory on `s`'s device from
   /// `root`. Returns with the data in place (stream ordered on `s`).
   virtual void Broadcast(gpu::Session& s, void* d_buffer, size_t bytes, int root) = 0;
@@ -40,6 +46,7 @@ class RcclCommunicator final : public Communicator {
   int Rank() const override { return rank_; }
   int Size() const override { return size_; }
   float AllreduceMax(gpu::Session& s, float value) override;
+  void AllreduceMax(gpu::Session& s, float* values, std::size_t n) override;
   void Broadcast(gpu::Session& s, void* d_buffer, size_t bytes, int root) override;
   /// A fresh RCCL unique id (rank 0 only), `IdSize()` bytes.
   static std::size_t IdSize();
@@ -75,10 +82,17 @@ class HostCommunicator final : public Communicator {
   MaxFn max_;
 };
 
-/// The rank that deconvolves subimage `index` of `n_subimages` (round robin:
+/// The rank that runs subimage `index` in the find-peak pass (round robin:
 /// every rank computes the same assignment, no exchange needed).
 inline int SubImageOwner(std::size_t index, int n_ranks) {
   return n_ranks <= 1 ? 0 : int(index % std::size_t(n_ranks));
 }
+
+/// Owners for the cleaning pass: longest-processing-time-first over the
+/// per-subimage cost estimates (every rank holds the same estimates after
+/// the find-peak exchange, so every rank computes the same assignment):
+/// subimages by decreasing cost (ties: lower index first) each go to the
+/// rank with the least assigned cost (ties: lower rank).
+std::vector<int> LptOwners(const std::vector<double>& costs, int n_ranks);
 
 }  // namespace radler

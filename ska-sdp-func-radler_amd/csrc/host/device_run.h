@@ -40,6 +40,7 @@ class DeviceRun {
   /// Outer-loop steps of the last IUWT major iteration (subimage `index`).
   std::vector<algorithms::IuwtDeconvolution::Step> IuwtSteps(size_t index = 0) const;
   /// Tiles of the last Execute (empty for a 1x1 grid).
+  const std::vector<int>& CleanOwners() const { return parallel_->CleanOwners(); }
   const std::vector<algorithms::SubImage>& SubImages() const {
     return parallel_->SubImages();
   }

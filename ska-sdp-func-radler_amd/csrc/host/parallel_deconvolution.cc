@@ -8,6 +8,8 @@
 #include <cmath>
 #include <cstdlib>
 #include <exception>
+#include <functional>
+#include <limits>
 #include <map>
 #include <stdexcept>
 #include <string>
@@ -592,7 +594,7 @@ void ParallelDeconvolution::RunSubImagesConcurrently(
     ImageSet& data_image, const ImageSet& model_image, ImageSet& result_model,
     const std::vector<gpu::Planes>& psf_images,
     const std::vector<size_t>& psf_indices, double major_iteration_threshold,
-    bool find_peak_only) {
+    bool find_peak_only, const std::vector<char>* run, const SubImageSink& sink) {
   // The reference runs RunSubImage on settings.parallel.max_threads threads
   // (parallel_deconvolution.cc:583-616), each trimming from the shared
   // residual and copying back under a mutex. Here every subimage trims from
@@ -622,12 +624,16 @@ void ParallelDeconvolution::RunSubImagesConcurrently(
     bool converging = false;
   };
   std::vector<Slot> slots(n_sub);
-  for (size_t i = 0; i != n_sub; ++i) {
+  std::vector<size_t> todo;  // the subimages this call runs, in index order
+  for (size_t i = 0; i != n_sub; ++i)
+    if (!run || (*run)[i]) todo.push_back(i);
+  for (size_t k = 0; k != todo.size(); ++k) {
+    const size_t i = todo[k];
     Slot& slot = slots[i];
     const SubImage& sub = subimages_[i];
     const size_t n = sub.width * sub.height;
     const gpu::Planes& psfs = psf_images[psf_indices[i]];
-    slot.ws = workers_[i % W].get();
+    slot.ws = workers_[k % W].get();
     slot.remote = force_staging || slot.ws->Device() != main_device;
     slot.boundary = std::make_unique<gpu::Buffer>(s, n);
     s.H2D(slot.boundary->Ptr(), MaskBytes(sub.boundary_mask).data(), n);
@@ -647,7 +653,8 @@ void ParallelDeconvolution::RunSubImagesConcurrently(
     try {
       gpu::Session& ws = *workers_[w];
       ws.Bind();
-      for (size_t i = w; i < n_sub; i += W) {
+      for (size_t k = w; k < todo.size(); k += W) {
+        const size_t i = todo[k];
         Slot& slot = slots[i];
         SubImage& sub = subimages_[i];
         const size_t sw = sub.width, sh = sub.height, n = sw * sh;
@@ -710,7 +717,7 @@ void ParallelDeconvolution::RunSubImagesConcurrently(
     if (e) std::rethrow_exception(e);
   if (find_peak_only) return;
 
-  for (size_t i = 0; i != n_sub; ++i) {
+  for (const size_t i : todo) {
     Slot& slot = slots[i];
     const SubImage& sub = subimages_[i];
     const size_t n = sub.width * sub.height;
@@ -723,9 +730,12 @@ void ParallelDeconvolution::RunSubImagesConcurrently(
       d_data = slot.data->Base();
       d_model = (slot.converging ? slot.model : slot.initial)->Base();
     }
-    MergeSubImage(s, sub, data_image, result_model, d_data, d_model,
-                  static_cast<const uint8_t*>(slot.boundary->Ptr()),
-                  slot.converging);
+    if (sink)
+      sink(i, d_data, d_model, slot.converging);
+    else
+      MergeSubImage(s, sub, data_image, result_model, d_data, d_model,
+                    static_cast<const uint8_t*>(slot.boundary->Ptr()),
+                    slot.converging);
   }
   s.Sync();
 }
@@ -757,9 +767,42 @@ double ParallelDeconvolution::RunSubImagesDistributed(
   constexpr size_t kHeaderFloats = sizeof(Record) / sizeof(float);
   std::vector<std::unique_ptr<gpu::Buffer>> packs(n_sub);
   std::vector<std::vector<std::vector<uint8_t>>> mask_sets(n_sub);
-  double local_peak = 0.0;
-  for (size_t i = 0; i != n_sub; ++i) {
-    if (SubImageOwner(i, n_ranks) != rank) continue;
+  const bool lpt = !find_peak_only && clean_owners_.size() == n_sub;
+  auto owner_of = [&](size_t i) {
+    return lpt ? clean_owners_[i] : SubImageOwner(i, n_ranks);
+  };
+  // a packed result: the record, then the residual and model boxes
+  auto pack_result = [&](size_t i, const float* d_data, const float* d_model,
+                         bool converging) {
+    SubImage& sub = subimages_[i];
+    const size_t n = sub.width * sub.height;
+    auto pack = std::make_unique<gpu::Buffer>(
+        s, (kHeaderFloats + 2 * n_img * n) * sizeof(float));
+    Record rec{};
+    rec.peak = sub.peak;
+    rec.iteration_number = algorithms_[i]->IterationNumber();
+    rec.reached_major_threshold = sub.reached_major_threshold ? 1u : 0u;
+    rec.converging = converging ? 1u : 0u;
+    if (track_masks_ && converging) {
+      mask_sets[i] = SubImageScaleMasks(sub);
+      rec.n_mask_scales = uint32_t(mask_sets[i].size());
+    }
+    s.H2D(pack->Ptr(), &rec, sizeof(rec));
+    float* base = pack->F() + kHeaderFloats;
+    s.D2D(base, d_data, n_img * n * sizeof(float));
+    s.D2D(base + n_img * n, d_model, n_img * n * sizeof(float));
+    packs[i] = std::move(pack);
+  };
+  if (!workers_.empty()) {
+    // this rank's subimages on its worker pool (concurrent streams)
+    std::vector<char> mine(n_sub, 0);
+    for (size_t i = 0; i != n_sub; ++i) mine[i] = owner_of(i) == rank ? 1 : 0;
+    RunSubImagesConcurrently(data_image, model_image, result_model, psf_images,
+                             psf_indices, major_iteration_threshold, find_peak_only,
+                             &mine, pack_result);
+  }
+  for (size_t i = 0; i != n_sub && workers_.empty(); ++i) {
+    if (owner_of(i) != rank) continue;
     SubImage& sub = subimages_[i];
     const size_t sw = sub.width, sh = sub.height, n = sw * sh;
     const gpu::Planes& psfs = psf_images[psf_indices[i]];
@@ -780,31 +823,36 @@ double ParallelDeconvolution::RunSubImagesDistributed(
     const bool converging = DeconvolveSubImage(sub, sub_data, sub_model, sub_psfs,
                                                major_iteration_threshold,
                                                find_peak_only);
-    if (find_peak_only) {
-      if (sub.peak > local_peak) local_peak = sub.peak;  // :592-599, from 0.0
-      continue;
-    }
-    auto pack = std::make_unique<gpu::Buffer>(
-        s, (kHeaderFloats + 2 * n_img * n) * sizeof(float));
-    Record rec{};
-    rec.peak = sub.peak;
-    rec.iteration_number = algorithms_[i]->IterationNumber();
-    rec.reached_major_threshold = sub.reached_major_threshold ? 1u : 0u;
-    rec.converging = converging ? 1u : 0u;
-    if (track_masks_ && converging) {
-      mask_sets[i] = SubImageScaleMasks(sub);
-      rec.n_mask_scales = uint32_t(mask_sets[i].size());
-    }
-    s.H2D(pack->Ptr(), &rec, sizeof(rec));
-    float* base = pack->F() + kHeaderFloats;
-    s.D2D(base, sub_data.Base(), n_img * n * sizeof(float));
-    s.D2D(base + n_img * n, (converging ? sub_model : *initial).Base(),
-          n_img * n * sizeof(float));
-    packs[i] = std::move(pack);
+    if (find_peak_only) continue;
+    pack_result(i, sub_data.Base(), (converging ? sub_model : *initial).Base(),
+                converging);
   }
   s.Sync();
-  if (find_peak_only)  // the RCCL allreduce of the start peak
-    return double(comm.AllreduceMax(s, float(local_peak)));
+  if (find_peak_only) {
+    // every rank gets every subimage's start peak (one RCCL allreduce(max)
+    // of n_sub floats, the owners' entries against lowest()): the global
+    // start peak (:592-599, signed, from 0.0) and the cost estimates of the
+    // cleaning pass's ownership
+    std::vector<float> peaks(n_sub, std::numeric_limits<float>::lowest());
+    for (size_t i = 0; i != n_sub; ++i)
+      if (SubImageOwner(i, n_ranks) == rank) peaks[i] = float(subimages_[i].peak);
+    comm.AllreduceMax(s, peaks.data(), n_sub);
+    double start_peak = 0.0;
+    std::vector<double> costs(n_sub);
+    const double thr = std::max<double>(algorithms_.front()->Threshold(), 1e-30);
+    for (size_t i = 0; i != n_sub; ++i) {
+      SubImage& sub = subimages_[i];
+      sub.peak = peaks[i];
+      if (sub.peak > start_peak) start_peak = sub.peak;
+      // cleaning work grows with the subimage area and with how far its
+      // peak lies above the threshold (components ~ log(peak/threshold)
+      // per CLEANed source at a fixed gain)
+      const double above = std::max(std::fabs(sub.peak), thr) / thr;
+      costs[i] = double(sub.width * sub.height) * (1.0 + std::log2(above));
+    }
+    clean_owners_ = LptOwners(costs, n_ranks);
+    return start_peak;
+  }
 
   // copy-back (:458-484) in subimage order, identical on every rank
   std::unique_ptr<gpu::Buffer> staging;
@@ -812,7 +860,7 @@ double ParallelDeconvolution::RunSubImagesDistributed(
     SubImage& sub = subimages_[i];
     const size_t n = sub.width * sub.height;
     const size_t bytes = (kHeaderFloats + 2 * n_img * n) * sizeof(float);
-    const int owner = SubImageOwner(i, n_ranks);
+    const int owner = owner_of(i);
     gpu::Buffer* pack = packs[i].get();
     if (owner != rank) {
       if (!staging || staging->Bytes() < bytes)
@@ -874,12 +922,22 @@ ParallelDeconvolutionResult ParallelDeconvolution::ExecuteParallelRun(
   }
   ImageSet result_model(model_image, width, height);
   result_model.Fill(0.0f);
+  // settings.parallel.max_threads subimages in flight (:583-616), at most
+  // kMaxStreams streams per GPU: beyond that the streams only share the
+  // hardware queues (Settings' default is the host's processor count)
+  constexpr size_t kMaxStreams = 16;
   const size_t n_workers =
-      std::min<size_t>(std::max<size_t>(settings_.parallel.max_threads, 1),
+      std::min<size_t>(std::min<size_t>(std::max<size_t>(settings_.parallel.max_threads, 1),
+                                        kMaxStreams * PoolDevices(s.Device()).size()),
                        subimages_.size());
   const bool distributed = comm_ != nullptr;
   const bool concurrent = !distributed && n_workers > 1;
-  if (concurrent) EnsureWorkers(s, n_workers);
+  // with a communicator each rank runs its own subimages on a pool of its own
+  const size_t rank_workers =
+      distributed ? std::min<size_t>(n_workers, (subimages_.size() + comm_->Size() - 1) /
+                                                    size_t(comm_->Size()))
+                  : n_workers;
+  if (rank_workers > 1) EnsureWorkers(s, rank_workers);
   double start_peak = 0.0;
   if (distributed) {
     start_peak = RunSubImagesDistributed(data_image, model_image, result_model,

@@ -5,6 +5,7 @@
 // peak, and deconvolves every subimage on the device.
 #pragma once
 
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <optional>
@@ -75,6 +76,9 @@ class ParallelDeconvolution {
 
   /// Tiles of the last ExecuteParallelRun (empty for a 1x1 grid).
   const std::vector<SubImage>& SubImages() const { return subimages_; }
+  /// Process-per-GPU: the rank that cleaned each subimage in the last major
+  /// iteration (empty without a communicator).
+  const std::vector<int>& CleanOwners() const { return clean_owners_; }
 
   void FreeDeconvolutionAlgorithms() {
     algorithms_.clear();
@@ -108,12 +112,22 @@ class ParallelDeconvolution {
   bool DeconvolveSubImage(SubImage& sub, ImageSet& sub_data, ImageSet& sub_model,
                           const gpu::Planes& sub_psfs,
                           double major_iteration_threshold, bool find_peak_only);
+  /// Per-subimage result of a concurrent pass (device planes on the main
+  /// device, valid during the call): the residual box, the model box to add
+  /// (the initial one when it diverged) and whether it converged.
+  using SubImageSink = std::function<void(size_t index, const float* d_data,
+                                          const float* d_model, bool converging)>;
+  /// Runs the subimages (those with run[i] != 0 when `run` is given) on the
+  /// worker pool; merges the results in subimage order, or hands each to
+  /// `sink` in subimage order instead.
   void RunSubImagesConcurrently(ImageSet& data_image, const ImageSet& model_image,
                                 ImageSet& result_model,
                                 const std::vector<gpu::Planes>& psf_images,
                                 const std::vector<size_t>& psf_indices,
                                 double major_iteration_threshold,
-                                bool find_peak_only);
+                                bool find_peak_only,
+                                const std::vector<char>* run = nullptr,
+                                const SubImageSink& sink = nullptr);
   /// Process-per-GPU split: this rank deconvolves the subimages it owns
   /// (SubImageOwner) from the pass-start residual, then every subimage's
   /// boxes are broadcast by their owner and merged by all ranks in subimage
@@ -136,6 +150,9 @@ class ParallelDeconvolution {
   // worker sessions (one stream each) outlive the algorithms, whose cached
   // transforms and scratch live on them
   std::vector<std::shared_ptr<gpu::Session>> workers_;
+  // process-per-GPU: the cleaning pass's subimage owners (LptOwners over the
+  // find-peak pass's estimates), identical on every rank
+  std::vector<int> clean_owners_;
   int worker_main_device_ = -1;
   std::vector<std::unique_ptr<DeconvolutionAlgorithm>> algorithms_;
   std::vector<SubImage> subimages_;

@@ -570,6 +570,7 @@ void InitDistributed(py::module& m) {
            [](radler::HostCommunicator& self, float v) { return self.AllreduceMaxHost(v); },
            py::arg("value"));
   d.def("subimage_owner", &radler::SubImageOwner, py::arg("index"), py::arg("n_ranks"));
+  d.def("lpt_owners", &radler::LptOwners, py::arg("costs"), py::arg("n_ranks"));
 }
 
 void InitGpu(py::module& m) {
@@ -936,6 +937,7 @@ void InitGpu(py::module& m) {
                                     s.min_scale, s.area, s.max_value, s.trimmed_width));
         return out;
       }, py::arg("index") = 0)
+      .def("clean_owners", [](const radler::DeviceRun& self) { return self.CleanOwners(); })
       .def("subimages", [](const radler::DeviceRun& self, size_t width, size_t height) {
         // (boxes [n][x, y, w, h], labels [h][w]: subimage index + 1 inside its
         // boundary mask)

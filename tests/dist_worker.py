@@ -98,8 +98,10 @@ def main():
             out[f"model{major}"] = run.model()
             out[f"iterations{major}"] = np.int64(r["iterations"])
             out[f"another{major}"] = np.int64(r["another_iteration_required"])
+            owners = run.clean_owners()  # cost-ordered (LPT) cleaning-pass owners
+            out[f"owners{major}"] = np.array(owners, np.int64)
             for i in range(gw * gh):
-                if rd.distributed.subimage_owner(i, args.world) == args.rank:
+                if owners[i] == args.rank:
                     out[f"trace{major}_{i}"] = run.trace(i)
         run.sync()
         del run

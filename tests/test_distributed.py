@@ -61,6 +61,26 @@ def test_subimage_owner_round_robin():
     assert [owner(i, 3) for i in range(7)] == [0, 1, 2, 0, 1, 2, 0]
 
 
+def test_lpt_owners():
+    """Cost-ordered ownership of the cleaning pass: deterministic, balanced,
+    lower index / lower rank first on ties."""
+    from radler_import import radler as rd
+    lpt = rd.distributed.lpt_owners
+    assert lpt([5.0, 1.0, 1.0], 1) == [0, 0, 0]
+    assert lpt([1.0, 1.0, 1.0, 1.0], 2) == [0, 1, 0, 1]
+    # 8 on rank 0; 5 and 3 share rank 1 (8 = 5 + 3); 2 goes to rank 0
+    assert lpt([3.0, 8.0, 5.0, 2.0], 2) == [1, 0, 1, 0]
+    rng = np.random.default_rng(5)
+    costs = list(rng.uniform(1, 100, 64))
+    owners = lpt(costs, 8)
+    assert owners == lpt(costs, 8)
+    loads = np.zeros(8)
+    for c, o in zip(costs, owners):
+        loads[o] += c
+    # LPT is within 4/3 of optimal; the mean is a lower bound for the optimum
+    assert loads.max() <= 4.0 / 3.0 * max(loads.mean(), max(costs))
+
+
 def test_host_communicator_gloo_world2(tmp_path):
     outs = _launch(tmp_path, 2, "host")
     expect = ((np.arange(1 << 16) * 7 + 3) % 251).astype(np.uint8)
@@ -100,9 +120,12 @@ def test_distributed_tiled_matches_oracle_snapshot(tmp_path, world, kind, w, gw,
             assert np.array_equal(o[f"model{major}"], outs[0][f"model{major}"])
             assert o[f"iterations{major}"] == outs[0][f"iterations{major}"]
             assert o[f"another{major}"] == outs[0][f"another{major}"]
+        owners = outs[0][f"owners{major}"]
+        for o in outs[1:]:  # every rank computed the same LPT ownership
+            assert np.array_equal(o[f"owners{major}"], owners)
         for i in range(gw * gh):
             t_o = trace_o[trace_o[:, 0] == i][:, 1:]
-            t_g = outs[i % world][f"trace{major}_{i}"]
+            t_g = outs[int(owners[i])][f"trace{major}_{i}"]
             assert np.array_equal(t_g if kind == 1 else t_g[:, :2],
                                   t_o if kind == 1 else t_o[:, :2]), (major, i)
         assert int(outs[0][f"iterations{major}"]) == r_o.total_iterations - prev
