@@ -253,13 +253,15 @@ def main():
                     help="image side (default 8192; joined: 4096, SURVEY.md C3)")
     ap.add_argument("--channels", type=int, default=8, help="joined: channels")
     ap.add_argument("--grid", type=int, default=8, help="tiled: subimages per axis")
-    ap.add_argument("--pool", type=int, default=8,
+    ap.add_argument("--pool", type=int, default=16,
                     help="tiled: subimages in flight per GPU (settings.parallel.max_threads)")
     ap.add_argument("--scales", type=int, default=6)
     ap.add_argument("--points", type=int, default=2000)
     ap.add_argument("--blobs", type=int, default=200)
     ap.add_argument("--max-iter", type=int, default=10 ** 9)
     ap.add_argument("--sigma", type=float, default=5.0)
+    ap.add_argument("--tiled-reference", type=int, default=1,
+                    help="N = 1 fields: also time the tiled N > 1 workload on this GPU")
     ap.add_argument("--device-resident", type=int, default=1,
                     help="also time the HBM-resident major iteration (0 = skip)")
     ap.add_argument("--cpu-outer", type=int, default=2,
@@ -445,6 +447,30 @@ def main():
         print(f"[breakdown] device {device_ms:.1f} ms (all streams) of "
               f"{1e3 * elapsed:.1f} ms wall", file=sys.stderr)
 
+    # the N > 1 default workload (tiled 8 x 8) on this one GPU: the
+    # same-workload reference point of the scaling curve
+    tiled_ref = None
+    if args.tiled_reference and world == 1 and workload == "fields":
+        st = settings_for(rd, args.size, args.max_iter, args.scales, threshold,
+                          args.grid, args.pool)
+
+        def tiled_once():
+            arrays = (psf, dirty.copy(), np.zeros_like(dirty))
+            r = rd.Radler(st, *arrays, BEAM_PX * PIXEL_SCALE)
+            t = time.perf_counter()
+            r.perform(0)
+            return rd.gpu.total_iteration_number(r), time.perf_counter() - t
+
+        print("[bench] tiled reference (warm-up + 1 step) ...", file=sys.stderr, flush=True)
+        tiled_once()
+        t_comps, t_el = tiled_once()
+        tiled_ref = {"workload": (f"multiscale-{args.size}x{args.size}-{args.scales}scales"
+                                  f"-tiled{args.grid}x{args.grid}"),
+                     "value": round(t_comps / t_el, 2), "ms_per_step": round(1e3 * t_el, 2),
+                     "components_per_step": t_comps, "pool": args.pool,
+                     "note": "the default N > 1 workload (ParallelDeconvolution subimages) "
+                             "on one GPU, for the same-workload scaling curve"}
+
     cpu = None
     if args.cpu_outer > 0 and world == 1 and workload == "fields":
         threads = args.cpu_threads or cpu_share()
@@ -479,6 +505,7 @@ def main():
                    "parallelism": (f"subimages{args.grid * args.grid}/ranks{world}"
                                    f"/pool{args.pool}" if split else f"fields{world}")},
         "device_resident": resident,
+        "tiled_n1": tiled_ref,
         "roofline": roofline,
         "cpu_baseline": cpu,
     }
