@@ -46,6 +46,9 @@ struct rdl_subminor {
   uint32_t wave_max = 128;            // largest selection on the single-wave kernel
   uint32_t big_max = 3584;            // largest selection on one 1024-thread workgroup
   uint32_t big_target = 0;            // > 0: larger selections on 1024-thread grids
+  uint32_t table_max = 2048;          // largest selection given a pairwise PSF table
+  void* table = nullptr;              // [n_psf][n_sel][n_sel] PSF values at the
+  size_t table_bytes = 0;             //   selected pixels' pairwise offsets
 };
 
 namespace rdl {
@@ -181,6 +184,7 @@ struct LoopArgs {
   int32_t allow_negative, stop_on_negative;
   int32_t use_lds;
   int32_t prof;           // accumulate per-phase cycles (block 0, wave 0)
+  const float* table;     // pairwise PSF table (BuildPairTable) or nullptr
 };
 
 struct LoopResult {
@@ -609,6 +613,34 @@ __global__ __launch_bounds__(kStampThreads) void StampShapeModel(
   }
 }
 
+// ------------------------------------------------- pairwise PSF table
+// table[q][p][j] = PSF q at the offset of selected pixel j from selected
+// pixel p (the value the loop gathers for pixel j when p is the component),
+// or kOutsideBits where that offset leaves the PSF plane (no subtraction,
+// subminor_loop.cc:100-106). Built once per loop by the whole GPU; the loop
+// then reads ONE contiguous row per component (coalesced, L2-reusable when a
+// component repeats) instead of n_sel scattered gathers.
+constexpr uint32_t kOutsideBits = 0x7fbadbadu;  // a NaN payload no PSF value carries
+
+__global__ __launch_bounds__(256) void BuildPairTable(const uint32_t* __restrict__ pos,
+                                                      const float* __restrict__ psfs,
+                                                      uint32_t n_sel, uint32_t n_psf,
+                                                      uint32_t width, uint32_t height,
+                                                      float* __restrict__ table) {
+  const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t p = blockIdx.y;
+  if (j >= n_sel) return;
+  const uint32_t pp = pos[p], pj = pos[j];
+  const int dx = int(pj & 0xffffu) - int(pp & 0xffffu) + int(width / 2);
+  const int dy = int(pj >> 16) - int(pp >> 16) + int(height / 2);
+  const bool in = dx >= 0 && dx < int(width) && dy >= 0 && dy < int(height);
+  const size_t plane = size_t(width) * height;
+  const size_t off = in ? size_t(dy) * width + size_t(dx) : 0;
+  for (uint32_t q = 0; q < n_psf; ++q)
+    table[(size_t(q) * n_sel + p) * n_sel + j] =
+        in ? psfs[size_t(q) * plane + off] : __uint_as_float(kOutsideBits);
+}
+
 // ------------------------------------------------- register-resident loop
 // SubminorLoopReg: the same loop with each thread's ITEMS selected pixels
 // (positions, residuals, model values) held in VGPRs, so one iteration is
@@ -752,6 +784,7 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopReg(LoopArgs a) {
   float c[NI];
 #pragma unroll
   for (int k = 0; k < NI; ++k) c[k] = 0.0f;
+  uint32_t cp = 0;  // the component's selection index (its table row)
   int cx = 0, cy = 0;
   bool have_component = false;
   float start_abs = 0.0f;
@@ -776,6 +809,20 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopReg(LoopArgs a) {
     if (have_component) {
       float pv[ITEMS][NI];
       bool in[ITEMS];
+      if (a.table) {
+        // the component's row of the pairwise table: contiguous over j
+        const size_t sq = size_t(a.n_sel) * a.n_sel;
+        const float* row = a.table + size_t(cp) * a.n_sel + base;
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) {
+          const uint32_t j = tid + uint32_t(i) * THREADS;
+          const bool valid = j < cnt;
+#pragma unroll
+          for (int k = 0; k < NI; ++k)
+            pv[i][k] = (valid && k < n_img) ? row[size_t(k / n_pol) * sq + j] : 0.0f;
+          in[i] = valid && __float_as_uint(pv[i][0]) != kOutsideBits;
+        }
+      } else {
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
         const uint32_t j = tid + uint32_t(i) * THREADS;
@@ -786,6 +833,7 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopReg(LoopArgs a) {
 #pragma unroll
         for (int k = 0; k < NI; ++k)
           pv[i][k] = k < n_img ? a.psfs[size_t(k / n_pol) * plane + off] : 0.0f;
+      }
       }
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i)
@@ -1023,6 +1071,7 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopReg(LoopArgs a) {
     flux += m * a.gain;
     cx = int(wpos & 0xffffu);
     cy = int(wpos >> 16);
+    cp = uint32_t(winner_p);
     if (winner_p >= base && winner_p < base + cnt) {
       const uint32_t j = uint32_t(winner_p - base);
       if (j % THREADS == tid) {
@@ -1199,6 +1248,9 @@ int rdl_subminor_create(rdl_session* s, rdl_subminor** out) {
     h->big_max = uint32_t(std::strtoul(e, nullptr, 10));
   if (const char* e = std::getenv("RDL_SUBMINOR_BIG_TARGET"))
     h->big_target = uint32_t(std::strtoul(e, nullptr, 10));
+  // RDL_SUBMINOR_TABLE_MAX=0 keeps the per-iteration PSF gathers
+  if (const char* e = std::getenv("RDL_SUBMINOR_TABLE_MAX"))
+    h->table_max = uint32_t(std::strtoul(e, nullptr, 10));
   *out = h;
   return RDL_OK;
 }
@@ -1209,6 +1261,7 @@ int rdl_subminor_destroy(rdl_subminor* h) {
   if (h->counts) (void)hipFree(h->counts);
   if (h->sel) (void)hipFree(h->sel);
   if (h->sync) (void)hipFree(h->sync);
+  if (h->table) (void)hipFree(h->table);
   delete h;
   return RDL_OK;
 }
@@ -1424,6 +1477,18 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   la.trace_cap = n_trace;
   // zero counter, result and (register kernel) the epoch-tagged granules
   RDL_HIP_CHECK(hipMemsetAsync(sb, 0, use_reg ? 512 + rec_bytes : 512, st));
+  la.table = nullptr;
+  const uint32_t n_psf = ni / p->n_pol;
+  if (use_reg && n_sel >= 2 && n_sel <= h->table_max) {
+    const size_t table_bytes = size_t(n_psf) * n_sel * n_sel * sizeof(float);
+    RDL_TRY(rdl::Grow(&h->table, &h->table_bytes, table_bytes, st));
+    rdl::ScopedTiming t(s, "subminor_table", 8.0 * double(n_psf) * n_sel * n_sel);
+    rdl::BuildPairTable<<<dim3(rdl::DivUp(n_sel, 256), uint32_t(n_sel)), 256, 0, st>>>(
+        h->d_pos, d_psfs, uint32_t(n_sel), n_psf, p->width, p->height,
+        static_cast<float*>(h->table));
+    RDL_HIP_CHECK(hipGetLastError());
+    la.table = static_cast<const float*>(h->table);
+  }
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   if (s->trace_subminor) {
     ev0 = s->GetEvent();
