@@ -5,6 +5,8 @@
 // derivative gather, the line-search sums and the value updates are masked
 // elementwise passes around the padded FFT convolutions (host:
 // csrc/host/component_optimization.cc). HBM-bound.
+#include <algorithm>
+
 #include "rdl_internal.h"
 
 namespace rdl {
@@ -31,9 +33,15 @@ __global__ __launch_bounds__(256) void MaskedAddKernel(float* model, const float
     if (model[i] != 0.0f) model[i] += v[i];
 }
 
-// sums[0] += sum a*b, sums[1] += sum a*a (double)
-__global__ __launch_bounds__(256) void DotPairKernel(const float* a, const float* b, size_t n,
-                                                     double* sums) {
+// Fixed-order two-stage dot products (reproducible: no atomics). Stage 1:
+// block b writes partials[2b] = its sum of a*b, partials[2b+1] = its sum of
+// a*a (double), over a fixed grid-stride partition; stage 2: one block sums
+// the partials in a fixed tree.
+constexpr uint32_t kDotBlocks = 1024;
+
+__global__ __launch_bounds__(256) void DotPairPartials(const float* a, const float* b,
+                                                       size_t n, double* partials) {
+  __shared__ double lds[2][4];
   double ab = 0.0, aa = 0.0;
   for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n;
        i += size_t(gridDim.x) * blockDim.x) {
@@ -46,9 +54,35 @@ __global__ __launch_bounds__(256) void DotPairKernel(const float* a, const float
     ab += __shfl_xor(ab, off, 64);
     aa += __shfl_xor(aa, off, 64);
   }
+  const int wave = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
-    atomicAdd(&sums[0], ab);
-    atomicAdd(&sums[1], aa);
+    lds[0][wave] = ab;
+    lds[1][wave] = aa;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    partials[2 * blockIdx.x] = (lds[0][0] + lds[0][1]) + (lds[0][2] + lds[0][3]);
+    partials[2 * blockIdx.x + 1] = (lds[1][0] + lds[1][1]) + (lds[1][2] + lds[1][3]);
+  }
+}
+
+__global__ __launch_bounds__(1024) void DotPairFinal(const double* partials, uint32_t n_blocks,
+                                                     double* sums) {
+  __shared__ double lds[2][1024];
+  const uint32_t t = threadIdx.x;
+  lds[0][t] = t < n_blocks ? partials[2 * t] : 0.0;
+  lds[1][t] = t < n_blocks ? partials[2 * t + 1] : 0.0;
+  __syncthreads();
+  for (uint32_t half = 512; half > 0; half >>= 1) {
+    if (t < half) {
+      lds[0][t] += lds[0][t + half];
+      lds[1][t] += lds[1][t + half];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    sums[0] = lds[0][0];
+    sums[1] = lds[1][0];
   }
 }
 
@@ -80,12 +114,15 @@ int rdl_masked_add(rdl_session* s, float* d_model, const float* d_values, size_t
 int rdl_dot_pair(rdl_session* s, const float* d_a, const float* d_b, size_t n,
                  double* ab, double* aa) {
   RDL_ARG_CHECK(s && d_a && d_b && ab && aa, "NULL argument");
-  RDL_TRY(s->EnsureScratch(s->partials, 256));
-  double* d_sums = static_cast<double*>(s->partials.ptr);
+  RDL_TRY(s->EnsureScratch(s->partials, (2 * rdl::kDotBlocks + 2) * sizeof(double)));
+  double* d_partials = static_cast<double*>(s->partials.ptr);
+  double* d_sums = d_partials + 2 * rdl::kDotBlocks;
   RDL_HIP_CHECK(hipMemsetAsync(d_sums, 0, 2 * sizeof(double), s->stream));
   if (n > 0) {
     rdl::ScopedTiming t(s, "component_optimization", 8.0 * double(n));
-    rdl::DotPairKernel<<<rdl::Grid(n), rdl::kThreads, 0, s->stream>>>(d_a, d_b, n, d_sums);
+    const uint32_t blocks = std::min<uint32_t>(rdl::kDotBlocks, rdl::DivUp(n, 256));
+    rdl::DotPairPartials<<<blocks, 256, 0, s->stream>>>(d_a, d_b, n, d_partials);
+    rdl::DotPairFinal<<<1, 1024, 0, s->stream>>>(d_partials, blocks, d_sums);
     RDL_HIP_CHECK(hipGetLastError());
   }
   double h[2] = {0.0, 0.0};

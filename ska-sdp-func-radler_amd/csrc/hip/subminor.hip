@@ -46,7 +46,7 @@ struct rdl_subminor {
   uint32_t wave_max = 128;            // largest selection on the single-wave kernel
   uint32_t big_max = 3584;            // largest selection on one 1024-thread workgroup
   uint32_t big_target = 0;            // > 0: larger selections on 1024-thread grids
-  uint32_t table_max = 2048;          // largest selection given a pairwise PSF table
+  uint32_t table_max = 16384;         // largest selection given a pairwise PSF table
   void* table = nullptr;              // [n_psf][n_sel][n_sel] PSF values at the
   size_t table_bytes = 0;             //   selected pixels' pairwise offsets
 };
@@ -1359,8 +1359,17 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   // joined channels one workgroup's memory pipe, not the exchange, bounds an
   // iteration (8 channels x 3000 pixels on one CU: 26 us per component)
   const uint64_t work = n_sel * ni;
+  // with the pairwise table an iteration reads one contiguous row per PSF:
+  // one workgroup (up to 1024 threads) then holds selections that would
+  // otherwise pay a cross-workgroup exchange per component
+  const uint64_t big_cap = 1024ull * (ni_t <= 2 ? 8 : 4);
+  const bool want_table = h->mode == 0 && ni <= 8 && n_sel >= 2 && n_sel <= h->table_max &&
+                          uint64_t(ni / p->n_pol) * n_sel * n_sel <= (uint64_t(1) << 27);
+  // (one CU's memory pipe streams those rows: at most 8192 values per
+  // iteration, so joined channels keep the grid above 8192 / N_img pixels)
+  const bool table_single = want_table && n_sel <= big_cap && work <= 8192;
   if (use_reg) {
-    if (n_sel > reg_cap || work > h->single_max) {
+    if (!table_single && (n_sel > reg_cap || work > h->single_max)) {
       const uint64_t target = std::max<uint64_t>(
           std::max<uint32_t>(h->target_per_block, 512) / ni, 64);
       g = uint32_t(std::min<uint64_t>(max_blocks, (n_sel + target - 1) / target));
@@ -1384,10 +1393,10 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
     return RDL_ERR_ARG;
   }
   // one sixteen-wave workgroup (mode 4 forces it)
-  const uint64_t big_cap = 1024ull * (ni_t <= 2 ? 8 : 4);
   bool use_big =
       !use_wave && ni <= 8 && h->mode != 1 && h->mode != 2 &&
-      ((h->mode == 0 && n_sel <= big_cap && work <= h->big_max && work > 1024) ||
+      ((h->mode == 0 && n_sel <= big_cap &&
+        ((work <= h->big_max && work > 1024) || (table_single && n_sel > 1024))) ||
        (h->mode == 4 && n_sel <= big_cap));
   // 1024-thread workgroups on a cooperative grid (mode 5, target pixels per
   // workgroup from set_tuning; mode 0 when big_target is set)
@@ -1479,7 +1488,7 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   RDL_HIP_CHECK(hipMemsetAsync(sb, 0, use_reg ? 512 + rec_bytes : 512, st));
   la.table = nullptr;
   const uint32_t n_psf = ni / p->n_pol;
-  if (use_reg && n_sel >= 2 && n_sel <= h->table_max) {
+  if (use_reg && want_table) {
     const size_t table_bytes = size_t(n_psf) * n_sel * n_sel * sizeof(float);
     RDL_TRY(rdl::Grow(&h->table, &h->table_bytes, table_bytes, st));
     rdl::ScopedTiming t(s, "subminor_table", 8.0 * double(n_psf) * n_sel * n_sel);

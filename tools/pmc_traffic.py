@@ -5,7 +5,7 @@ passes (MI355X_MICROARCH.md, "HBM" and "rocprofv3 PMC slots"):
   FETCH_SIZE and WRITE_SIZE do not fit one pass on gfx950, so each gets its
   own run of the same command:
     rocprofv3 --pmc FETCH_SIZE --kernel-trace -d D1 -o run -- python3 bench.py \
-        --warmup 0 --steps 1 --cpu-outer 0 --timing-all --dump-families D1/fams.json
+        --warmup 0 --steps 1 --cpu-outer 0 --tiled-reference 0 --device-resident 0 --timing-all --dump-families D1/fams.json
     rocprofv3 --pmc WRITE_SIZE ...  (same, into D2)
   then
     python tools/pmc_traffic.py D1/run_results.db D2/run_results.db D1/fams.json \
@@ -33,6 +33,7 @@ FAMILY_KERNELS = {
     "fft": r"_sp_",  # rocFFT single-precision kernels (only rdl_fft_* launches them)
     "spectrum_multiply": r"^rdl::SpectrumMultiply\(",
     "subminor_loop": r"SubminorLoop",
+    "subminor_table": r"BuildPairTable",
     "subminor_select": r"^rdl::Sel(Count|Scan|Scatter)\(",
     "find_peak": r"^void rdl::FindPeak|^rdl::FindPeakFinal",
     "integrate": r"^rdl::IntegrateKernel\(",
