@@ -352,6 +352,8 @@ def main():
     timing = Timing()
     if args.timing_all:
         timing.enable(True)
+    print(f"[bench] rank {rank}: {workload} {args.size}^2 inputs ready; {args.warmup} warm-up "
+          f"+ {args.steps} timed Perform steps", file=sys.stderr, flush=True)
     for _ in range(args.warmup):
         r, arrays = make_radler()
         r.perform(0)

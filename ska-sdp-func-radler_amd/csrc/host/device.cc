@@ -56,9 +56,11 @@ Fft::Fft(Session& s, size_t width, size_t height, bool f64)
   // (tools/bench_fft.py). RADLER_FFT=rocfft / lds overrides.
   const char* force = std::getenv("RADLER_FFT");
   const std::string mode = force ? force : "";
-  // float: the LDS engine where its four-step tiled plans exist (the 4096 /
-  // 8192 scale-convolution planes), rocFFT elsewhere (RADLER_FFT=lds forces
-  // the LDS engine)
+  // float: the LDS engine at every size it holds (compile-time four-step
+  // plans at 4096 / 8192, runtime plans elsewhere): at the subimage planes of
+  // a tiled run it beat rocFFT (8192^2 split 8 x 8: 7.2 vs 8.1 s per
+  // Perform) and plans in microseconds where rocFFT compiles kernels for
+  // 0.2-0.3 s per size. RADLER_FFT=rocfft restores rocFFT.
   const bool want_lds = mode != "rocfft";
   // RADLER_FFT_COLUMNS=single / split overrides the column-pass choice
   const char* cols_env = std::getenv("RADLER_FFT_COLUMNS");
@@ -66,14 +68,9 @@ Fft::Fft(Session& s, size_t width, size_t height, bool f64)
   const int strategy = cols == "single"  ? RDL_CONV_COLUMNS_SINGLE
                        : cols == "split" ? RDL_CONV_COLUMNS_SPLIT
                                          : RDL_CONV_COLUMNS_AUTO;
-  const bool lds_ok = want_lds &&
-                      rdl_conv_create_ex(s.Handle(), uint32_t(width), uint32_t(height),
-                                         f64 ? 1 : 0, strategy, &conv_) == RDL_OK;
-  const int fast = lds_ok ? rdl_conv_fast(conv_) : 0;
-  if (lds_ok && !f64 && mode != "lds" && !(fast & RDL_CONV_FAST_TILED)) {
-    rdl_conv_destroy(conv_);
+  if (!want_lds || rdl_conv_create_ex(s.Handle(), uint32_t(width), uint32_t(height),
+                                      f64 ? 1 : 0, strategy, &conv_) != RDL_OK)
     conv_ = nullptr;
-  }
   if (conv_) {
     // the compile-time-planned column kernels read and write any layout:
     // spectra are then stored column by column (contiguous column reads)

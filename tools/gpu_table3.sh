@@ -13,3 +13,5 @@ timeout -k 10 300 python -u bench.py --workload tiled --grid 8 --steps 1 --break
   > gpurun_out/tiled8_u.json 2> gpurun_out/tiled8_u.err || exit $?
 RADLER_FFT=lds timeout -k 10 300 python -u bench.py --workload tiled --grid 8 --steps 1 --breakdown \
   > gpurun_out/tiled8_lds.json 2> gpurun_out/tiled8_lds.err || exit $?
+timeout -k 10 500 python -u bench.py --workload tiled --size 16384 --grid 8 --steps 1 --breakdown \
+  > gpurun_out/bench_c5_16384.json 2> gpurun_out/bench_c5_16384.err || exit $?
