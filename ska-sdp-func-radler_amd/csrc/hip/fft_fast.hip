@@ -634,6 +634,15 @@ const FastColumns* FindFastColumns(uint32_t n, bool f64) {
       // float32 scale convolutions (two workgroups per CU)
       RDL_FAST_COLS(float, 512, true, 8, 8, 8, 16),            // 8192
       RDL_FAST_COLS(float, 512, true, 8, 8, 8, 8),             // 4096
+      // the periodically extended subimage planes of a tiled run
+      // (MultiScaleTransforms' CanonicalFftSize ladder)
+      RDL_FAST_COLS(float, 512, true, 8, 8, 8, 7),             // 3584
+      RDL_FAST_COLS(float, 512, true, 8, 8, 16, 3),            // 3072
+      RDL_FAST_COLS(float, 512, true, 8, 8, 8, 5),             // 2560
+      RDL_FAST_COLS(float, 512, true, 8, 8, 8, 4),             // 2048
+      RDL_FAST_COLS(float, 512, true, 8, 8, 4, 7),             // 1792
+      RDL_FAST_COLS(float, 512, true, 8, 8, 8, 3),             // 1536
+      RDL_FAST_COLS(float, 512, true, 8, 8, 4, 5),             // 1280
   };
   for (const FastColumns& p : kPlans)
     if (p.n == n && p.f64 == f64) return &p;
@@ -653,6 +662,13 @@ const FastRows* FindFastRows(uint32_t n, bool f64) {
       RDL_FAST_ROWS(double, 256, 4, 5, 5, 5, 5),   // 5000
       RDL_FAST_ROWS(float, 256, 16, 16, 16),       // 8192
       RDL_FAST_ROWS(float, 256, 16, 16, 8),        // 4096
+      RDL_FAST_ROWS(float, 256, 16, 16, 7),        // 3584
+      RDL_FAST_ROWS(float, 256, 16, 16, 2, 3),     // 3072
+      RDL_FAST_ROWS(float, 256, 16, 16, 5),        // 2560
+      RDL_FAST_ROWS(float, 256, 16, 16, 4),        // 2048
+      RDL_FAST_ROWS(float, 256, 16, 8, 7),         // 1792
+      RDL_FAST_ROWS(float, 256, 16, 16, 3),        // 1536
+      RDL_FAST_ROWS(float, 256, 16, 8, 5),         // 1280
   };
   for (const FastRows& p : kPlans)
     if (p.n == n && p.f64 == f64) return &p;
@@ -675,6 +691,13 @@ const FastSteps* FindFastSteps(uint32_t n) {
   static const FastSteps kPlans[] = {
       RDL_FAST_STEPS(64, 128, 4, 2, RDL_R(8, 8), RDL_R(16, 8)),  // 8192
       RDL_FAST_STEPS(64, 64, 4, 4, RDL_R(8, 8), RDL_R(8, 8)),    // 4096
+      RDL_FAST_STEPS(64, 56, 4, 4, RDL_R(8, 8), RDL_R(8, 7)),    // 3584
+      RDL_FAST_STEPS(64, 48, 4, 4, RDL_R(8, 8), RDL_R(16, 3)),   // 3072
+      RDL_FAST_STEPS(64, 40, 4, 4, RDL_R(8, 8), RDL_R(8, 5)),    // 2560
+      RDL_FAST_STEPS(32, 64, 4, 4, RDL_R(8, 4), RDL_R(8, 8)),    // 2048
+      RDL_FAST_STEPS(32, 56, 4, 4, RDL_R(8, 4), RDL_R(8, 7)),    // 1792
+      RDL_FAST_STEPS(32, 48, 4, 4, RDL_R(8, 4), RDL_R(16, 3)),   // 1536
+      RDL_FAST_STEPS(32, 40, 4, 4, RDL_R(8, 4), RDL_R(8, 5)),    // 1280
   };
   for (const FastSteps& p : kPlans)
     if (p.n == n) return &p;

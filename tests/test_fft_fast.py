@@ -59,7 +59,9 @@ def natural(sess, c, flat, w, h):
 # (width, height, f64): rows use the half-length plan of `width`, columns the
 # plan of `height`
 CASES = [(4536, 4608, True), (4800, 5000, True), (4704, 4536, True), (9072, 9216, True),
-         (9450, 9408, True), (8192, 4096, False), (4096, 8192, False)]
+         (9450, 9408, True), (8192, 4096, False), (4096, 8192, False),
+         # the subimage planes of tiled runs (CanonicalFftSize ladder)
+         (2560, 3072, False), (3584, 1280, False), (1536, 2048, False), (2048, 1792, False)]
 
 
 @pytest.mark.parametrize("w,h,f64", CASES)

@@ -590,7 +590,8 @@ def test_lds_fft_correction_sparse_rows(sess, w, h, pw, ph, rows, columns):
     sess.rdl.rdl_conv_destroy(c)
 
 
-@pytest.mark.parametrize("w,h", [(256, 256), (301, 257), (262, 222), (498, 350)])
+@pytest.mark.parametrize("w,h", [(256, 256), (301, 257), (262, 222), (498, 350),
+                                 (1100, 1000), (2100, 1900)])
 @pytest.mark.parametrize("shape", [0, 1])
 def test_ms_transform_any_size(orc, w, h, shape):
     """MultiScaleTransforms::Transform (circular at W x H): sizes that are not
