@@ -11,6 +11,16 @@ namespace rdl {
 
 constexpr size_t kFftLdsBytesFast = 160 * 1024;
 
+/* Float transforms keep one pad element per 16 in LDS (ff::Lx): a pass's
+ * butterfly outputs land R elements apart, and ds_write_b64 serves 16
+ * contiguous lanes per bank cycle over 128 B, so a power-of-two stride put all
+ * 16 lanes on one bank (16-way). Double plans run an odd radix first instead
+ * (odd strides are conflict-free) and keep the LDS for the transform. */
+constexpr uint32_t kFastPadShift = 4;
+inline size_t FastLdsBytes(uint32_t n, bool f64) {
+  return f64 ? size_t(n) * 16 : (size_t(n) + (n >> kFastPadShift)) * 8;
+}
+
 /* radices of a compile-time plan, in pass order */
 struct RadixList {
   uint8_t r[8];

@@ -38,6 +38,15 @@ __device__ __forceinline__ void LdsSync() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// LDS slot of logical element i of a transform (see kFastPadShift)
+template <typename T>
+__device__ __forceinline__ uint32_t Lx(uint32_t i) {
+  if constexpr (sizeof(T) == 4)
+    return i + (i >> kFastPadShift);
+  else
+    return i;
+}
+
 // One Stockham pass (radix R, span NS) over a length-N transform in LDS, in
 // place (inputs read to registers before the barrier). Twiddles come from the
 // plan's pass table (MakePassTable, host): pass p's W_N^{k (q+1) M} at
@@ -63,7 +72,7 @@ __device__ __forceinline__ void Pass(Cx<T>* buf, const Cx<T>* __restrict__ ptw,
         for (uint32_t q = 0; q < NW; ++q) w[i][q] = ptw[OFF + q * NS + k];
       }
 #pragma unroll
-      for (uint32_t r = 0; r < R; ++r) v[i][r] = buf[j + r * NB];
+      for (uint32_t r = 0; r < R; ++r) v[i][r] = buf[Lx<T>(j + r * NB)];
     }
   }
   LdsSync();
@@ -89,7 +98,7 @@ __device__ __forceinline__ void Pass(Cx<T>* buf, const Cx<T>* __restrict__ ptw,
       Dft<T, int(R)>::Run(v[i]);
       const uint32_t d = (j / NS) * NS * R + k;
 #pragma unroll
-      for (uint32_t r = 0; r < R; ++r) buf[d + r * NS] = v[i][r];
+      for (uint32_t r = 0; r < R; ++r) buf[Lx<T>(d + r * NS)] = v[i][r];
     }
   }
   LdsSync();
@@ -149,7 +158,7 @@ __global__ __launch_bounds__(TH) void Columns(ColArgs a, const Cx<T>* __restrict
 #pragma unroll
     for (uint32_t i = 0; i < E; ++i) {
       const uint32_t y = tid + i * TH;
-      if (N % TH == 0 || y < N) buf[y] = Cx<T>{T(0), T(0)};
+      if (N % TH == 0 || y < N) buf[Lx<T>(y)] = Cx<T>{T(0), T(0)};
     }
     LdsSync();
   }
@@ -179,13 +188,13 @@ __global__ __launch_bounds__(TH) void Columns(ColArgs a, const Cx<T>* __restrict
       if (sparse) {
         for (uint32_t q = tid; q < n_rows; q += TH) {
           const uint32_t y = listed ? a.rows[q] : a.row0 + q;
-          buf[y] = in_c[y * in_stride];
+          buf[Lx<T>(y)] = in_c[y * in_stride];
         }
       } else {
 #pragma unroll
         for (uint32_t i = 0; i < E; ++i) {
           const uint32_t y = tid + i * TH;
-          if (N % TH == 0 || y < N) buf[y] = in_c[y * in_stride];
+          if (N % TH == 0 || y < N) buf[Lx<T>(y)] = in_c[y * in_stride];
         }
       }
       if (PF && a.mode != 0) load_kernel();
@@ -198,7 +207,7 @@ __global__ __launch_bounds__(TH) void Columns(ColArgs a, const Cx<T>* __restrict
 #pragma unroll
       for (uint32_t i = 0; i < E; ++i) {
         const uint32_t y = tid + i * TH;
-        if (N % TH == 0 || y < N) buf[y] = Conj(Scale(Mul(buf[y], K[i]), s));
+        if (N % TH == 0 || y < N) buf[Lx<T>(y)] = Conj(Scale(Mul(buf[Lx<T>(y)], K[i]), s));
       }
       LdsSync();
       Fft<T, TH, N, 0, 1, Rs...>(buf, ptw, tid);
@@ -210,17 +219,17 @@ __global__ __launch_bounds__(TH) void Columns(ColArgs a, const Cx<T>* __restrict
       for (uint32_t i = 0; i < E; ++i) {
         const uint32_t y = tid + i * TH;
         if (N % TH == 0 || y < N) {
-          Cx<T> v = buf[y];
+          Cx<T> v = buf[Lx<T>(y)];
           if (a.mode != 0) v = Conj(v);
           out_c[y * o_stride] = v;
-          if (sparse) buf[y] = Cx<T>{T(0), T(0)};
+          if (sparse) buf[Lx<T>(y)] = Cx<T>{T(0), T(0)};
         }
       }
     } else if (sparse) {
 #pragma unroll
       for (uint32_t i = 0; i < E; ++i) {
         const uint32_t y = tid + i * TH;
-        if (N % TH == 0 || y < N) buf[y] = Cx<T>{T(0), T(0)};
+        if (N % TH == 0 || y < N) buf[Lx<T>(y)] = Cx<T>{T(0), T(0)};
       }
     }
     LdsSync();
@@ -293,8 +302,8 @@ __global__ __launch_bounds__(TH) void RowsInverse(RowArgs a, const Cx<T>* __rest
       xk.y = T(0);
       xm.y = T(0);
     }
-    buf[k] = zc(xk, xm, k);
-    if (k != 0 && m != k) buf[m] = zc(xm, xk, m);
+    buf[Lx<T>(k)] = zc(xk, xm, k);
+    if (k != 0 && m != k) buf[Lx<T>(m)] = zc(xm, xk, m);
   }
   LdsSync();
   Fft<T, TH, H, 0, 1, Rs...>(buf, ptw, tid);
@@ -307,7 +316,7 @@ __global__ __launch_bounds__(TH) void RowsInverse(RowArgs a, const Cx<T>* __rest
       if (H % TH != 0 && n >= H) continue;
       const uint32_t x0 = 2 * n;
       if (x0 < a.ox || x0 >= a.ox + a.img_w) continue;
-      const Cx<T> z = buf[n];  // conj(result): x[2n] = z.x, x[2n+1] = -z.y
+      const Cx<T> z = buf[Lx<T>(n)];  // conj(result): x[2n] = z.x, x[2n+1] = -z.y
       float2* p = reinterpret_cast<float2*>(o + (x0 - a.ox));
       float2 v = {float(z.x), float(-z.y)};
       if (a.subtract) {
@@ -322,7 +331,7 @@ __global__ __launch_bounds__(TH) void RowsInverse(RowArgs a, const Cx<T>* __rest
   for (uint32_t i = 0; i < EH; ++i) {
     const uint32_t n = tid + i * TH;
     if (H % TH != 0 && n >= H) continue;
-    const Cx<T> z = buf[n];
+    const Cx<T> z = buf[Lx<T>(n)];
     const uint32_t x0 = 2 * n, x1 = x0 + 1;
     if (x0 >= a.ox && x0 < a.ox + a.img_w) {
       float* p = o + (x0 - a.ox);
@@ -375,7 +384,7 @@ __global__ __launch_bounds__(TH) void RowsForward(RowArgs a, const float* __rest
         e = in_y && x0 >= a.ox && x0 < a.ox + a.img_w ? T(row[x0 - a.ox]) : T(0);
         od = in_y && x1 >= a.ox && x1 < a.ox + a.img_w ? T(row[x1 - a.ox]) : T(0);
       }
-      buf[n] = {e, od};
+      buf[Lx<T>(n)] = {e, od};
     }
     LdsSync();
     Fft<T, TH, H, 0, 1, Rs...>(buf, ptw, tid);
@@ -385,8 +394,8 @@ __global__ __launch_bounds__(TH) void RowsForward(RowArgs a, const float* __rest
     for (uint32_t i = 0; i < EX; ++i) {
       const uint32_t k = tid + i * TH;
       if (k > H) continue;
-      const Cx<T> zk = buf[k == H ? 0 : k];
-      const Cx<T> zc = Conj(buf[k == 0 ? 0 : H - k]);
+      const Cx<T> zk = buf[Lx<T>(k == H ? 0 : k)];
+      const Cx<T> zc = Conj(buf[Lx<T>(k == 0 ? 0 : H - k)]);
       const Cx<T> ev = {h * (zk.x + zc.x), h * (zk.y + zc.y)};
       const Cx<T> od = {h * (zk.y - zc.y), -h * (zk.x - zc.x)};  // (zk - zc) / 2i
       const Cx<T> v = Add(ev, Mul(tw[k], od));
@@ -622,15 +631,15 @@ __global__ __launch_bounds__(1024) void CompactRows(const uint8_t* __restrict__ 
 const FastColumns* FindFastColumns(uint32_t n, bool f64) {
   static const FastColumns kPlans[] = {
       // float64 padded correction sizes of 8192^2 (scales 0..256) and 4096^2
-      RDL_FAST_COLS(double, 1024, true, 4, 4, 9, 9, 7),        // 9072
-      RDL_FAST_COLS(double, 1024, true, 4, 4, 4, 4, 4, 9),     // 9216
-      RDL_FAST_COLS(double, 1024, true, 4, 4, 4, 3, 7, 7),     // 9408
-      RDL_FAST_COLS(double, 1024, true, 2, 3, 3, 3, 5, 5, 7),  // 9450
-      RDL_FAST_COLS(double, 1024, true, 8, 9, 9, 7),           // 4536
-      RDL_FAST_COLS(double, 1024, true, 8, 8, 8, 9),           // 4608
-      RDL_FAST_COLS(double, 1024, true, 8, 4, 3, 7, 7),        // 4704
-      RDL_FAST_COLS(double, 1024, true, 8, 8, 3, 5, 5),        // 4800
-      RDL_FAST_COLS(double, 1024, true, 8, 5, 5, 5, 5),        // 5000
+      RDL_FAST_COLS(double, 1024, true, 7, 9, 9, 4, 4),        // 9072
+      RDL_FAST_COLS(double, 1024, true, 9, 4, 4, 4, 4, 4),     // 9216
+      RDL_FAST_COLS(double, 1024, true, 7, 3, 7, 4, 4, 4),     // 9408
+      RDL_FAST_COLS(double, 1024, true, 7, 5, 3, 5, 3, 3, 2),  // 9450
+      RDL_FAST_COLS(double, 1024, true, 7, 9, 9, 8),           // 4536
+      RDL_FAST_COLS(double, 1024, true, 9, 8, 8, 8),           // 4608
+      RDL_FAST_COLS(double, 1024, true, 7, 3, 7, 8, 4),        // 4704
+      RDL_FAST_COLS(double, 1024, true, 5, 3, 5, 8, 8),        // 4800
+      RDL_FAST_COLS(double, 1024, true, 5, 5, 5, 5, 8),        // 5000
       // float32 scale convolutions (two workgroups per CU)
       RDL_FAST_COLS(float, 512, true, 8, 8, 8, 16),            // 8192
       RDL_FAST_COLS(float, 512, true, 8, 8, 8, 8),             // 4096
@@ -651,15 +660,15 @@ const FastColumns* FindFastColumns(uint32_t n, bool f64) {
 
 const FastRows* FindFastRows(uint32_t n, bool f64) {
   static const FastRows kPlans[] = {
-      RDL_FAST_ROWS(double, 512, 8, 9, 9, 7),      // 9072
-      RDL_FAST_ROWS(double, 512, 8, 8, 8, 9),      // 9216
-      RDL_FAST_ROWS(double, 512, 8, 4, 3, 7, 7),   // 9408
-      RDL_FAST_ROWS(double, 512, 9, 3, 5, 5, 7),   // 9450
-      RDL_FAST_ROWS(double, 256, 4, 9, 9, 7),      // 4536
-      RDL_FAST_ROWS(double, 256, 4, 4, 4, 4, 9),   // 4608
-      RDL_FAST_ROWS(double, 256, 4, 4, 3, 7, 7),   // 4704
-      RDL_FAST_ROWS(double, 256, 8, 4, 3, 5, 5),   // 4800
-      RDL_FAST_ROWS(double, 256, 4, 5, 5, 5, 5),   // 5000
+      RDL_FAST_ROWS(double, 512, 7, 9, 9, 8),      // 9072
+      RDL_FAST_ROWS(double, 512, 9, 8, 8, 8),      // 9216
+      RDL_FAST_ROWS(double, 512, 7, 3, 7, 8, 4),   // 9408
+      RDL_FAST_ROWS(double, 512, 7, 5, 3, 5, 9),   // 9450
+      RDL_FAST_ROWS(double, 256, 7, 9, 9, 4),      // 4536
+      RDL_FAST_ROWS(double, 256, 9, 4, 4, 4, 4),   // 4608
+      RDL_FAST_ROWS(double, 256, 7, 3, 7, 4, 4),   // 4704
+      RDL_FAST_ROWS(double, 256, 5, 3, 5, 8, 4),   // 4800
+      RDL_FAST_ROWS(double, 256, 5, 5, 5, 5, 4),   // 5000
       RDL_FAST_ROWS(float, 256, 16, 16, 16),       // 8192
       RDL_FAST_ROWS(float, 256, 16, 16, 8),        // 4096
       RDL_FAST_ROWS(float, 256, 16, 16, 7),        // 3584
@@ -733,7 +742,7 @@ int FastColumnsLaunch(rdl_session* s, const FastColumns* p, const void* in, void
                       int in_cm, int out_cm, int kern_cm, const uint32_t* rows,
                       const uint32_t* n_rows, uint32_t row0, uint32_t row_n,
                       double scale) {
-  const size_t lds = size_t(p->n) * (p->f64 ? 16 : 8);
+  const size_t lds = FastLdsBytes(p->n, p->f64);
   const int slots = SlotsPerCu(s, p->kernel, p->threads, lds);
   if (slots < 0) {
     SetError("fast FFT columns: occupancy query failed");
@@ -763,7 +772,7 @@ int FastColumnsLaunch(rdl_session* s, const FastColumns* p, const void* in, void
 int FastRowsInverseLaunch(rdl_session* s, const FastRows* p, const void* spec, float* out,
                           const void* tw, const void* ptw, uint32_t height, uint32_t img_w, uint32_t img_h,
                           uint32_t ox, uint32_t oy, int subtract, int tiled) {
-  const size_t lds = size_t(p->n / 2) * (p->f64 ? 16 : 8);
+  const size_t lds = FastLdsBytes(p->n / 2, p->f64);
   if (SlotsPerCu(s, p->inverse, p->threads, lds) < 0) {
     SetError("fast FFT rows: occupancy query failed");
     return RDL_ERR_HIP;
@@ -788,7 +797,7 @@ int FastRowsForwardLaunch(rdl_session* s, const FastRows* p, const float* in, vo
                           const void* tw, const void* ptw, uint32_t height, uint32_t img_w, uint32_t img_h,
                           uint32_t ox, uint32_t oy, const uint32_t* rows,
                           const uint32_t* n_rows, int tiled) {
-  const size_t lds = size_t(p->n / 2) * (p->f64 ? 16 : 8);
+  const size_t lds = FastLdsBytes(p->n / 2, p->f64);
   const int slots = SlotsPerCu(s, p->forward, p->threads, lds);
   if (slots < 0) {
     SetError("fast FFT rows: occupancy query failed");

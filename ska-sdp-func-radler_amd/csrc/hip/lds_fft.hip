@@ -453,6 +453,9 @@ __global__ __launch_bounds__(kFftThreads) void ColumnsSplitB(SplitArgs a,
 // butterflies hold twice their inputs in registers, which in double spills
 // past the 128 VGPRs a 1024-thread workgroup leaves each wave (the spill
 // traffic showed up as 4-5x the algorithmic HBM writes).
+// Odd radices run first: the first pass writes its outputs R elements apart,
+// and an odd stride spreads a wave's stores over the LDS banks where a
+// power-of-two one piles them on a few (ds_write_b128: 8-way at stride 8).
 bool Factorize(uint32_t n, bool f64, std::vector<uint8_t>& radix) {
   radix.clear();
   uint32_t m = n;
@@ -460,6 +463,19 @@ bool Factorize(uint32_t n, bool f64, std::vector<uint8_t>& radix) {
   while (m % 2 == 0) {
     m /= 2;
     ++twos;
+  }
+  for (uint32_t r : {7u, 5u})
+    while (m % r == 0) {
+      m /= r;
+      radix.push_back(uint8_t(r));
+    }
+  while (!f64 && m % 9 == 0) {
+    m /= 9;
+    radix.push_back(9);
+  }
+  while (m % 3 == 0) {
+    m /= 3;
+    radix.push_back(3);
   }
   const uint32_t big2 = f64 ? 3 : 4;
   while (twos >= big2) {
@@ -469,15 +485,6 @@ bool Factorize(uint32_t n, bool f64, std::vector<uint8_t>& radix) {
   if (twos == 3) radix.push_back(8);
   if (twos == 2) radix.push_back(4);
   if (twos == 1) radix.push_back(2);
-  while (!f64 && m % 9 == 0) {
-    m /= 9;
-    radix.push_back(9);
-  }
-  for (uint32_t r : {7u, 5u, 3u})
-    while (m % r == 0) {
-      m /= r;
-      radix.push_back(uint8_t(r));
-    }
   return m == 1 && radix.size() <= kFftMaxPasses;
 }
 

@@ -38,6 +38,18 @@ FAMILY_KERNELS = {
     "find_peak": r"^void rdl::FindPeak|^rdl::FindPeakFinal",
     "integrate": r"^rdl::IntegrateKernel\(",
     "add": r"^rdl::AddKernel\(",
+    # the LDS FFT engine: float32 scale convolutions (four-step columns)
+    "conv_cols": r"rdl::ff::(ColStepA|ColStepB|Columns<float)",
+    "conv_rows": r"rdl::ff::Rows(Inverse|Forward)<float",
+}
+# families whose kernels are shared with a sibling family: measured together,
+# over the summed launches and algorithmic bytes of both (the *_sparse
+# families count a lower bound: the skipped zero rows are not known on the host)
+GROUPS = {
+    "conv64_cols+conv64_cols_sparse": (r"rdl::ff::Columns<double",
+                                       ("conv64_cols", "conv64_cols_sparse")),
+    "conv64_rows+conv64_rows_sparse": (r"rdl::ff::Rows(Inverse|Forward)<double",
+                                       ("conv64_rows", "conv64_rows_sparse")),
 }
 CALIBRATION = ("integrate", "add")
 
@@ -104,6 +116,18 @@ def main():
             "launches": n, "read_bytes_per_launch": rd / n, "write_bytes_per_launch": wr / n,
             "traffic_per_launch": (rd + wr) / n, "algorithmic_per_launch": alg,
             "traffic_over_algorithmic": (rd + wr) / n / alg if alg else None}
+    for g, (pattern, members) in GROUPS.items():
+        n = sum(fams[f]["launches"] for f in members if f in fams)
+        alg_total = sum(fams[f]["bytes"] for f in members if f in fams)
+        if not n:
+            continue
+        rd = 2.0 * family_sum(fetch, "FETCH_SIZE", pattern) * unit
+        wr = family_sum(write, "WRITE_SIZE", pattern) * unit
+        result["families"][g] = {
+            "launches": n, "read_bytes_per_launch": rd / n, "write_bytes_per_launch": wr / n,
+            "traffic_per_launch": (rd + wr) / n, "algorithmic_per_launch": alg_total / n,
+            "traffic_over_algorithmic": (rd + wr) / alg_total if alg_total else None,
+            "note": "shared kernels; sparse members count a lower bound of their bytes"}
     text = json.dumps(result, indent=1)
     if a.out:
         open(a.out, "w").write(text + "\n")
