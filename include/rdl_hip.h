@@ -270,6 +270,34 @@ int rdl_masked_add(rdl_session* s, float* d_model, const float* d_values, size_t
 int rdl_dot_pair(rdl_session* s, const float* d_a, const float* d_b, size_t n,
                  double* ab, double* aa);
 
+/* ------------------------------------------- log-polynomial spectral fit */
+/* schaapcommon's SpectralFitter in kLogPolynomial mode (the fitter behind
+ * DeconvolutionAlgorithm::PerformSpectralFit, cpp/algorithms/
+ * deconvolution_algorithm.cc:29-46, and ImageSet::InterpolateAndStoreModel,
+ * cpp/image_set.cc:238-285): S(nu) = t0 10^(t1 lg + t2 lg^2 + ...),
+ * lg = log10(nu / nu_ref), least squares over the channels in fit_mask.
+ * Non-linear, so it is passed as this description rather than as a matrix
+ * (csrc/hip/logpoly.h states the algorithm). */
+#define RDL_LOGPOLY_MAX_CHANNELS 16
+#define RDL_LOGPOLY_MAX_TERMS 8
+typedef struct {
+  uint32_t n_channels;  /* deconvolution channels (per polarization) */
+  uint32_t n_terms;     /* 1 .. RDL_LOGPOLY_MAX_TERMS */
+  uint32_t fit_mask;    /* bit c: channel c has weight > 0 and is fitted */
+  uint32_t reserved;
+  double lg[RDL_LOGPOLY_MAX_CHANNELS]; /* log10(nu_c / nu_ref) per channel */
+} rdl_logpoly;
+
+/* ImageSet::InterpolateAndStoreModel for log-polynomial fitting, one
+ * polarization: d_in holds n_channels planes of n_pixels (plane c at
+ * d_in + c * in_stride); every pixel with a non-zero value is fitted and the
+ * fit evaluated at out_lg[g] = log10(nu_g / nu_ref) into d_out + g * out_stride
+ * (zero pixels give zero). */
+int rdl_logpoly_interpolate(rdl_session* s, const float* d_in, size_t in_stride,
+                            size_t n_pixels, const rdl_logpoly* fit,
+                            const double* out_lg, uint32_t n_out, float* d_out,
+                            size_t out_stride);
+
 /* ---------------------------------------------------------------- Högbom */
 typedef struct {
   uint32_t width, height;
@@ -296,6 +324,9 @@ typedef struct {
   /* DeconvolutionAlgorithm::RmsFactorImage (W x H factors multiplied into
    * every peak search, generic_clean.cc:255-264); NULL = none */
   const float* d_rms;
+  /* log-polynomial PerformSpectralFit instead of d_spectral (host pointer,
+   * copied at the call; NULL = none) */
+  const rdl_logpoly* logpoly;
 } rdl_hogbom_params;
 
 typedef struct {
@@ -336,6 +367,9 @@ typedef struct {
    * selection and the loop's argmax (subminor_loop.cc:13-36, 143-149);
    * NULL = none */
   const float* d_rms;
+  /* log-polynomial PerformSpectralFit of each component's gain-scaled values
+   * instead of d_spectral (host pointer, copied at the call; NULL = none) */
+  const rdl_logpoly* logpoly;
 } rdl_subminor_params;
 
 typedef struct {

@@ -23,7 +23,139 @@ SpectralFit::SpectralFit(int m, size_t n, std::vector<double> f, std::vector<flo
   }
 }
 
+namespace {
+
+// x of (a + ridge * max diag) x = b by Gauss-Jordan elimination with partial
+// pivoting; false when singular
+bool SolveNormal(std::vector<double> a, std::vector<double>& b, size_t n) {
+  double big = 0.0;
+  for (size_t i = 0; i != n; ++i) big = std::max(big, a[i * n + i]);
+  if (!(big > 0.0)) return false;
+  for (size_t i = 0; i != n; ++i) a[i * n + i] += 1e-14 * big;
+  for (size_t col = 0; col != n; ++col) {
+    size_t piv = col;
+    for (size_t r = col + 1; r != n; ++r)
+      if (std::fabs(a[r * n + col]) > std::fabs(a[piv * n + col])) piv = r;
+    if (a[piv * n + col] == 0.0) return false;
+    for (size_t c = 0; c != n; ++c) std::swap(a[col * n + c], a[piv * n + c]);
+    std::swap(b[col], b[piv]);
+    for (size_t r = 0; r != n; ++r) {
+      if (r == col) continue;
+      const double f = a[r * n + col] / a[col * n + col];
+      for (size_t c = col; c != n; ++c) a[r * n + c] -= f * a[col * n + c];
+      b[r] -= f * b[col];
+    }
+  }
+  for (size_t i = 0; i != n; ++i) b[i] /= a[i * n + i];
+  return true;
+}
+
+// s 10^(a0 + a1 lg + a2 lg^2 + ...)
+double PowerLaw(const std::vector<double>& a, double s, double lg) {
+  double e = 0.0, p = 1.0;
+  for (size_t k = 0; k != a.size(); ++k) {
+    e += a[k] * p;
+    p *= lg;
+  }
+  return s * std::pow(10.0, e);
+}
+
+}  // namespace
+
+void SpectralFit::FitLogPolynomial(std::vector<float>& terms, const float* values) const {
+  terms.assign(n_terms, 0.0f);
+  std::vector<double> lg, y;
+  for (size_t i = 0; i != frequencies.size(); ++i)
+    if (weights[i] > 0.0f) {
+      lg.push_back(std::log10(frequencies[i] / reference));
+      y.push_back(values[i]);
+    }
+  const size_t m = lg.size();
+  if (m == 0 || n_terms == 0) return;
+  double mean = 0.0;
+  for (double v : y) mean += v;
+  mean /= double(m);
+  if (n_terms == 1) {
+    terms[0] = float(mean);
+    return;
+  }
+  const double s = mean >= 0.0 ? 1.0 : -1.0;
+  std::vector<size_t> pos;
+  for (size_t i = 0; i != m; ++i)
+    if (s * y[i] > 0.0) pos.push_back(i);
+  if (pos.empty()) {
+    terms[0] = float(mean);
+    return;
+  }
+  // log-space start: least squares of log10(s y) on powers of lg
+  std::vector<double> a(n_terms, 0.0);
+  size_t d = std::min(n_terms, pos.size());
+  for (;; --d) {
+    std::vector<double> g(d * d, 0.0), b(d, 0.0);
+    for (size_t i : pos) {
+      const double ly = std::log10(s * y[i]);
+      for (size_t r = 0; r != d; ++r) {
+        b[r] += std::pow(lg[i], double(r)) * ly;
+        for (size_t c = 0; c != d; ++c) g[r * d + c] += std::pow(lg[i], double(r + c));
+      }
+    }
+    if (d == 1) {
+      double acc = 0.0;
+      for (size_t i : pos) acc += std::log10(s * y[i]);
+      a[0] = acc / double(pos.size());
+      break;
+    }
+    if (SolveNormal(g, b, d)) {
+      for (size_t k = 0; k != d; ++k) a[k] = b[k];
+      break;
+    }
+  }
+  // Gauss-Newton in linear space with step halving
+  auto sse_of = [&](const std::vector<double>& p) {
+    double e = 0.0;
+    for (size_t i = 0; i != m; ++i) {
+      const double r = y[i] - PowerLaw(p, s, lg[i]);
+      e += r * r;
+    }
+    return e;
+  };
+  double sse = sse_of(a);
+  const size_t n = n_terms;
+  for (int it = 0; it != 32; ++it) {
+    std::vector<double> g(n * n, 0.0), b(n, 0.0);
+    for (size_t i = 0; i != m; ++i) {
+      const double f = PowerLaw(a, s, lg[i]);
+      for (size_t r = 0; r != n; ++r) {
+        const double jr = f * std::log(10.0) * std::pow(lg[i], double(r));
+        b[r] += jr * (y[i] - f);
+        for (size_t c = 0; c != n; ++c)
+          g[r * n + c] += jr * f * std::log(10.0) * std::pow(lg[i], double(c));
+      }
+    }
+    if (!SolveNormal(g, b, n)) break;
+    std::vector<double> trial(n);
+    double step = 1.0, next = sse;
+    bool accepted = false;
+    for (int h = 0; h != 24 && !accepted; ++h, step *= 0.5) {
+      for (size_t k = 0; k != n; ++k) trial[k] = a[k] + step * b[k];
+      next = sse_of(trial);
+      accepted = next <= sse;
+    }
+    if (!accepted) break;
+    a = trial;
+    const double change = sse - next;
+    sse = next;
+    if (!(change > 1e-13 * sse) || sse == 0.0) break;
+  }
+  terms[0] = float(s * std::pow(10.0, a[0]));
+  for (size_t k = 1; k != n; ++k) terms[k] = float(a[k]);
+}
+
 void SpectralFit::Fit(std::vector<float>& terms, const float* values) const {
+  if (mode == 2) {
+    FitLogPolynomial(terms, values);
+    return;
+  }
   terms.assign(n_terms, 0.0f);
   std::vector<long double> xs, ys, ws;
   for (size_t i = 0; i != frequencies.size(); ++i) {
@@ -66,6 +198,15 @@ void SpectralFit::Fit(std::vector<float>& terms, const float* values) const {
 
 float SpectralFit::Evaluate(const std::vector<float>& terms, double frequency) const {
   if (terms.empty()) return 0.0f;
+  if (mode == 2) {
+    const double lg = std::log10(frequency / reference);
+    double e = 0.0, p = lg;
+    for (size_t k = 1; k != terms.size(); ++k) {
+      e += double(terms[k]) * p;
+      p *= lg;
+    }
+    return float(double(terms[0]) * std::pow(10.0, e));
+  }
   const float x = float(frequency / reference - 1.0);
   float value = terms[0], power = 1.0f;
   for (size_t i = 1; i != terms.size(); ++i) {

@@ -31,7 +31,9 @@ CXX = os.environ.get("CXX", "g++")
 # float math that must match the reference bit-for-bit (scale kernels,
 # thresholds) is written with explicit std::fma where GCC contracts.
 CXX_FLAGS = ["-O2", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall",
-             "-pthread", f"-I{INCLUDE}", f"-I{os.path.join(CSRC, 'host')}"]
+             "-pthread", f"-I{INCLUDE}", f"-I{os.path.join(CSRC, 'host')}",
+             # logpoly.h: the log-polynomial fitter shared by kernels and host
+             f"-I{os.path.join(CSRC, 'hip')}"]
 
 
 def newest_header():

@@ -16,6 +16,7 @@
 // memory, so the host enqueues batches of iterations without synchronising;
 // launches after the loop ended return immediately.
 #include "rdl_internal.h"
+#include "logpoly.h"
 
 namespace rdl {
 
@@ -85,6 +86,8 @@ struct HogbomArgs {
   float gain, threshold, initial_max, divergence_limit;
   uint64_t max_iterations;
   int32_t allow_negative, stop_on_negative;
+  rdl_logpoly lp;  // log-polynomial fit (has_lp), instead of spectral
+  int32_t has_lp;
 };
 
 // Iteration pass: subtract the current component from every image inside its
@@ -164,7 +167,17 @@ __device__ void HogbomPrepare(const HogbomArgs& a, HogbomState& st) {
   }
   const uint32_t n = a.width * a.height;
   const uint32_t idx = st.peak_index;
-  for (uint32_t i = 0; i < a.n_images; ++i) {
+  if (a.has_lp) {  // log-polynomial PerformSpectralFit before the gain
+    float v[RDL_MAX_IMAGES];
+    for (uint32_t i = 0; i < a.n_images; ++i) v[i] = a.residuals[size_t(i) * n + idx];
+    lp::PerformSpectralFit(a.lp, a.n_pol, v);
+    for (uint32_t i = 0; i < a.n_images; ++i) {
+      const float f = v[i] * a.gain;
+      st.factors[i] = f;
+      a.models[size_t(i) * n + idx] += f;
+    }
+  }
+  for (uint32_t i = 0; i < a.n_images && !a.has_lp; ++i) {
     float v = a.residuals[size_t(i) * n + idx];
     if (a.spectral) {  // PerformSpectralFit before the gain (:186-189)
       v = 0.0f;
@@ -251,8 +264,17 @@ int rdl_hogbom_run(rdl_session* s, float* d_residuals, float* d_models,
   a.models = d_models;
   a.psfs = d_psfs;
   a.mask = p->d_mask;
-  a.spectral = p->d_spectral;
+  a.spectral = p->logpoly ? nullptr : p->d_spectral;
   a.rms = p->d_rms;
+  if (p->logpoly) {
+    RDL_ARG_CHECK(p->logpoly->n_channels * p->n_pol == p->n_images &&
+                      p->logpoly->n_channels <= RDL_LOGPOLY_MAX_CHANNELS &&
+                      p->logpoly->n_terms >= 1 &&
+                      p->logpoly->n_terms <= RDL_LOGPOLY_MAX_TERMS,
+                  "log-polynomial fit does not match the images");
+    a.lp = *p->logpoly;
+    a.has_lp = 1;
+  }
   a.width = p->width;
   a.height = p->height;
   a.n_images = p->n_images;

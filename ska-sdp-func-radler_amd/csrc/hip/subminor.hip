@@ -25,6 +25,7 @@
 #include <cstdlib>
 
 #include "rdl_internal.h"
+#include "logpoly.h"
 
 struct rdl_subminor {
   rdl_session* s = nullptr;
@@ -185,6 +186,8 @@ struct LoopArgs {
   int32_t use_lds;
   int32_t prof;           // accumulate per-phase cycles (block 0, wave 0)
   const float* table;     // pairwise PSF table (BuildPairTable) or nullptr
+  rdl_logpoly lp;         // log-polynomial fit (has_lp; SubminorLoop only)
+  int32_t has_lp;
 };
 
 struct LoopResult {
@@ -435,7 +438,17 @@ __global__ __launch_bounds__(kLoopThreads) void SubminorLoop(LoopArgs a) {
                     (!a.stop_on_negative || m >= 0.0f) && !diverging;
     if (!go) break;
     // next component (subminor_loop.cc:64-89)
-    if (a.spectral) {
+    if (a.has_lp) {
+      // PerformSpectralFit of the gain-scaled values (subminor_loop.cc:66-76)
+      // with the log-polynomial fitter: every thread runs the same fit on
+      // the same values (identical bits, no broadcast needed)
+      float v[NI];
+      for (int k = 0; k < NI; ++k)
+        v[k] = k < int(n_img) ? __uint_as_float(win[4 + k]) * a.gain : 0.0f;
+      lp::PerformSpectralFit(a.lp, a.n_pol, v);
+#pragma unroll
+      for (int k = 0; k < NI; ++k) c[k] = k < int(n_img) ? v[k] : 0.0f;
+    } else if (a.spectral) {
       // PerformSpectralFit of the gain-scaled values (subminor_loop.cc:66-76)
 #pragma unroll
       for (int k = 0; k < NI; ++k) {
@@ -1274,6 +1287,11 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   RDL_ARG_CHECK(p->n_images >= 1 && p->n_images <= RDL_MAX_IMAGES,
                 "n_images out of range");
   RDL_ARG_CHECK(p->n_pol >= 1 && p->n_images % p->n_pol == 0, "bad n_pol");
+  RDL_ARG_CHECK(!p->logpoly || (p->logpoly->n_channels * p->n_pol == p->n_images &&
+                                p->logpoly->n_channels <= RDL_LOGPOLY_MAX_CHANNELS &&
+                                p->logpoly->n_terms >= 1 &&
+                                p->logpoly->n_terms <= RDL_LOGPOLY_MAX_TERMS),
+                "log-polynomial fit does not match the images");
   RDL_ARG_CHECK(p->width > 0 && p->height > 0 && p->width <= 65535 &&
                     p->height <= 65535,
                 "image size out of range (1..65535)");
@@ -1353,7 +1371,10 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   uint32_t ni_t = ni <= 1 ? 1 : ni <= 2 ? 2 : ni <= 4 ? 4 : 8;
   uint32_t g = 1;
   uint64_t per = n_sel;
-  bool use_reg = ni <= 8 && h->mode != 1;
+  // the log-polynomial fit runs in the LDS-resident loop only
+  const bool lpfit = p->logpoly != nullptr;
+  const bool reg_ok = ni <= 8 && !lpfit;
+  bool use_reg = reg_ok && h->mode != 1;
   const uint64_t reg_cap = uint64_t(rdl::kRegThreads) * rdl::RegMaxItems(ni_t);
   // the size limits count PSF gathers per iteration (pixels x images): with
   // joined channels one workgroup's memory pipe, not the exchange, bounds an
@@ -1363,7 +1384,7 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   // one workgroup (up to 1024 threads) then holds selections that would
   // otherwise pay a cross-workgroup exchange per component
   const uint64_t big_cap = 1024ull * (ni_t <= 2 ? 8 : 4);
-  const bool want_table = h->mode == 0 && ni <= 8 && n_sel >= 2 && n_sel <= h->table_max &&
+  const bool want_table = h->mode == 0 && reg_ok && n_sel >= 2 && n_sel <= h->table_max &&
                           uint64_t(ni / p->n_pol) * n_sel * n_sel <= (uint64_t(1) << 27);
   // (one CU's memory pipe streams those rows: at most 8192 values per
   // iteration, so joined channels keep the grid above 8192 / N_img pixels)
@@ -1394,14 +1415,14 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   }
   // one sixteen-wave workgroup (mode 4 forces it)
   bool use_big =
-      !use_wave && ni <= 8 && h->mode != 1 && h->mode != 2 &&
+      !use_wave && reg_ok && h->mode != 1 && h->mode != 2 &&
       ((h->mode == 0 && n_sel <= big_cap &&
         ((work <= h->big_max && work > 1024) || (table_single && n_sel > 1024))) ||
        (h->mode == 4 && n_sel <= big_cap));
   // 1024-thread workgroups on a cooperative grid (mode 5, target pixels per
   // workgroup from set_tuning; mode 0 when big_target is set)
   bool use_big_grid = false;
-  if (!use_wave && !use_big && ni <= 8 &&
+  if (!use_wave && !use_big && reg_ok &&
       ((h->mode == 5) || (h->mode == 0 && h->big_target > 0 && n_sel > h->big_max))) {
     const uint64_t target = h->mode == 5 ? std::max<uint32_t>(h->target_per_block, 1024)
                                          : h->big_target;
@@ -1463,8 +1484,12 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   la.integ = p->integ;
   la.threshold = p->threshold;
   la.gain = p->gain;
-  la.spectral = p->d_spectral;
+  la.spectral = lpfit ? nullptr : p->d_spectral;
   la.rms = p->d_rms;
+  if (lpfit) {
+    la.lp = *p->logpoly;
+    la.has_lp = 1;
+  }
   la.divergence_limit = p->divergence_limit;
   la.iteration_start = p->iteration_start;
   la.max_iterations = p->max_iterations;

@@ -82,6 +82,7 @@ class DeconvolutionAlgorithm {
     spectral_fitter_ = std::move(fitter);
     n_polarizations_ = n_polarizations;
     spectral_map_.reset();
+    has_logpoly_ = spectral_fitter_ && MakeLogPoly(*spectral_fitter_, &logpoly_);
   }
   const schaapcommon::fitters::SpectralFitter& Fitter() const {
     return *spectral_fitter_;
@@ -106,6 +107,8 @@ class DeconvolutionAlgorithm {
         iteration_number_(o.iteration_number_),
         spectral_fitter_(o.spectral_fitter_),
         n_polarizations_(o.n_polarizations_),
+        logpoly_(o.logpoly_),
+        has_logpoly_(o.has_logpoly_),
         rms_factor_(o.rms_factor_) {}
 
   /// Device copy (uint8) of CleanMask() for the current call, or nullptr.
@@ -118,6 +121,10 @@ class DeconvolutionAlgorithm {
   /// loops (rdl_subminor_params / rdl_hogbom_params d_spectral); nullptr
   /// when the fit leaves values unchanged.
   const float* DeviceSpectralMap(gpu::Session& s, size_t n_images);
+  /// The log-polynomial fit's description for the device loops
+  /// (rdl_subminor_params / rdl_hogbom_params logpoly), or nullptr for the
+  /// other modes (which DeviceSpectralMap covers).
+  const rdl_logpoly* LogPolyFit() const { return has_logpoly_ ? &logpoly_ : nullptr; }
   /// Device copy of RmsFactorImage() on session s, or nullptr.
   const float* DeviceRmsFactor(gpu::Session& s, size_t width, size_t height);
   /// The peak-search input: d_image itself, or d_image x the RMS factor in
@@ -144,6 +151,8 @@ class DeconvolutionAlgorithm {
   std::shared_ptr<gpu::Buffer> mask_buffer_;
   std::shared_ptr<const schaapcommon::fitters::SpectralFitter> spectral_fitter_;
   size_t n_polarizations_ = 1;
+  rdl_logpoly logpoly_{};
+  bool has_logpoly_ = false;
   std::shared_ptr<gpu::Buffer> spectral_map_;
   size_t spectral_map_images_ = 0;
   bool spectral_map_identity_ = false;

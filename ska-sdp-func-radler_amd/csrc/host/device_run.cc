@@ -85,9 +85,9 @@ DeviceRun::DeviceRun(const Settings& settings, const float* psf,
      // 100 MHz + c x 10 MHz
     using schaapcommon::fitters::SpectralFittingMode;
     const SpectralFittingMode mode = settings.spectral_fitting.mode;
-    if (mode == SpectralFittingMode::kLogPolynomial ||
-        mode == SpectralFittingMode::kForcedTerms)
-      throw std::runtime_error("DeviceRun: only polynomial spectral fitting is available");
+    if (mode == SpectralFittingMode::kForcedTerms)
+      throw std::runtime_error(
+          "DeviceRun: forced-term spectral fitting is not available");
     std::vector<double> frequencies;
     std::vector<float> channel_weights;
     if (mode != SpectralFittingMode::kNoFitting)

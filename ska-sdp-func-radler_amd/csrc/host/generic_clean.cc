@@ -66,6 +66,21 @@ void GenericClean::FitSpectra(ImageSet& model_set) {
   // the per-component matrix)
   gpu::Session& s = model_set.Session();
   const size_t n_img = model_set.Size(), n = model_set.Width() * model_set.Height();
+  if (const rdl_logpoly* lp = LogPolyFit()) {
+    // the non-linear fit per pixel and polarization, evaluated at the
+    // deconvolution channels themselves
+    const size_t n_pol = model_set.NPolarizations();
+    const std::vector<double> lg(lp->lg, lp->lg + lp->n_channels);
+    gpu::Buffer out(s, lp->n_channels * n * sizeof(float));
+    for (size_t p = 0; p != n_pol; ++p) {
+      gpu::Check(rdl_logpoly_interpolate(s.Handle(), model_set.Data(p), n_pol * n, n, lp,
+                                         lg.data(), lp->n_channels, out.F(), n),
+                 "rdl_logpoly_interpolate");
+      for (size_t c = 0; c != lp->n_channels; ++c)
+        s.D2D(model_set.Data(c * n_pol + p), out.F() + c * n, n * sizeof(float));
+    }
+    return;
+  }
   const float* d_map = DeviceSpectralMap(s, n_img);
   if (!d_map) return;
   std::vector<float> map(n_img * n_img);
@@ -128,6 +143,7 @@ DeconvolutionResult GenericClean::ExecuteMajorIteration(
     sub.SetDivergenceLimit(DivergenceLimit());
     sub.SetMask(d_mask);
     sub.SetSpectralMap(DeviceSpectralMap(s, dirty_set.Size()));
+    sub.SetLogPolyFit(LogPolyFit());
     sub.SetRmsFactor(DeviceRmsFactor(s, width, height));  // :126-128
     sub.SetCleanBorders(size_t(std::round(width * CleanBorderRatio())),
                         size_t(std::round(height * CleanBorderRatio())));
@@ -170,6 +186,7 @@ DeconvolutionResult GenericClean::ExecuteMajorIteration(
     p.v_border = uint32_t(std::round(height * CleanBorderRatio()));
     p.d_mask = d_mask;
     p.d_spectral = DeviceSpectralMap(s, dirty_set.Size());
+    p.logpoly = LogPolyFit();
     p.d_rms = DeviceRmsFactor(s, width, height);
     p.start_x = max_value.x;
     p.start_y = max_value.y;

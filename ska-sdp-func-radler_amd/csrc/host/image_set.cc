@@ -302,6 +302,35 @@ void ImageSet::InterpolateAndStoreModel(
     }
     return;
   }
+  rdl_logpoly lp;
+  if (fitter && MakeLogPoly(*fitter, &lp)) {
+    // the non-linear fit per non-zero pixel (image_set.cc:238-268), evaluated
+    // at every original channel of the polarization (:270-285)
+    if (lp.n_channels != NDeconvolutionChannels())
+      throw std::runtime_error(
+          "InterpolateAndStoreModel: the fitter's channels do not match the image set");
+    const size_t n_orig = NOriginalChannels();
+    const size_t chunk = std::min<size_t>(n_orig, RDL_MAX_IMAGES);
+    gpu::Buffer out(*session_, chunk * PlaneSize() * sizeof(float));
+    for (size_t p = 0; p != n_pol_; ++p) {
+      for (size_t g0 = 0; g0 < n_orig; g0 += chunk) {
+        const size_t n_out = std::min(chunk, n_orig - g0);
+        std::vector<double> out_lg;
+        for (size_t g = g0; g != g0 + n_out; ++g)
+          out_lg.push_back(std::log10(table_.OriginalGroups()[g][p]->CentralFrequency() /
+                                      fitter->ReferenceFrequency()));
+        gpu::Check(rdl_logpoly_interpolate(session_->Handle(), Data(p), n_pol_ * PlaneSize(),
+                                           PlaneSize(), &lp, out_lg.data(), uint32_t(n_out),
+                                           out.F(), PlaneSize()),
+                   "rdl_logpoly_interpolate");
+        for (size_t g = g0; g != g0 + n_out; ++g) {
+          session_->D2H(host, out.F() + (g - g0) * PlaneSize(), PlaneSize() * sizeof(float));
+          table_.OriginalGroups()[g][p]->model_accessor->Store(host);
+        }
+      }
+    }
+    return;
+  }
   const SpectralMaps maps = fitter ? MakeSpectralMaps(*fitter) : SpectralMaps{};
   if (maps.Empty()) {
     // kNoFitting (schaapcommon's fitter would evaluate nothing here; parity

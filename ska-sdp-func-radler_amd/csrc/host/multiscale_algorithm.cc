@@ -467,6 +467,7 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
                            scale_border));
       sub.SetMask(MaskFor(scale_with_peak));
       sub.SetSpectralMap(DeviceSpectralMap(session, data_image.Size()));
+      sub.SetLogPolyFit(LogPolyFit());
       sub.SetRmsFactor(DeviceRmsFactor(session, width, height));  // :401-402
       std::vector<uint32_t> xy;
       sub.SetTrace(&xy);

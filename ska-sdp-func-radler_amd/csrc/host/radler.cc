@@ -280,9 +280,6 @@ void Radler::InitializeDeconvolutionAlgorithm(
     beam_size_ = 0.0;
   }
   if (settings_.spectral_fitting.mode ==
-      schaapcommon::fitters::SpectralFittingMode::kLogPolynomial)
-    Unsupported("Logarithmic polynomial spectral fitting");
-  if (settings_.spectral_fitting.mode ==
       schaapcommon::fitters::SpectralFittingMode::kForcedTerms)
     Unsupported("Forced-term spectral fitting (a FITS spectral-term cube)");
   if (!settings_.fits_mask.empty() || !settings_.casa_mask.empty() ||

@@ -4,6 +4,9 @@
 #include <cfloat>
 #include <cmath>
 #include <stdexcept>
+#include <string>
+
+#include "logpoly.h"
 
 namespace radler {
 namespace {
@@ -159,6 +162,27 @@ std::vector<float> ComponentFitMatrix(
   return g;
 }
 
+bool MakeLogPoly(const schaapcommon::fitters::SpectralFitter& f, rdl_logpoly* out) {
+  if (f.Mode() != schaapcommon::fitters::SpectralFittingMode::kLogPolynomial) return false;
+  const std::vector<double>& freqs = f.Frequencies();
+  const std::vector<float>& weights = f.Weights();
+  if (freqs.empty() || freqs.size() > RDL_LOGPOLY_MAX_CHANNELS)
+    throw std::runtime_error("Log-polynomial spectral fitting supports 1 to " +
+                             std::to_string(RDL_LOGPOLY_MAX_CHANNELS) + " channels");
+  if (f.NTerms() < 1 || f.NTerms() > RDL_LOGPOLY_MAX_TERMS)
+    throw std::runtime_error("Log-polynomial spectral fitting supports 1 to " +
+                             std::to_string(RDL_LOGPOLY_MAX_TERMS) + " terms");
+  rdl_logpoly lp{};
+  lp.n_channels = uint32_t(freqs.size());
+  lp.n_terms = uint32_t(f.NTerms());
+  for (size_t c = 0; c != freqs.size(); ++c) {
+    if (c < weights.size() && weights[c] > 0.0f) lp.fit_mask |= 1u << c;
+    lp.lg[c] = std::log10(freqs[c] / f.ReferenceFrequency());
+  }
+  *out = lp;
+  return true;
+}
+
 }  // namespace radler
 
 #ifndef RADLER_AMD_USE_EXTERNAL_AOCOMMON
@@ -195,18 +219,26 @@ void SpectralFitter::Fit(std::vector<float>& terms, const float* values, size_t,
       }
       return;
     }
-    case SpectralFittingMode::kLogPolynomial:
+    case SpectralFittingMode::kLogPolynomial: {
+      rdl_logpoly lp;
+      radler::MakeLogPoly(*this, &lp);
+      terms.assign(n_terms_, 0.0f);
+      rdl::lp::Fit(lp, values, terms.data());
+      return;
+    }
     case SpectralFittingMode::kForcedTerms:
       break;
   }
   throw std::runtime_error(
-      "SpectralFitter: only no_fitting and polynomial fitting are available in "
-      "the MI355X build");
+      "SpectralFitter: forced-term fitting is not available in the MI355X build");
 }
 
 float SpectralFitter::Evaluate(const std::vector<float>& terms,
                                double frequency) const {
   if (terms.empty()) return 0.0f;
+  if (mode_ == SpectralFittingMode::kLogPolynomial)
+    return rdl::lp::Evaluate(terms.data(), int(terms.size()),
+                             std::log10(frequency / reference_frequency_));
   const float x = float(frequency / reference_frequency_ - 1.0);
   float value = terms[0], power = 1.0f;
   for (size_t i = 1; i != terms.size(); ++i) {

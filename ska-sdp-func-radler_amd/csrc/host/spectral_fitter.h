@@ -8,8 +8,12 @@
 //                  x = frequency / reference_frequency - 1 over the channels
 //                  with weight > 0 (at most one term per such channel), then
 //                  evaluated at every channel frequency.
-// kLogPolynomial (a non-linear power-law fit) and kForcedTerms (terms read
-// from a FITS cube) stay unavailable: Radler rejects them with an error.
+//   kLogPolynomial S = t0 10^(t1 lg + t2 lg^2 + ...), lg = log10(f / ref),
+//                  a non-linear least-squares fit over the same channels
+//                  (csrc/hip/logpoly.h states it; the same code runs in the
+//                  device loops, so host and device fits agree).
+// kForcedTerms (terms read from a FITS cube) stays unavailable: Radler
+// rejects it with an error.
 //
 // Fitting then evaluating a polynomial at fixed frequencies and weights is a
 // linear map of the channel values, independent of the pixel. SpectralMaps
@@ -23,6 +27,7 @@
 #include <vector>
 
 #include "aocommon_compat.h"
+#include "rdl_hip.h"
 
 #ifndef RADLER_AMD_USE_EXTERNAL_AOCOMMON
 namespace schaapcommon::fitters {
@@ -99,5 +104,9 @@ std::vector<double> PseudoInverse(std::vector<double> a, size_t m, size_t p);
 /// fitter leaves values unchanged.
 std::vector<float> ComponentFitMatrix(
     const schaapcommon::fitters::SpectralFitter& f, size_t n_pol);
+
+/// The device description of a kLogPolynomial fitter (false for the other
+/// modes); throws when the channel or term count exceeds the device limits.
+bool MakeLogPoly(const schaapcommon::fitters::SpectralFitter& f, rdl_logpoly* out);
 
 }  // namespace radler

@@ -35,6 +35,7 @@ SubMinorLoop::RunResult SubMinorLoop::Run(ImageSet& residual,
   p.max_iterations = max_iterations_;
   p.d_mask = d_mask_;
   p.d_spectral = d_spectral_;
+  p.logpoly = logpoly_;
   p.d_rms = d_rms_;
   n_images_ = residual.Size();
   uint64_t cap = 0;

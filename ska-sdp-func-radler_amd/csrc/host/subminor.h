@@ -38,6 +38,9 @@ class SubMinorLoop {
   /// _parentAlgorithm->PerformSpectralFit (subminor_loop.cc:76) as a device
   /// matrix (DeconvolutionAlgorithm::DeviceSpectralMap), nullptr = none.
   void SetSpectralMap(const float* d_map) { d_spectral_ = d_map; }
+  /// The same fit when it is log-polynomial (non-linear: no matrix);
+  /// nullptr = none.
+  void SetLogPolyFit(const rdl_logpoly* fit) { logpoly_ = fit; }
   /// SetRmsFactorImage (subminor_loop.h:162-164): the full-image device
   /// factor plane, nullptr = none.
   void SetRmsFactor(const float* d_rms) { d_rms_ = d_rms; }
@@ -97,6 +100,7 @@ class SubMinorLoop {
   bool allow_negative_ = true, stop_on_negative_ = false;
   const uint8_t* d_mask_ = nullptr;
   const float* d_spectral_ = nullptr;
+  const rdl_logpoly* logpoly_ = nullptr;
   const float* d_rms_ = nullptr;
   float flux_cleaned_ = 0.0f;
   size_t n_selected_ = 0, n_images_ = 0;

@@ -67,7 +67,8 @@ class HogbomParams(C.Structure):
                 ("v_border", C.c_uint32), ("d_mask", C.c_void_p),
                 ("start_x", C.c_uint32), ("start_y", C.c_uint32),
                 ("start_value", C.c_float), ("start_found", C.c_int32),
-                ("d_spectral", C.c_void_p), ("d_rms", C.c_void_p)]
+                ("d_spectral", C.c_void_p), ("d_rms", C.c_void_p),
+                ("logpoly", C.c_void_p)]
 
 
 class HogbomResult(C.Structure):
@@ -83,13 +84,33 @@ class SubminorParams(C.Structure):
                 ("gain", C.c_float), ("divergence_limit", C.c_float),
                 ("iteration_start", C.c_uint64), ("max_iterations", C.c_uint64),
                 ("d_mask", C.c_void_p), ("d_spectral", C.c_void_p),
-                ("d_rms", C.c_void_p)]
+                ("d_rms", C.c_void_p), ("logpoly", C.c_void_p)]
 
 
 class SubminorResult(C.Structure):
     _fields_ = [("n_selected", C.c_uint64), ("iteration", C.c_uint64),
                 ("has_peak", C.c_int32), ("peak", C.c_float), ("diverging", C.c_int32),
                 ("flux_cleaned", C.c_float)]
+
+
+class LogPoly(C.Structure):
+    """rdl_logpoly: the log-polynomial fitter's description."""
+    _fields_ = [("n_channels", C.c_uint32), ("n_terms", C.c_uint32),
+                ("fit_mask", C.c_uint32), ("reserved", C.c_uint32),
+                ("lg", C.c_double * 16)]
+
+
+def logpoly(frequencies, weights, n_terms):
+    """The rdl_logpoly of a fitter (reference = weighted mean frequency)."""
+    f = np.asarray(frequencies, np.float64)
+    w = np.asarray(weights, np.float32)
+    ref = np.sum(f * w) / np.sum(w) if np.sum(w) > 0 else np.mean(f)
+    lp = LogPoly()
+    lp.n_channels, lp.n_terms = len(f), n_terms
+    lp.fit_mask = sum(1 << c for c in range(len(f)) if w[c] > 0)
+    for c in range(len(f)):
+        lp.lg[c] = np.log10(f[c] / ref)
+    return lp
 
 
 class RdlError(RuntimeError):
