@@ -50,6 +50,10 @@ struct rdl_subminor {
   uint32_t table_max = 16384;         // largest selection given a pairwise PSF table
   void* table = nullptr;              // [n_psf][n_sel][n_sel] PSF values at the
   size_t table_bytes = 0;             //   selected pixels' pairwise offsets
+  void* pos_buf = nullptr;            // single-pass selection: positions
+  size_t pos_bytes = 0;
+  int select_passes = 1;              // 1 single pass, 3 count + scan + scatter
+  int select_ticket = 1;              // single pass: chunk order by ticket
 };
 
 namespace rdl {
@@ -70,12 +74,39 @@ struct SelArgs {
   const float* rms;  // RMS factor image (W x H) or nullptr
 };
 
-__device__ __forceinline__ bool Selected(const SelArgs& a, uint64_t b,
+// A thread's box position, advanced by a fixed stride without dividing (a
+// 64-bit divide per pixel made the selection passes ALU-bound).
+struct BoxWalker {
+  uint64_t b;
+  uint32_t x, y;  // inside the box
+  __device__ BoxWalker(const SelArgs& a, uint64_t b0)
+      : b(b0), x(uint32_t(b0 % a.bw)), y(uint32_t(b0 / a.bw)) {}
+  __device__ void Advance(const SelArgs& a, uint32_t stride) {
+    b += stride;
+    x += stride;
+    while (x >= a.bw) {
+      x -= a.bw;
+      ++y;
+    }
+  }
+};
+
+// the selection test of pixel idx whose first image's residual v0 the
+// caller loaded (so a thread's loads can all be in flight at once)
+__device__ __forceinline__ bool SelectedValue(const SelArgs& a, uint32_t idx, float v0) {
+  if (a.mask && !a.mask[idx]) return false;
+  float v = IntegratePixel(a.integ, [&](uint32_t k) {
+    return k == 0 ? v0 : a.residuals[size_t(k) * a.n + idx];
+  });
+  if (a.rms) v *= a.rms[idx];  // integratedScratch *= rms (subminor_loop.cc:147-149)
+  const float value = a.allow_negative ? fabsf(v) : v;
+  return value >= a.threshold;
+}
+
+__device__ __forceinline__ bool Selected(const SelArgs& a, const BoxWalker& w,
                                          uint32_t& idx) {
-  if (b >= a.box_pixels) return false;
-  const uint32_t x = a.xs + uint32_t(b % a.bw);
-  const uint32_t y = a.ys + uint32_t(b / a.bw);
-  idx = y * a.width + x;
+  if (w.b >= a.box_pixels) return false;
+  idx = (a.ys + w.y) * a.width + a.xs + w.x;
   if (a.mask && !a.mask[idx]) return false;
   float v = IntegratePixel(
       a.integ, [&](uint32_t k) { return a.residuals[size_t(k) * a.n + idx]; });
@@ -89,10 +120,21 @@ __global__ __launch_bounds__(kSelThreads) void SelCount(SelArgs a,
   __shared__ uint32_t lds[kSelThreads / 64];
   uint32_t c = 0;
   const uint64_t base = uint64_t(blockIdx.x) * kChunk;
-  for (uint32_t j = threadIdx.x; j < kChunk; j += kSelThreads) {
-    uint32_t idx;
-    c += Selected(a, base + j, idx) ? 1u : 0u;
+  BoxWalker bw(a, base + threadIdx.x);
+  constexpr uint32_t kItems = kChunk / kSelThreads;
+  uint32_t idx[kItems];
+  float v0[kItems];
+#pragma unroll
+  for (uint32_t i = 0; i < kItems; ++i) {
+    idx[i] = bw.b < a.box_pixels ? (a.ys + bw.y) * a.width + a.xs + bw.x : 0xffffffffu;
+    bw.Advance(a, kSelThreads);
   }
+#pragma unroll
+  for (uint32_t i = 0; i < kItems; ++i)
+    v0[i] = a.residuals[idx[i] == 0xffffffffu ? 0u : idx[i]];
+#pragma unroll
+  for (uint32_t i = 0; i < kItems; ++i)
+    c += (idx[i] != 0xffffffffu && SelectedValue(a, idx[i], v0[i])) ? 1u : 0u;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
   if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = c;
@@ -105,30 +147,31 @@ __global__ __launch_bounds__(kSelThreads) void SelCount(SelArgs a,
 }
 
 // Exclusive scan of the chunk counts in one workgroup; writes the total.
+// Thread t owns the contiguous segment [t seg, (t + 1) seg): sums it, one
+// block scan of the 1024 sums, then rewrites its segment as offsets.
 __global__ __launch_bounds__(1024) void SelScan(uint32_t* counts, uint32_t n,
                                                 uint64_t* total) {
   __shared__ uint64_t lds[1024];
-  __shared__ uint64_t carry;
-  if (threadIdx.x == 0) carry = 0;
+  const uint32_t t = threadIdx.x;
+  const uint32_t seg = (n + 1023) / 1024;
+  const uint32_t lo = min(n, t * seg), hi = min(n, lo + seg);
+  uint64_t sum = 0;
+  for (uint32_t i = lo; i < hi; ++i) sum += counts[i];
+  lds[t] = sum;
   __syncthreads();
-  for (uint32_t base = 0; base < n; base += 1024) {
-    const uint32_t i = base + threadIdx.x;
-    const uint64_t v = i < n ? counts[i] : 0;
-    lds[threadIdx.x] = v;
+  for (uint32_t off = 1; off < 1024; off <<= 1) {
+    const uint64_t v = t >= off ? lds[t - off] : 0;
     __syncthreads();
-    for (uint32_t off = 1; off < 1024; off <<= 1) {
-      const uint64_t t = threadIdx.x >= off ? lds[threadIdx.x - off] : 0;
-      __syncthreads();
-      lds[threadIdx.x] += t;
-      __syncthreads();
-    }
-    const uint64_t incl = lds[threadIdx.x];
-    if (i < n) counts[i] = uint32_t(carry + incl - v);
-    __syncthreads();
-    if (threadIdx.x == 1023) carry += incl;
+    lds[t] += v;
     __syncthreads();
   }
-  if (threadIdx.x == 0) *total = carry;
+  uint64_t run = lds[t] - sum;  // exclusive
+  for (uint32_t i = lo; i < hi; ++i) {
+    const uint32_t c = counts[i];
+    counts[i] = uint32_t(run);
+    run += c;
+  }
+  if (t == 1023) *total = lds[1023];
 }
 
 __global__ __launch_bounds__(kSelThreads) void SelScatter(
@@ -138,9 +181,11 @@ __global__ __launch_bounds__(kSelThreads) void SelScatter(
   const uint64_t base = uint64_t(blockIdx.x) * kChunk;
   uint32_t running = offsets[blockIdx.x];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  BoxWalker bw(a, base + threadIdx.x);
   for (uint32_t j0 = 0; j0 < kChunk; j0 += kSelThreads) {
     uint32_t idx = 0;
-    const bool sel = Selected(a, base + j0 + threadIdx.x, idx);
+    const bool sel = Selected(a, bw, idx);
+    bw.Advance(a, kSelThreads);
     const uint64_t ballot = __ballot(sel);
     const uint32_t before = __popcll(ballot & ((1ull << lane) - 1ull));
     if (lane == 0) wave_tot[wave] = __popcll(ballot);
@@ -158,6 +203,140 @@ __global__ __launch_bounds__(kSelThreads) void SelScatter(
     }
     running += step;
     __syncthreads();
+  }
+}
+
+// Single-pass selection (replaces SelCount + SelScan + SelScatter): each
+// workgroup takes the next chunk in launch order (a ticket), flags its
+// pixels once, publishes its count, and finds its output offset by
+// decoupled look-back over its predecessors' published counts / prefixes
+// (status words {flag, value}, single-copy-atomic 8-byte stores; flag 1 =
+// the chunk's count, 2 = the inclusive prefix). Positions only; the residual
+// values follow in SelGather once the host knows the count. One read of the
+// box instead of two, no scan launch. Output order = ascending box order,
+// as the three-kernel path.
+constexpr uint32_t kSpThreads = 512;
+constexpr uint32_t kSelItems = 16;
+constexpr uint32_t kSpChunk = kSpThreads * kSelItems;  // box pixels per workgroup
+constexpr uint64_t kStatusAggregate = uint64_t(1) << 32;
+constexpr uint64_t kStatusPrefix = uint64_t(2) << 32;
+
+__global__ __launch_bounds__(kSpThreads) void SelSinglePass(SelArgs a, uint32_t* ticket,
+                                                             uint64_t* status,
+                                                             uint32_t n_chunks, uint32_t* pos,
+                                                             uint64_t* total) {
+  __shared__ uint32_t chunk_s;
+  __shared__ uint32_t wave_tot[kSelItems][kSpThreads / 64];
+  __shared__ uint32_t excl_s;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  // ticket: chunks in the order workgroups start (NULL: blockIdx, which the
+  // dispatcher hands out in order on each XCD)
+  if (tid == 0) chunk_s = ticket ? atomicAdd(ticket, 1u) : blockIdx.x;
+  __syncthreads();
+  const uint32_t b = chunk_s;
+  const uint64_t base = uint64_t(b) * kSpChunk;
+  uint64_t ballots[kSelItems];
+  uint32_t idx[kSelItems];
+  BoxWalker bw(a, base + tid);
+  float v0[kSelItems];
+#pragma unroll
+  for (uint32_t i = 0; i < kSelItems; ++i) {
+    idx[i] = bw.b < a.box_pixels ? (a.ys + bw.y) * a.width + a.xs + bw.x : 0xffffffffu;
+    bw.Advance(a, kSpThreads);
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < kSelItems; ++i)  // every load in flight at once
+    v0[i] = a.residuals[idx[i] == 0xffffffffu ? 0u : idx[i]];
+#pragma unroll
+  for (uint32_t i = 0; i < kSelItems; ++i) {
+    const bool sel = idx[i] != 0xffffffffu && SelectedValue(a, idx[i], v0[i]);
+    ballots[i] = __ballot(sel);
+    if (lane == 0) wave_tot[i][wave] = uint32_t(__popcll(ballots[i]));
+  }
+  __syncthreads();
+  uint32_t count = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < kSelItems; ++i)
+#pragma unroll
+    for (uint32_t w = 0; w < kSpThreads / 64; ++w) count += wave_tot[i][w];
+  if (wave == 0) {
+    uint64_t excl = 0;
+    if (b == 0) {
+      if (lane == 0)
+        __hip_atomic_store(&status[0], kStatusPrefix | count, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      if (lane == 0)
+        __hip_atomic_store(&status[b], kStatusAggregate | count, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      // look back 64 predecessors at a time (lane l: chunk b - 1 - l)
+      int64_t p = int64_t(b) - 1 - int64_t(lane);
+      uint64_t spins = 0;
+      while (true) {
+        uint64_t st = p >= 0 ? __hip_atomic_load(&status[p], __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)
+                             : kStatusPrefix;  // before chunk 0: prefix 0
+        // every predecessor publishes its count before it looks back
+        while (!__all((st >> 32) != 0u)) {
+          __builtin_amdgcn_s_sleep(1);
+          if ((st >> 32) == 0u)
+            st = __hip_atomic_load(&status[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (++spins > (uint64_t(1) << 26)) break;  // never expected; ends the wave
+        }
+        const uint64_t pm = __ballot((st >> 32) == 2u);
+        const uint32_t v = uint32_t(st);
+        if (pm) {
+          const uint32_t first = uint32_t(__builtin_ctzll(pm));  // nearest prefix
+          uint64_t part = lane <= first ? uint64_t(v) : 0ull;
+#pragma unroll
+          for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off, 64);
+          excl += part;
+          break;
+        }
+        uint64_t part = v;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off, 64);
+        excl += part;
+        p -= 64;
+        if (spins > (uint64_t(1) << 26)) break;
+      }
+      if (lane == 0)
+        __hip_atomic_store(&status[b], kStatusPrefix | uint32_t(excl + count),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0) {
+      excl_s = uint32_t(excl);
+      if (b == n_chunks - 1) *total = excl + count;
+    }
+  }
+  __syncthreads();
+  uint32_t o = excl_s;
+#pragma unroll
+  for (uint32_t i = 0; i < kSelItems; ++i) {
+    uint32_t woff = 0, step = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kSpThreads / 64; ++w) {
+      woff += w < wave ? wave_tot[i][w] : 0u;
+      step += wave_tot[i][w];
+    }
+    if ((ballots[i] >> lane) & 1ull) {
+      const uint32_t before = uint32_t(__popcll(ballots[i] & ((1ull << lane) - 1ull)));
+      const uint32_t x = idx[i] % a.width, y = idx[i] / a.width;
+      pos[o + woff + before] = (y << 16) | x;
+    }
+    o += step;
+  }
+}
+
+// the selected pixels' residual values, [image][n_sel]
+__global__ __launch_bounds__(256) void SelGather(const float* residuals, uint32_t width,
+                                                 uint32_t n, const uint32_t* pos,
+                                                 uint64_t n_sel, uint32_t n_img, float* r) {
+  for (uint64_t j = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; j < n_sel;
+       j += uint64_t(gridDim.x) * blockDim.x) {
+    const uint32_t p = pos[j];
+    const uint32_t idx = (p >> 16) * width + (p & 0xffffu);
+    for (uint32_t k = 0; k < n_img; ++k) r[k * n_sel + j] = residuals[size_t(k) * n + idx];
   }
 }
 
@@ -1261,6 +1440,12 @@ int rdl_subminor_create(rdl_session* s, rdl_subminor** out) {
     h->big_max = uint32_t(std::strtoul(e, nullptr, 10));
   if (const char* e = std::getenv("RDL_SUBMINOR_BIG_TARGET"))
     h->big_target = uint32_t(std::strtoul(e, nullptr, 10));
+  // RDL_SUBMINOR_SELECT=3: the count + scan + scatter selection
+  if (const char* e = std::getenv("RDL_SUBMINOR_SELECT")) {
+    const int v = std::atoi(e);
+    h->select_passes = v == 3 ? 3 : 1;
+    h->select_ticket = v == 2 ? 0 : 1;  // 2: single pass ordered by blockIdx
+  }
   // RDL_SUBMINOR_TABLE_MAX=0 keeps the per-iteration PSF gathers
   if (const char* e = std::getenv("RDL_SUBMINOR_TABLE_MAX"))
     h->table_max = uint32_t(std::strtoul(e, nullptr, 10));
@@ -1273,6 +1458,7 @@ int rdl_subminor_destroy(rdl_subminor* h) {
   (void)hipStreamSynchronize(h->s->stream);
   if (h->counts) (void)hipFree(h->counts);
   if (h->sel) (void)hipFree(h->sel);
+  if (h->pos_buf) (void)hipFree(h->pos_buf);
   if (h->sync) (void)hipFree(h->sync);
   if (h->table) (void)hipFree(h->table);
   delete h;
@@ -1322,14 +1508,28 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   sa.threshold = p->threshold;
   sa.allow_negative = p->allow_negative;
   sa.rms = p->d_rms;
-  const uint32_t n_chunks =
-      std::max<uint32_t>(1, rdl::DivUp(sa.box_pixels, rdl::kChunk));
-  RDL_TRY(rdl::Grow(&h->counts, &h->counts_bytes,
-                    size_t(n_chunks) * sizeof(uint32_t) + 64, st));
-  uint32_t* counts = static_cast<uint32_t*>(h->counts);
+  const uint32_t n_chunks = std::max<uint32_t>(
+      1, rdl::DivUp(sa.box_pixels, h->select_passes == 1 ? rdl::kSpChunk : rdl::kChunk));
   uint64_t* d_total = reinterpret_cast<uint64_t*>(s->d_small);
   const double sel_bytes = double(sa.box_pixels) * 4.0 * p->n_images;
-  {
+  // positions of up to the whole box (single pass) or the counts (three
+  // kernels: RDL_SUBMINOR_SELECT=3, for comparison)
+  uint32_t* counts = nullptr;
+  if (h->select_passes == 1) {
+    RDL_TRY(rdl::Grow(&h->counts, &h->counts_bytes,
+                      size_t(n_chunks) * sizeof(uint64_t) + 64, st));
+    RDL_TRY(rdl::Grow(&h->pos_buf, &h->pos_bytes,
+                      std::max<size_t>(sa.box_pixels, 1) * sizeof(uint32_t), st));
+    uint64_t* status = static_cast<uint64_t*>(h->counts);
+    uint32_t* ticket = reinterpret_cast<uint32_t*>(status + n_chunks);
+    RDL_HIP_CHECK(hipMemsetAsync(status, 0, size_t(n_chunks) * sizeof(uint64_t) + 64, st));
+    rdl::ScopedTiming t(s, "subminor_select", sel_bytes);
+    rdl::SelSinglePass<<<n_chunks, rdl::kSpThreads, 0, st>>>(
+        sa, h->select_ticket ? ticket : nullptr, status, n_chunks, static_cast<uint32_t*>(h->pos_buf), d_total);
+  } else {
+    RDL_TRY(rdl::Grow(&h->counts, &h->counts_bytes,
+                      size_t(n_chunks) * sizeof(uint32_t) + 64, st));
+    counts = static_cast<uint32_t*>(h->counts);
     rdl::ScopedTiming t(s, "subminor_select", 2.0 * sel_bytes);
     rdl::SelCount<<<n_chunks, rdl::kSelThreads, 0, st>>>(sa, counts);
     rdl::SelScan<<<1, 1024, 0, st>>>(counts, n_chunks, d_total);
@@ -1351,13 +1551,23 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
     return RDL_OK;
   }
   const uint32_t ni = p->n_images;
-  const size_t sel_need = n_sel * sizeof(uint32_t) + 2 * n_sel * ni * sizeof(float) + 256;
-  RDL_TRY(rdl::Grow(&h->sel, &h->sel_bytes, sel_need, st));
-  h->d_pos = static_cast<uint32_t*>(h->sel);
-  h->d_r = reinterpret_cast<float*>(
-      static_cast<char*>(h->sel) + (n_sel * sizeof(uint32_t) + 15) / 16 * 16);
-  h->d_m = h->d_r + n_sel * ni;
-  {
+  if (h->select_passes == 1) {
+    RDL_TRY(rdl::Grow(&h->sel, &h->sel_bytes, 2 * n_sel * ni * sizeof(float) + 256, st));
+    h->d_pos = static_cast<uint32_t*>(h->pos_buf);
+    h->d_r = static_cast<float*>(h->sel);
+    h->d_m = h->d_r + n_sel * ni;
+    rdl::ScopedTiming t(s, "subminor_select", 12.0 * n_sel * ni);
+    const unsigned grid = unsigned(std::min<uint64_t>(rdl::DivUp(n_sel, 256), 4096));
+    rdl::SelGather<<<grid, 256, 0, st>>>(d_residuals, p->width, p->width * p->height,
+                                         h->d_pos, n_sel, ni, h->d_r);
+  } else {
+    const size_t sel_need =
+        n_sel * sizeof(uint32_t) + 2 * n_sel * ni * sizeof(float) + 256;
+    RDL_TRY(rdl::Grow(&h->sel, &h->sel_bytes, sel_need, st));
+    h->d_pos = static_cast<uint32_t*>(h->sel);
+    h->d_r = reinterpret_cast<float*>(
+        static_cast<char*>(h->sel) + (n_sel * sizeof(uint32_t) + 15) / 16 * 16);
+    h->d_m = h->d_r + n_sel * ni;
     rdl::ScopedTiming t(s, "subminor_select", sel_bytes + 8.0 * n_sel * ni);
     rdl::SelScatter<<<n_chunks, rdl::kSelThreads, 0, st>>>(
         sa, counts, ni, n_sel, h->d_pos, h->d_r);
