@@ -9,8 +9,10 @@
 
 namespace rdl {
 
+// Aligned to its size so that a complex element moves as one 8- or 16-byte
+// access (global and LDS), never as two scalar halves.
 template <typename T>
-struct Cx {
+struct alignas(2 * sizeof(T)) Cx {
   T x, y;
 };
 

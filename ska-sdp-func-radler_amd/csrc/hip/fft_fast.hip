@@ -279,9 +279,7 @@ __global__ __launch_bounds__(TH) void RowsInverse(RowArgs a, const Cx<T>* __rest
   if (iy >= a.img_h) return;
   const uint32_t y = iy + a.oy;
   const Cx<T>* X = spec + size_t(y) * a.ld;
-  auto load = [&](uint32_t k) {
-    return a.tiled ? spec[TileIndex(y, k, a.height)] : X[k];
-  };
+  auto load = [&](uint32_t k) { return *(a.tiled ? spec + TileIndex(y, k, a.height) : X + k); };
   // conj(Z) for bin k from X[k] = xk and X[H-k] = xm
   auto zc = [&](Cx<T> xk, Cx<T> xm, uint32_t k) {
     const Cx<T> sum = {xk.x + xm.x, xk.y - xm.y};  // X[k] + conj X[H-k]
@@ -399,10 +397,9 @@ __global__ __launch_bounds__(TH) void RowsForward(RowArgs a, const float* __rest
       const Cx<T> ev = {h * (zk.x + zc.x), h * (zk.y + zc.y)};
       const Cx<T> od = {h * (zk.y - zc.y), -h * (zk.x - zc.x)};  // (zk - zc) / 2i
       const Cx<T> v = Add(ev, Mul(tw[k], od));
-      if (a.tiled)
-        spec[TileIndex(y, k, a.height)] = v;
-      else
-        X[k] = v;
+      // one address, one 8/16-byte store (a store per layout branch was
+      // split into scalar halves)
+      *(a.tiled ? spec + TileIndex(y, k, a.height) : X + k) = v;
     }
     LdsSync();
   }
