@@ -72,6 +72,7 @@ struct rdl_session {
   rdl::Scratch partials;         // per-block partial keys
   rdl::Scratch radix;            // radix-select histograms
   bool poison = false;
+  bool trace_subminor_phases = false;  // RDL_TRACE_SUBMINOR=1 (2: timing only)
   bool trace_subminor = false;    // RDL_TRACE_SUBMINOR=1: per-launch stats            // RDL_POISON=1: NaN-fill fresh allocations
   rdl::Scratch kernel;           // host-provided kernels (H2D destination)
   rdl::Scratch loop_state;

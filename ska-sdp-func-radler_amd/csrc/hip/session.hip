@@ -121,7 +121,8 @@ int rdl_session_create(int device, rdl_session** out) {
   const char* poison = std::getenv("RDL_POISON");
   s->poison = poison && poison[0] == '1';
   const char* trace = std::getenv("RDL_TRACE_SUBMINOR");
-  s->trace_subminor = trace && trace[0] == '1';
+  s->trace_subminor = trace && (trace[0] == '1' || trace[0] == '2');
+  s->trace_subminor_phases = trace && trace[0] == '1';  // 2: timing only
   RDL_HIP_CHECK(hipMalloc(&s->d_small, 1 << 16));
   RDL_HIP_CHECK(hipHostMalloc(&s->h_small, 1 << 16, hipHostMallocDefault));
   {

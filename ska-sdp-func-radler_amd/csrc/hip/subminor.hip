@@ -1706,7 +1706,7 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   la.allow_negative = p->allow_negative;
   la.stop_on_negative = p->stop_on_negative;
   la.use_lds = use_lds ? 1 : 0;
-  la.prof = s->trace_subminor ? 1 : 0;
+  la.prof = s->trace_subminor_phases ? 1 : 0;
   const uint64_t n_trace = (h_trace && trace_cap) ? trace_cap : 0;
   const size_t rec_bytes =
       use_reg ? (size_t(2) * g * (3 + ni_t) * sizeof(uint64_t) + 15) / 16 * 16
@@ -1811,9 +1811,11 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
     const rdl::SmallRead r{ph, la.result + 16, sizeof(ph)};
     RDL_TRY(rdl::ReadSmall(s, &r, 1));
     std::fprintf(stderr,
-                 "[subminor] n_sel=%llu g=%u kind=%d iters=%llu us=%.1f "
+                 "[subminor] n_sel=%llu g=%u kind=%d threads=%d table=%d iters=%llu us=%.1f "
                  "gather=%llu integ=%llu wred=%llu bar=%llu xchg=%llu dec=%llu\n",
                  (unsigned long long)n_sel, g, use_reg ? 10 + int(items) : int(use_lds),
+                 use_wave ? 64 : use_big ? 1024 : use_reg ? int(rdl::kRegThreads) : 512,
+                 la.table ? 1 : 0,
                  (unsigned long long)(res.iteration - p->iteration_start),
                  double(ms) * 1e3, (unsigned long long)ph[0], (unsigned long long)ph[1],
                  (unsigned long long)ph[2], (unsigned long long)ph[3],
