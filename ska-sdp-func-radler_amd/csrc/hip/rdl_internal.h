@@ -71,13 +71,23 @@ struct rdl_session {
   void* h_small = nullptr;       // 64 KiB pinned host
   rdl::Scratch partials;         // per-block partial keys
   rdl::Scratch radix;            // radix-select histograms
-  bool poison = false;
+  bool poison = false;                 // RDL_POISON=1: NaN-fill fresh allocations
   bool trace_subminor_phases = false;  // RDL_TRACE_SUBMINOR=1 (2: timing only)
-  bool trace_subminor = false;    // RDL_TRACE_SUBMINOR=1: per-launch stats            // RDL_POISON=1: NaN-fill fresh allocations
+  bool trace_subminor = false;         // RDL_TRACE_SUBMINOR=1/2: per-launch stats
   rdl::Scratch kernel;           // host-provided kernels (H2D destination)
-  rdl::Scratch loop_state;
-  rdl::Scratch iuwt;             // IUWT i0 / recompose accumulator plane       // Högbom loop state / partials / trace
+  rdl::Scratch loop_state;       // Högbom loop state / partials / trace
+  rdl::Scratch iuwt;             // IUWT i0 / recompose accumulator plane
   void* comm = nullptr;          // ncclComm_t when initialised
+  // rdl_malloc / rdl_free block cache: a freed block is kept for reuse by a
+  // later allocation of this session (stream-ordered on `stream`), so the
+  // per-Perform buffers cost no hipFree (which idles the device) and no
+  // hipMalloc; RDL_ALLOC_CACHE=0 frees immediately
+  std::mutex cache_mutex;
+  std::multimap<size_t, void*> cache_free;      // size -> block
+  std::map<void*, size_t> cache_live;           // block -> size
+  size_t cache_bytes = 0;                       // bytes held in cache_free
+  bool cache_on = true;
+  int FlushCache();
 
   hipEvent_t GetEvent();
   void BeginTiming(const char* family, hipEvent_t* start);

@@ -122,6 +122,8 @@ int rdl_session_create(int device, rdl_session** out) {
   s->poison = poison && poison[0] == '1';
   const char* trace = std::getenv("RDL_TRACE_SUBMINOR");
   s->trace_subminor = trace && (trace[0] == '1' || trace[0] == '2');
+  const char* cache = std::getenv("RDL_ALLOC_CACHE");
+  s->cache_on = !(cache && cache[0] == '0');
   s->trace_subminor_phases = trace && trace[0] == '1';  // 2: timing only
   RDL_HIP_CHECK(hipMalloc(&s->d_small, 1 << 16));
   RDL_HIP_CHECK(hipHostMalloc(&s->h_small, 1 << 16, hipHostMallocDefault));
@@ -133,10 +135,24 @@ int rdl_session_create(int device, rdl_session** out) {
   return RDL_OK;
 }
 
+int rdl_session::FlushCache() {
+  std::multimap<size_t, void*> blocks;
+  {
+    const std::lock_guard<std::mutex> lock(cache_mutex);
+    blocks.swap(cache_free);
+    cache_bytes = 0;
+  }
+  if (blocks.empty()) return RDL_OK;
+  RDL_HIP_CHECK(hipStreamSynchronize(stream));
+  for (auto& [bytes, p] : blocks) RDL_HIP_CHECK(hipFree(p));
+  return RDL_OK;
+}
+
 int rdl_session_destroy(rdl_session* s) {
   if (!s) return RDL_OK;
   (void)hipSetDevice(s->device);
   (void)hipStreamSynchronize(s->stream);
+  (void)s->FlushCache();
   {
     const std::lock_guard<std::mutex> lock(rdl::g_registry_mutex);
     auto& v = rdl::g_sessions;
@@ -187,12 +203,34 @@ int rdl_malloc(rdl_session* s, size_t bytes, void** d_out) {
   RDL_ARG_CHECK(s && d_out, "NULL argument");
   *d_out = nullptr;
   if (bytes == 0) return RDL_OK;
-  int prev = 0;
-  RDL_HIP_CHECK(hipGetDevice(&prev));
-  if (prev != s->device) RDL_HIP_CHECK(hipSetDevice(s->device));
-  const hipError_t e = hipMalloc(d_out, bytes);
-  if (prev != s->device) (void)hipSetDevice(prev);
-  RDL_HIP_CHECK(e);
+  if (s->cache_on) {
+    // best fit among cached blocks of at most 1.25x the request
+    const std::lock_guard<std::mutex> lock(s->cache_mutex);
+    auto it = s->cache_free.lower_bound(bytes);
+    if (it != s->cache_free.end() && it->first <= bytes + bytes / 4) {
+      *d_out = it->second;
+      s->cache_bytes -= it->first;
+      s->cache_live[it->second] = it->first;
+      s->cache_free.erase(it);
+    }
+  }
+  if (!*d_out) {
+    int prev = 0;
+    RDL_HIP_CHECK(hipGetDevice(&prev));
+    if (prev != s->device) RDL_HIP_CHECK(hipSetDevice(s->device));
+    hipError_t e = hipMalloc(d_out, bytes);
+    if (e == hipErrorOutOfMemory && s->cache_on) {  // give the cache back, retry
+      (void)hipGetLastError();
+      RDL_TRY(s->FlushCache());
+      e = hipMalloc(d_out, bytes);
+    }
+    if (prev != s->device) (void)hipSetDevice(prev);
+    RDL_HIP_CHECK(e);
+    if (s->cache_on) {
+      const std::lock_guard<std::mutex> lock(s->cache_mutex);
+      s->cache_live[*d_out] = bytes;
+    }
+  }
   if (s->poison) {
     RDL_HIP_CHECK(hipMemsetAsync(*d_out, 0xff, bytes, s->stream));
     RDL_HIP_CHECK(hipStreamSynchronize(s->stream));
@@ -200,9 +238,27 @@ int rdl_malloc(rdl_session* s, size_t bytes, void** d_out) {
   return RDL_OK;
 }
 
+// Blocks this session allocated go back to its cache (reused in stream order
+// on the session's stream: every buffer is used on its owner's stream, or by
+// other streams only between host synchronisations); anything else, and
+// everything beyond the cache cap, is freed after the stream drains.
 int rdl_free(rdl_session* s, void* d_ptr) {
   RDL_ARG_CHECK(s, "NULL session");
   if (!d_ptr) return RDL_OK;
+  constexpr size_t kCacheCap = size_t(96) << 30;
+  if (s->cache_on) {
+    const std::lock_guard<std::mutex> lock(s->cache_mutex);
+    auto it = s->cache_live.find(d_ptr);
+    if (it != s->cache_live.end()) {
+      const size_t bytes = it->second;
+      s->cache_live.erase(it);
+      if (s->cache_bytes + bytes <= kCacheCap) {
+        s->cache_free.emplace(bytes, d_ptr);
+        s->cache_bytes += bytes;
+        return RDL_OK;
+      }
+    }
+  }
   RDL_HIP_CHECK(hipStreamSynchronize(s->stream));
   RDL_HIP_CHECK(hipFree(d_ptr));
   return RDL_OK;
