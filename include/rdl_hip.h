@@ -111,6 +111,18 @@ int rdl_find_peak(rdl_session* s, const float* d_image, uint32_t width,
                   uint32_t h_border, uint32_t v_border, int allow_negative,
                   const uint8_t* d_mask, int avx_semantics, rdl_peak* out);
 
+/* rdl_find_peak without the host round trip: the result goes to device
+ * slot `slot` (< RDL_PEAK_SLOTS) and rdl_find_peak_collect reads slots
+ * 0..n-1 with one synchronisation (the per-scale peak searches of
+ * FindActiveScaleConvolvedMaxima, multiscale_algorithm.cc:578-634, queue
+ * back to back instead of idling the device between scales). */
+#define RDL_PEAK_SLOTS 64
+int rdl_find_peak_enqueue(rdl_session* s, const float* d_image, uint32_t width,
+                          uint32_t height, uint32_t start_y, uint32_t end_y,
+                          uint32_t h_border, uint32_t v_border, int allow_negative,
+                          const uint8_t* d_mask, int avx_semantics, uint32_t slot);
+int rdl_find_peak_collect(rdl_session* s, uint32_t n, rdl_peak* out);
+
 /* Sum of squares in double (ThreadedDeconvolutionTools::RMS,
  * cpp/algorithms/threaded_deconvolution_tools.h:40-44; logging only). */
 int rdl_rms(rdl_session* s, const float* d_image, size_t n, float* out);

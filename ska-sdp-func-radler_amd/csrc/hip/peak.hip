@@ -203,6 +203,47 @@ int rdl_find_peak(rdl_session* s, const float* d_image, uint32_t width,
   return RDL_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// the deferred peak slots: the upper half of the session's small buffer
+rdl::PeakOut* PeakSlots(rdl_session* s) {
+  return reinterpret_cast<rdl::PeakOut*>(static_cast<char*>(s->d_small) + 32 * 1024);
+}
+static_assert(RDL_PEAK_SLOTS * sizeof(rdl::PeakOut) <= 32 * 1024, "peak slots");
+}  // namespace
+
+extern "C" {
+
+int rdl_find_peak_enqueue(rdl_session* s, const float* d_image, uint32_t width,
+                          uint32_t height, uint32_t start_y, uint32_t end_y,
+                          uint32_t h_border, uint32_t v_border, int allow_negative,
+                          const uint8_t* d_mask, int avx_semantics, uint32_t slot) {
+  RDL_ARG_CHECK(s && d_image, "NULL argument");
+  RDL_ARG_CHECK(width > 0 && height > 0, "empty image");
+  RDL_ARG_CHECK(uint64_t(width) * height < 0xffffffffull,
+                "image too large for 32-bit pixel index");
+  RDL_ARG_CHECK(slot < RDL_PEAK_SLOTS, "peak slot out of range");
+  return rdl::LaunchFindPeak(s, d_image, width, height, start_y, end_y, h_border, v_border,
+                             allow_negative, d_mask, avx_semantics, PeakSlots(s) + slot);
+}
+
+int rdl_find_peak_collect(rdl_session* s, uint32_t n, rdl_peak* out) {
+  RDL_ARG_CHECK(s && (out || n == 0), "NULL argument");
+  RDL_ARG_CHECK(n <= RDL_PEAK_SLOTS, "peak slot out of range");
+  if (n == 0) return RDL_OK;
+  rdl::PeakOut o[RDL_PEAK_SLOTS];
+  const rdl::SmallRead r{o, PeakSlots(s), n * sizeof(rdl::PeakOut)};
+  RDL_TRY(rdl::ReadSmall(s, &r, 1));
+  for (uint32_t i = 0; i < n; ++i) {
+    out[i].value = o[i].value;
+    out[i].x = o[i].x;
+    out[i].y = o[i].y;
+    out[i].found = o[i].found;
+  }
+  return RDL_OK;
+}
+
 int rdl_rms(rdl_session* s, const float* d_image, size_t n, float* out) {
   RDL_ARG_CHECK(s && d_image && out, "NULL argument");
   RDL_ARG_CHECK(n > 0, "empty image");

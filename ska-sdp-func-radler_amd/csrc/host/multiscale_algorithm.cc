@@ -221,6 +221,9 @@ void MultiScaleAlgorithm::FindActiveScaleConvolvedMaxima(
   }
   if (!need_fft) return;
   transforms_->Forward(d_integrated, spectrum_->Ptr());
+  std::vector<size_t> pending;  // scale of each queued peak search
+  if (scale_infos_.size() > RDL_PEAK_SLOTS)
+    throw std::runtime_error("MultiScaleAlgorithm: too many scales");
   for (size_t si = 0; si != scale_infos_.size(); ++si) {
     ScaleInfo& e = scale_infos_[si];
     if (!e.is_active || e.scale == 0.0f) continue;
@@ -241,11 +244,20 @@ void MultiScaleAlgorithm::FindActiveScaleConvolvedMaxima(
         std::max<size_t>(size_t(std::round(h * CleanBorderRatio())), border_scale));
     if (report_rms)
       gpu::Check(rdl_rms(s, d_conv, w * h, &e.rms), "rdl_rms");
-    rdl_peak p;
-    gpu::Check(rdl_find_peak(s, PeakSearchInput(d_conv, w, h), uint32_t(w), uint32_t(h), 0,
-                             uint32_t(h), xb, yb, AllowNegativeComponents(),
-                             MaskFor(si), 1, &p),
-               "rdl_find_peak");
+    // the scales' searches queue back to back; one read collects them
+    gpu::Check(rdl_find_peak_enqueue(s, PeakSearchInput(d_conv, w, h), uint32_t(w),
+                                     uint32_t(h), 0, uint32_t(h), xb, yb,
+                                     AllowNegativeComponents(), MaskFor(si), 1,
+                                     uint32_t(pending.size())),
+               "rdl_find_peak_enqueue");
+    pending.push_back(si);
+  }
+  std::vector<rdl_peak> peaks(pending.size());
+  gpu::Check(rdl_find_peak_collect(s, uint32_t(pending.size()), peaks.data()),
+             "rdl_find_peak_collect");
+  for (size_t k = 0; k != pending.size(); ++k) {
+    ScaleInfo& e = scale_infos_[pending[k]];
+    const rdl_peak& p = peaks[k];
     e.max_normalized_image_value = p.found ? Normalized(p.value, p.x, p.y, w) : 0.0f;
     e.max_unnormalized_image_value = p.found ? p.value : 0.0f;
     e.max_image_value_x = p.x;
