@@ -34,7 +34,7 @@ FAMILY_KERNELS = {
     "spectrum_multiply": r"^rdl::SpectrumMultiply\(",
     "subminor_loop": r"SubminorLoop",
     "subminor_table": r"BuildPairTable",
-    "subminor_select": r"^rdl::Sel(Count|Scan|Scatter)\(",
+    "subminor_select": r"^rdl::Sel(Count|Scan|Scatter|SinglePass|Gather)\(",
     "find_peak": r"^void rdl::FindPeak|^rdl::FindPeakFinal",
     "integrate": r"^rdl::IntegrateKernel\(",
     "add": r"^rdl::AddKernel\(",
