@@ -916,6 +916,46 @@ __device__ __forceinline__ int FirstLane(bool pred) {
   return b ? __builtin_ctzll(b) : 0;
 }
 
+// 32-bit max over lanes (DPP, one fused max per step); LANES = 8, 16 or 64
+// (lanes beyond LANES must hold 0); uniform result.
+template <int LANES>
+__device__ __forceinline__ uint32_t MaxU32(uint32_t v) {
+  auto step = [](uint32_t x, uint32_t t) { return x > t ? x : t; };
+  v = step(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0xb1, 0xf, 0xf, false)));
+  v = step(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x4e, 0xf, 0xf, false)));
+  v = step(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x141, 0xf, 0xf, false)));
+  if constexpr (LANES == 8) return uint32_t(__builtin_amdgcn_readlane(int(v), 0));
+  v = step(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x140, 0xf, 0xf, false)));
+  if constexpr (LANES == 16) return uint32_t(__builtin_amdgcn_readlane(int(v), 0));
+  v = step(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x142, 0xa, 0xf, false)));
+  v = step(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x143, 0xc, 0xf, false)));
+  return uint32_t(__builtin_amdgcn_readlane(int(v), 63));
+}
+
+// The largest 64-bit argmax key over lanes and its lane (the lowest lane
+// holding it; lane 0 when every key is 0). The value word (high half) is
+// reduced alone; the index word only settles exact value ties, which are
+// rare (keys are unique per pixel, and a high word of 0 means a 0 key).
+template <int LANES>
+__device__ __forceinline__ uint64_t KeyMax(uint64_t key, int& lane_out) {
+  const uint32_t hi = uint32_t(key >> 32);
+  const uint32_t mh = MaxU32<LANES>(hi);
+  if (mh == 0u) {
+    lane_out = 0;
+    return 0ull;
+  }
+  const uint64_t tie = __ballot(hi == mh);
+  if ((tie & (tie - 1ull)) == 0ull) {
+    lane_out = __builtin_ctzll(tie);
+    return (uint64_t(mh) << 32) |
+           uint32_t(__builtin_amdgcn_readlane(int(uint32_t(key)), lane_out));
+  }
+  const uint64_t k = hi == mh ? key : 0ull;
+  const uint64_t m = LANES == 8 ? Max8U64(k) : LANES == 16 ? Max16U64(k) : Max64U64(k);
+  lane_out = FirstLane(key == m);
+  return m;
+}
+
 template <int NI>
 struct RegSlot {
   uint64_t key;
@@ -1059,9 +1099,9 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopReg(LoopArgs a) {
     // ---- wave argmax; the owner (or lane 0 when nothing qualifies, which
     // stands for selection index 0) writes the wave's slot
     RDL_PHASE(1)
-    const uint64_t wmax = Max64U64(best);
+    int owner_lane;
+    const uint64_t wmax = KeyMax<64>(best, owner_lane);
     const uint32_t par = epoch & 1u;
-    const int owner_lane = wmax != 0 ? FirstLane(best == wmax) : 0;
     uint64_t gkey;
     uint32_t wpos;
     float wr[NI];
@@ -1124,8 +1164,8 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopReg(LoopArgs a) {
 #pragma unroll
       for (int k = 0; k < NI; ++k) sr[k] = sl.r[k];
     }
-    const uint64_t bkey = WAVES <= 8 ? Max8U64(sk) : Max16U64(sk);
-    const int bw = bkey != 0 ? FirstLane(sk == bkey && lane < uint32_t(WAVES)) : 0;
+    int bw;
+    const uint64_t bkey = KeyMax<(WAVES <= 8 ? 8 : 16)>(sk, bw);
     gkey = bkey;
     wpos = uint32_t(__builtin_amdgcn_readlane(int(spos), bw));
 #pragma unroll
