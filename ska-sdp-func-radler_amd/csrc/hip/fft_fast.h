@@ -83,10 +83,20 @@ int FastColumnsLaunch(rdl_session* s, const FastColumns* p, const void* in, void
                       int in_cm, int out_cm, int kern_cm, const uint32_t* rows,
                       const uint32_t* n_rows, uint32_t row0, uint32_t row_n,
                       double scale);
+/* Peak search fused into the inverse row pass (peak_finder::Find semantics,
+ * rdl_find_peak): every written row's max key in the box x in [xs, xe),
+ * y in [ys, ye) (and mask) goes to partials[row] (0 outside the box). */
+struct RowPeak {
+  uint64_t* partials;
+  const uint8_t* mask;
+  uint32_t xs, xe, ys, ye;
+  int allow_negative;
+};
 /* spectrum rows oy .. oy+img_h-1 -> the img_w x img_h window at (ox, oy) */
 int FastRowsInverseLaunch(rdl_session* s, const FastRows* p, const void* spec, float* out,
                           const void* tw, const void* ptw, uint32_t height, uint32_t img_w, uint32_t img_h,
-                          uint32_t ox, uint32_t oy, int subtract, int tiled = 0);
+                          uint32_t ox, uint32_t oy, int subtract, int tiled = 0,
+                          const RowPeak* peak = nullptr);
 /* the window's rows (or the listed plane rows) -> spectrum rows */
 int FastRowsForwardLaunch(rdl_session* s, const FastRows* p, const float* in, void* spec,
                           const void* tw, const void* ptw, uint32_t height, uint32_t img_w, uint32_t img_h,

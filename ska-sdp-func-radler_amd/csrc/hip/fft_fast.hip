@@ -250,6 +250,7 @@ struct RowArgs {
   int subtract;         // inverse: 0 write, 1 subtract from out
   int tiled;            // spectrum in column tiles (see TileIndex), else row-major
   int all_rows;         // forward: every plane row (zero outside the window)
+  RowPeak peak;         // inverse: fused peak search when peak.partials
 };
 
 // Tiled spectrum layout of the four-step column passes: 16 adjacent columns
@@ -275,6 +276,7 @@ __global__ __launch_bounds__(TH) void RowsInverse(RowArgs a, const Cx<T>* __rest
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   Cx<T>* buf = reinterpret_cast<Cx<T>*>(lds_raw);
   const uint32_t tid = threadIdx.x;
+  __shared__ uint64_t red[TH / 64];  // fused peak search
   const uint32_t iy = blockIdx.x;  // output row of the window
   if (iy >= a.img_h) return;
   const uint32_t y = iy + a.oy;
@@ -306,6 +308,22 @@ __global__ __launch_bounds__(TH) void RowsInverse(RowArgs a, const Cx<T>* __rest
   LdsSync();
   Fft<T, TH, H, 0, 1, Rs...>(buf, ptw, tid);
   float* o = out + size_t(iy) * a.img_w;
+  // fused peak search over the values as written (window coordinates)
+  const bool peak = a.peak.partials != nullptr;
+  const bool peak_row = peak && iy >= a.peak.ys && iy < a.peak.ye;
+  uint64_t best = 0;
+  auto consider = [&](uint32_t x, float v) {
+    if (peak_row && x >= a.peak.xs && x < a.peak.xe &&
+        (!a.peak.mask || a.peak.mask[size_t(iy) * a.img_w + x])) {
+      const uint64_t k = PeakKey(v, a.peak.allow_negative != 0, iy * a.img_w + x);
+      best = k > best ? k : best;
+    }
+  };
+  auto finish_peak = [&]() {
+    if (!peak) return;
+    best = BlockMaxU64(best, red);
+    if (tid == 0) a.peak.partials[iy] = best;
+  };
   if (((a.ox | a.img_w) & 1u) == 0) {
     // even window: (x[2n], x[2n+1]) both in or both out, one 8-B access
 #pragma unroll
@@ -322,7 +340,10 @@ __global__ __launch_bounds__(TH) void RowsInverse(RowArgs a, const Cx<T>* __rest
         v = {r.x - v.x, r.y - v.y};
       }
       *p = v;
+      consider(x0 - a.ox, v.x);
+      consider(x0 - a.ox + 1, v.y);
     }
+    finish_peak();
     return;
   }
 #pragma unroll
@@ -333,13 +354,18 @@ __global__ __launch_bounds__(TH) void RowsInverse(RowArgs a, const Cx<T>* __rest
     const uint32_t x0 = 2 * n, x1 = x0 + 1;
     if (x0 >= a.ox && x0 < a.ox + a.img_w) {
       float* p = o + (x0 - a.ox);
-      *p = a.subtract ? *p - float(z.x) : float(z.x);
+      const float v = a.subtract ? *p - float(z.x) : float(z.x);
+      *p = v;
+      consider(x0 - a.ox, v);
     }
     if (x1 >= a.ox && x1 < a.ox + a.img_w) {
       float* p = o + (x1 - a.ox);
-      *p = a.subtract ? *p - float(-z.y) : float(-z.y);
+      const float v = a.subtract ? *p - float(-z.y) : float(-z.y);
+      *p = v;
+      consider(x1 - a.ox, v);
     }
   }
+  finish_peak();
 }
 
 // real plane rows (the window's image rows, zero outside) -> spectrum rows
@@ -723,8 +749,10 @@ int SlotsPerCu(rdl_session* s, const void* fn, uint32_t threads, size_t lds) {
   const auto key = std::make_tuple(fn, s->device, lds);
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
+  // (a little below the CU's LDS: the row kernels also hold a static
+  // reduction array for the fused peak search)
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          int(kFftLdsBytesFast)) != hipSuccess)
+                          int(kFftLdsBytesFast - 1024)) != hipSuccess)
     return -1;
   int n = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, int(threads), lds) != hipSuccess)
@@ -768,7 +796,7 @@ int FastColumnsLaunch(rdl_session* s, const FastColumns* p, const void* in, void
 
 int FastRowsInverseLaunch(rdl_session* s, const FastRows* p, const void* spec, float* out,
                           const void* tw, const void* ptw, uint32_t height, uint32_t img_w, uint32_t img_h,
-                          uint32_t ox, uint32_t oy, int subtract, int tiled) {
+                          uint32_t ox, uint32_t oy, int subtract, int tiled, const RowPeak* peak) {
   const size_t lds = FastLdsBytes(p->n / 2, p->f64);
   if (SlotsPerCu(s, p->inverse, p->threads, lds) < 0) {
     SetError("fast FFT rows: occupancy query failed");
@@ -784,6 +812,7 @@ int FastRowsInverseLaunch(rdl_session* s, const FastRows* p, const void* spec, f
   a.oy = oy;
   a.subtract = subtract;
   a.tiled = tiled;
+  if (peak) a.peak = *peak;
   void* args[] = {&a, (void*)&spec, (void*)&out, (void*)&tw, (void*)&ptw};
   RDL_HIP_CHECK(hipLaunchKernel(p->inverse, dim3(img_h), dim3(p->threads), args, lds,
                                 s->stream));

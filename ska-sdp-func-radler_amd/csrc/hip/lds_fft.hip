@@ -1047,6 +1047,47 @@ int rdl_conv_rows_inverse(rdl_conv* c, const void* d_spec, float* d_out,
                                            subtract);
 }
 
+int rdl_conv_rows_inverse_peak(rdl_conv* c, const void* d_spec, float* d_out,
+                               uint32_t out_w, uint32_t out_h, uint32_t h_border,
+                               uint32_t v_border, int allow_negative,
+                               const uint8_t* d_mask, uint32_t slot) {
+  RDL_ARG_CHECK(c && d_spec && d_out, "NULL argument");
+  RDL_ARG_CHECK(out_w <= c->width && out_h <= c->height, "output window outside the plane");
+  RDL_ARG_CHECK(slot < RDL_PEAK_SLOTS, "peak slot out of range");
+  RDL_ARG_CHECK(uint64_t(out_w) * out_h < 0xffffffffull, "image too large for 32-bit index");
+  if (!c->fast_rows) {
+    rdl::SetError("fused peak search needs the compile-time-planned row kernels");
+    return RDL_ERR_UNSUPPORTED;
+  }
+  rdl_session* s = c->s;
+  // the box of rdl_find_peak(start_y 0, end_y out_h) (peak_finder.cc:27-32)
+  rdl::RowPeak pk{};
+  pk.xs = h_border;
+  pk.xe = out_w - h_border;
+  pk.ys = v_border;
+  pk.ye = out_h - v_border;
+  if (pk.xe < pk.xs) pk.xe = pk.xs;
+  if (pk.ye < pk.ys) pk.ye = pk.ys;
+  if (pk.xe > out_w) pk.xe = out_w;
+  if (pk.ye > out_h) pk.ye = out_h;
+  pk.mask = d_mask;
+  pk.allow_negative = allow_negative;
+  RDL_TRY(s->EnsureScratch(s->partials, std::max<size_t>(out_h, 1) * sizeof(uint64_t)));
+  pk.partials = static_cast<uint64_t*>(s->partials.ptr);
+  {
+    rdl::ScopedTiming t(s, "conv_rows",
+                        SpectrumBytes(c) + double(out_w) * out_h * 4.0);
+    if (out_h == 0)
+      RDL_HIP_CHECK(hipMemsetAsync(pk.partials, 0, sizeof(uint64_t), s->stream));
+    else
+      RDL_TRY(rdl::FastRowsInverseLaunch(s, c->fast_rows, d_spec, d_out, c->tw_row,
+                                         c->ptw_row, c->height, out_w, out_h, 0, 0, 0,
+                                         c->tiled ? 1 : 0, &pk));
+  }
+  return rdl::LaunchPeakFinal(s, pk.partials, std::max<uint32_t>(out_h, 1), d_out, out_w,
+                              out_h, 1, d_mask != nullptr, rdl::PeakSlot(s, slot));
+}
+
 int rdl_conv_forward(rdl_conv* c, const float* d_in, void* d_spec) {
   RDL_TRY(rdl_conv_rows_forward(c, d_in, c->width, c->height, 0, 0, d_spec));
   return rdl_conv_columns(c, d_spec, d_spec, nullptr, 0, 1.0);

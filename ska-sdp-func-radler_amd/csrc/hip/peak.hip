@@ -131,6 +131,19 @@ __global__ void SumSquaresFinal(const double* partials, uint32_t n, size_t count
   }
 }
 
+int LaunchPeakFinal(rdl_session* s, const uint64_t* partials, uint32_t n,
+                    const float* image, uint32_t width, uint32_t height, int avx_semantics,
+                    int has_mask, void* d_out) {
+  FindPeakFinal<<<1, 1024, 0, s->stream>>>(partials, n, image, width, height, avx_semantics,
+                                           has_mask, static_cast<PeakOut*>(d_out));
+  RDL_HIP_CHECK(hipGetLastError());
+  return RDL_OK;
+}
+
+void* PeakSlot(rdl_session* s, uint32_t slot) {
+  return static_cast<char*>(s->d_small) + 32 * 1024 + size_t(slot) * sizeof(PeakOut);
+}
+
 int LaunchFindPeak(rdl_session* s, const float* d_image, uint32_t width,
                    uint32_t height, uint32_t start_y, uint32_t end_y,
                    uint32_t h_border, uint32_t v_border, int allow_negative,
@@ -208,7 +221,7 @@ int rdl_find_peak(rdl_session* s, const float* d_image, uint32_t width,
 namespace {
 // the deferred peak slots: the upper half of the session's small buffer
 rdl::PeakOut* PeakSlots(rdl_session* s) {
-  return reinterpret_cast<rdl::PeakOut*>(static_cast<char*>(s->d_small) + 32 * 1024);
+  return static_cast<rdl::PeakOut*>(rdl::PeakSlot(s, 0));
 }
 static_assert(RDL_PEAK_SLOTS * sizeof(rdl::PeakOut) <= 32 * 1024, "peak slots");
 }  // namespace

@@ -218,6 +218,13 @@ __device__ __forceinline__ uint64_t WaveMaxU64(uint64_t v) {
   return v;
 }
 
+// peak.hip: the second stage of a peak search over per-block/per-row keys,
+// and the deferred result slots of rdl_find_peak_enqueue / _collect
+int LaunchPeakFinal(rdl_session* s, const uint64_t* partials, uint32_t n,
+                    const float* image, uint32_t width, uint32_t height, int avx_semantics,
+                    int has_mask, void* d_out);
+void* PeakSlot(rdl_session* s, uint32_t slot);
+
 // Block-wide max of a uint64 (blockDim multiple of 64, <= 1024).
 __device__ __forceinline__ uint64_t BlockMaxU64(uint64_t v, uint64_t* lds) {
   v = WaveMaxU64(v);

@@ -147,6 +147,22 @@ void Fft::ConvolveSpectrum(const void* d_spectrum, const void* d_kernel_spectrum
   }
 }
 
+bool Fft::ConvolveSpectrumPeak(const void* d_spectrum, const void* d_kernel_spectrum,
+                               void* d_work, float* d_out, uint32_t h_border,
+                               uint32_t v_border, bool allow_negative,
+                               const uint8_t* d_mask, uint32_t slot) {
+  if (!conv_ || !(rdl_conv_fast(conv_) & RDL_CONV_FAST_ROWS)) return false;
+  const double norm = 1.0 / (double(width_) * double(height_));
+  Check(rdl_conv_columns_layout(conv_, d_spectrum, d_work, d_kernel_spectrum, 2,
+                                f64_ ? norm : double(float(norm)), nullptr, Layout(),
+                                Layout(), RDL_CONV_ROW_MAJOR),
+        "rdl_conv_columns_layout");
+  Check(rdl_conv_rows_inverse_peak(conv_, d_work, d_out, uint32_t(width_), uint32_t(height_),
+                                   h_border, v_border, allow_negative ? 1 : 0, d_mask, slot),
+        "rdl_conv_rows_inverse_peak");
+  return true;
+}
+
 void Fft::ForwardColumnMajor(const float* d_in, void* d_spectrum) {
   if (!conv_) throw std::logic_error("Fft::ForwardColumnMajor needs the LDS engine");
   Check(rdl_conv_rows_forward(conv_, d_in, uint32_t(width_), uint32_t(height_), 0, 0,

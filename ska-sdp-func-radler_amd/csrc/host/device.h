@@ -65,6 +65,14 @@ class Fft {
   /// (d_spectrum is preserved; d_work is spectrum-sized scratch).
   void ConvolveSpectrum(const void* d_spectrum, const void* d_kernel_spectrum,
                         void* d_work, float* d_out);
+  /// ConvolveSpectrum with the image's peak search (rdl_find_peak box,
+  /// mask and sign rules) fused into the last pass; the result goes to peak
+  /// slot `slot` (rdl_find_peak_collect). False (nothing done) when this
+  /// plan has no fused form.
+  bool ConvolveSpectrumPeak(const void* d_spectrum, const void* d_kernel_spectrum,
+                            void* d_work, float* d_out, uint32_t h_border,
+                            uint32_t v_border, bool allow_negative, const uint8_t* d_mask,
+                            uint32_t slot);
   /// LDS engine only: residual(window) -= Trim(conv(Untrim(image), kernel)),
   /// the image (img_w x img_h) placed at (ox, oy) in the plane.
   /// d_row_mask (plane rows, 0 = the image row is all zero) skips the empty

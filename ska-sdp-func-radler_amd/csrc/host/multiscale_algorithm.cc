@@ -235,13 +235,22 @@ void MultiScaleAlgorithm::FindActiveScaleConvolvedMaxima(
       d_conv = kept.Base();
       scale_image_valid_[si] = true;
     }
-    transforms_->ConvolveSpectrum(spectrum_->Ptr(), e.scale, spectrum_work_->Ptr(),
-                                  d_conv);
     const size_t border_scale = size_t(std::ceil(e.scale * 0.5));
     const uint32_t xb = uint32_t(
         std::max<size_t>(size_t(std::round(w * CleanBorderRatio())), border_scale));
     const uint32_t yb = uint32_t(
         std::max<size_t>(size_t(std::round(h * CleanBorderRatio())), border_scale));
+    // the peak search fused into the inverse row pass where it can be (the
+    // RMS-weighted search reads a weighted copy, so it stays separate)
+    if (!report_rms && !RmsFactorImage() &&
+        transforms_->ConvolveSpectrumPeak(spectrum_->Ptr(), e.scale, spectrum_work_->Ptr(),
+                                          d_conv, xb, yb, AllowNegativeComponents(),
+                                          MaskFor(si), uint32_t(pending.size()))) {
+      pending.push_back(si);
+      continue;
+    }
+    transforms_->ConvolveSpectrum(spectrum_->Ptr(), e.scale, spectrum_work_->Ptr(),
+                                  d_conv);
     if (report_rms)
       gpu::Check(rdl_rms(s, d_conv, w * h, &e.rms), "rdl_rms");
     // the scales' searches queue back to back; one read collects them

@@ -238,4 +238,14 @@ void MultiScaleTransforms::ConvolveSpectrum(const void* d_spectrum, float scale,
   Crop(d_out);
 }
 
+bool MultiScaleTransforms::ConvolveSpectrumPeak(const void* d_spectrum, float scale,
+                                                void* d_work, float* d_out,
+                                                uint32_t h_border, uint32_t v_border,
+                                                bool allow_negative, const uint8_t* d_mask,
+                                                uint32_t slot) {
+  if (Extended()) return false;
+  return TheFft().ConvolveSpectrumPeak(d_spectrum, KernelSpectrum(scale), d_work, d_out,
+                                       h_border, v_border, allow_negative, d_mask, slot);
+}
+
 }  // namespace radler::algorithms::multiscale

@@ -48,6 +48,12 @@ class MultiScaleTransforms {
   /// d_out (W x H) = image of d_spectrum convolved with the scale kernel;
   /// d_spectrum is preserved, d_work is spectrum-sized scratch.
   void ConvolveSpectrum(const void* d_spectrum, float scale, void* d_work, float* d_out);
+  /// ConvolveSpectrum with the peak search fused (Fft::ConvolveSpectrumPeak);
+  /// false (nothing done) for the periodically extended planes and plans
+  /// without the fused form.
+  bool ConvolveSpectrumPeak(const void* d_spectrum, float scale, void* d_work, float* d_out,
+                            uint32_t h_border, uint32_t v_border, bool allow_negative,
+                            const uint8_t* d_mask, uint32_t slot);
 
   // multiscale_transforms.h:41-195
   static std::vector<float> MakeShapeFunction(float scale, size_t& n,

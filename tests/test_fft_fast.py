@@ -228,3 +228,55 @@ def test_pipeline_fast_vs_runtime_plan_kernels(tmp_path):
         c = assert_tie_aware(a["trace"], fx["trace"], fx["margins"], fx["values"], RTOL)
         print(f"RDL_FFT_FAST={fast}: {c}")
         assert c.matched > 1000
+
+
+class _Peak(C.Structure):
+    _fields_ = [("value", C.c_float), ("x", C.c_uint32), ("y", C.c_uint32),
+                ("found", C.c_int32)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,h,hb,vb,neg,masked", [
+    (4096, 4096, 204, 204, 1, False), (4096, 4096, 0, 0, 0, False),
+    (2048, 1536, 17, 40, 1, True), (8192, 4096, 410, 205, 0, True),
+    (1280, 1280, 700, 0, 1, False)])
+def test_rows_inverse_fused_peak_matches_find_peak(sess, w, h, hb, vb, neg, masked):
+    """rdl_conv_rows_inverse_peak (the per-scale peak search fused into the
+    inverse row pass) writes the same image as rdl_conv_rows_inverse and
+    returns exactly rdl_find_peak's result on it (box, mask, sign rules,
+    first index on ties)."""
+    c = conv(sess, w, h, False)
+    rng = np.random.default_rng(w + h + hb)
+    img = rng.standard_normal((h, w)).astype(np.float32)
+    img[h // 3, w // 5] = 40.0
+    img[h // 2, w // 2] = -55.0  # wins only with allow_negative
+    di = sess.array(img)
+    spec = spectrum_array(sess, c, w, h, np.complex64)
+    work = spectrum_array(sess, c, w, h, np.complex64)
+    kspec = spectrum_array(sess, c, w, h, np.complex64)
+    delta = np.zeros((h, w), np.float32)
+    delta[0, 0] = 1.0
+    dk = sess.array(delta)
+    sess.rdl.rdl_conv_forward(c, dk.vp, kspec.vp)
+    sess.rdl.rdl_conv_forward(c, di.vp, spec.vp)
+    mask = (rng.random((h, w)) < 0.7).astype(np.uint8)
+    dmask = sess.array(mask) if masked else None
+    mptr = dmask.vp if masked else None
+    out_a = sess.array(shape=(h, w))
+    out_b = sess.array(shape=(h, w))
+    norm = C.c_double(1.0 / (w * h))
+    sess.rdl.rdl_conv_columns(c, spec.vp, work.vp, kspec.vp, 2, norm)
+    sess.rdl.rdl_conv_rows_inverse(c, work.vp, out_a.vp, w, h, 0, 0, 0)
+    ref = _Peak()
+    sess.rdl.rdl_find_peak(sess.h, out_a.vp, w, h, 0, h, hb, vb, neg, mptr, 1, C.byref(ref))
+    sess.rdl.rdl_conv_columns(c, spec.vp, work.vp, kspec.vp, 2, norm)
+    sess.rdl.rdl_conv_rows_inverse_peak(c, work.vp, out_b.vp, w, h, hb, vb, neg, mptr, 3)
+    got = (_Peak * 4)()
+    sess.rdl.rdl_find_peak_collect(sess.h, 4, got)
+    a, b = out_a.get(), out_b.get()
+    assert np.array_equal(a, b)
+    g = got[3]
+    assert (g.value, g.x, g.y, g.found) == (ref.value, ref.x, ref.y, ref.found)
+    for x in (di, spec, work, kspec, dk, out_a, out_b) + ((dmask,) if masked else ()):
+        x.free()
+    sess.rdl.rdl_conv_destroy(c)

@@ -1,6 +1,6 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_multiscale_gpu.py tests/test_radler_gpu.py tests/test_configs_gpu.py tests/test_spectral.py tests/test_automask.py tests/test_local_rms.py tests/test_tiling.py -m gpu -x -q \
+timeout -k 10 600 python -u -m pytest tests/test_fft_fast.py tests/test_multiscale_gpu.py tests/test_radler_gpu.py tests/test_configs_gpu.py tests/test_spectral.py tests/test_automask.py tests/test_local_rms.py tests/test_tiling.py -m gpu -x -q \
   --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/ms_tests.log 2>&1 || exit $?
 timeout -k 10 300 python -u bench.py --cpu-outer 0 --tiled-reference 0 > gpurun_out/ms_bench.json 2> gpurun_out/ms_bench.err || exit $?
