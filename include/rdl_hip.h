@@ -510,15 +510,16 @@ int rdl_conv_columns(rdl_conv* c, const void* d_in, void* d_out,
 int rdl_conv_rows_inverse(rdl_conv* c, const void* d_spec, float* d_out,
                           uint32_t out_w, uint32_t out_h, uint32_t ox,
                           uint32_t oy, int subtract);
-/* rdl_conv_rows_inverse of the whole out_w x out_h window (write mode) with
- * the peak search of rdl_find_peak(start_y 0, end_y out_h, avx_semantics 1)
- * fused into it: the result goes to peak slot `slot` (rdl_find_peak_collect)
- * without re-reading the image (FindMultiScalePeak's per-scale search,
- * threaded_deconvolution_tools.cc:52-107). Needs the compile-time-planned
- * row kernels (RDL_ERR_UNSUPPORTED otherwise). */
+/* rdl_conv_rows_inverse (write mode) of the out_w x out_h window at (ox, oy)
+ * with the peak search of rdl_find_peak(start_y 0, end_y out_h,
+ * avx_semantics 1) on that window fused into it: the result goes to peak
+ * slot `slot` (rdl_find_peak_collect) without re-reading the image
+ * (FindMultiScalePeak's per-scale search, threaded_deconvolution_tools.cc:
+ * 52-107). Needs the compile-time-planned row kernels (RDL_ERR_UNSUPPORTED
+ * otherwise). */
 int rdl_conv_rows_inverse_peak(rdl_conv* c, const void* d_spec, float* d_out,
-                               uint32_t out_w, uint32_t out_h, uint32_t h_border,
-                               uint32_t v_border, int allow_negative,
+                               uint32_t out_w, uint32_t out_h, uint32_t ox, uint32_t oy,
+                               uint32_t h_border, uint32_t v_border, int allow_negative,
                                const uint8_t* d_mask, uint32_t slot);
 /* Full 2-D forward transform of a width x height float image. */
 int rdl_conv_forward(rdl_conv* c, const float* d_in, void* d_spec);

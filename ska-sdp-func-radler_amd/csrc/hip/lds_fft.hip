@@ -1048,11 +1048,12 @@ int rdl_conv_rows_inverse(rdl_conv* c, const void* d_spec, float* d_out,
 }
 
 int rdl_conv_rows_inverse_peak(rdl_conv* c, const void* d_spec, float* d_out,
-                               uint32_t out_w, uint32_t out_h, uint32_t h_border,
-                               uint32_t v_border, int allow_negative,
+                               uint32_t out_w, uint32_t out_h, uint32_t ox, uint32_t oy,
+                               uint32_t h_border, uint32_t v_border, int allow_negative,
                                const uint8_t* d_mask, uint32_t slot) {
   RDL_ARG_CHECK(c && d_spec && d_out, "NULL argument");
-  RDL_ARG_CHECK(out_w <= c->width && out_h <= c->height, "output window outside the plane");
+  RDL_ARG_CHECK(uint64_t(ox) + out_w <= c->width && uint64_t(oy) + out_h <= c->height,
+                "output window outside the plane");
   RDL_ARG_CHECK(slot < RDL_PEAK_SLOTS, "peak slot out of range");
   RDL_ARG_CHECK(uint64_t(out_w) * out_h < 0xffffffffull, "image too large for 32-bit index");
   if (!c->fast_rows) {
@@ -1081,7 +1082,7 @@ int rdl_conv_rows_inverse_peak(rdl_conv* c, const void* d_spec, float* d_out,
       RDL_HIP_CHECK(hipMemsetAsync(pk.partials, 0, sizeof(uint64_t), s->stream));
     else
       RDL_TRY(rdl::FastRowsInverseLaunch(s, c->fast_rows, d_spec, d_out, c->tw_row,
-                                         c->ptw_row, c->height, out_w, out_h, 0, 0, 0,
+                                         c->ptw_row, c->height, out_w, out_h, ox, oy, 0,
                                          c->tiled ? 1 : 0, &pk));
   }
   return rdl::LaunchPeakFinal(s, pk.partials, std::max<uint32_t>(out_h, 1), d_out, out_w,

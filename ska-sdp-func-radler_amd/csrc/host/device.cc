@@ -151,15 +151,58 @@ bool Fft::ConvolveSpectrumPeak(const void* d_spectrum, const void* d_kernel_spec
                                void* d_work, float* d_out, uint32_t h_border,
                                uint32_t v_border, bool allow_negative,
                                const uint8_t* d_mask, uint32_t slot) {
+  return ConvolveSpectrumWindowPeak(d_spectrum, d_kernel_spectrum, d_work, d_out, width_,
+                                    height_, 0, 0, h_border, v_border, allow_negative, d_mask,
+                                    slot);
+}
+
+bool Fft::ConvolveSpectrumWindowPeak(const void* d_spectrum, const void* d_kernel_spectrum,
+                                     void* d_work, float* d_out, size_t out_w, size_t out_h,
+                                     size_t ox, size_t oy, uint32_t h_border,
+                                     uint32_t v_border, bool allow_negative,
+                                     const uint8_t* d_mask, uint32_t slot) {
   if (!conv_ || !(rdl_conv_fast(conv_) & RDL_CONV_FAST_ROWS)) return false;
   const double norm = 1.0 / (double(width_) * double(height_));
   Check(rdl_conv_columns_layout(conv_, d_spectrum, d_work, d_kernel_spectrum, 2,
                                 f64_ ? norm : double(float(norm)), nullptr, Layout(),
                                 Layout(), RDL_CONV_ROW_MAJOR),
         "rdl_conv_columns_layout");
-  Check(rdl_conv_rows_inverse_peak(conv_, d_work, d_out, uint32_t(width_), uint32_t(height_),
-                                   h_border, v_border, allow_negative ? 1 : 0, d_mask, slot),
+  Check(rdl_conv_rows_inverse_peak(conv_, d_work, d_out, uint32_t(out_w), uint32_t(out_h),
+                                   uint32_t(ox), uint32_t(oy), h_border, v_border,
+                                   allow_negative ? 1 : 0, d_mask, slot),
         "rdl_conv_rows_inverse_peak");
+  return true;
+}
+
+bool Fft::ConvolveSpectrumWindow(const void* d_spectrum, const void* d_kernel_spectrum,
+                                 void* d_work, float* d_out, size_t out_w, size_t out_h,
+                                 size_t ox, size_t oy) {
+  if (!conv_) return false;
+  const double norm = 1.0 / (double(width_) * double(height_));
+  Check(rdl_conv_columns_layout(conv_, d_spectrum, d_work, d_kernel_spectrum, 2,
+                                f64_ ? norm : double(float(norm)), nullptr, Layout(),
+                                Layout(), RDL_CONV_ROW_MAJOR),
+        "rdl_conv_columns_layout");
+  Check(rdl_conv_rows_inverse(conv_, d_work, d_out, uint32_t(out_w), uint32_t(out_h),
+                              uint32_t(ox), uint32_t(oy), 0),
+        "rdl_conv_rows_inverse");
+  return true;
+}
+
+bool Fft::ConvolveWindow(const float* d_plane, const void* d_kernel_spectrum, float* d_out,
+                         size_t out_w, size_t out_h, size_t ox, size_t oy) {
+  if (!conv_) return false;
+  const double norm = 1.0 / (double(width_) * double(height_));
+  Check(rdl_conv_rows_forward(conv_, d_plane, uint32_t(width_), uint32_t(height_), 0, 0,
+                              work_.Ptr()),
+        "rdl_conv_rows_forward");
+  Check(rdl_conv_columns_layout(conv_, work_.Ptr(), work_.Ptr(), d_kernel_spectrum, 1,
+                                f64_ ? norm : double(float(norm)), nullptr,
+                                RDL_CONV_ROW_MAJOR, Layout(), RDL_CONV_ROW_MAJOR),
+        "rdl_conv_columns_layout");
+  Check(rdl_conv_rows_inverse(conv_, work_.Ptr(), d_out, uint32_t(out_w), uint32_t(out_h),
+                              uint32_t(ox), uint32_t(oy), 0),
+        "rdl_conv_rows_inverse");
   return true;
 }
 

@@ -73,6 +73,19 @@ class Fft {
                             void* d_work, float* d_out, uint32_t h_border,
                             uint32_t v_border, bool allow_negative, const uint8_t* d_mask,
                             uint32_t slot);
+  /// LDS engine: ConvolveSpectrum / Convolve writing only the out_w x out_h
+  /// window at (ox, oy) of the plane into d_out (out_w wide), and the peak
+  /// form on that window; false (nothing done) without the LDS engine (or,
+  /// for the peak form, without compile-time row plans).
+  bool ConvolveSpectrumWindow(const void* d_spectrum, const void* d_kernel_spectrum,
+                              void* d_work, float* d_out, size_t out_w, size_t out_h,
+                              size_t ox, size_t oy);
+  bool ConvolveSpectrumWindowPeak(const void* d_spectrum, const void* d_kernel_spectrum,
+                                  void* d_work, float* d_out, size_t out_w, size_t out_h,
+                                  size_t ox, size_t oy, uint32_t h_border, uint32_t v_border,
+                                  bool allow_negative, const uint8_t* d_mask, uint32_t slot);
+  bool ConvolveWindow(const float* d_plane, const void* d_kernel_spectrum, float* d_out,
+                      size_t out_w, size_t out_h, size_t ox, size_t oy);
   /// LDS engine only: residual(window) -= Trim(conv(Untrim(image), kernel)),
   /// the image (img_w x img_h) placed at (ox, oy) in the plane.
   /// d_row_mask (plane rows, 0 = the image row is all zero) skips the empty

@@ -207,6 +207,8 @@ void MultiScaleTransforms::Transform(float* d_image, float scale) {
                                  d_image, uint32_t(width_), uint32_t(height_),
                                  uint32_t(radius_), uint32_t(radius_)),
              "rdl_periodic_extend");
+  // the window of the convolved plane straight into the image (no Crop pass)
+  if (fft_->ConvolveWindow(plane, spectrum, d_image, width_, height_, radius_, radius_)) return;
   fft_->Convolve(plane, spectrum);
   Crop(d_image);
 }
@@ -234,6 +236,9 @@ void MultiScaleTransforms::ConvolveSpectrum(const void* d_spectrum, float scale,
     fft_->ConvolveSpectrum(d_spectrum, kernel, d_work, d_out);
     return;
   }
+  if (fft_->ConvolveSpectrumWindow(d_spectrum, kernel, d_work, d_out, width_, height_,
+                                   radius_, radius_))
+    return;
   fft_->ConvolveSpectrum(d_spectrum, kernel, d_work, Plane());
   Crop(d_out);
 }
@@ -243,9 +248,15 @@ bool MultiScaleTransforms::ConvolveSpectrumPeak(const void* d_spectrum, float sc
                                                 uint32_t h_border, uint32_t v_border,
                                                 bool allow_negative, const uint8_t* d_mask,
                                                 uint32_t slot) {
-  if (Extended()) return false;
-  return TheFft().ConvolveSpectrumPeak(d_spectrum, KernelSpectrum(scale), d_work, d_out,
-                                       h_border, v_border, allow_negative, d_mask, slot);
+  if (Extended() && KernelRadius(scale) > radius_)
+    throw std::logic_error("ConvolveSpectrumPeak: scale larger than the planned margin");
+  const void* kernel = KernelSpectrum(scale);
+  if (!Extended())
+    return fft_->ConvolveSpectrumPeak(d_spectrum, kernel, d_work, d_out, h_border, v_border,
+                                      allow_negative, d_mask, slot);
+  return fft_->ConvolveSpectrumWindowPeak(d_spectrum, kernel, d_work, d_out, width_, height_,
+                                          radius_, radius_, h_border, v_border,
+                                          allow_negative, d_mask, slot);
 }
 
 }  // namespace radler::algorithms::multiscale

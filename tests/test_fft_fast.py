@@ -236,15 +236,19 @@ class _Peak(C.Structure):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("w,h,hb,vb,neg,masked", [
-    (4096, 4096, 204, 204, 1, False), (4096, 4096, 0, 0, 0, False),
-    (2048, 1536, 17, 40, 1, True), (8192, 4096, 410, 205, 0, True),
-    (1280, 1280, 700, 0, 1, False)])
-def test_rows_inverse_fused_peak_matches_find_peak(sess, w, h, hb, vb, neg, masked):
+@pytest.mark.parametrize("w,h,hb,vb,neg,masked,win", [
+    (4096, 4096, 204, 204, 1, False, None), (4096, 4096, 0, 0, 0, False, None),
+    (2048, 1536, 17, 40, 1, True, None), (8192, 4096, 410, 205, 0, True, None),
+    (1280, 1280, 700, 0, 1, False, None),
+    # windows of periodically extended planes (tiled subimages), even and odd
+    (1536, 1536, 10, 12, 1, True, (1400, 1300, 68, 118)),
+    (2560, 3072, 0, 5, 0, False, (2301, 2999, 33, 41))])
+def test_rows_inverse_fused_peak_matches_find_peak(sess, w, h, hb, vb, neg, masked, win):
     """rdl_conv_rows_inverse_peak (the per-scale peak search fused into the
-    inverse row pass) writes the same image as rdl_conv_rows_inverse and
-    returns exactly rdl_find_peak's result on it (box, mask, sign rules,
+    inverse row pass) writes the same image (window) as rdl_conv_rows_inverse
+    and returns exactly rdl_find_peak's result on it (box, mask, sign rules,
     first index on ties)."""
+    ww, wh, ox, oy = win if win else (w, h, 0, 0)
     c = conv(sess, w, h, False)
     rng = np.random.default_rng(w + h + hb)
     img = rng.standard_normal((h, w)).astype(np.float32)
@@ -259,18 +263,19 @@ def test_rows_inverse_fused_peak_matches_find_peak(sess, w, h, hb, vb, neg, mask
     dk = sess.array(delta)
     sess.rdl.rdl_conv_forward(c, dk.vp, kspec.vp)
     sess.rdl.rdl_conv_forward(c, di.vp, spec.vp)
-    mask = (rng.random((h, w)) < 0.7).astype(np.uint8)
+    mask = (rng.random((wh, ww)) < 0.7).astype(np.uint8)
     dmask = sess.array(mask) if masked else None
     mptr = dmask.vp if masked else None
-    out_a = sess.array(shape=(h, w))
-    out_b = sess.array(shape=(h, w))
+    out_a = sess.array(shape=(wh, ww))
+    out_b = sess.array(shape=(wh, ww))
     norm = C.c_double(1.0 / (w * h))
     sess.rdl.rdl_conv_columns(c, spec.vp, work.vp, kspec.vp, 2, norm)
-    sess.rdl.rdl_conv_rows_inverse(c, work.vp, out_a.vp, w, h, 0, 0, 0)
+    sess.rdl.rdl_conv_rows_inverse(c, work.vp, out_a.vp, ww, wh, ox, oy, 0)
     ref = _Peak()
-    sess.rdl.rdl_find_peak(sess.h, out_a.vp, w, h, 0, h, hb, vb, neg, mptr, 1, C.byref(ref))
+    sess.rdl.rdl_find_peak(sess.h, out_a.vp, ww, wh, 0, wh, hb, vb, neg, mptr, 1, C.byref(ref))
     sess.rdl.rdl_conv_columns(c, spec.vp, work.vp, kspec.vp, 2, norm)
-    sess.rdl.rdl_conv_rows_inverse_peak(c, work.vp, out_b.vp, w, h, hb, vb, neg, mptr, 3)
+    sess.rdl.rdl_conv_rows_inverse_peak(c, work.vp, out_b.vp, ww, wh, ox, oy, hb, vb, neg, mptr,
+                                        3)
     got = (_Peak * 4)()
     sess.rdl.rdl_find_peak_collect(sess.h, 4, got)
     a, b = out_a.get(), out_b.get()
