@@ -663,6 +663,33 @@ const FastColumns* FindFastColumns(uint32_t n, bool f64) {
       RDL_FAST_COLS(double, 1024, true, 7, 3, 7, 8, 4),        // 4704
       RDL_FAST_COLS(double, 1024, true, 5, 3, 5, 8, 8),        // 4800
       RDL_FAST_COLS(double, 1024, true, 5, 5, 5, 5, 8),        // 5000
+      // float64 padded corrections of gridded runs' subimages
+      // (GetConvolutionSize of ~1000-1700 pixel subimages; 1 KiB-36 KiB per
+      // column, several workgroups per CU)
+      RDL_FAST_COLS(double, 256, true, 7, 5, 5, 3, 2),                 // 1050
+      RDL_FAST_COLS(double, 256, true, 5, 9, 3, 8),                    // 1080
+      RDL_FAST_COLS(double, 256, true, 7, 5, 8, 4),                    // 1120
+      RDL_FAST_COLS(double, 256, true, 7, 9, 9, 2),                    // 1134
+      RDL_FAST_COLS(double, 256, true, 9, 8, 4, 4),                    // 1152
+      RDL_FAST_COLS(double, 256, true, 7, 7, 3, 8),                    // 1176
+      RDL_FAST_COLS(double, 256, true, 5, 5, 3, 4, 4),                 // 1200
+      RDL_FAST_COLS(double, 256, true, 5, 5, 5, 5, 2),                 // 1250
+      RDL_FAST_COLS(double, 256, true, 7, 5, 9, 4),                    // 1260
+      RDL_FAST_COLS(double, 256, true, 5, 8, 8, 4),                    // 1280
+      RDL_FAST_COLS(double, 256, true, 9, 9, 4, 4),                    // 1296
+      RDL_FAST_COLS(double, 256, true, 7, 3, 8, 8),                    // 1344
+      RDL_FAST_COLS(double, 256, true, 7, 7, 7, 4),                    // 1372
+      RDL_FAST_COLS(double, 256, true, 7, 5, 5, 8),                    // 1400
+      RDL_FAST_COLS(double, 256, true, 5, 9, 8, 4),                    // 1440
+      RDL_FAST_COLS(double, 256, true, 9, 9, 9, 2),                    // 1458
+      RDL_FAST_COLS(double, 256, true, 7, 7, 5, 3, 2),                 // 1470
+      RDL_FAST_COLS(double, 256, true, 5, 5, 5, 3, 4),                 // 1500
+      RDL_FAST_COLS(double, 256, true, 7, 9, 3, 8),                    // 1512
+      RDL_FAST_COLS(double, 256, true, 3, 8, 8, 8),                    // 1536
+      RDL_FAST_COLS(double, 256, true, 7, 7, 8, 4),                    // 1568
+      RDL_FAST_COLS(double, 256, true, 5, 9, 9, 4),                    // 1620
+      RDL_FAST_COLS(double, 256, true, 7, 5, 3, 4, 4),                 // 1680
+      RDL_FAST_COLS(double, 256, true, 7, 5, 9, 3, 2),                 // 1890
       // float32 scale convolutions (two workgroups per CU)
       RDL_FAST_COLS(float, 512, true, 8, 8, 8, 16),            // 8192
       RDL_FAST_COLS(float, 512, true, 8, 8, 8, 8),             // 4096
@@ -692,6 +719,30 @@ const FastRows* FindFastRows(uint32_t n, bool f64) {
       RDL_FAST_ROWS(double, 256, 7, 3, 7, 4, 4),   // 4704
       RDL_FAST_ROWS(double, 256, 5, 3, 5, 8, 4),   // 4800
       RDL_FAST_ROWS(double, 256, 5, 5, 5, 5, 4),   // 5000
+      RDL_FAST_ROWS(double, 128, 7, 5, 5, 3),            // 1050
+      RDL_FAST_ROWS(double, 128, 5, 9, 3, 4),            // 1080
+      RDL_FAST_ROWS(double, 128, 7, 5, 4, 4),            // 1120
+      RDL_FAST_ROWS(double, 128, 7, 9, 9),               // 1134
+      RDL_FAST_ROWS(double, 128, 9, 8, 8),               // 1152
+      RDL_FAST_ROWS(double, 128, 7, 7, 3, 4),            // 1176
+      RDL_FAST_ROWS(double, 128, 5, 5, 3, 8),            // 1200
+      RDL_FAST_ROWS(double, 128, 5, 5, 5, 5),            // 1250
+      RDL_FAST_ROWS(double, 128, 7, 5, 9, 2),            // 1260
+      RDL_FAST_ROWS(double, 128, 5, 8, 4, 4),            // 1280
+      RDL_FAST_ROWS(double, 128, 9, 9, 8),               // 1296
+      RDL_FAST_ROWS(double, 128, 7, 3, 8, 4),            // 1344
+      RDL_FAST_ROWS(double, 128, 7, 7, 7, 2),            // 1372
+      RDL_FAST_ROWS(double, 128, 7, 5, 5, 4),            // 1400
+      RDL_FAST_ROWS(double, 128, 5, 9, 4, 4),            // 1440
+      RDL_FAST_ROWS(double, 128, 9, 9, 9),               // 1458
+      RDL_FAST_ROWS(double, 128, 7, 7, 5, 3),            // 1470
+      RDL_FAST_ROWS(double, 128, 5, 5, 5, 3, 2),         // 1500
+      RDL_FAST_ROWS(double, 128, 7, 9, 3, 4),            // 1512
+      RDL_FAST_ROWS(double, 128, 3, 8, 8, 4),            // 1536
+      RDL_FAST_ROWS(double, 128, 7, 7, 4, 4),            // 1568
+      RDL_FAST_ROWS(double, 128, 5, 9, 9, 2),            // 1620
+      RDL_FAST_ROWS(double, 128, 7, 5, 3, 8),            // 1680
+      RDL_FAST_ROWS(double, 128, 7, 5, 9, 3),            // 1890
       RDL_FAST_ROWS(float, 256, 16, 16, 16),       // 8192
       RDL_FAST_ROWS(float, 256, 16, 16, 8),        // 4096
       RDL_FAST_ROWS(float, 256, 16, 16, 7),        // 3584

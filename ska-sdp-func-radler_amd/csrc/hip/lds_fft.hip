@@ -23,6 +23,7 @@
 // Twiddles come from a float64 table (rounded to T for float plans).
 #include <cmath>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 
 #include "fft_dft.h"
@@ -897,6 +898,15 @@ int rdl_conv_create_ex(rdl_session* s, uint32_t width, uint32_t height, int f64,
         1, std::min<uint32_t>(c->f64 ? 16 : 32,
                               rdl::kMaxWgElems / (std::max(n1, n2) + 1)));
   }
+  // RDL_LOG_FFT_PLANS=1: one line per plan (sizes, precision, which kernels)
+  static const bool log_plans = [] {
+    const char* e = std::getenv("RDL_LOG_FFT_PLANS");
+    return e && e[0] == '1';
+  }();
+  if (log_plans)
+    std::fprintf(stderr, "[fft-plan] %ux%u %s rows=%s cols=%s\n", width, height,
+                 c->f64 ? "f64" : "f32", c->fast_rows ? "fast" : "runtime",
+                 c->tiled ? "four-step" : c->fast_cols ? "fast" : "runtime");
   *out = c.release();
   return RDL_OK;
 }
