@@ -690,6 +690,44 @@ const FastColumns* FindFastColumns(uint32_t n, bool f64) {
       RDL_FAST_COLS(double, 256, true, 5, 9, 9, 4),                    // 1620
       RDL_FAST_COLS(double, 256, true, 7, 5, 3, 4, 4),                 // 1680
       RDL_FAST_COLS(double, 256, true, 7, 5, 9, 3, 2),                 // 1890
+      RDL_FAST_COLS(double, 256, true, 5, 3, 8, 8, 2),              // 1920
+      RDL_FAST_COLS(double, 256, true, 9, 9, 3, 8),                 // 1944
+      RDL_FAST_COLS(double, 256, true, 7, 7, 5, 8),                 // 1960
+      RDL_FAST_COLS(double, 256, true, 5, 5, 5, 8, 2),              // 2000
+      RDL_FAST_COLS(double, 256, true, 7, 9, 8, 4),                 // 2016
+      RDL_FAST_COLS(double, 256, true, 8, 8, 8, 4),                 // 2048
+      RDL_FAST_COLS(double, 256, true, 7, 5, 5, 3, 4),              // 2100
+      RDL_FAST_COLS(double, 256, true, 5, 9, 3, 8, 2),              // 2160
+      RDL_FAST_COLS(double, 256, true, 7, 5, 8, 8),                 // 2240
+      RDL_FAST_COLS(double, 256, true, 5, 5, 5, 9, 2),              // 2250
+      RDL_FAST_COLS(double, 256, true, 7, 9, 9, 4),                 // 2268
+      RDL_FAST_COLS(double, 256, true, 9, 8, 8, 4),                 // 2304
+      RDL_FAST_COLS(double, 256, true, 7, 7, 3, 8, 2),              // 2352
+      RDL_FAST_COLS(double, 256, true, 5, 5, 3, 8, 4),              // 2400
+      RDL_FAST_COLS(double, 256, true, 5, 9, 9, 3, 2),              // 2430
+      RDL_FAST_COLS(double, 256, true, 7, 7, 5, 5, 2),              // 2450
+      RDL_FAST_COLS(double, 256, true, 5, 5, 5, 5, 4),              // 2500
+      RDL_FAST_COLS(double, 256, true, 7, 5, 9, 8),                 // 2520
+      RDL_FAST_COLS(double, 256, true, 5, 8, 8, 8),                 // 2560
+      RDL_FAST_COLS(double, 256, true, 9, 9, 8, 4),                 // 2592
+      RDL_FAST_COLS(double, 256, true, 7, 7, 9, 3, 2),              // 2646
+      RDL_FAST_COLS(double, 256, true, 7, 3, 8, 8, 2),              // 2688
+      RDL_FAST_COLS(double, 256, true, 7, 7, 7, 8),                 // 2744
+      RDL_FAST_COLS(double, 256, true, 7, 5, 5, 8, 2),              // 2800
+      RDL_FAST_COLS(double, 256, true, 5, 9, 8, 8),                 // 2880
+      RDL_FAST_COLS(double, 256, true, 9, 9, 9, 4),                 // 2916
+      RDL_FAST_COLS(double, 256, true, 7, 7, 5, 3, 4),              // 2940
+      RDL_FAST_COLS(double, 256, true, 5, 5, 5, 3, 8),              // 3000
+      RDL_FAST_COLS(double, 256, true, 7, 9, 3, 8, 2),              // 3024
+      RDL_FAST_COLS(double, 256, true, 3, 8, 8, 8, 2),              // 3072
+      RDL_FAST_COLS(double, 256, true, 7, 7, 8, 8),                 // 3136
+      RDL_FAST_COLS(double, 256, true, 7, 5, 5, 9, 2),              // 3150
+      RDL_FAST_COLS(double, 256, true, 5, 5, 8, 8, 2),              // 3200
+      RDL_FAST_COLS(double, 256, true, 5, 9, 9, 8),                 // 3240
+      RDL_FAST_COLS(double, 256, true, 7, 5, 3, 8, 4),              // 3360
+      RDL_FAST_COLS(double, 256, true, 7, 9, 9, 3, 2),              // 3402
+      RDL_FAST_COLS(double, 256, true, 7, 7, 7, 5, 2),              // 3430
+      RDL_FAST_COLS(double, 256, true, 7, 5, 5, 5, 4),              // 3500
       // float32 scale convolutions (two workgroups per CU)
       RDL_FAST_COLS(float, 512, true, 8, 8, 8, 16),            // 8192
       RDL_FAST_COLS(float, 512, true, 8, 8, 8, 8),             // 4096
@@ -743,6 +781,44 @@ const FastRows* FindFastRows(uint32_t n, bool f64) {
       RDL_FAST_ROWS(double, 128, 5, 9, 9, 2),            // 1620
       RDL_FAST_ROWS(double, 128, 7, 5, 3, 8),            // 1680
       RDL_FAST_ROWS(double, 128, 7, 5, 9, 3),            // 1890
+      RDL_FAST_ROWS(double, 256, 5, 3, 8, 8),         // 1920
+      RDL_FAST_ROWS(double, 256, 9, 9, 3, 4),         // 1944
+      RDL_FAST_ROWS(double, 256, 7, 7, 5, 4),         // 1960
+      RDL_FAST_ROWS(double, 256, 5, 5, 5, 8),         // 2000
+      RDL_FAST_ROWS(double, 256, 7, 9, 8, 2),         // 2016
+      RDL_FAST_ROWS(double, 256, 8, 8, 8, 2),         // 2048
+      RDL_FAST_ROWS(double, 256, 7, 5, 5, 3, 2),      // 2100
+      RDL_FAST_ROWS(double, 256, 5, 9, 3, 8),         // 2160
+      RDL_FAST_ROWS(double, 256, 7, 5, 8, 4),         // 2240
+      RDL_FAST_ROWS(double, 256, 5, 5, 5, 9),         // 2250
+      RDL_FAST_ROWS(double, 256, 7, 9, 9, 2),         // 2268
+      RDL_FAST_ROWS(double, 256, 9, 8, 8, 2),         // 2304
+      RDL_FAST_ROWS(double, 256, 7, 7, 3, 8),         // 2352
+      RDL_FAST_ROWS(double, 256, 5, 5, 3, 8, 2),      // 2400
+      RDL_FAST_ROWS(double, 256, 5, 9, 9, 3),         // 2430
+      RDL_FAST_ROWS(double, 256, 7, 7, 5, 5),         // 2450
+      RDL_FAST_ROWS(double, 256, 5, 5, 5, 5, 2),      // 2500
+      RDL_FAST_ROWS(double, 256, 7, 5, 9, 4),         // 2520
+      RDL_FAST_ROWS(double, 256, 5, 8, 8, 4),         // 2560
+      RDL_FAST_ROWS(double, 256, 9, 9, 8, 2),         // 2592
+      RDL_FAST_ROWS(double, 256, 7, 7, 9, 3),         // 2646
+      RDL_FAST_ROWS(double, 256, 7, 3, 8, 8),         // 2688
+      RDL_FAST_ROWS(double, 256, 7, 7, 7, 4),         // 2744
+      RDL_FAST_ROWS(double, 256, 7, 5, 5, 8),         // 2800
+      RDL_FAST_ROWS(double, 256, 5, 9, 8, 4),         // 2880
+      RDL_FAST_ROWS(double, 256, 9, 9, 9, 2),         // 2916
+      RDL_FAST_ROWS(double, 256, 7, 7, 5, 3, 2),      // 2940
+      RDL_FAST_ROWS(double, 256, 5, 5, 5, 3, 4),      // 3000
+      RDL_FAST_ROWS(double, 256, 7, 9, 3, 8),         // 3024
+      RDL_FAST_ROWS(double, 256, 3, 8, 8, 8),         // 3072
+      RDL_FAST_ROWS(double, 256, 7, 7, 8, 4),         // 3136
+      RDL_FAST_ROWS(double, 256, 7, 5, 5, 9),         // 3150
+      RDL_FAST_ROWS(double, 256, 5, 5, 8, 8),         // 3200
+      RDL_FAST_ROWS(double, 256, 5, 9, 9, 4),         // 3240
+      RDL_FAST_ROWS(double, 256, 7, 5, 3, 8, 2),      // 3360
+      RDL_FAST_ROWS(double, 256, 7, 9, 9, 3),         // 3402
+      RDL_FAST_ROWS(double, 256, 7, 7, 7, 5),         // 3430
+      RDL_FAST_ROWS(double, 256, 7, 5, 5, 5, 2),      // 3500
       RDL_FAST_ROWS(float, 256, 16, 16, 16),       // 8192
       RDL_FAST_ROWS(float, 256, 16, 16, 8),        // 4096
       RDL_FAST_ROWS(float, 256, 16, 16, 7),        // 3584

@@ -63,7 +63,8 @@ CASES = [(4536, 4608, True), (4800, 5000, True), (4704, 4536, True), (9072, 9216
          # the subimage planes of tiled runs (CanonicalFftSize ladder)
          (2560, 3072, False), (3584, 1280, False), (1536, 2048, False), (2048, 1792, False),
          # the float64 corrections of gridded runs' subimages
-         (1440, 1344, True), (1250, 1176, True), (1890, 1512, True), (1050, 1620, True)]
+         (1440, 1344, True), (1250, 1176, True), (1890, 1512, True), (1050, 1620, True),
+         (2646, 3430, True), (3500, 2160, True), (2048, 2916, True)]
 
 
 @pytest.mark.parametrize("w,h,f64", CASES)
