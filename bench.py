@@ -100,6 +100,10 @@ class Timing:
     def enable(self, on):
         self.lib.rdl_timing_enable_all(int(on))
 
+    def only(self, family):
+        """Record events for this family only (None: every family)."""
+        self.lib.rdl_timing_filter_all(family.encode() if family else None)
+
     def reset(self):
         self.lib.rdl_timing_reset_all()
 
@@ -354,16 +358,58 @@ def main():
         timing.enable(True)
     print(f"[bench] rank {rank}: {workload} {args.size}^2 inputs ready; {args.warmup} warm-up "
           f"+ {args.steps} timed Perform steps", file=sys.stderr, flush=True)
-    for _ in range(args.warmup):
+    # the N > 1 default workload (tiled 8 x 8) on this one GPU, the
+    # same-workload reference point of the scaling curve
+    tiled_ref = None
+    if args.tiled_reference and world == 1 and workload == "fields":
+        st = settings_for(rd, args.size, args.max_iter, args.scales, threshold,
+                          args.grid, args.pool)
+
+        def tiled_once():
+            arrays = (psf, dirty.copy(), np.zeros_like(dirty))
+            r = rd.Radler(st, *arrays, BEAM_PX * PIXEL_SCALE)
+            t = time.perf_counter()
+            r.perform(0)
+            return rd.gpu.total_iteration_number(r), time.perf_counter() - t
+
+        print("[bench] tiled reference (warm-up + 1 step) ...", file=sys.stderr, flush=True)
+        # measured before the headline: after the fields runs the subimage
+        # streams of this process ran 1.3x slower (7.96 vs 6.07 s per step)
+        tiled_once()
+        t_comps, t_el = tiled_once()
+        tiled_ref = {"workload": (f"multiscale-{args.size}x{args.size}-{args.scales}scales"
+                                  f"-tiled{args.grid}x{args.grid}"),
+                     "value": round(t_comps / t_el, 2), "ms_per_step": round(1e3 * t_el, 2),
+                     "components_per_step": t_comps, "pool": args.pool,
+                     "note": "the default N > 1 workload (ParallelDeconvolution subimages) "
+                             "on one GPU, for the same-workload scaling curve"}
+
+    # Per-launch HIP events cost time (in the gridded runs, with 16 streams of
+    # small kernels, 15-35 % of a step), so every family is timed on the last
+    # warm-up step only; the timed steps record events for the dominant
+    # family alone (its roofline stays measured live over the timed region).
+    fams_all = None
+    for w in range(args.warmup):
+        profile = w == args.warmup - 1 and not args.timing_all
+        if profile:
+            timing.reset()
+            timing.only(None)
+            timing.enable(True)
         r, arrays = make_radler()
         r.perform(0)
         del r, arrays
+        if profile:
+            timing.enable(False)
+            fams_all = timing.get()
+    dominant = (max(fams_all.items(), key=lambda kv: kv[1]["ms"])[0]
+                if fams_all else None)
     steps = [make_radler() for _ in range(args.steps)]
     if os.environ.get("RADLER_HOST_PROFILE") == "1":
         rd.gpu.host_profile_reset()  # the printed host profile covers the timed steps
 
     if not args.timing_all:
         timing.reset()
+        timing.only(dominant)
     timing.enable(True)
     barrier()
     t0 = time.perf_counter()
@@ -375,6 +421,7 @@ def main():
     elapsed = time.perf_counter() - t0
     if not args.timing_all:
         timing.enable(False)
+        timing.only(None)
     fams = timing.get()
     if args.dump_families and rank == 0:
         with open(args.dump_families, "w") as f:
@@ -425,8 +472,11 @@ def main():
         return
 
     ms_per_step = 1e3 * max_elapsed / args.steps
-    device_ms = sum(v["ms"] for v in fams.values())
-    # dominant kernel family by device time
+    # device-time shares from the every-family profile of the last warm-up
+    # step (the timed steps record the dominant family only)
+    prof = fams_all if fams_all else fams
+    device_ms = sum(v["ms"] for v in prof.values())
+    # dominant kernel family by device time, timed over the timed region
     dom_name, dom = max(fams.items(), key=lambda kv: kv[1]["ms"]) if fams else (None, None)
     roofline = None
     if dom is not None and dom["ms"] > 0:
@@ -440,11 +490,12 @@ def main():
                     "traffic_source": traffic_src,
                     "avg_launch_us": round(avg_ms * 1e3, 2),
                     "bytes_per_launch": bytes_per_launch,
-                    "share_of_device_time": round(dom["ms"] / device_ms, 3) if device_ms else None}
+                    "share_of_device_time": (round(prof[dom_name]["ms"] / device_ms, 3)
+                                             if device_ms and dom_name in prof else None)}
     # the other large families against the same HBM roofline (algorithmic
     # bytes per launch / average launch time)
     families = []
-    for k, v in sorted(fams.items(), key=lambda kv: -kv[1]["ms"])[:8]:
+    for k, v in sorted(prof.items(), key=lambda kv: -kv[1]["ms"])[:8]:
         if v["ms"] <= 0 or v["bytes"] <= 0:
             continue
         gbs = v["bytes"] / (v["ms"] * 1e-3) / 1e9
@@ -454,37 +505,17 @@ def main():
                          "achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)})
     if roofline is not None:
         roofline["families"] = families
+        roofline["families_source"] = ("last warm-up step, every family timed"
+                                       if fams_all else "timed steps")
     if args.breakdown:
-        for k, v in sorted(fams.items(), key=lambda kv: -kv[1]["ms"]):
+        # per family over the profiled warm-up step (one step)
+        for k, v in sorted(prof.items(), key=lambda kv: -kv[1]["ms"]):
             gbs = v["bytes"] / (v["ms"] * 1e-3) / 1e9 if v["ms"] else 0.0
             print(f"[breakdown] {k:18s} {v['ms']:10.2f} ms {v['launches']:8d} launches "
                   f"{gbs:8.1f} GB/s", file=sys.stderr)
-        print(f"[breakdown] device {device_ms:.1f} ms (all streams) of "
-              f"{1e3 * elapsed:.1f} ms wall", file=sys.stderr)
-
-    # the N > 1 default workload (tiled 8 x 8) on this one GPU: the
-    # same-workload reference point of the scaling curve
-    tiled_ref = None
-    if args.tiled_reference and world == 1 and workload == "fields":
-        st = settings_for(rd, args.size, args.max_iter, args.scales, threshold,
-                          args.grid, args.pool)
-
-        def tiled_once():
-            arrays = (psf, dirty.copy(), np.zeros_like(dirty))
-            r = rd.Radler(st, *arrays, BEAM_PX * PIXEL_SCALE)
-            t = time.perf_counter()
-            r.perform(0)
-            return rd.gpu.total_iteration_number(r), time.perf_counter() - t
-
-        print("[bench] tiled reference (warm-up + 1 step) ...", file=sys.stderr, flush=True)
-        tiled_once()
-        t_comps, t_el = tiled_once()
-        tiled_ref = {"workload": (f"multiscale-{args.size}x{args.size}-{args.scales}scales"
-                                  f"-tiled{args.grid}x{args.grid}"),
-                     "value": round(t_comps / t_el, 2), "ms_per_step": round(1e3 * t_el, 2),
-                     "components_per_step": t_comps, "pool": args.pool,
-                     "note": "the default N > 1 workload (ParallelDeconvolution subimages) "
-                             "on one GPU, for the same-workload scaling curve"}
+        print(f"[breakdown] device {device_ms:.1f} ms (all streams) in "
+              f"{'one warm-up step' if fams_all else f'{1e3 * elapsed:.1f} ms wall'}",
+              file=sys.stderr)
 
     cpu = None
     if args.cpu_outer > 0 and world == 1 and workload == "fields":

@@ -88,6 +88,10 @@ int rdl_timing_reset(rdl_session* s);
  * reset): what one Radler::Perform launched, wherever it ran. Call get/reset
  * only while no other thread launches work. */
 int rdl_timing_enable_all(int enable);
+/* Record events for this family only (NULL or "": every family); applies to
+ * every session. Lets a timed region keep one family's HIP-event timing
+ * without the others' per-launch event overhead. */
+int rdl_timing_filter_all(const char* family);
 int rdl_timing_get_all(const char* family, double* ms, uint64_t* launches,
                        double* bytes);
 int rdl_timing_reset_all(void);

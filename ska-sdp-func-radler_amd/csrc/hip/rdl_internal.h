@@ -102,14 +102,21 @@ extern std::atomic<bool> g_timing_all;
 inline bool TimingOn(const rdl_session* s) {
   return s->timing || g_timing_all.load(std::memory_order_relaxed);
 }
-
-// RAII-less helper used by launchers: records start/end events when timing.
+// rdl_timing_filter_all: when set, only this family records events (the
+// event pairs of every other launch are skipped, so a timed region can keep
+// the dominant family's HIP-event timing without the per-launch overhead of
+// all the others); empty = every family
+extern char g_timing_family[64];
+inline bool FamilyOn(const char* family) {
+  return g_timing_family[0] == 0 || std::strcmp(family, g_timing_family) == 0;
+}
 // Adds algorithmic bytes to a family after the fact (e.g. the sub-minor loop,
 // whose iteration count is known only when it returns).
 inline void AddTimingBytes(rdl_session* s, const char* family, double bytes) {
-  if (TimingOn(s)) s->timings[family].bytes += bytes;
+  if (TimingOn(s) && FamilyOn(family)) s->timings[family].bytes += bytes;
 }
 
+// Records start/end events around a launcher's kernels when timing.
 struct ScopedTiming {
   rdl_session* s;
   const char* family;
@@ -117,7 +124,7 @@ struct ScopedTiming {
   hipEvent_t start = nullptr;
   ScopedTiming(rdl_session* s_, const char* f, double b)
       : s(s_), family(f), bytes(b) {
-    if (TimingOn(s)) s->BeginTiming(family, &start);
+    if (TimingOn(s) && FamilyOn(family)) s->BeginTiming(family, &start);
   }
   ~ScopedTiming() {
     if (start) s->EndTiming(family, start, bytes);

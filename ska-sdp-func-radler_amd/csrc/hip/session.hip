@@ -26,6 +26,7 @@ void Fold(std::map<std::string, TimingEntry>& into,
 }
 }  // namespace
 std::atomic<bool> g_timing_all{false};
+char g_timing_family[64] = {0};
 void SetError(const std::string& msg) { g_last_error = msg; }
 }  // namespace rdl
 
@@ -352,6 +353,13 @@ int rdl_timing_reset(rdl_session* s) {
   RDL_ARG_CHECK(s, "NULL session");
   RDL_TRY(s->CollectTimings());
   s->timings.clear();
+  return RDL_OK;
+}
+
+int rdl_timing_filter_all(const char* family) {
+  const std::lock_guard<std::mutex> lock(rdl::g_registry_mutex);
+  std::memset(rdl::g_timing_family, 0, sizeof(rdl::g_timing_family));
+  if (family) std::strncpy(rdl::g_timing_family, family, sizeof(rdl::g_timing_family) - 1);
   return RDL_OK;
 }
 
