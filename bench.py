@@ -274,10 +274,10 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="threads of the all-cores CPU run (0: OMP_NUM_THREADS, else the "
                          "affinity core count)")
-    ap.add_argument("--cpu-single-thread", type=int, default=0,
+    ap.add_argument("--cpu-single-thread", type=int, default=1,
                     help="outer iterations of the CPU baseline on one thread after the "
                          "all-threads ones (0 = skip; one 8192^2 outer iteration on one "
-                         "thread takes minutes, so it is a separate measurement)")
+                         "thread takes one to two minutes)")
     ap.add_argument("--breakdown", action="store_true", help="per-kernel times to stderr")
     ap.add_argument("--timing-all", action="store_true",
                     help="count every launch of the process (PMC passes, tools/pmc_traffic.py)")

@@ -874,7 +874,13 @@ int rdl_conv_create_ex(rdl_session* s, uint32_t width, uint32_t height, int f64,
   if (fast_ok) {
     c->fast_cols = rdl::FindFastColumns(height, c->f64);
     if (width % 2 == 0) c->fast_rows = rdl::FindFastRows(width, c->f64);
-    if (!c->f64 && c->fast_rows) {
+    // four-step column passes from this length up (RDL_FFT_STEPS_MIN,
+    // experiments; below it the one-pass column kernel)
+    static const uint32_t steps_min = [] {
+      const char* e = std::getenv("RDL_FFT_STEPS_MIN");
+      return e ? uint32_t(std::strtoul(e, nullptr, 10)) : 0u;
+    }();
+    if (!c->f64 && c->fast_rows && height >= steps_min) {
       c->steps = rdl::FindFastSteps(height);
       c->tiled = c->steps != nullptr;
     }
