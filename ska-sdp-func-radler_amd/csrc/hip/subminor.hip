@@ -972,6 +972,105 @@ __device__ __forceinline__ uint64_t LoadGranule(uint64_t* g) {
   return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// IntegratePixel over NI register-resident values, with every per-image
+// decision (weight zero, polarization joined, i % n_pol) made once per
+// launch: the same floating-point operations in the same order as
+// IntegratePixel (rdl_internal.h), without its per-pixel index arithmetic
+// and runtime-indexed weight reads.
+template <int NI>
+struct RegIntegration {
+  uint32_t mode = 0, copy = 0, n_img = 0, n_ch = 0, np = 1;
+  uint32_t incl = 0;     // LINEAR / SQUARED_JOINS: image k enters the sum
+  uint32_t ch_live = 0;  // SQUARE, > 1 channel: channel ch has weight != 0
+  uint32_t pol_mask = 0;
+  float w[NI];           // weight of image k (SQUARE > 1 ch: of channel k)
+  float factor = 1.0f;
+
+  __device__ void Init(const rdl_integration& g) {
+    mode = g.mode;
+    copy = g.copy_fast_path;
+    n_img = g.n_images;
+    n_ch = g.n_channels;
+    np = g.n_pol;
+    pol_mask = g.pol_mask;
+    factor = g.factor;
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+      w[k] = 0.0f;
+      if (uint32_t(k) < n_img && mode != RDL_INTEGRATE_SQUARE) {
+        w[k] = g.weights[k];
+        if (w[k] != 0.0f && ((pol_mask >> (uint32_t(k) % np)) & 1u)) incl |= 1u << k;
+      }
+      if (mode == RDL_INTEGRATE_SQUARE && uint32_t(k) < n_ch && uint32_t(k) * np < n_img) {
+        w[k] = g.weights[uint32_t(k) * np];
+        if (w[k] != 0.0f) ch_live |= 1u << k;
+      }
+    }
+  }
+
+  __device__ float operator()(const float (&v)[NI]) const {
+    if (copy) return v[0];
+    if (mode == RDL_INTEGRATE_LINEAR) {
+      float acc = 0.0f;
+      bool first = true;
+#pragma unroll
+      for (int k = 0; k < NI; ++k)
+        if ((incl >> k) & 1u) {
+          acc = first ? v[k] * w[k] : __builtin_fmaf(v[k], w[k], acc);
+          first = false;
+        }
+      return first ? 0.0f : acc * factor;
+    }
+    if (mode == RDL_INTEGRATE_SQUARE) {
+      if (n_ch == 1) {
+        float acc = 0.0f;
+        bool first = true;
+#pragma unroll
+        for (int p = 0; p < NI; ++p)
+          if (uint32_t(p) < np && ((pol_mask >> p) & 1u)) {
+            acc = first ? v[p] * v[p] : __builtin_fmaf(v[p], v[p], acc);
+            first = false;
+          }
+        return __builtin_sqrtf(acc) * factor;
+      }
+      float dest = 0.0f;
+#pragma unroll
+      for (int ch = 0; ch < NI; ++ch) {
+        if (uint32_t(ch) >= n_ch) continue;
+        float scratch = 0.0f;
+        if ((ch_live >> ch) & 1u) {
+          if (np == 1) {
+            scratch = v[ch];
+          } else {
+            float acc = 0.0f;
+            bool first = true;
+#pragma unroll
+            for (int q = 0; q < NI; ++q) {
+              const uint32_t p = uint32_t(q) - uint32_t(ch) * np;  // image q = ch np + p
+              if (uint32_t(q) >= uint32_t(ch) * np && p < np && ((pol_mask >> p) & 1u)) {
+                acc = first ? v[q] * v[q] : __builtin_fmaf(v[q], v[q], acc);
+                first = false;
+              }
+            }
+            scratch = first ? 0.0f : __builtin_sqrtf(acc);
+          }
+        }
+        dest = ch == 0 ? scratch * w[ch] : __builtin_fmaf(scratch, w[ch], dest);
+      }
+      return dest * factor;
+    }
+    float acc = 0.0f;  // RDL_INTEGRATE_SQUARED_JOINS
+    bool first = true;
+#pragma unroll
+    for (int k = 0; k < NI; ++k)
+      if ((incl >> k) & 1u) {
+        acc = first ? v[k] * v[k] * w[k] : __builtin_fmaf(v[k] * v[k], w[k], acc);
+        first = false;
+      }
+    return first ? 0.0f : __builtin_sqrtf(acc) * factor;
+  }
+};
+
 // FAST: one image whose integration is the identity (ImageSet copy fast path,
 // cpp/image_set.cc:425-430): the integrated value is the residual itself.
 // THREADS = 512 (eight waves, one LDS barrier per iteration) or 64: the
@@ -991,6 +1090,8 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopReg(LoopArgs a) {
       base >= a.n_sel ? 0u : uint32_t(min<uint64_t>(a.per_block, a.n_sel - base));
   const int n_img = int(a.n_img);
   const int n_pol = int(a.n_pol);
+  RegIntegration<NI> ri;
+  if constexpr (!FAST) ri.Init(a.integ);
 
   uint32_t pos[ITEMS];
   float R[ITEMS][NI];
@@ -1081,12 +1182,7 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopReg(LoopArgs a) {
     for (int i = 0; i < ITEMS; ++i) {
       const uint32_t j = tid + uint32_t(i) * THREADS;
       if (j < cnt) {
-        float integ = FAST ? R[i][0] : IntegratePixel(a.integ, [&](uint32_t kk) {
-          float r = R[i][0];
-#pragma unroll
-          for (int q = 1; q < NI; ++q) r = (uint32_t(q) == kk) ? R[i][q] : r;
-          return r;
-        });
+        float integ = FAST ? R[i][0] : ri(R[i]);
         if (a.rms) integ *= F[i];  // scratch *= rms (subminor_loop.cc:16-18)
         uint64_t key = MaxKey(integ, a.allow_negative, base + j);
         if (base + j == 0 && integ != integ) key = ~0ull;  // scratch[0] is NaN
@@ -1261,12 +1357,7 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopReg(LoopArgs a) {
     const uint64_t winner_p = (gkey == 0 || gkey == ~0ull)
                                   ? 0ull
                                   : uint64_t(0xffffffffu - uint32_t(gkey));
-    m = FAST ? wr[0] : IntegratePixel(a.integ, [&](uint32_t kk) {
-      float r = wr[0];
-#pragma unroll
-      for (int q = 1; q < NI; ++q) r = (uint32_t(q) == kk) ? wr[q] : r;
-      return r;
-    });
+    m = FAST ? wr[0] : ri(wr);
     if (a.rms) {
       // the winner's integrated x factor is the value its key was made from
       // (with its sign from the integrated value, the factor being >= 0)
