@@ -379,7 +379,6 @@ __global__ __launch_bounds__(TH) void RowsForward(RowArgs a, const float* __rest
                                                   const Cx<T>* __restrict__ ptw) {
   constexpr uint32_t H = Product<Rs...>();
   constexpr uint32_t EH = (H + TH - 1) / TH;
-  constexpr uint32_t EX = (H + 1 + TH - 1) / TH;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   Cx<T>* buf = reinterpret_cast<Cx<T>*>(lds_raw);
   const uint32_t tid = threadIdx.x;
@@ -414,18 +413,27 @@ __global__ __launch_bounds__(TH) void RowsForward(RowArgs a, const float* __rest
     Fft<T, TH, H, 0, 1, Rs...>(buf, ptw, tid);
     Cx<T>* X = spec + size_t(y) * a.ld;
     const T h = T(0.5);
-#pragma unroll
-    for (uint32_t i = 0; i < EX; ++i) {
-      const uint32_t k = tid + i * TH;
-      if (k > H) continue;
-      const Cx<T> zk = buf[Lx<T>(k == H ? 0 : k)];
-      const Cx<T> zc = Conj(buf[Lx<T>(k == 0 ? 0 : H - k)]);
+    // X[k] from (Z[k], conj Z[H-k]) and X[H-k] from (Z[H-k], conj Z[k]): the
+    // bins in pairs, each LDS value read once (X[0] and X[H] both come from
+    // Z[0]); every output is the same expression as bin by bin
+    auto put = [&](uint32_t k, Cx<T> zk, Cx<T> zc) {
       const Cx<T> ev = {h * (zk.x + zc.x), h * (zk.y + zc.y)};
       const Cx<T> od = {h * (zk.y - zc.y), -h * (zk.x - zc.x)};  // (zk - zc) / 2i
       const Cx<T> v = Add(ev, Mul(tw[k], od));
       // one address, one 8/16-byte store (a store per layout branch was
       // split into scalar halves)
       *(a.tiled ? spec + TileIndex(y, k, a.height) : X + k) = v;
+    };
+    constexpr uint32_t NP = H / 2 + 1;
+    constexpr uint32_t EP = (NP + TH - 1) / TH;
+#pragma unroll
+    for (uint32_t i = 0; i < EP; ++i) {
+      const uint32_t k = tid + i * TH;
+      if (NP % TH != 0 && k >= NP) continue;
+      const Cx<T> zlo = buf[Lx<T>(k)];
+      const Cx<T> zhi = k == 0 ? zlo : buf[Lx<T>(H - k)];
+      put(k, zlo, Conj(zhi));
+      if (H - k != k) put(H - k, zhi, Conj(zlo));
     }
     LdsSync();
   }
