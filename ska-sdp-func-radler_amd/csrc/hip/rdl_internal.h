@@ -64,6 +64,9 @@ struct rdl_session {
   int n_cus = 256;
   uint32_t coop_limit = 0;       // cap on cooperative grids (0: n_cus)
   bool timing = false;
+  // timings and event_pool are written by the thread driving this session
+  // (ScopedTiming) and read by rdl_timing_*_all from any thread
+  std::recursive_mutex timing_mutex;
   std::map<std::string, rdl::TimingEntry> timings;
   std::vector<hipEvent_t> event_pool;
   // small device/host scratch used by reductions
@@ -86,6 +89,7 @@ struct rdl_session {
   std::multimap<size_t, void*> cache_free;      // size -> block
   std::map<void*, size_t> cache_live;           // block -> size
   size_t cache_bytes = 0;                       // bytes held in cache_free
+  size_t cache_cap = size_t(96) << 30;          // min(96 GiB, device memory / 4)
   bool cache_on = true;
   int FlushCache();
 
@@ -97,6 +101,8 @@ struct rdl_session {
 };
 
 namespace rdl {
+// hands every cached block of every session on `device` back (out of memory)
+int FlushDeviceCaches(int device);
 // rdl_timing_enable_all: time every session of the process
 extern std::atomic<bool> g_timing_all;
 inline bool TimingOn(const rdl_session* s) {
@@ -113,7 +119,10 @@ inline bool FamilyOn(const char* family) {
 // Adds algorithmic bytes to a family after the fact (e.g. the sub-minor loop,
 // whose iteration count is known only when it returns).
 inline void AddTimingBytes(rdl_session* s, const char* family, double bytes) {
-  if (TimingOn(s) && FamilyOn(family)) s->timings[family].bytes += bytes;
+  if (TimingOn(s) && FamilyOn(family)) {
+    const std::lock_guard<std::recursive_mutex> lock(s->timing_mutex);
+    s->timings[family].bytes += bytes;
+  }
 }
 
 // Records start/end events around a launcher's kernels when timing.

@@ -31,6 +31,7 @@ void SetError(const std::string& msg) { g_last_error = msg; }
 }  // namespace rdl
 
 hipEvent_t rdl_session::GetEvent() {
+  const std::lock_guard<std::recursive_mutex> lock(timing_mutex);
   if (!event_pool.empty()) {
     hipEvent_t e = event_pool.back();
     event_pool.pop_back();
@@ -51,6 +52,7 @@ void rdl_session::EndTiming(const char* family, hipEvent_t start,
                             double bytes) {
   hipEvent_t end = GetEvent();
   (void)hipEventRecord(end, stream);
+  const std::lock_guard<std::recursive_mutex> lock(timing_mutex);
   rdl::TimingEntry& t = timings[family];
   t.pending.emplace_back(start, end);
   t.launches += 1;
@@ -58,6 +60,7 @@ void rdl_session::EndTiming(const char* family, hipEvent_t start,
 }
 
 int rdl_session::CollectTimings() {
+  const std::lock_guard<std::recursive_mutex> lock(timing_mutex);
   for (auto& [name, t] : timings) {
     for (auto& [a, b] : t.pending) {
       RDL_HIP_CHECK(hipEventSynchronize(b));
@@ -85,6 +88,20 @@ int rdl_session::EnsureScratch(rdl::Scratch& s, size_t bytes) {
   if (poison) RDL_HIP_CHECK(hipMemsetAsync(s.ptr, 0xff, bytes, stream));
   return RDL_OK;
 }
+
+namespace rdl {
+int FlushDeviceCaches(int device) {
+  std::vector<rdl_session*> same;
+  {
+    const std::lock_guard<std::mutex> lock(g_registry_mutex);
+    for (rdl_session* o : g_sessions)
+      if (o->device == device) same.push_back(o);
+  }
+  // sessions are only destroyed by their owners, never while they allocate
+  for (rdl_session* o : same) RDL_TRY(o->FlushCache());
+  return RDL_OK;
+}
+}  // namespace rdl
 
 extern "C" {
 
@@ -118,6 +135,7 @@ int rdl_session_create(int device, rdl_session** out) {
   hipDeviceProp_t prop;
   RDL_HIP_CHECK(hipGetDeviceProperties(&prop, device));
   s->n_cus = prop.multiProcessorCount;
+  s->cache_cap = std::min(s->cache_cap, size_t(prop.totalGlobalMem) / 4);
   // debug aid: fill every fresh allocation with NaN bytes (0xff)
   const char* poison = std::getenv("RDL_POISON");
   s->poison = poison && poison[0] == '1';
@@ -158,6 +176,7 @@ int rdl_session_destroy(rdl_session* s) {
     const std::lock_guard<std::mutex> lock(rdl::g_registry_mutex);
     auto& v = rdl::g_sessions;
     v.erase(std::remove(v.begin(), v.end(), s), v.end());
+    const std::lock_guard<std::recursive_mutex> tlock(s->timing_mutex);
     if (s->CollectTimings() == RDL_OK) rdl::Fold(rdl::g_retired, s->timings);
   }
   for (auto& [name, t] : s->timings)
@@ -220,9 +239,11 @@ int rdl_malloc(rdl_session* s, size_t bytes, void** d_out) {
     RDL_HIP_CHECK(hipGetDevice(&prev));
     if (prev != s->device) RDL_HIP_CHECK(hipSetDevice(s->device));
     hipError_t e = hipMalloc(d_out, bytes);
-    if (e == hipErrorOutOfMemory && s->cache_on) {  // give the cache back, retry
+    if (e == hipErrorOutOfMemory) {
+      // give back every cached block on this device (the main session's and
+      // every worker's: a pool's sessions live for the process), then retry
       (void)hipGetLastError();
-      RDL_TRY(s->FlushCache());
+      RDL_TRY(rdl::FlushDeviceCaches(s->device));
       e = hipMalloc(d_out, bytes);
     }
     if (prev != s->device) (void)hipSetDevice(prev);
@@ -246,14 +267,13 @@ int rdl_malloc(rdl_session* s, size_t bytes, void** d_out) {
 int rdl_free(rdl_session* s, void* d_ptr) {
   RDL_ARG_CHECK(s, "NULL session");
   if (!d_ptr) return RDL_OK;
-  constexpr size_t kCacheCap = size_t(96) << 30;
   if (s->cache_on) {
     const std::lock_guard<std::mutex> lock(s->cache_mutex);
     auto it = s->cache_live.find(d_ptr);
     if (it != s->cache_live.end()) {
       const size_t bytes = it->second;
       s->cache_live.erase(it);
-      if (s->cache_bytes + bytes <= kCacheCap) {
+      if (s->cache_bytes + bytes <= s->cache_cap) {
         s->cache_free.emplace(bytes, d_ptr);
         s->cache_bytes += bytes;
         return RDL_OK;
@@ -335,6 +355,7 @@ int rdl_timing_enable(rdl_session* s, int enable) {
 int rdl_timing_get(rdl_session* s, const char* family, double* ms,
                    uint64_t* launches, double* bytes) {
   RDL_ARG_CHECK(s && family, "NULL argument");
+  const std::lock_guard<std::recursive_mutex> lock(s->timing_mutex);
   RDL_TRY(s->CollectTimings());
   auto it = s->timings.find(family);
   if (it == s->timings.end()) {
@@ -351,6 +372,7 @@ int rdl_timing_get(rdl_session* s, const char* family, double* ms,
 
 int rdl_timing_reset(rdl_session* s) {
   RDL_ARG_CHECK(s, "NULL session");
+  const std::lock_guard<std::recursive_mutex> lock(s->timing_mutex);
   RDL_TRY(s->CollectTimings());
   s->timings.clear();
   return RDL_OK;
@@ -375,6 +397,7 @@ int rdl_timing_get_all(const char* family, double* ms, uint64_t* launches,
   std::map<std::string, rdl::TimingEntry> total;
   rdl::Fold(total, rdl::g_retired);
   for (rdl_session* s : rdl::g_sessions) {
+    const std::lock_guard<std::recursive_mutex> tlock(s->timing_mutex);
     RDL_TRY(s->CollectTimings());
     rdl::Fold(total, s->timings);
   }
@@ -390,6 +413,7 @@ int rdl_timing_reset_all(void) {
   const std::lock_guard<std::mutex> lock(rdl::g_registry_mutex);
   rdl::g_retired.clear();
   for (rdl_session* s : rdl::g_sessions) {
+    const std::lock_guard<std::recursive_mutex> tlock(s->timing_mutex);
     RDL_TRY(s->CollectTimings());
     s->timings.clear();
   }

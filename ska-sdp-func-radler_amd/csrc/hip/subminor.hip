@@ -54,6 +54,7 @@ struct rdl_subminor {
   size_t pos_bytes = 0;
   int select_passes = 1;              // 1 single pass, 3 count + scan + scatter
   int select_ticket = 1;              // single pass: chunk order by ticket
+  uint64_t select_spin_limit = uint64_t(1) << 26;  // look-back polls before failing
 };
 
 namespace rdl {
@@ -224,7 +225,9 @@ constexpr uint64_t kStatusPrefix = uint64_t(2) << 32;
 __global__ __launch_bounds__(kSpThreads) void SelSinglePass(SelArgs a, uint32_t* ticket,
                                                              uint64_t* status,
                                                              uint32_t n_chunks, uint32_t* pos,
-                                                             uint64_t* total) {
+                                                             uint64_t* total,
+                                                             uint32_t* failed,
+                                                             uint64_t spin_limit) {
   __shared__ uint32_t chunk_s;
   __shared__ uint32_t wave_tot[kSelItems][kSpThreads / 64];
   __shared__ uint32_t excl_s;
@@ -281,7 +284,7 @@ __global__ __launch_bounds__(kSpThreads) void SelSinglePass(SelArgs a, uint32_t*
           __builtin_amdgcn_s_sleep(1);
           if ((st >> 32) == 0u)
             st = __hip_atomic_load(&status[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (++spins > (uint64_t(1) << 26)) break;  // never expected; ends the wave
+          if (++spins > spin_limit) break;  // never expected; ends the wave
         }
         const uint64_t pm = __ballot((st >> 32) == 2u);
         const uint32_t v = uint32_t(st);
@@ -298,8 +301,11 @@ __global__ __launch_bounds__(kSpThreads) void SelSinglePass(SelArgs a, uint32_t*
         for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off, 64);
         excl += part;
         p -= 64;
-        if (spins > (uint64_t(1) << 26)) break;
+        if (spins > spin_limit) break;
       }
+      // a predecessor never published (never expected): the prefix is wrong,
+      // so the selection is reported failed rather than silently corrupt
+      if (spins > spin_limit && lane == 0) atomicOr(failed, 1u);
       if (lane == 0)
         __hip_atomic_store(&status[b], kStatusPrefix | uint32_t(excl + count),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1577,6 +1583,9 @@ int rdl_subminor_create(rdl_session* s, rdl_subminor** out) {
     h->select_passes = v == 3 ? 3 : 1;
     h->select_ticket = v == 2 ? 0 : 1;  // 2: single pass ordered by blockIdx
   }
+  // test hook: RDL_SELECT_SPIN_LIMIT=0 makes any look-back wait fail
+  if (const char* e = std::getenv("RDL_SELECT_SPIN_LIMIT"))
+    h->select_spin_limit = std::strtoull(e, nullptr, 10);
   // RDL_SUBMINOR_TABLE_MAX=0 keeps the per-iteration PSF gathers
   if (const char* e = std::getenv("RDL_SUBMINOR_TABLE_MAX"))
     h->table_max = uint32_t(std::strtoul(e, nullptr, 10));
@@ -1646,6 +1655,7 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   // positions of up to the whole box (single pass) or the counts (three
   // kernels: RDL_SUBMINOR_SELECT=3, for comparison)
   uint32_t* counts = nullptr;
+  uint32_t* sel_failed = nullptr;  // single pass: set by a timed-out look-back
   if (h->select_passes == 1) {
     RDL_TRY(rdl::Grow(&h->counts, &h->counts_bytes,
                       size_t(n_chunks) * sizeof(uint64_t) + 64, st));
@@ -1653,10 +1663,12 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
                       std::max<size_t>(sa.box_pixels, 1) * sizeof(uint32_t), st));
     uint64_t* status = static_cast<uint64_t*>(h->counts);
     uint32_t* ticket = reinterpret_cast<uint32_t*>(status + n_chunks);
+    sel_failed = ticket + 1;
     RDL_HIP_CHECK(hipMemsetAsync(status, 0, size_t(n_chunks) * sizeof(uint64_t) + 64, st));
     rdl::ScopedTiming t(s, "subminor_select", sel_bytes);
     rdl::SelSinglePass<<<n_chunks, rdl::kSpThreads, 0, st>>>(
-        sa, h->select_ticket ? ticket : nullptr, status, n_chunks, static_cast<uint32_t*>(h->pos_buf), d_total);
+        sa, h->select_ticket ? ticket : nullptr, status, n_chunks,
+        static_cast<uint32_t*>(h->pos_buf), d_total, sel_failed, h->select_spin_limit);
   } else {
     RDL_TRY(rdl::Grow(&h->counts, &h->counts_bytes,
                       size_t(n_chunks) * sizeof(uint32_t) + 64, st));
@@ -1667,9 +1679,15 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   }
   RDL_HIP_CHECK(hipGetLastError());
   uint64_t n_sel = 0;
+  uint32_t failed = 0;
   {
-    const rdl::SmallRead r{&n_sel, d_total, sizeof(n_sel)};
-    RDL_TRY(rdl::ReadSmall(s, &r, 1));
+    const rdl::SmallRead r[2] = {{&n_sel, d_total, sizeof(n_sel)},
+                                 {&failed, sel_failed, sizeof(failed)}};
+    RDL_TRY(rdl::ReadSmall(s, r, sel_failed ? 2 : 1));
+  }
+  if (failed) {
+    rdl::SetError("rdl_subminor_run: selection look-back timed out");
+    return RDL_ERR_TIMEOUT;
   }
   h->n_selected = n_sel;
   out->n_selected = n_sel;
@@ -1936,8 +1954,11 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   if (s->trace_subminor) {
     float ms = 0.0f;
     RDL_HIP_CHECK(hipEventElapsedTime(&ms, ev0, ev1));
-    s->event_pool.push_back(ev0);
-    s->event_pool.push_back(ev1);
+    {
+      const std::lock_guard<std::recursive_mutex> lock(s->timing_mutex);
+      s->event_pool.push_back(ev0);
+      s->event_pool.push_back(ev1);
+    }
     uint64_t ph[6] = {};
     const rdl::SmallRead r{ph, la.result + 16, sizeof(ph)};
     RDL_TRY(rdl::ReadSmall(s, &r, 1));

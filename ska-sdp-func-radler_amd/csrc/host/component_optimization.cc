@@ -1,6 +1,7 @@
 #include "component_optimization.h"
 
 #include <cmath>
+#include <stdexcept>
 
 #include "multiscale_transforms.h"
 #include "spectral_fitter.h"
@@ -174,8 +175,16 @@ void LinearComponentSolve(gpu::Session& s, float* d_model, const float* d_image,
   const size_t n_active = active.size();
   if (n_active == 0) return;
   std::vector<double> x_matrix(n_active * n_active), y(n_active);
-  for (size_t i = 0; i != n_active; ++i)  // :204-208 (the index uses the height)
-    y[i] = image[active[i].first + active[i].second * height];
+  for (size_t i = 0; i != n_active; ++i) {  // :204-208 (the index uses the height)
+    const size_t idx = active[i].first + active[i].second * height;
+    // the reference's index reads past its image when width < height; that
+    // is undefined behaviour there, an error here
+    if (idx >= n)
+      throw std::runtime_error(
+          "LinearComponentSolve: component index x + y * height outside the image "
+          "(width < height, as the reference indexes)");
+    y[i] = image[idx];
+  }
   const size_t mid_x = width + width / 2, mid_y = height + height / 2;
   for (size_t i = 0; i != n_active; ++i)
     for (size_t j = 0; j != n_active; ++j) {

@@ -3,9 +3,11 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 
+#include "logger.h"
 #include "logpoly.h"
 
 namespace radler {
@@ -200,6 +202,18 @@ SpectralFitter::SpectralFitter(SpectralFittingMode mode, size_t n_terms,
   reference_frequency_ = radler::ReferenceOf(frequencies_, weights_);
   if (mode_ == SpectralFittingMode::kPolynomial)
     fit_ = radler::MakeSpectralMaps(*this).fit;
+  if (mode_ == SpectralFittingMode::kLogPolynomial) {
+    // schaapcommon's NonLinearPowerLawFitter is not vendored with the
+    // reference: the restated fitter (csrc/hip/logpoly.h) is unpinned
+    static std::once_flag warned;
+    std::call_once(warned, [] {
+      radler::log::Warn()
+          << "Warning: log-polynomial spectral fitting uses a restated "
+             "Gauss-Newton power-law fitter; its parity with schaapcommon's "
+             "NonLinearPowerLawFitter is unverified (term convention and "
+             "convergence criteria are assumptions).\n";
+    });
+  }
 }
 
 void SpectralFitter::Fit(std::vector<float>& terms, const float* values, size_t,

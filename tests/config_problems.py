@@ -59,16 +59,21 @@ def joined_channels(size, n_points, n_blobs, seed=SEED, frequencies=C3_FREQUENCI
 
 
 # Problem sizes and the settings each configuration runs with. `cap` is the
-# component (or IUWT step) budget of the committed oracle fixture.
+# component (or IUWT step) budget of the committed oracle fixture's trace;
+# `image_cap` (multiscale) a second, shorter oracle run whose residual and
+# model are stored as the image checkpoint: it stops before the first
+# decision the float32-vs-float64 rounding could flip on the GPU (the full
+# trace's first divergence, tests/test_configs_gpu.py), so the images are
+# comparable pixel for pixel.
 CONFIGS = {
     "c1": dict(kind="hogbom", size=1024, points=200, blobs=20, threshold=0.0,
                max_iterations=1000),
     "c2": dict(kind="multiscale", size=4096, points=1000, blobs=100, threshold=5 * NOISE,
-               max_scales=6, cap=20000),
+               max_scales=6, cap=20000, image_cap=7000),
     "c3": dict(kind="joined", size=4096, points=1000, blobs=100, threshold=5 * NOISE,
-               max_scales=6, cap=3000),
+               max_scales=6, cap=20000),
     "c4": dict(kind="iuwt", size=4096, points=1000, blobs=100, threshold=5 * NOISE,
-               cap=6),
+               cap=24),
     "c5": dict(kind="tiled", size=16384, points=2000, blobs=200, threshold=5 * NOISE,
                max_scales=6, grid=8, cap=200),
 }

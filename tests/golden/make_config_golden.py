@@ -94,9 +94,45 @@ def make(name):
     if c["kind"] == "hogbom":  # sparse model, exact
         nz = np.flatnonzero(mod.reshape(-1))
         out.update(model_index=nz.astype(np.int64), model_value=mod.reshape(-1)[nz])
-    np.savez_compressed(os.path.join(HERE, f"config_{name}.npz"), **out)
+    out["oracle_seconds"] = np.float64(time.time() - t0)
+    path = os.path.join(HERE, f"config_{name}.npz")
+    np.savez_compressed(path, **out)
+    if "image_cap" in c:
+        checkpoint(name)
+
+
+def checkpoint(name):
+    """Add the image checkpoint (`ck_*` keys) to an existing fixture: the
+    oracle rerun with max_iterations = image_cap from the same inputs; its
+    trace is the full run's prefix (checked here)."""
+    c = cp.CONFIGS[name]
+    path = os.path.join(HERE, f"config_{name}.npz")
+    out = dict(np.load(path))
+    psfs, dirty = cp.problem(name)
+    assert cp.sha256(dirty) == str(out["dirty_sha256"])
+    orc = get_oracle()
+    orc.set_threads(os.cpu_count() or 8)
+    res, mod = dirty.copy(), np.zeros_like(dirty)
+    st = settings(c)
+    st["max_iterations"] = c["image_cap"]
+    t0 = time.time()
+    alg = OracleAlgorithm(orc, 1, **st)
+    r, trace = alg.execute(res, mod, psfs)
+    n = len(trace)
+    assert n == r.iteration_number == c["image_cap"], (n, r.iteration_number)
+    assert np.array_equal(trace, out["trace"][:n]), "checkpoint trace is not the full prefix"
+    print(f"{name}: checkpoint at {n} components, oracle {time.time() - t0:.1f} s", flush=True)
+    out["ck_iterations"] = np.int64(n)
+    out.update({f"ck_{k}": v for k, v in image_summary("residual", res).items()})
+    out.update({f"ck_{k}": v for k, v in image_summary("model", mod).items()})
+    np.savez_compressed(path, **out)
 
 
 if __name__ == "__main__":
-    for name in sys.argv[1:] or list(cp.CONFIGS):
-        make(name)
+    args = sys.argv[1:]
+    if args[:1] == ["--checkpoint"]:
+        for name in args[1:]:
+            checkpoint(name)
+    else:
+        for name in args or list(cp.CONFIGS):
+            make(name)

@@ -4,17 +4,23 @@
 
 * C1 Högbom 1024^2, 1000 iterations: bit-exact trace, residual (SHA-256) and
   model — no FFT on this path.
-* C2 multiscale 4096^2 (6 scales) and C3 joined 8 x 4096^2: the component
-  traces (position and scale) are compared tie-aware (tests/trace_compare.py):
-  identical up to the first divergence, and a divergence is accepted only
-  where the oracle's decision margin is below RTOL x |peak| — the GPU runs the
-  scale convolutions in float32 (the reference: FFTW float), the oracle in
-  float64. Identical traces also get their residual/model samples checked.
+* C2 multiscale 4096^2 (6 scales, 20 000 components) and C3 joined
+  8 x 4096^2 (20 000 components): the component traces (position and scale)
+  are compared tie-aware (tests/trace_compare.py): identical up to the first
+  divergence, a divergence is accepted only where the oracle's decision
+  margin is below RTOL x |peak| (the GPU runs the scale convolutions in
+  float32 — the reference: FFTW float — the oracle in float64), and never
+  before the fixture's first such near-tie (`min_prefix`).
+* Residual and model pixels: C2 reruns to the fixture's image checkpoint
+  (7 000 components, before its first divergence) and requires an identical
+  trace and the oracle's residual/model samples within IMG_TOL x max|dirty|;
+  a fully identical trace (C3) gets the same check at its end.
 * C4 IUWT 4096^2: the outer-loop step records (success, scale, pixel, scale
-  window, area) for the fixture's steps.
+  window, area) for the fixture's 24 steps, then residual/model samples.
 * C5 tiling 16384^2 8 x 8: subimage geometry bit-exact, then every
-  subimage's trace tie-aware (one worker: the reference's max_threads = 1
-  order), each subimage capped at the fixture's component budget.
+  subimage's trace (one worker: the reference's max_threads = 1 order), each
+  subimage capped at the fixture's component budget; all 64 identical, then
+  the full image's residual/model samples.
 
 The inputs are regenerated from seeds and checked against the fixture's
 SHA-256 before anything runs.
@@ -28,11 +34,13 @@ import config_problems as cp
 from trace_compare import assert_tie_aware
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-# float32 vs float64 scale convolutions: measured differences are ~1e-7 of the
-# image peak (test_scale_convolution_error_4096); a decision whose two sides
-# differ by less than RTOL x |peak| may go either way
-RTOL = 1e-5
-# residual / model agreement when the traces are identical (FFT rounding)
+# float32 vs float64 scale convolutions: the measured difference is below
+# RTOL / 4 of the convolved image's peak (test_scale_convolution_error_4096);
+# a decision whose two sides differ by less than RTOL x |peak| may go either
+# way (the oracle's margins put C2's one observed divergence at 1.55e-7)
+RTOL = 1e-6
+# residual / model agreement (x max|dirty|) when the traces are identical:
+# FFT rounding of the residual corrections and scale-convolved PSFs
 IMG_TOL = 2e-5
 
 
@@ -80,12 +88,27 @@ def sample_index(n_pixels, seed=1):
     return np.sort(np.random.default_rng(seed).choice(n_pixels, 65536, replace=False))
 
 
-def check_samples(fx, residual, model, tol):
+def check_samples(fx, residual, model, tol, prefix=""):
+    """The oracle's residual/model at the fixture's 65 536 sampled pixels of
+    every plane; returns the largest differences (printed by the tests)."""
     idx = sample_index(residual.shape[-1] * residual.shape[-2])
-    r = residual.reshape(len(fx["residual_sample"]), -1)[:, idx]
-    m = model.reshape(len(fx["model_sample"]), -1)[:, idx]
-    assert np.abs(r - fx["residual_sample"]).max() <= tol
-    assert np.abs(m - fx["model_sample"]).max() <= tol
+    rs, ms = fx[prefix + "residual_sample"], fx[prefix + "model_sample"]
+    r = residual.reshape(len(rs), -1)[:, idx]
+    m = model.reshape(len(ms), -1)[:, idx]
+    dr, dm = float(np.abs(r - rs).max()), float(np.abs(m - ms).max())
+    print(f"  residual max |gpu - oracle| {dr:.3g}, model {dm:.3g} (tolerance {tol:.3g})")
+    assert dr <= tol, dr
+    assert dm <= tol, dm
+    return dr, dm
+
+
+def min_prefix(fx, rtol=None):
+    """The fixture's first near-tie: the first component whose oracle
+    decision margin is below rtol x |peak|; the GPU trace must be identical
+    at least up to there."""
+    r = fx["margins"] / np.maximum(np.abs(fx["values"]), 1e-30)
+    near = np.flatnonzero(r < (RTOL if rtol is None else rtol))
+    return int(near[0]) if len(near) else len(fx["trace"])
 
 
 @pytest.mark.gpu
@@ -123,36 +146,102 @@ def test_c1_hogbom_1024_through_perform():
     assert cp.sha256(model[None]) == str(fx["model_sha256"])
 
 
+def _device_run(rd, name, psfs, dirty, cap=None):
+    s = settings(rd, name)
+    if cap is not None:
+        s.minor_iteration_count = cap
+    n = len(dirty)
+    return rd.gpu.DeviceRun(s, psfs if n > 1 else psfs[0], dirty if n > 1 else dirty[0],
+                            [] if n == 1 else [1.0] * n, cp.BEAM_PX * cp.PIXEL_SCALE)
+
+
 def _multiscale(name):
     from radler_import import radler as rd
     fx = fixture(name)
     psfs, dirty = inputs(name, fx)
-    n = len(dirty)
-    run = rd.gpu.DeviceRun(settings(rd, name), psfs if n > 1 else psfs[0],
-                           dirty if n > 1 else dirty[0], [] if n == 1 else [1.0] * n,
-                           cp.BEAM_PX * cp.PIXEL_SCALE)
+    run = _device_run(rd, name, psfs, dirty)
     r = run.execute()
-    c = assert_tie_aware(run.trace(), fx["trace"], fx["margins"], fx["values"], RTOL)
-    print(f"{name}: {c}")
+    k = min_prefix(fx)
+    c = assert_tie_aware(run.trace(), fx["trace"], fx["margins"], fx["values"], RTOL,
+                         min_prefix=k)
+    print(f"{name}: {c}; first oracle near-tie (margin < {RTOL:g} x |peak|) at {k}")
+    tol = IMG_TOL * float(fx["dirty_absmax"])
+    checked = False
     if c.identical:
         assert r["iterations"] == int(fx["iteration_number"])
-        tol = IMG_TOL * float(fx["dirty_absmax"])
         check_samples(fx, run.residual().reshape(dirty.shape),
                       run.model().reshape(dirty.shape), tol)
+        checked = True
+    del run
+    if "ck_iterations" in fx.files:
+        # the image checkpoint: the same run stopped before the first
+        # divergence, so residual and model are comparable pixel for pixel
+        n_ck = int(fx["ck_iterations"])
+        assert n_ck <= c.matched, (n_ck, c)
+        run = _device_run(rd, name, psfs, dirty, cap=n_ck)
+        r = run.execute()
+        assert r["iterations"] == n_ck
+        assert np.array_equal(run.trace(), fx["trace"][:n_ck])
+        print(f"{name}: image checkpoint at {n_ck} components")
+        check_samples(fx, run.residual().reshape(dirty.shape),
+                      run.model().reshape(dirty.shape), tol, prefix="ck_")
+        checked = True
+    assert checked, "no residual/model comparison for this configuration"
     return c
 
 
 @pytest.mark.gpu
 def test_c2_multiscale_4096_trace():
     c = _multiscale("c2")
-    # the fixture's budget is 20000 components; report how far the traces agree
-    assert c.matched > 0
+    assert c.matched >= 7000
 
 
 @pytest.mark.gpu
 def test_c3_joined_8x4096_trace():
-    c = _multiscale("c3")
-    assert c.matched > 0
+    _multiscale("c3")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scale", [16.0, 64.0, 256.0])
+def test_scale_convolution_error_4096(scale):
+    """RTOL's measurement: the float32 scale convolution of the C2 dirty image
+    (the 4096^2 compile-time-planned engine the multiscale path runs,
+    csrc/hip/fft_fast.hip) with the tapered-quadratic scale kernel against
+    numpy float64; max |error| relative to the convolved image's peak, the
+    scale of every peak decision made on it."""
+    import ctypes as C
+    from oracle_lib import get_oracle
+    from rdl_lib import Session
+    _, dirty = cp.problem("c2")
+    img = dirty[0]
+    h, w = img.shape
+    k = get_oracle().shape_function(scale, w)
+    n = k.shape[0]
+    ker = np.zeros((h, w), np.float32)
+    ker[:n, :n] = k
+    ker = np.roll(ker, (-(n // 2), -(n // 2)), axis=(0, 1))
+    ref = np.fft.irfft2(np.fft.rfft2(img.astype(np.float64)) *
+                        np.fft.rfft2(ker.astype(np.float64)), s=(h, w))
+    sess = Session(0)
+    c = C.c_void_p()
+    sess.rdl.rdl_conv_create_ex(sess.h, w, h, 0, 1, C.byref(c))
+    nspec = sess.rdl.lib.rdl_conv_spectrum_bytes(c) // 8
+    dk, di = sess.array(ker), sess.array(img)
+    kspec = sess.array(shape=(nspec,), dtype=np.complex64)
+    work = sess.array(shape=(nspec,), dtype=np.complex64)
+    sess.rdl.rdl_conv_forward(c, dk.vp, kspec.vp)
+    sess.rdl.rdl_conv_rows_forward(c, di.vp, w, h, 0, 0, work.vp)
+    sess.rdl.rdl_conv_columns_ex(c, work.vp, work.vp, kspec.vp, 1,
+                                 C.c_double(float(np.float32(1.0 / (w * h)))), None, 0, 0)
+    sess.rdl.rdl_conv_rows_inverse(c, work.vp, di.vp, w, h, 0, 0, 0)
+    got = di.get()
+    for x in (dk, di, kspec, work):
+        x.free()
+    sess.rdl.rdl_conv_destroy(c)
+    sess.close()
+    err = float(np.abs(got - ref).max() / np.abs(ref).max())
+    print(f"scale {scale:g} (kernel {n}^2): max |float32 - float64| = {err:.3g} x peak")
+    assert err <= RTOL / 4, err
 
 
 @pytest.mark.gpu
@@ -202,4 +291,8 @@ def test_c5_tiled_16384_8x8():
     identical = sum(c.identical for c in summary)
     print(f"c5: {identical}/{n_sub} subimage traces identical; "
           f"{sum(c.matched for c in summary)} of {len(trace)} components matched")
-    assert r["iterations"] > 0
+    assert identical == n_sub
+    print(f"c5: {r['iterations']} iterations reported, oracle {int(fx['total_iterations'])}")
+    tol = IMG_TOL * float(fx["dirty_absmax"])
+    check_samples(fx, run.residual().reshape(dirty.shape), run.model().reshape(dirty.shape),
+                  tol)

@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 from oracle_lib import OracleAlgorithm, get_oracle
-from rdl_lib import (HogbomParams, HogbomResult, Session, SubminorParams, SubminorResult,
+from rdl_lib import (HogbomParams, HogbomResult, RdlError, Session, SubminorParams, SubminorResult,
                      integration)
 
 pytestmark = pytest.mark.gpu
@@ -609,3 +609,72 @@ def test_ms_transform_any_size(orc, w, h, shape):
         expect = orc.ms_transform(img.copy(), sc, shape)
         err = np.abs(out[i] - expect).max()
         assert err <= 2e-6 * np.abs(img).max() * np.sqrt(np.log2(pw * ph)), (sc, err)
+
+
+def test_subminor_selection_lookback_timeout_is_reported(sess):
+    """The single-pass selection's decoupled look-back gives up after a spin
+    limit (never reached in practice). With the limit forced to 0
+    (RDL_SELECT_SPIN_LIMIT, read by rdl_subminor_create) any chunk that has
+    to wait for a predecessor gives up: the run must then fail with an error,
+    never return a wrong selection (every pixel of a 4096^2 box is selected
+    at threshold 0, so a correct run selects exactly 4096^2)."""
+    import os
+    w = h = 4096
+    rng = np.random.default_rng(11)
+    img = rng.standard_normal((h, w)).astype(np.float32) + np.float32(2.0)
+    psf = np.zeros((h, w), np.float32)
+    psf[h // 2, w // 2] = 1.0
+    dres, dpsf = sess.array(img), sess.array(psf)
+    failed = ok = 0
+    for _ in range(8):
+        os.environ["RDL_SELECT_SPIN_LIMIT"] = "0"
+        sm = C.c_void_p()
+        try:
+            sess.rdl.rdl_subminor_create(sess.h, C.byref(sm))
+        finally:
+            del os.environ["RDL_SELECT_SPIN_LIMIT"]
+        p = SubminorParams()
+        p.width, p.height, p.n_images, p.n_pol = w, h, 1, 1
+        p.integ = integration(1, 1, mode=0)
+        p.allow_negative, p.stop_on_negative = 1, 0
+        p.threshold, p.gain, p.divergence_limit = 0.0, 0.1, 4.0
+        p.iteration_start, p.max_iterations = 0, 1
+        out = SubminorResult()
+        trace = np.zeros((1, 2), np.uint32)
+        try:
+            sess.rdl.rdl_subminor_run(sm, dres.vp, dpsf.vp, C.byref(p), C.byref(out),
+                                      trace.ctypes.data_as(C.c_void_p), C.c_uint64(1))
+            assert out.n_selected == w * h, out.n_selected
+            ok += 1
+        except RdlError as e:
+            assert "timed out" in str(e), e
+            failed += 1
+        sess.sync()
+        sess.rdl.rdl_subminor_destroy(sm)
+    print(f"look-back with spin limit 0: {failed} runs reported a timeout, {ok} exact")
+    assert failed >= 1
+    for a in (dres, dpsf):
+        a.free()
+
+
+def test_out_of_memory_flushes_every_session_cache():
+    """rdl_malloc keeps freed blocks in its session's cache. A block cached by
+    one session (a pool worker's, which live for the process) must not make
+    another session's allocation fail: on out-of-memory every cache on the
+    device is handed back before the retry."""
+    import torch
+    a, b = Session(0), Session(0)
+    try:
+        free0, total = torch.cuda.mem_get_info(0)
+        block = int(0.2 * total)
+        x = a.array(shape=(block // 4,))
+        x.free()  # cached by session a (within its cap of total / 4)
+        # more than what is free while a's block is cached, less than what is
+        # free without it
+        want = free0 - block // 2
+        p = C.c_void_p()
+        b.rdl.rdl_malloc(b.h, C.c_size_t(want), C.byref(p))
+        b.rdl.rdl_free(b.h, p)
+    finally:
+        a.close()
+        b.close()
