@@ -232,6 +232,77 @@ def cpu_baseline(psf, dirty, max_scales, threshold, threads, outer_all, outer_si
                           f"({runs[1]['components']} components)" if len(runs) > 1 else ""))}
 
 
+def cpu_to_threshold(out_path, threads):
+    """The CPU baseline to the threshold (north_star's wall-clock-to-threshold
+    beside the CPU): the oracle's MultiScale major iteration on the C2
+    configuration (tests/config_problems.py: 4096^2, 6 scales, 1000 points +
+    100 blobs, threshold 5 sigma, no component cap), setup (scale-convolved
+    PSFs, first peak search) included and also reported alone. Runs on the
+    host only (no GPU call) and writes one JSON object to `out_path`; bench.py
+    reads the committed copy (profiles/r*_cpu_c2_to_threshold.json) into the
+    line beside the GPU's live run of the same problem (`c2_to_threshold`)."""
+    import threading
+    import config_problems as cp
+    from oracle_lib import OracleAlgorithm, get_oracle
+    psfs, dirty = cp.problem("c2")
+    c = cp.CONFIGS["c2"]
+    orc = get_oracle()
+    orc.set_threads(threads)
+    res, mod = dirty.copy(), np.zeros_like(dirty)
+    alg = OracleAlgorithm(orc, 1, threshold=c["threshold"], max_iterations=10 ** 9,
+                          border_ratio=0.0, max_scales=c["max_scales"],
+                          beam_size_in_pixels=cp.BEAM_PX, minor_loop_gain=0.1,
+                          major_loop_gain=1.0, allow_negative=1)
+    done = threading.Event()
+
+    def heartbeat():
+        t = time.perf_counter()
+        while not done.wait(30.0):
+            print(f"[cpu_to_threshold] running {time.perf_counter() - t:.0f} s",
+                  file=sys.stderr, flush=True)
+
+    hb = threading.Thread(target=heartbeat, daemon=True)
+    hb.start()
+    t0 = time.perf_counter()
+    try:
+        r, _ = alg.execute(res, mod, psfs, trace_cap=1)
+    finally:
+        done.set()
+        hb.join()
+    total = time.perf_counter() - t0
+    setup = alg.setup_seconds()
+    n = int(r.iteration_number)
+    out = {"workload": "c2: multiscale 4096x4096, 6 scales, 1000 points + 100 blobs, "
+                       "threshold 5 sigma (tests/config_problems.py)",
+           "kind": "port", "threads": threads, "cpu_model": cpu_model(),
+           "affinity_cores": affinity_cores(),
+           "wall_clock_to_threshold_s": round(total, 2), "setup_s": round(setup, 2),
+           "clean_s": round(total - setup, 2), "components": n,
+           "final_peak": float(r.final_peak),
+           "reached_threshold": bool(abs(r.final_peak) <= c["threshold"] * 1.0000001),
+           "components_per_s_with_setup": round(n / total, 2),
+           "components_per_s_after_setup": round(n / max(total - setup, 1e-9), 2),
+           "note": "oracle MultiScale (C++ restatement of the reference, std::thread, "
+                   "float64 FFT; the reference uses FFTW float), one major iteration "
+                   "(major_loop_gain 1) to the threshold"}
+    with open(out_path, "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out), flush=True)
+
+
+def committed_cpu_to_threshold():
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_cpu_c2_to_threshold.json")))
+    if not files:
+        return None
+    try:
+        d = json.load(open(files[-1]))
+    except (OSError, ValueError):
+        return None
+    d["source"] = os.path.relpath(files[-1], ROOT)
+    return d
+
+
 def relaunch(args):
     """--gpus N without a launcher: run this script under
     torch.distributed.run as a child (nothing here has touched the GPU) and
@@ -278,12 +349,22 @@ def main():
                     help="outer iterations of the CPU baseline on one thread after the "
                          "all-threads ones (0 = skip; one 8192^2 outer iteration on one "
                          "thread takes one to two minutes)")
+    ap.add_argument("--c2-reference", type=int, default=1,
+                    help="N = 1 fields: also time Radler.perform to the threshold on the C2 "
+                         "configuration (4096^2), the workload of the committed CPU "
+                         "to-threshold run")
+    ap.add_argument("--cpu-to-threshold", metavar="OUT_JSON",
+                    help="host only: run the CPU oracle to the threshold on C2 (setup "
+                         "included), write the JSON and exit")
     ap.add_argument("--breakdown", action="store_true", help="per-kernel times to stderr")
     ap.add_argument("--timing-all", action="store_true",
                     help="count every launch of the process (PMC passes, tools/pmc_traffic.py)")
     ap.add_argument("--dump-families", help="write the per-family launch/byte counts here")
     args = ap.parse_args()
 
+    if args.cpu_to_threshold:
+        cpu_to_threshold(args.cpu_to_threshold, args.cpu_threads or cpu_share())
+        return
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(relaunch(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -383,6 +464,32 @@ def main():
                      "components_per_step": t_comps, "pool": args.pool,
                      "note": "the default N > 1 workload (ParallelDeconvolution subimages) "
                              "on one GPU, for the same-workload scaling curve"}
+
+    # C2 (4096^2) to the threshold on this GPU: the same problem as the
+    # committed CPU to-threshold run (wall clock against wall clock)
+    c2_ref = None
+    if args.c2_reference and world == 1 and workload == "fields":
+        import config_problems as cp
+        c2 = cp.CONFIGS["c2"]
+        c2_psf, c2_dirty = cp.problem("c2")
+        sc = settings_for(rd, c2["size"], 10 ** 9, c2["max_scales"], c2["threshold"], 1, 1)
+
+        def c2_once():
+            arrays = (c2_psf[0], c2_dirty[0].copy(), np.zeros_like(c2_dirty[0]))
+            r = rd.Radler(sc, *arrays, cp.BEAM_PX * cp.PIXEL_SCALE)
+            t = time.perf_counter()
+            r.perform(0)
+            return rd.gpu.total_iteration_number(r), time.perf_counter() - t
+
+        print("[bench] C2 4096^2 to threshold (warm-up + 1 step) ...", file=sys.stderr,
+              flush=True)
+        c2_once()
+        c_comps, c_el = c2_once()
+        c2_ref = {"workload": "c2: multiscale 4096x4096, 6 scales (tests/config_problems.py)",
+                  "wall_clock_to_threshold_s": round(c_el, 4), "components": c_comps,
+                  "value": round(c_comps / c_el, 2),
+                  "step": "Radler.perform (accessor load + major iteration + store)"}
+        del c2_psf, c2_dirty
 
     # Per-launch HIP events cost time (in the gridded runs, with 16 streams of
     # small kernels, 15-35 % of a step), so every family is timed on the last
@@ -522,6 +629,18 @@ def main():
         threads = args.cpu_threads or cpu_share()
         cpu = cpu_baseline(psf, dirty, args.scales, threshold, threads, args.cpu_outer,
                            args.cpu_single_thread if threads > 1 else 0)
+        cpu["cores_note"] = (
+            "threads = OMP_NUM_THREADS, the job's CPU share on the pool's one-GPU boxes "
+            "(16); the affinity mask lists all of the machine's cores, which other jobs "
+            "share, so they are not used")
+        tt = committed_cpu_to_threshold()
+        if tt is not None:
+            if c2_ref is not None:
+                tt["gpu_wall_clock_to_threshold_s"] = c2_ref["wall_clock_to_threshold_s"]
+                tt["gpu_components"] = c2_ref["components"]
+                tt["speedup_wall_clock"] = round(
+                    tt["wall_clock_to_threshold_s"] / c2_ref["wall_clock_to_threshold_s"], 1)
+            cpu["to_threshold"] = tt
 
     grid = f"-tiled{args.grid}x{args.grid}" if split else ""
     chans = f"joined{args.channels}ch-" if joined else ""
@@ -552,6 +671,7 @@ def main():
                                    f"/pool{args.pool}" if split else f"fields{world}")},
         "device_resident": resident,
         "tiled_n1": tiled_ref,
+        "c2_to_threshold": c2_ref,
         "roofline": roofline,
         "cpu_baseline": cpu,
     }

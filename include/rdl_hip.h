@@ -414,8 +414,12 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
 
 /* Kernel choice for rdl_subminor_run (results are identical): mode 0 picks
  * automatically, 1 forces the LDS-resident loop, 2 the register-resident
- * loop; target_per_block (0 = keep) sets the selected pixels per workgroup
- * above which the register loop spreads over more workgroups. */
+ * loop, 3 the single-wave loop, 4 one 1024-thread workgroup, 5 a grid of
+ * 1024-thread workgroups, 6 the single-workgroup pairwise-table loop (one
+ * image, identity integration, no RMS / spectral / log-polynomial fit, at
+ * most 8192 pixels); target_per_block (0 = keep) sets the selected pixels
+ * per workgroup above which the register loop spreads over more workgroups
+ * (mode 6: 512 or 1024 picks the workgroup size). */
 int rdl_subminor_set_tuning(rdl_subminor* h, int mode, uint32_t target_per_block);
 
 /* SubMinorLoop::GetFullIndividualModel (subminor_loop.cc:186-193), fused

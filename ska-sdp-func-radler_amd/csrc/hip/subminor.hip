@@ -41,7 +41,8 @@ struct rdl_subminor {
   uint32_t* d_pos = nullptr;
   float* d_r = nullptr;
   float* d_m = nullptr;
-  int mode = 0;  // 0 auto, 1 LDS kernel, 2 register kernel, 3 single-wave kernel
+  int mode = 0;  // 0 auto, 1 LDS kernel, 2 register kernel, 3 single-wave kernel,
+                 // 4 one 1024-thread workgroup, 5 1024-thread grid, 6 table kernel
   uint32_t target_per_block = 1024;  // pixels per workgroup (multi-workgroup)
   uint32_t single_max = 2048;         // largest selection kept on one workgroup
   uint32_t wave_max = 128;            // largest selection on the single-wave kernel
@@ -55,6 +56,9 @@ struct rdl_subminor {
   int select_passes = 1;              // 1 single pass, 3 count + scan + scatter
   int select_ticket = 1;              // single pass: chunk order by ticket
   uint64_t select_spin_limit = uint64_t(1) << 26;  // look-back polls before failing
+  int tab = 1;                        // SubminorLoopTab where it applies (RDL_SUBMINOR_TAB=0: off)
+  uint32_t tab_threads = 0;           // 0: 512 up to 2048 pixels per participant, else 1024
+  uint32_t tab_target = 1024;         // pixels per participant (RDL_SUBMINOR_TAB_TARGET)
 };
 
 namespace rdl {
@@ -1446,6 +1450,298 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopReg(LoopArgs a) {
   }
 }
 
+// ------------------------------------------------- pairwise-table loop
+// SubminorLoopTab: SubminorLoopReg<1, ITEMS, true, THREADS> specialised for
+// the multiscale hot path's common shape — one image whose integration is the
+// identity, the pairwise PSF table, no RMS factor, spectral map or
+// log-polynomial fit — with the per-iteration dependency chain cut to: the
+// table row's loads, FMAs and 32-bit value keys, a DPP wave max whose owner
+// is found by one ballot per item (the lowest selection index among equal
+// values, as the 64-bit keys order them), one 16-byte LDS slot per wave and
+// one LDS barrier, an 8/16-lane DPP max of the slots, scalar decisions.
+//
+// G > 1 participants split the selection; their block winners are exchanged
+// through epoch-tagged 8-byte granules {epoch, word} every wave polls. The
+// grid is launched as 8 G blocks of which blocks 0, 8, 16, ... participate
+// (one XCD under the dispatcher's round-robin dealing; speed only): the
+// participants first exchange their HW_REG_XCC_ID through the placement-
+// independent protocol (sc1 stores and sc1 loads) and, only when all of them
+// are on one XCD, exchange through that XCD's L2 (plain stores, which keep
+// the line in L2, polled by sc1 loads, which bypass only L1); otherwise every
+// granule goes through sc1 stores as well. RDL_TRACE_SUBMINOR=1 measured the
+// sc1 exchange at ~4 700 of ~7 800 cycles per iteration.
+//
+// Same operations in the same order, same argmax order and tie rules as the
+// generic kernels: traces and model values are identical.
+constexpr uint32_t kTabParticipantStride = 8;  // blocks per participant
+
+__device__ __forceinline__ uint32_t XccId() {
+  // HW_REG_XCC_ID (hwreg 20), bits [3:0]
+  return uint32_t(__builtin_amdgcn_s_getreg((20) | (0 << 6) | ((4 - 1) << 11)));
+}
+
+template <int ITEMS, int THREADS>
+__global__ __launch_bounds__(THREADS) void SubminorLoopTab(LoopArgs a) {
+  constexpr int WAVES = THREADS / 64;
+  constexpr int SLANES = WAVES <= 8 ? 8 : 16;
+  // {key hi, key lo, value bits, -}, parity double-buffered
+  __shared__ uint4 slots[2][WAVES];
+  const uint32_t G = a.n_blocks;
+  if (G > 1 && blockIdx.x % kTabParticipantStride != 0u) return;
+  const uint32_t rank = G > 1 ? blockIdx.x / kTabParticipantStride : 0u;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t n = uint32_t(a.n_sel), per = a.per_block;
+  const uint32_t base = rank * per;
+  const uint32_t cnt = base >= n ? 0u : min(per, n - base);
+  const bool neg = a.allow_negative != 0;
+  // exchange granules (zeroed per launch): [G] XCC ids, then [2][G][3] records
+  uint64_t* gran = reinterpret_cast<uint64_t*>(a.records);
+  uint64_t* recs = gran + G;
+  float R[ITEMS], M[ITEMS];
+#pragma unroll
+  for (int i = 0; i < ITEMS; ++i) {
+    const uint32_t j = tid + uint32_t(i) * THREADS;
+    // beyond the slice: NaN (key 0, never a winner; see the padded table)
+    R[i] = j < cnt ? a.r[base + j] : __int_as_float(0x7fc00000);
+    M[i] = 0.0f;
+  }
+  bool fast = true;  // G > 1: exchange through the one L2 of the participants
+  bool failed = false;
+  if (G > 1) {
+    if (tid == 0)
+      __hip_atomic_store(gran + rank, (uint64_t(1) << 32) | XccId(), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t xcc = 0u;
+    bool ok = false;
+    for (uint64_t spins = 0; !failed; ++spins) {
+      uint64_t v = 0;
+      if (lane < G)
+        v = __hip_atomic_load(gran + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ok = lane >= G || (v >> 32) == 1u;
+      if (__all(ok)) {
+        xcc = uint32_t(v);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      failed = spins > (uint64_t(1) << 24);
+    }
+    const uint32_t x0 = uint32_t(__builtin_amdgcn_readlane(int(xcc), 0));
+    fast = __all(lane >= G || xcc == x0);
+  }
+  const float* table = a.table;
+  float c = 0.0f, m = 0.0f, start_abs = 0.0f, flux = 0.0f;
+  uint32_t cp = 0, par = 0, epoch = 0;
+  uint32_t pend_pos = 0;
+  bool pend = false;  // a trace entry waiting for its position's load
+  bool have = false, diverging = false;
+  uint64_t iteration = a.iteration_start;
+  const bool tracer = rank == 0 && tid == 0 && a.trace;
+  // RDL_TRACE_SUBMINOR=1: per-phase cycles of participant 0, wave 0
+  uint64_t ph[6] = {0, 0, 0, 0, 0, 0};
+  const bool prof = a.prof && rank == 0 && wave == 0;
+  uint64_t t_prev = prof ? __builtin_amdgcn_s_memtime() : 0;
+#define RDL_TPHASE(i)                                      \
+  if (prof) {                                              \
+    const uint64_t t_now = __builtin_amdgcn_s_memtime();   \
+    ph[i] += t_now - t_prev;                               \
+    t_prev = t_now;                                        \
+  }
+  while (!failed) {
+    if (have) {
+      // the component's row of the pairwise table (contiguous over j): all
+      // loads in flight, then the FMAs (subminor_loop.cc:93-108)
+      const float* row = table + size_t(cp) * n + base;
+      float pv[ITEMS];
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) pv[i] = row[tid + uint32_t(i) * THREADS];
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i)
+        if (__float_as_uint(pv[i]) != kOutsideBits) R[i] = __builtin_fmaf(-pv[i], c, R[i]);
+      if (pend) {  // the previous component's position has arrived with the row
+        const uint64_t t = iteration - a.iteration_start;
+        if (t < a.trace_cap) {
+          a.trace[2 * t] = pend_pos & 0xffffu;
+          a.trace[2 * t + 1] = pend_pos >> 16;
+        }
+        pend = false;
+      }
+    }
+    RDL_TPHASE(0)
+    // ---- 32-bit value keys (MaxKey's high word; NaN 0, index 0's NaN ~0)
+    uint32_t H[ITEMS];
+    uint32_t hmax = 0u;
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+      const float v = neg ? fabsf(R[i]) : R[i];
+      const uint32_t u = __float_as_uint(v);
+      uint32_t h = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+      if (v != v) h = (base + tid + uint32_t(i) * THREADS == 0u && cnt > 0u) ? 0xffffffffu : 0u;
+      H[i] = h;
+      hmax = max(hmax, h);
+    }
+    RDL_TPHASE(1)
+    // ---- wave winner: the largest key, then the lowest selection index
+    const uint32_t mh = MaxU32<64>(hmax);
+    uint32_t wj = 0u, wv = 0u;
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+      const uint64_t b = __ballot(H[i] == mh);
+      if (b) {
+        const int l = __builtin_ctzll(b);
+        wj = base + wave * 64u + uint32_t(l) + uint32_t(i) * THREADS;
+        wv = uint32_t(__builtin_amdgcn_readlane(__float_as_int(R[i]), l));
+        break;
+      }
+    }
+    // a key-0 wave stands for its first pixel (see SubminorLoopReg)
+    const uint32_t wl = mh == 0u ? 0u : 0xffffffffu - wj;
+    if (lane == 0) slots[par][wave] = make_uint4(mh, wl, wv, 0u);
+    RDL_TPHASE(2)
+    LdsBarrier();
+    RDL_TPHASE(3)
+    // ---- block winner over the wave slots
+    const uint4 s4 = lane < uint32_t(WAVES) ? slots[par][lane] : make_uint4(0u, 0u, 0u, 0u);
+    par ^= 1u;
+    uint32_t gh = MaxU32<SLANES>(s4.x);
+    bool mine = lane < uint32_t(WAVES) && s4.x == gh;
+    uint64_t t2 = __ballot(mine);
+    int win;
+    if ((t2 & (t2 - 1ull)) == 0ull) {
+      win = __builtin_ctzll(t2);
+    } else {
+      const uint32_t l2 = MaxU32<SLANES>(mine ? s4.y : 0u);
+      win = FirstLane(mine && s4.y == l2);
+    }
+    uint32_t gl = uint32_t(__builtin_amdgcn_readlane(int(s4.y), win));
+    uint32_t gv = uint32_t(__builtin_amdgcn_readlane(int(s4.z), win));
+    if (G > 1) {
+      // ---- exchange of the participants' winners
+      ++epoch;  // 1, 2, ... (granules are zeroed per launch)
+      uint64_t* mine_rec = recs + (size_t(epoch & 1u) * G + rank) * 3;
+      if (wave == 0 && lane < 3u) {
+        const uint32_t w = lane == 0 ? gh : lane == 1 ? gl : gv;
+        const uint64_t g = (uint64_t(epoch) << 32) | w;
+        if (fast)
+          __hip_atomic_store(mine_rec + lane, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        else
+          __hip_atomic_store(mine_rec + lane, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      uint32_t xh = 0u, xl = 0u, xv = 0u;
+      for (uint64_t spins = 0;; ++spins) {
+        bool ok = true;
+        if (lane < G) {
+          const uint64_t* rr = recs + (size_t(epoch & 1u) * G + lane) * 3;
+          const uint64_t g0 = __hip_atomic_load(rr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const uint64_t g1 =
+              __hip_atomic_load(rr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const uint64_t g2 =
+              __hip_atomic_load(rr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok = uint32_t(g0 >> 32) == epoch && uint32_t(g1 >> 32) == epoch &&
+               uint32_t(g2 >> 32) == epoch;
+          xh = uint32_t(g0);
+          xl = uint32_t(g1);
+          xv = uint32_t(g2);
+        }
+        if (__all(ok)) break;
+        if (spins > (uint64_t(1) << 26)) {
+          failed = true;
+          break;
+        }
+      }
+      if (failed) break;
+      // lexicographic (hi, lo) max over the participants (lanes < G)
+      gh = MaxU32<64>(lane < G ? xh : 0u);
+      mine = lane < G && xh == gh;
+      t2 = __ballot(mine);
+      if ((t2 & (t2 - 1ull)) == 0ull) {
+        win = __builtin_ctzll(t2);
+      } else {
+        const uint32_t l2 = MaxU32<64>(mine ? xl : 0u);
+        win = FirstLane(mine && xl == l2);
+      }
+      gl = uint32_t(__builtin_amdgcn_readlane(int(xl), win));
+      gv = uint32_t(__builtin_amdgcn_readlane(int(xv), win));
+    }
+    RDL_TPHASE(4)
+    // ---- identical decisions everywhere (subminor_loop.cc:56-89)
+    const bool none = gh == 0u || (gh == 0xffffffffu && gl == 0xffffffffu);
+    const uint32_t wp = none ? 0u : 0xffffffffu - gl;
+    m = __uint_as_float(gv);
+    if (!have) {
+      start_abs = fabsf(m);
+    } else {
+      if (a.divergence_limit != 0.0f) diverging = fabsf(m) > start_abs * a.divergence_limit;
+      ++iteration;
+    }
+    const bool go = fabsf(m) > a.threshold && iteration < a.max_iterations &&
+                    (!a.stop_on_negative || m >= 0.0f) && !diverging;
+    if (!go) break;
+    c = m * a.gain;
+    flux += m * a.gain;
+    cp = wp;
+    // the owner adds the component (M is never -0, so the select form is exact)
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+      const float mi = M[i] + c;
+      M[i] = wp == base + tid + uint32_t(i) * THREADS ? mi : M[i];
+    }
+    if (tracer) {  // the load lands with the next row's (one wait for both)
+      pend_pos = a.pos[wp];
+      pend = true;
+    }
+    have = true;
+    RDL_TPHASE(5)
+  }
+#undef RDL_TPHASE
+  if (prof && lane == 0) {
+    uint64_t* out = reinterpret_cast<uint64_t*>(a.result + 16);
+    for (int i = 0; i < 6; ++i) out[i] = ph[i];
+  }
+  if (pend) {
+    const uint64_t t = iteration - a.iteration_start;
+    if (t < a.trace_cap) {
+      a.trace[2 * t] = pend_pos & 0xffffu;
+      a.trace[2 * t + 1] = pend_pos >> 16;
+    }
+  }
+  if (failed) {
+    if (tid == 0) StoreSc1(&a.result[8], 1u);
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < ITEMS; ++i) {
+    const uint32_t j = tid + uint32_t(i) * THREADS;
+    if (j < cnt) a.m[base + j] = M[i];
+  }
+  if (rank == 0 && tid == 0) {
+    LoopResult* r = reinterpret_cast<LoopResult*>(a.result);
+    r->iteration = iteration;
+    r->peak = m;
+    r->diverging = diverging ? 1 : 0;
+    r->flux = flux;
+  }
+}
+
+template <int THREADS>
+int LaunchTab(const LoopArgs& a, uint32_t items, hipStream_t stream) {
+  auto k = items <= 1    ? SubminorLoopTab<1, THREADS>
+           : items <= 2  ? SubminorLoopTab<2, THREADS>
+           : items <= 4  ? SubminorLoopTab<4, THREADS>
+           : items <= 8  ? SubminorLoopTab<8, THREADS>
+           : items <= 16 ? SubminorLoopTab<(THREADS <= 256 ? 16 : 8), THREADS>
+                         : SubminorLoopTab<(THREADS <= 256 ? 32 : 8), THREADS>;
+  if (a.n_blocks > 1) {
+    void* args[] = {const_cast<LoopArgs*>(&a)};
+    RDL_HIP_CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k),
+                                             dim3(a.n_blocks * kTabParticipantStride),
+                                             dim3(THREADS), args, 0, stream));
+  } else {
+    k<<<1, THREADS, 0, stream>>>(a);
+    RDL_HIP_CHECK(hipGetLastError());
+  }
+  return RDL_OK;
+}
+
 template <int NI, int ITEMS>
 int LaunchWave(const LoopArgs& a, hipStream_t stream) {
   auto kernel = (NI == 1 && a.integ.copy_fast_path)
@@ -1583,6 +1879,11 @@ int rdl_subminor_create(rdl_session* s, rdl_subminor** out) {
     h->select_passes = v == 3 ? 3 : 1;
     h->select_ticket = v == 2 ? 0 : 1;  // 2: single pass ordered by blockIdx
   }
+  if (const char* e = std::getenv("RDL_SUBMINOR_TAB")) h->tab = std::atoi(e);
+  if (const char* e = std::getenv("RDL_SUBMINOR_TAB_TARGET"))
+    h->tab_target = uint32_t(std::strtoul(e, nullptr, 10));
+  if (const char* e = std::getenv("RDL_SUBMINOR_TAB_THREADS"))
+    h->tab_threads = uint32_t(std::strtoul(e, nullptr, 10));
   // test hook: RDL_SELECT_SPIN_LIMIT=0 makes any look-back wait fail
   if (const char* e = std::getenv("RDL_SELECT_SPIN_LIMIT"))
     h->select_spin_limit = std::strtoull(e, nullptr, 10);
@@ -1743,7 +2044,7 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   // one workgroup (up to 1024 threads) then holds selections that would
   // otherwise pay a cross-workgroup exchange per component
   const uint64_t big_cap = 1024ull * (ni_t <= 2 ? 8 : 4);
-  const bool want_table = h->mode == 0 && reg_ok && n_sel >= 2 && n_sel <= h->table_max &&
+  const bool want_table = (h->mode == 0 || h->mode == 6) && reg_ok && n_sel >= 2 && n_sel <= h->table_max &&
                           uint64_t(ni / p->n_pol) * n_sel * n_sel <= (uint64_t(1) << 27);
   // (one CU's memory pipe streams those rows: at most 8192 values per
   // iteration, so joined channels keep the grid above 8192 / N_img pixels)
@@ -1827,6 +2128,40 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
     }
     lds_bytes = use_lds ? per * bytes_per_px : 0;
   }
+  // the pairwise-table loop (mode 6 forces it): one image, identity
+  // integration, no RMS / spectral / log-polynomial fit; participants of
+  // about tab_target pixels each (one workgroup up to tab_target)
+  const bool tab_shape = want_table && ni == 1 && p->integ.copy_fast_path && !p->d_rms &&
+                         !p->d_spectral && !lpfit;
+  const bool use_tab = tab_shape && ((h->mode == 0 && h->tab) || h->mode == 6) &&
+                       !(h->mode == 0 && use_wave);
+  if (h->mode == 6 && !use_tab) {
+    rdl::SetError("table sub-minor kernel does not apply to this selection");
+    return RDL_ERR_ARG;
+  }
+  uint32_t tab_g = 1, tab_threads = 512, tab_items = 1;
+  uint64_t tab_per = n_sel;
+  if (use_tab) {
+    const uint64_t target = std::max<uint32_t>(h->tab_target, 256);
+    tab_g = uint32_t(std::min<uint64_t>({(n_sel + target - 1) / target, 32, max_blocks}));
+    tab_g = std::max<uint32_t>(tab_g, 1);
+    tab_per = (n_sel + tab_g - 1) / tab_g;
+    tab_threads = h->tab_threads == 256 || h->tab_threads == 512 || h->tab_threads == 1024
+                      ? h->tab_threads
+                      : (tab_per <= 2048 ? 512u : 1024u);
+    const uint64_t need = (tab_per + tab_threads - 1) / tab_threads;
+    const uint32_t cap = tab_threads == 256 ? 32 : 8;
+    if (need > cap) tab_threads = 1024;
+    const uint64_t need2 = (tab_per + tab_threads - 1) / tab_threads;
+    tab_items = need2 <= 1 ? 1 : need2 <= 2 ? 2 : need2 <= 4 ? 4 : need2 <= 8 ? 8
+                : need2 <= 16 ? 16 : 32;
+    if (need2 > (tab_threads == 256 ? 32u : 8u)) {
+      rdl::SetError("table sub-minor kernel: too many pixels per participant");
+      return RDL_ERR_ARG;
+    }
+    g = tab_g;
+    per = tab_per;
+  }
   rdl::LoopArgs la{};
   la.pos = h->d_pos;
   la.r = h->d_r;
@@ -1858,8 +2193,9 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   la.prof = s->trace_subminor_phases ? 1 : 0;
   const uint64_t n_trace = (h_trace && trace_cap) ? trace_cap : 0;
   const size_t rec_bytes =
-      use_reg ? (size_t(2) * g * (3 + ni_t) * sizeof(uint64_t) + 15) / 16 * 16
-              : size_t(2) * g * la.rec_words * sizeof(uint32_t);
+      use_tab   ? (size_t(7) * g * sizeof(uint64_t) + 15) / 16 * 16
+      : use_reg ? (size_t(2) * g * (3 + ni_t) * sizeof(uint64_t) + 15) / 16 * 16
+                : size_t(2) * g * la.rec_words * sizeof(uint32_t);
   const size_t sync_need = 256 + 256 + rec_bytes + n_trace * 8;
   RDL_TRY(rdl::Grow(&h->sync, &h->sync_bytes, sync_need, st));
   char* sb = static_cast<char*>(h->sync);
@@ -1869,11 +2205,12 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   la.trace = n_trace ? reinterpret_cast<uint32_t*>(sb + 512 + rec_bytes) : nullptr;
   la.trace_cap = n_trace;
   // zero counter, result and (register kernel) the epoch-tagged granules
-  RDL_HIP_CHECK(hipMemsetAsync(sb, 0, use_reg ? 512 + rec_bytes : 512, st));
+  RDL_HIP_CHECK(hipMemsetAsync(sb, 0, (use_reg || use_tab) ? 512 + rec_bytes : 512, st));
   la.table = nullptr;
   const uint32_t n_psf = ni / p->n_pol;
-  if (use_reg && want_table) {
-    const size_t table_bytes = size_t(n_psf) * n_sel * n_sel * sizeof(float);
+  if ((use_reg || use_tab) && want_table) {
+    // (+ 32 KiB: the table loop reads whole workgroup-sized slices of a row)
+    const size_t table_bytes = size_t(n_psf) * n_sel * n_sel * sizeof(float) + (32 << 10);
     RDL_TRY(rdl::Grow(&h->table, &h->table_bytes, table_bytes, st));
     rdl::ScopedTiming t(s, "subminor_table", 8.0 * double(n_psf) * n_sel * n_sel);
     rdl::BuildPairTable<<<dim3(rdl::DivUp(n_sel, 256), uint32_t(n_sel)), 256, 0, st>>>(
@@ -1890,7 +2227,14 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   }
   {
     rdl::ScopedTiming t(s, "subminor_loop", 0.0);
-    if (use_big) {
+    if (use_tab) {
+      if (tab_threads == 256)
+        RDL_TRY(rdl::LaunchTab<256>(la, tab_items, st));
+      else if (tab_threads == 512)
+        RDL_TRY(rdl::LaunchTab<512>(la, tab_items, st));
+      else
+        RDL_TRY(rdl::LaunchTab<1024>(la, tab_items, st));
+    } else if (use_big) {
       const uint64_t bi = (per + 1023) / 1024;
       const uint32_t bitems = bi <= 1 ? 1 : bi <= 2 ? 2 : bi <= 4 ? 4 : 8;
       if (ni_t == 1)
@@ -1965,8 +2309,10 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
     std::fprintf(stderr,
                  "[subminor] n_sel=%llu g=%u kind=%d threads=%d table=%d iters=%llu us=%.1f "
                  "gather=%llu integ=%llu wred=%llu bar=%llu xchg=%llu dec=%llu\n",
-                 (unsigned long long)n_sel, g, use_reg ? 10 + int(items) : int(use_lds),
-                 use_wave ? 64 : use_big ? 1024 : use_reg ? int(rdl::kRegThreads) : 512,
+                 (unsigned long long)n_sel, g,
+                 use_tab ? 30 + int(tab_items) : use_reg ? 10 + int(items) : int(use_lds),
+                 use_tab ? int(tab_threads)
+                 : use_wave ? 64 : use_big ? 1024 : use_reg ? int(rdl::kRegThreads) : 512,
                  la.table ? 1 : 0,
                  (unsigned long long)(res.iteration - p->iteration_start),
                  double(ms) * 1e3, (unsigned long long)ph[0], (unsigned long long)ph[1],
@@ -1990,8 +2336,12 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
 int rdl_subminor_set_tuning(rdl_subminor* h, int mode,
                             uint32_t target_per_block) {
   RDL_ARG_CHECK(h, "NULL argument");
-  RDL_ARG_CHECK(mode >= 0 && mode <= 5, "mode must be 0 to 5");
+  RDL_ARG_CHECK(mode >= 0 && mode <= 6, "mode must be 0 to 6");
   h->mode = mode;
+  if (mode == 6) {  // the table kernel: target_per_block = pixels per participant
+    if (target_per_block) h->tab_target = target_per_block;
+    return RDL_OK;
+  }
   if (target_per_block) h->target_per_block = target_per_block;
   return RDL_OK;
 }

@@ -455,6 +455,7 @@ SUBMINOR_CASES = [
     (128, 10, 0.0, 0.8, 300, 1, 4, 0),        # one 1024-thread workgroup forced
     (512, 200, 0.002, 1.0, 2000, 1, 5, 2048),  # grid of 1024-thread workgroups
     (200, 30, 0.002, 0.9, 800, 3, 5, 1024),
+    (128, 10, 0.0, 0.8, 300, 1, 6, 512),     # table kernel forced (pixels per participant)
 ]
 
 
@@ -531,6 +532,49 @@ def test_subminor_loop_bit_exact(sess, orc, w, n_src, threshold_frac, mgain, max
     sess.rdl.rdl_fft_destroy(f)
     sess.rdl.rdl_subminor_destroy(sm)
     for a in (dres, dpsf, dmod, kern, spec_k, padded, work):
+        a.free()
+
+
+@pytest.mark.parametrize("n_target,per_participant", [
+    (300, 1 << 20), (1500, 512), (1500, 1 << 20), (5000, 256), (5000, 1024), (5000, 1 << 20),
+    (11000, 512), (11000, 4096)])
+def test_subminor_table_kernel_bit_exact(sess, orc, n_target, per_participant):
+    """The pairwise-table loop (rdl_subminor_set_tuning mode 6) on one
+    workgroup and on grids of 2..22 participants: the threshold is set so
+    that about n_target pixels are selected; trace and model values bit-exact
+    against the oracle's sub-minor loop (GenericClean's Clark path)."""
+    w = h = 512
+    psf, dirty = synthetic(w, h, 200, 7)
+    thr = float(np.sort(np.abs(dirty).ravel())[-n_target])
+    max_iter = 1500
+    res_o, mod_o = dirty[None].copy(), np.zeros((1, h, w), np.float32)
+    alg = OracleAlgorithm(orc, 0, threshold=thr, max_iterations=max_iter, border_ratio=0.0,
+                          use_sub_minor=1, major_loop_gain=1.0)
+    r, trace_o = alg.execute(res_o, mod_o, psf[None])
+    dres, dpsf = sess.array(dirty[None]), sess.array(psf[None])
+    sm = C.c_void_p()
+    sess.rdl.rdl_subminor_create(sess.h, C.byref(sm))
+    sess.rdl.rdl_subminor_set_tuning(sm, 6, per_participant)
+    p = SubminorParams()
+    p.width, p.height, p.n_images, p.n_pol = w, h, 1, 1
+    p.integ = integration(1, 1, mode=0)
+    p.allow_negative, p.stop_on_negative = 1, 0
+    p.threshold, p.gain, p.divergence_limit = np.float32(thr), 0.1, 4.0
+    p.iteration_start, p.max_iterations = 0, max_iter
+    out = SubminorResult()
+    trace = np.zeros((max_iter, 2), np.uint32)
+    sess.rdl.rdl_subminor_run(sm, dres.vp, dpsf.vp, C.byref(p), C.byref(out),
+                              trace.ctypes.data_as(C.c_void_p), C.c_uint64(max_iter))
+    n_it = out.iteration
+    print(f"n_sel {out.n_selected}, {n_it} iterations")
+    assert abs(int(out.n_selected) - n_target) <= n_target // 10 + 5
+    assert n_it == r.iteration_number
+    assert np.array_equal(trace[:n_it], trace_o[:n_it, :2])
+    dmod = sess.array(shape=(h, w))
+    sess.rdl.rdl_subminor_model(sm, 0, dmod.vp, w, h, 0, 0, 1)
+    assert np.array_equal(bits(dmod.get()), bits(mod_o[0]))
+    sess.rdl.rdl_subminor_destroy(sm)
+    for a in (dres, dpsf, dmod):
         a.free()
 
 
@@ -662,10 +706,12 @@ def test_out_of_memory_flushes_every_session_cache():
     one session (a pool worker's, which live for the process) must not make
     another session's allocation fail: on out-of-memory every cache on the
     device is handed back before the retry."""
-    import torch
+    hip = C.CDLL("/opt/rocm/lib/libamdhip64.so")
     a, b = Session(0), Session(0)
     try:
-        free0, total = torch.cuda.mem_get_info(0)
+        f, t = C.c_size_t(), C.c_size_t()
+        assert hip.hipSetDevice(0) == 0 and hip.hipMemGetInfo(C.byref(f), C.byref(t)) == 0
+        free0, total = f.value, t.value
         block = int(0.2 * total)
         x = a.array(shape=(block // 4,))
         x.free()  # cached by session a (within its cap of total / 4)

@@ -22,6 +22,11 @@ def main():
     rng = np.random.default_rng(1)
     sm = C.c_void_p()
     s.rdl.rdl_subminor_create(s.h, C.byref(sm))
+    # mode -1: the generic kernels (auto policy with the table loop off)
+    os.environ["RDL_SUBMINOR_TAB"] = "0"
+    sm_old = C.c_void_p()
+    s.rdl.rdl_subminor_create(s.h, C.byref(sm_old))
+    del os.environ["RDL_SUBMINOR_TAB"]
     sizes = (256, 1024, 4096, 16384, 65536, 262144)
     variants = ((1, 0), (2, 512), (2, 1024), (2, 2048), (2, 4096))
     if os.environ.get("RDL_BENCH_WAVE"):  # single-wave vs eight-wave kernel
@@ -30,6 +35,10 @@ def main():
     if os.environ.get("RDL_BENCH_BIGGRID"):  # grids of 1024- vs 512-thread workgroups
         sizes = (4096, 6144, 8192, 12288, 16384, 32768)
         variants = ((0, 1024), (5, 2048), (5, 3072), (5, 4096))
+    if os.environ.get("RDL_BENCH_TAB"):  # the table kernel (pixels per participant)
+        sizes = (200, 400, 800, 1024, 1500, 2048, 3000, 4096, 6000, 8192, 11000)
+        variants = ((-1, 0), (6, 1024), (6, 4096), (6, 1 << 20))
+        threads = os.environ.get("RDL_SUBMINOR_TAB_THREADS", "")
     if os.environ.get("RDL_BENCH_BIG"):  # one 1024-thread workgroup vs the grid
         sizes = (1536, 2048, 3072, 4096, 6144, 8192)
         variants = ((0, 1024), (4, 0))
@@ -45,7 +54,8 @@ def main():
         img.flat[flat] = rng.uniform(1.0, 2.0, flat.size).astype(np.float32)
         dres = s.array(img)
         for mode, target in variants:
-            s.rdl.rdl_subminor_set_tuning(sm, mode, target)
+            h = sm_old if mode < 0 else sm
+            s.rdl.rdl_subminor_set_tuning(h, max(mode, 0), target)
             p = SubminorParams()
             p.width = p.height = size
             p.n_images, p.n_pol = 1, 1
@@ -58,7 +68,13 @@ def main():
             s.rdl.rdl_session_sync(s.h)
             t = time.perf_counter()
             try:
-                s.rdl.rdl_subminor_run(sm, dres.vp, dpsf.vp, C.byref(p), C.byref(out), None,
+                # warm (buffers sized), then timed
+                s.rdl.rdl_subminor_run(h, dres.vp, dpsf.vp, C.byref(p), C.byref(out), None,
+                                       C.c_uint64(0))
+                dres.upload(img)
+                s.rdl.rdl_session_sync(s.h)
+                t = time.perf_counter()
+                s.rdl.rdl_subminor_run(h, dres.vp, dpsf.vp, C.byref(p), C.byref(out), None,
                                        C.c_uint64(0))
             except Exception as e:  # noqa: BLE001
                 print(f"n_sel={flat.size} mode={mode} target={target}: {e}", flush=True)
@@ -68,6 +84,7 @@ def main():
                   f"us/iter={1e6 * dt / max(out.iteration, 1):7.2f}", flush=True)
         dres.free()
     s.rdl.rdl_subminor_destroy(sm)
+    s.rdl.rdl_subminor_destroy(sm_old)
 
 
 if __name__ == "__main__":
