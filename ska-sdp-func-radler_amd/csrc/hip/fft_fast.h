@@ -102,6 +102,15 @@ int FastRowsForwardLaunch(rdl_session* s, const FastRows* p, const float* in, vo
                           const void* tw, const void* ptw, uint32_t height, uint32_t img_w, uint32_t img_h,
                           uint32_t ox, uint32_t oy, const uint32_t* rows,
                           const uint32_t* n_rows, int tiled = 0);
+/* float64 convolution columns (mode 1: forward, x K x s, inverse; row-major
+ * input and output) with LDS twiddles and a register-resident K multiply
+ * (ff::ColumnsConvD); nullptr where no plan exists or RDL_FFT_CONVD=0. tw:
+ * the plan's length-n table W_n^k. */
+const FastColumns* FindConvColumnsD(uint32_t n);
+int ConvColumnsDLaunch(rdl_session* s, const FastColumns* p, const void* in, void* out,
+                       const void* kern, const void* tw, uint32_t n_cols, int kern_cm,
+                       int out_cm, const uint32_t* rows, const uint32_t* n_rows, uint32_t row0,
+                       uint32_t row_n, double scale);
 /* ascending list of the rows whose mask byte is non-zero, and its length */
 int FastCompactRows(rdl_session* s, const uint8_t* mask, uint32_t n, uint32_t* rows,
                     uint32_t* count);

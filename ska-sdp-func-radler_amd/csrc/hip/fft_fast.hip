@@ -20,6 +20,7 @@
 //   * rows outside the output window are never transformed, sparse inputs
 //     (the sub-minor model's occupied rows) are read from a compacted list.
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -233,6 +234,173 @@ __global__ __launch_bounds__(TH) void Columns(ColArgs a, const Cx<T>* __restrict
       }
     }
     LdsSync();
+  }
+}
+
+// ----------------------------------- float64 correction columns (mode 1)
+// ColumnsConvD: the column pass of CorrectResidualDirty's padded convolution
+// (forward, x K x s, inverse; sparse input rows, output row-major), with the
+// per-round latency chain of Columns cut down:
+//   * pass twiddles from two small LDS tables (W^e = T1[e >> 7] T2[e & 127],
+//     both exact entries of the plan's length-N table) instead of a global
+//     load per butterfly and pass,
+//   * the first forward pass reads the input straight from global memory
+//     through a row bitmap in LDS (no staging, no zeroing sweep per column),
+//   * the last forward pass multiplies by K x s (prefetched into registers in
+//     that pass's output order) and conjugates before its LDS store (no
+//     separate multiply sweep),
+//   * the last inverse pass stores to global memory from its registers.
+// Same arithmetic as Columns up to the twiddle products' last bit (results
+// are rounded to float by the row pass; tests/test_fft_fast.py).
+constexpr uint32_t kTwShift = 7;
+constexpr uint32_t kTwLo = 1u << kTwShift;
+
+template <uint32_t TH, uint32_t N, uint32_t R, uint32_t NS, int SRC, int DST, typename Load,
+          typename Store>
+__device__ __forceinline__ void CPass(Cx<double>* buf, const Cx<double>* t1,
+                                      const Cx<double>* t2, uint32_t tid, Load load,
+                                      Store store) {
+  constexpr uint32_t NB = N / R;
+  constexpr uint32_t BPT = (NB + TH - 1) / TH;
+  Cx<double> v[BPT][R];
+#pragma unroll
+  for (uint32_t i = 0; i < BPT; ++i) {
+    const uint32_t j = tid + i * TH;
+    if (NB % TH == 0 || j < NB) {
+#pragma unroll
+      for (uint32_t r = 0; r < R; ++r)
+        v[i][r] = SRC == 0 ? buf[j + r * NB] : load(j + r * NB);
+    }
+  }
+  if constexpr (SRC == 0) LdsSync();  // every read done before any write
+#pragma unroll
+  for (uint32_t i = 0; i < BPT; ++i) {
+    const uint32_t j = tid + i * TH;
+    if (NB % TH == 0 || j < NB) {
+      const uint32_t k = j % NS;
+      if constexpr (NS > 1) {
+        const uint32_t e = k * (N / (NS * R));
+        const Cx<double> w = Mul(t1[e >> kTwShift], t2[e & (kTwLo - 1u)]);
+        Cx<double> wr = w;
+        v[i][1] = Mul(v[i][1], wr);
+#pragma unroll
+        for (uint32_t r = 2; r < R; ++r) {
+          wr = Mul(wr, w);
+          v[i][r] = Mul(v[i][r], wr);
+        }
+      }
+      Dft<double, int(R)>::Run(v[i]);
+      const uint32_t d = (j / NS) * NS * R + k;
+#pragma unroll
+      for (uint32_t r = 0; r < R; ++r) store(i, r, d + r * NS, v[i][r]);
+    }
+  }
+  if constexpr (DST == 0) LdsSync();
+}
+
+// passes 2 .. of the forward transform (LDS to LDS); the last one goes
+// through `last` (the K multiply)
+template <uint32_t TH, uint32_t N, uint32_t NS, typename Last, uint32_t R, uint32_t... Rest>
+__device__ __forceinline__ void CFwdTail(Cx<double>* buf, const Cx<double>* t1,
+                                         const Cx<double>* t2, uint32_t tid, Last last) {
+  auto nop = [](uint32_t) { return Cx<double>{0.0, 0.0}; };
+  if constexpr (sizeof...(Rest) == 0) {
+    CPass<TH, N, R, NS, 0, 0>(buf, t1, t2, tid, nop, last);
+  } else {
+    CPass<TH, N, R, NS, 0, 0>(buf, t1, t2, tid, nop,
+                              [&](uint32_t, uint32_t, uint32_t y, Cx<double> v) { buf[y] = v; });
+    CFwdTail<TH, N, NS * R, Last, Rest...>(buf, t1, t2, tid, last);
+  }
+}
+
+// the inverse transform's passes (LDS to LDS, the last one to `last`)
+template <uint32_t TH, uint32_t N, uint32_t NS, typename Last, uint32_t R, uint32_t... Rest>
+__device__ __forceinline__ void CInv(Cx<double>* buf, const Cx<double>* t1, const Cx<double>* t2,
+                                     uint32_t tid, Last last) {
+  auto nop = [](uint32_t) { return Cx<double>{0.0, 0.0}; };
+  if constexpr (sizeof...(Rest) == 0) {
+    CPass<TH, N, R, NS, 0, 1>(buf, t1, t2, tid, nop, last);
+  } else {
+    CPass<TH, N, R, NS, 0, 0>(buf, t1, t2, tid, nop,
+                              [&](uint32_t, uint32_t, uint32_t y, Cx<double> v) { buf[y] = v; });
+    CInv<TH, N, NS * R, Last, Rest...>(buf, t1, t2, tid, last);
+  }
+}
+
+template <uint32_t... Rs>
+constexpr uint32_t LastOf() {
+  constexpr uint32_t r[] = {Rs...};
+  return r[sizeof...(Rs) - 1];
+}
+
+template <uint32_t TH, uint32_t R1, uint32_t... Rs>
+__global__ __launch_bounds__(TH) void ColumnsConvD(ColArgs a, const Cx<double>* __restrict__ in,
+                                                   Cx<double>* out,
+                                                   const Cx<double>* __restrict__ kern,
+                                                   const Cx<double>* __restrict__ tw) {
+  constexpr uint32_t N = R1 * Product<Rs...>();
+  constexpr uint32_t RL = LastOf<R1, Rs...>();
+  constexpr uint32_t NBL = N / RL;  // last pass: butterflies, = its span
+  constexpr uint32_t BL = (NBL + TH - 1) / TH;
+  constexpr uint32_t NT1 = (N + kTwLo - 1) / kTwLo;
+  constexpr uint32_t NWORDS = (N + 31) / 32;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  Cx<double>* buf = reinterpret_cast<Cx<double>*>(lds_raw);
+  Cx<double>* t1 = buf + N;
+  Cx<double>* t2 = t1 + NT1;
+  uint32_t* bits = reinterpret_cast<uint32_t*>(t2 + kTwLo);
+  const uint32_t b = blockIdx.x, G = gridDim.x;
+  const double s = a.scale;
+  {
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t i = tid; i < NT1; i += TH) t1[i] = tw[i * kTwLo];
+    for (uint32_t i = tid; i < kTwLo; i += TH) t2[i] = tw[i];
+    for (uint32_t i = tid; i < NWORDS; i += TH) bits[i] = 0u;
+    __syncthreads();
+    // the input's non-zero rows (a list, or a range)
+    const bool listed = a.rows != nullptr;
+    const uint32_t n_rows = listed ? *a.n_rows : a.row_n;
+    for (uint32_t q = tid; q < n_rows; q += TH) {
+      const uint32_t y = listed ? a.rows[q] : a.row0 + q;
+      if (y < N) atomicOr(&bits[y >> 5], 1u << (y & 31u));
+    }
+    __syncthreads();
+  }
+  for (uint32_t round = 0; round * G < a.n_cols; ++round) {
+    uint32_t tid = threadIdx.x;  // opaque per round (see Columns)
+    asm volatile("" : "+v"(tid));
+    const uint32_t c = round * G + (b & 7u) * a.per_xcd + (b >> 3);
+    const bool active = c < a.n_cols;
+    const uint32_t cc = active ? c : 0u;
+    const Cx<double>* in_c = in + cc;
+    const uint32_t k_stride = a.kern_cm ? 1u : a.ld;
+    const Cx<double>* kern_c = a.kern_cm ? kern + size_t(cc) * N : kern + cc;
+    // K x s in the last forward pass's output order: rows j + r NBL
+    Cx<double> K[BL][RL];
+#pragma unroll
+    for (uint32_t i = 0; i < BL; ++i) {
+      const uint32_t j = tid + i * TH;
+      if (NBL % TH == 0 || j < NBL)
+#pragma unroll
+        for (uint32_t r = 0; r < RL; ++r) K[i][r] = kern_c[(j + r * NBL) * k_stride];
+    }
+    // forward pass 1: straight from global memory through the row bitmap
+    auto load = [&](uint32_t y) {
+      return ((bits[y >> 5] >> (y & 31u)) & 1u) && active ? in_c[size_t(y) * a.ld]
+                                                           : Cx<double>{0.0, 0.0};
+    };
+    CPass<TH, N, R1, 1, 1, 0>(buf, t1, t2, tid, load,
+                              [&](uint32_t, uint32_t, uint32_t y, Cx<double> v) { buf[y] = v; });
+    auto mulk = [&](uint32_t i, uint32_t r, uint32_t y, Cx<double> v) {
+      buf[y] = Conj(Scale(Mul(v, K[i][r]), s));
+    };
+    CFwdTail<TH, N, R1, decltype(mulk), Rs...>(buf, t1, t2, tid, mulk);
+    // inverse = conj(forward(conj(X K s))); the last pass stores row-major
+    auto store = [&](uint32_t, uint32_t, uint32_t y, Cx<double> v) {
+      if (active) out[a.out_cm ? size_t(c) * N + y : size_t(y) * a.ld + c] = Conj(v);
+    };
+    // (its LDS reads end in a barrier, before the next round's first stores)
+    CInv<TH, N, 1, decltype(store), R1, Rs...>(buf, t1, t2, tid, store);
   }
 }
 
@@ -845,6 +1013,40 @@ const FastRows* FindFastRows(uint32_t n, bool f64) {
 #undef RDL_FAST_COLS
 #undef RDL_FAST_ROWS
 
+#define RDL_CONV_D(TH, ...)                                                    \
+  FastColumns {                                                                \
+    ff::Product<__VA_ARGS__>(), true, TH,                                      \
+        reinterpret_cast<const void*>(&ff::ColumnsConvD<TH, __VA_ARGS__>),     \
+        MakeRadixList<__VA_ARGS__>()                                           \
+  }
+const FastColumns* FindConvColumnsD(uint32_t n) {
+  static const FastColumns kPlans[] = {
+      RDL_CONV_D(512, 7, 9, 9, 4, 4),        // 9072
+      RDL_CONV_D(512, 9, 4, 4, 4, 4, 4),     // 9216
+      RDL_CONV_D(512, 7, 3, 7, 4, 4, 4),     // 9408
+      RDL_CONV_D(512, 7, 5, 3, 5, 3, 3, 2),  // 9450
+      RDL_CONV_D(512, 7, 9, 9, 8),           // 4536
+      RDL_CONV_D(512, 9, 8, 8, 8),           // 4608
+      RDL_CONV_D(512, 7, 3, 7, 8, 4),        // 4704
+      RDL_CONV_D(512, 5, 3, 5, 8, 8),        // 4800
+      RDL_CONV_D(512, 5, 5, 5, 5, 8),        // 5000
+  };
+  static const bool off = [] {
+    const char* e = std::getenv("RDL_FFT_CONVD");
+    return e && e[0] == '0';
+  }();
+  if (off) return nullptr;
+  for (const FastColumns& p : kPlans)
+    if (p.n == n) return &p;
+  return nullptr;
+}
+#undef RDL_CONV_D
+
+size_t ConvColumnsDLdsBytes(uint32_t n) {
+  return size_t(n) * 16 + size_t((n + ff::kTwLo - 1) / ff::kTwLo + ff::kTwLo) * 16 +
+         size_t((n + 31) / 32) * 4;
+}
+
 #define RDL_FAST_STEPS(N1, N2, GA, GB, RA, RB)                                     \
   FastSteps {                                                                      \
     N1 * N2, N1, N2, GA, GB, 256,                                                  \
@@ -924,6 +1126,36 @@ int FastColumnsLaunch(rdl_session* s, const FastColumns* p, const void* in, void
   a.per_xcd = std::max<uint32_t>(1, (want + 7) / 8);
   const uint32_t grid = 8 * a.per_xcd;
   void* args[] = {&a, (void*)&in, (void*)&out, (void*)&kern, (void*)&ptw};
+  RDL_HIP_CHECK(hipLaunchKernel(p->kernel, dim3(grid), dim3(p->threads), args, lds,
+                                s->stream));
+  return RDL_OK;
+}
+
+int ConvColumnsDLaunch(rdl_session* s, const FastColumns* p, const void* in, void* out,
+                       const void* kern, const void* tw, uint32_t n_cols, int kern_cm,
+                       int out_cm, const uint32_t* rows, const uint32_t* n_rows, uint32_t row0,
+                       uint32_t row_n, double scale) {
+  const size_t lds = ConvColumnsDLdsBytes(p->n);
+  const int slots = SlotsPerCu(s, p->kernel, p->threads, lds);
+  if (slots < 0) {
+    SetError("float64 correction columns: occupancy query failed");
+    return RDL_ERR_HIP;
+  }
+  ff::ColArgs a{};
+  a.n_cols = n_cols;
+  a.ld = n_cols;
+  a.mode = 1;
+  a.kern_cm = kern_cm ? 1u : 0u;
+  a.out_cm = out_cm ? 1u : 0u;
+  a.rows = rows;
+  a.n_rows = n_rows;
+  a.row0 = rows ? 0u : row0;
+  a.row_n = rows ? p->n : row_n;
+  a.scale = scale;
+  const uint32_t want = std::min<uint32_t>(n_cols, uint32_t(s->n_cus) * uint32_t(slots));
+  a.per_xcd = std::max<uint32_t>(1, (want + 7) / 8);
+  const uint32_t grid = 8 * a.per_xcd;
+  void* args[] = {&a, (void*)&in, (void*)&out, (void*)&kern, (void*)&tw};
   RDL_HIP_CHECK(hipLaunchKernel(p->kernel, dim3(grid), dim3(p->threads), args, lds,
                                 s->stream));
   return RDL_OK;

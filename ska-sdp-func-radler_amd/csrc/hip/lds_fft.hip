@@ -510,6 +510,7 @@ struct rdl_conv {
   size_t scratch_bytes = 0;
   // compile-time-planned kernels (fft_fast.hip) where the size has a plan
   const rdl::FastColumns* fast_cols = nullptr;
+  const rdl::FastColumns* conv_cols = nullptr;  // float64 mode-1 columns (ColumnsConvD)
   const rdl::FastRows* fast_rows = nullptr;
   uint32_t* rows_list = nullptr;            // height words + the count
   const uint8_t* rows_list_mask = nullptr;  // mask the list was made from
@@ -689,6 +690,10 @@ int LaunchColumns(rdl_conv* c, const void* in, void* out, const void* kern,
       n_rows = c->rows_list + c->height;
       c->rows_list_mask = nullptr;  // the mask's contents may change next time
     }
+    if (c->conv_cols && mode == 1 && !in_cm && (!out_cm || in != out))
+      return rdl::ConvColumnsDLaunch(c->s, c->conv_cols, in, out, kern, c->tw_col,
+                                     c->width / 2 + 1, kern_cm, out_cm, rows, n_rows, 0,
+                                     c->height, scale);
     return rdl::FastColumnsLaunch(c->s, c->fast_cols, in, out, kern, c->ptw_col,
                                   c->width / 2 + 1, uint32_t(mode), in_cm, out_cm, kern_cm,
                                   rows, n_rows, 0, c->height, scale);
@@ -873,6 +878,7 @@ int rdl_conv_create_ex(rdl_session* s, uint32_t width, uint32_t height, int f64,
   const bool fast_ok = !(fast_env && fast_env[0] == '0') && !want_split;
   if (fast_ok) {
     c->fast_cols = rdl::FindFastColumns(height, c->f64);
+    if (c->f64) c->conv_cols = rdl::FindConvColumnsD(height);
     if (width % 2 == 0) c->fast_rows = rdl::FindFastRows(width, c->f64);
     // four-step column passes from this length up (RDL_FFT_STEPS_MIN,
     // experiments; below it the one-pass column kernel)
@@ -984,8 +990,9 @@ int rdl_conv_columns_ex(rdl_conv* c, const void* d_in, void* d_out,
   RDL_ARG_CHECK(mode >= 0 && mode <= 2, "mode must be 0, 1 or 2");
   RDL_ARG_CHECK(mode == 0 || d_kernel, "kernel spectrum required");
   RDL_ARG_CHECK(out_layout == RDL_CONV_ROW_MAJOR ||
-                    (mode == 0 && d_out != d_in),
-                "a column-major output needs mode 0 and a separate output");
+                    ((mode == 0 || (mode == 1 && c->conv_cols)) && d_out != d_in),
+                "a column-major output needs mode 0 (or mode 1 with a float64 "
+                "convolution-column plan) and a separate output");
   RDL_ARG_CHECK(kernel_layout == RDL_CONV_ROW_MAJOR ||
                     kernel_layout == RDL_CONV_COL_MAJOR,
                 "bad kernel layout");

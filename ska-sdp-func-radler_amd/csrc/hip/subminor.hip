@@ -1536,6 +1536,15 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTab(LoopArgs a) {
   bool have = false, diverging = false;
   uint64_t iteration = a.iteration_start;
   const bool tracer = rank == 0 && tid == 0 && a.trace;
+  // the loop's comparisons as integer tests on float bits (see decisions)
+  const uint32_t thr_bits = __float_as_uint(a.threshold) & 0x7fffffffu;
+  const uint32_t thr_mode = a.threshold != a.threshold        ? 0u
+                            : (__float_as_uint(a.threshold) >> 31) && thr_bits ? 1u
+                                                                                : 2u;
+  uint32_t lim_mode = 0u, lim_bits = 0u;
+  const bool stop_neg = a.stop_on_negative != 0;
+  uint64_t remaining =
+      a.max_iterations > a.iteration_start ? a.max_iterations - a.iteration_start : 0u;
   // RDL_TRACE_SUBMINOR=1: per-phase cycles of participant 0, wave 0
   uint64_t ph[6] = {0, 0, 0, 0, 0, 0};
   const bool prof = a.prof && rank == 0 && wave == 0;
@@ -1567,34 +1576,37 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTab(LoopArgs a) {
       }
     }
     RDL_TPHASE(0)
-    // ---- 32-bit value keys (MaxKey's high word; NaN 0, index 0's NaN ~0)
-    uint32_t H[ITEMS];
-    uint32_t hmax = 0u;
+    // ---- this thread's best: the largest key, then the lowest index
+    // (MaxKey's high word; NaN 0, index 0's NaN ~0); compares and selects
+    // only, no branch per item
+    uint32_t bh = 0u, bj = 0xffffffffu, bv = __float_as_uint(R[0]);
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
       const float v = neg ? fabsf(R[i]) : R[i];
       const uint32_t u = __float_as_uint(v);
       uint32_t h = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-      if (v != v) h = (base + tid + uint32_t(i) * THREADS == 0u && cnt > 0u) ? 0xffffffffu : 0u;
-      H[i] = h;
-      hmax = max(hmax, h);
+      const uint32_t j = base + tid + uint32_t(i) * THREADS;
+      if (v != v) h = (j == 0u && cnt > 0u) ? 0xffffffffu : 0u;
+      const bool better = h > bh;  // items ascend in j: equal keys keep the first
+      bh = better ? h : bh;
+      bj = better ? j : bj;
+      bv = better ? __float_as_uint(R[i]) : bv;
     }
     RDL_TPHASE(1)
-    // ---- wave winner: the largest key, then the lowest selection index
-    const uint32_t mh = MaxU32<64>(hmax);
-    uint32_t wj = 0u, wv = 0u;
-#pragma unroll
-    for (int i = 0; i < ITEMS; ++i) {
-      const uint64_t b = __ballot(H[i] == mh);
-      if (b) {
-        const int l = __builtin_ctzll(b);
-        wj = base + wave * 64u + uint32_t(l) + uint32_t(i) * THREADS;
-        wv = uint32_t(__builtin_amdgcn_readlane(__float_as_int(R[i]), l));
-        break;
-      }
+    // ---- wave winner: DPP max of the keys; the lowest index on exact ties
+    const uint32_t mh = MaxU32<64>(bh);
+    const uint64_t tie = __ballot(bh == mh);
+    int owner;
+    if ((tie & (tie - 1ull)) == 0ull) {
+      owner = __builtin_ctzll(tie);
+    } else {  // several lanes: the largest ~j among them (0: a key-0 wave)
+      const uint32_t ml = MaxU32<64>(bh == mh ? ~bj : 0u);
+      owner = FirstLane(bh == mh && ~bj == ml);
     }
-    // a key-0 wave stands for its first pixel (see SubminorLoopReg)
-    const uint32_t wl = mh == 0u ? 0u : 0xffffffffu - wj;
+    // a key-0 wave stands for its first pixel (lane 0's item 0, as
+    // SubminorLoopReg), whose value is lane 0's initial bv
+    const uint32_t wl = mh == 0u ? 0u : ~uint32_t(__builtin_amdgcn_readlane(int(bj), owner));
+    const uint32_t wv = uint32_t(__builtin_amdgcn_readlane(int(bv), mh == 0u ? 0 : owner));
     if (lane == 0) slots[par][wave] = make_uint4(mh, wl, wv, 0u);
     RDL_TPHASE(2)
     LdsBarrier();
@@ -1663,21 +1675,35 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTab(LoopArgs a) {
       gv = uint32_t(__builtin_amdgcn_readlane(int(xv), win));
     }
     RDL_TPHASE(4)
-    // ---- identical decisions everywhere (subminor_loop.cc:56-89)
+    // ---- identical decisions everywhere (subminor_loop.cc:56-89), on the
+    // bit patterns in scalar registers (exact: |x| > t for t >= 0 is the
+    // integer order of the bits; NaN never passes a comparison)
     const bool none = gh == 0u || (gh == 0xffffffffu && gl == 0xffffffffu);
     const uint32_t wp = none ? 0u : 0xffffffffu - gl;
     m = __uint_as_float(gv);
+    const uint32_t ab = gv & 0x7fffffffu;
+    const bool is_nan = ab > 0x7f800000u;
     if (!have) {
-      start_abs = fabsf(m);
+      start_abs = __uint_as_float(ab);
+      if (a.divergence_limit != 0.0f) {
+        const float lim = start_abs * a.divergence_limit;
+        lim_bits = __float_as_uint(lim) & 0x7fffffffu;
+        lim_mode = lim != lim ? 0u : ((__float_as_uint(lim) >> 31) && lim_bits) ? 1u : 2u;
+      }
     } else {
-      if (a.divergence_limit != 0.0f) diverging = fabsf(m) > start_abs * a.divergence_limit;
+      // fabsf(m) > start_abs * divergence_limit
+      diverging = lim_mode == 1u ? !is_nan : lim_mode == 2u ? (!is_nan && ab > lim_bits) : false;
       ++iteration;
+      --remaining;
     }
-    const bool go = fabsf(m) > a.threshold && iteration < a.max_iterations &&
-                    (!a.stop_on_negative || m >= 0.0f) && !diverging;
+    const bool above = thr_mode == 1u ? !is_nan : thr_mode == 2u ? (!is_nan && ab > thr_bits)
+                                                               : false;
+    // !stop_on_negative || m >= 0 (-0 included, NaN excluded)
+    const bool non_negative = !is_nan && ((gv >> 31) == 0u || gv == 0x80000000u);
+    const bool go = above && remaining != 0u && (!stop_neg || non_negative) && !diverging;
     if (!go) break;
     c = m * a.gain;
-    flux += m * a.gain;
+    flux += c;  // flux += m * gain (the same product)
     cp = wp;
     // the owner adds the component (M is never -0, so the select form is exact)
 #pragma unroll
@@ -2142,7 +2168,12 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   uint32_t tab_g = 1, tab_threads = 512, tab_items = 1;
   uint64_t tab_per = n_sel;
   if (use_tab) {
-    const uint64_t target = std::max<uint32_t>(h->tab_target, 256);
+    // one workgroup up to 8192 pixels (measured on MI355X: an exchange costs
+    // more than the row it splits below that; tools/bench_subminor.py), then
+    // participants of tab_target pixels; mode 6 always splits by tab_target
+    const uint64_t target = h->mode == 6 || n_sel > 8192
+                                ? std::max<uint32_t>(h->tab_target, 256)
+                                : std::max<uint64_t>(n_sel, 1);
     tab_g = uint32_t(std::min<uint64_t>({(n_sel + target - 1) / target, 32, max_blocks}));
     tab_g = std::max<uint32_t>(tab_g, 1);
     tab_per = (n_sel + tab_g - 1) / tab_g;
