@@ -45,6 +45,8 @@ struct FastRows {
   const void* inverse;
   const void* forward;
   RadixList radix;  // of the half-length transform
+  const void* inverse_lt;  // float: LDS double twiddles, persistent (else nullptr)
+  const void* forward_lt;
 };
 
 /* float four-step column passes (column tiles of 16, see ff::TileIndex) */
@@ -93,15 +95,19 @@ struct RowPeak {
   int allow_negative;
 };
 /* spectrum rows oy .. oy+img_h-1 -> the img_w x img_h window at (ox, oy) */
+/* twd: MakeTwiddleBase(n) for the float plans' LDS-twiddle kernels (NULL:
+ * the global pass tables) */
 int FastRowsInverseLaunch(rdl_session* s, const FastRows* p, const void* spec, float* out,
                           const void* tw, const void* ptw, uint32_t height, uint32_t img_w, uint32_t img_h,
                           uint32_t ox, uint32_t oy, int subtract, int tiled = 0,
-                          const RowPeak* peak = nullptr);
+                          const RowPeak* peak = nullptr, const void* twd = nullptr);
 /* the window's rows (or the listed plane rows) -> spectrum rows */
 int FastRowsForwardLaunch(rdl_session* s, const FastRows* p, const float* in, void* spec,
                           const void* tw, const void* ptw, uint32_t height, uint32_t img_w, uint32_t img_h,
                           uint32_t ox, uint32_t oy, const uint32_t* rows,
-                          const uint32_t* n_rows, int tiled = 0);
+                          const uint32_t* n_rows, int tiled = 0, const void* twd = nullptr);
+/* the two-level double twiddle base of length `base` (ff::TwdLds layout) */
+int MakeTwiddleBase(uint32_t base, void** out);
 /* float64 convolution columns (mode 1: forward, x K x s, inverse; row-major
  * input and output) with LDS twiddles and a register-resident K multiply
  * (ff::ColumnsConvD); nullptr where no plan exists or RDL_FFT_CONVD=0. tw:

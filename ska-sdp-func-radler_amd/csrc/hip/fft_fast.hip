@@ -122,6 +122,67 @@ constexpr uint32_t Product() {
   return (Rs * ... * 1u);
 }
 
+// Float transforms with their twiddles computed from two small double tables
+// in LDS instead of loaded per butterfly from the global pass tables (which
+// made three quarters of the row kernels' load instructions, PMC
+// SQ_INSTS_VMEM_RD): W_L^e = D1[e >> 6] x D2[e & 63] in double (exact table
+// entries), powers by recurrence in double, each rounded to float once —
+// the float pass table's values (long double, rounded) but for the rare
+// rounding tie. L = SC x N (the base length, rows: 2H).
+constexpr uint32_t kTwdLo = 64;
+struct TwdLds {
+  const Cx<double>* d1;  // W_L^{64 i}
+  const Cx<double>* d2;  // W_L^i, i < 64
+};
+__device__ __forceinline__ Cx<double> TwD(const TwdLds& t, uint32_t e) {
+  return Mul(t.d1[e / kTwdLo], t.d2[e % kTwdLo]);
+}
+__device__ __forceinline__ Cx<float> ToF(Cx<double> v) { return {float(v.x), float(v.y)}; }
+
+template <uint32_t TH, uint32_t N, uint32_t R, uint32_t NS, uint32_t SC>
+__device__ __forceinline__ void PassL(Cx<float>* buf, const TwdLds& td, uint32_t tid) {
+  constexpr uint32_t NB = N / R;
+  constexpr uint32_t BPT = (NB + TH - 1) / TH;
+  Cx<float> v[BPT][R];
+#pragma unroll
+  for (uint32_t i = 0; i < BPT; ++i) {
+    const uint32_t j = tid + i * TH;
+    if (NB % TH == 0 || j < NB) {
+#pragma unroll
+      for (uint32_t r = 0; r < R; ++r) v[i][r] = buf[Lx<float>(j + r * NB)];
+    }
+  }
+  LdsSync();
+#pragma unroll
+  for (uint32_t i = 0; i < BPT; ++i) {
+    const uint32_t j = tid + i * TH;
+    if (NB % TH == 0 || j < NB) {
+      const uint32_t k = j % NS;
+      if constexpr (NS > 1) {
+        const Cx<double> w = TwD(td, k * (N / (NS * R)) * SC);
+        Cx<double> wr = w;
+        v[i][1] = Mul(v[i][1], ToF(wr));
+#pragma unroll
+        for (uint32_t r = 2; r < R; ++r) {
+          wr = Mul(wr, w);
+          v[i][r] = Mul(v[i][r], ToF(wr));
+        }
+      }
+      Dft<float, int(R)>::Run(v[i]);
+      const uint32_t d = (j / NS) * NS * R + k;
+#pragma unroll
+      for (uint32_t r = 0; r < R; ++r) buf[Lx<float>(d + r * NS)] = v[i][r];
+    }
+  }
+  LdsSync();
+}
+
+template <uint32_t TH, uint32_t N, uint32_t SC, uint32_t NS, uint32_t R, uint32_t... Rest>
+__device__ __forceinline__ void FftL(Cx<float>* buf, const TwdLds& td, uint32_t tid) {
+  PassL<TH, N, R, NS, SC>(buf, td, tid);
+  if constexpr (sizeof...(Rest) > 0) FftL<TH, N, SC, NS * R, Rest...>(buf, td, tid);
+}
+
 // ------------------------------------------------------------- columns
 // One spectrum column of length N per workgroup round (persistent grid).
 struct ColArgs {
@@ -434,38 +495,79 @@ __device__ __forceinline__ size_t TileIndex(uint32_t y, uint32_t k, uint32_t hei
 // z = IFFT_H(Z) = N (x_even + i x_odd) (unnormalised, as C2R); the inverse
 // runs as conj(FFT(conj Z)). The imaginary parts of X[0] and X[H] are
 // ignored, as by C2R.
-template <typename T, uint32_t TH, uint32_t... Rs>
+// LT (float only): twiddles from the LDS double tables (TwdLds, `twd` = the
+// base table of length 2H: 2H / 64 entries W^{64 i}, then 64 entries W^i)
+// and persistent workgroups (rows blockIdx, blockIdx + grid, ...: the table
+// is loaded once per workgroup).
+template <typename T, uint32_t TH, bool LT, uint32_t... Rs>
 __global__ __launch_bounds__(TH) void RowsInverse(RowArgs a, const Cx<T>* __restrict__ spec,
                                                   float* __restrict__ out,
                                                   const Cx<T>* __restrict__ tw,
-                                                  const Cx<T>* __restrict__ ptw) {
+                                                  const Cx<T>* __restrict__ ptw,
+                                                  const Cx<double>* __restrict__ twd) {
   constexpr uint32_t H = Product<Rs...>();
   constexpr uint32_t EH = (H + TH - 1) / TH;
+  constexpr uint32_t ND1 = LT ? 2 * H / kTwdLo : 1;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   Cx<T>* buf = reinterpret_cast<Cx<T>*>(lds_raw);
-  const uint32_t tid = threadIdx.x;
   __shared__ uint64_t red[TH / 64];  // fused peak search
-  const uint32_t iy = blockIdx.x;  // output row of the window
-  if (iy >= a.img_h) return;
-  const uint32_t y = iy + a.oy;
-  const Cx<T>* X = spec + size_t(y) * a.ld;
-  auto load = [&](uint32_t k) { return *(a.tiled ? spec + TileIndex(y, k, a.height) : X + k); };
+  __shared__ Cx<double> tws[LT ? ND1 + kTwdLo : 1];
+  TwdLds td{tws, tws + ND1};
+  if constexpr (LT) {
+    for (uint32_t i = threadIdx.x; i < ND1 + kTwdLo; i += TH) tws[i] = twd[i];
+    __syncthreads();
+  }
+  // bins in pairs (k, H - k): every spectrum element is read once
+  constexpr uint32_t NP = H / 2 + 1;
+  constexpr uint32_t EP = (NP + TH - 1) / TH;
+  auto row_ptr = [&](uint32_t iy) { return spec + size_t(iy + a.oy) * a.ld; };
+  auto load_at = [&](uint32_t iy, uint32_t k) {
+    return *(a.tiled ? spec + TileIndex(iy + a.oy, k, a.height) : row_ptr(iy) + k);
+  };
+  // PF (off: measured 186.6 -> 205.8 us per 8192^2 pass on MI355X, the
+  // registers cost a wave per SIMD): the next row's bins loaded into
+  // registers before this row's transform and stores
+  constexpr bool PF = false;
+  Cx<T> pk[PF ? EP : 1], pm[PF ? EP : 1];
+  auto prefetch = [&](uint32_t iy, uint32_t tid) {
+#pragma unroll
+    for (uint32_t i = 0; i < EP; ++i) {
+      const uint32_t k = tid + i * TH;
+      if (NP % TH != 0 && k >= NP) continue;
+      pk[i] = load_at(iy, k);
+      pm[i] = load_at(iy, H - k);
+    }
+  };
+  if constexpr (LT && PF)
+    if (blockIdx.x < a.img_h) prefetch(blockIdx.x, threadIdx.x);
+  for (uint32_t iy = blockIdx.x; iy < a.img_h; iy += LT ? gridDim.x : a.img_h) {
+  uint32_t tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));  // opaque per row (see Columns)
   // conj(Z) for bin k from X[k] = xk and X[H-k] = xm
   auto zc = [&](Cx<T> xk, Cx<T> xm, uint32_t k) {
     const Cx<T> sum = {xk.x + xm.x, xk.y - xm.y};  // X[k] + conj X[H-k]
     const Cx<T> dif = {xk.x - xm.x, xk.y + xm.y};  // X[k] - conj X[H-k]
-    const Cx<T> t = Mul(Conj(tw[k]), dif);         // W_N^-k (...)
+    Cx<T> wk;
+    if constexpr (LT)
+      wk = ToF(TwD(td, k));
+    else
+      wk = tw[k];
+    const Cx<T> t = Mul(Conj(wk), dif);           // W_N^-k (...)
     return Cx<T>{sum.x - t.y, -(sum.y + t.x)};      // Z = sum + i t, conjugated
   };
-  // bins in pairs (k, H - k): every spectrum element is read once
-  constexpr uint32_t NP = H / 2 + 1;
-  constexpr uint32_t EP = (NP + TH - 1) / TH;
 #pragma unroll
   for (uint32_t i = 0; i < EP; ++i) {
     const uint32_t k = tid + i * TH;
     if (NP % TH != 0 && k >= NP) continue;
     const uint32_t m = H - k;
-    Cx<T> xk = load(k), xm = load(m);
+    Cx<T> xk, xm;
+    if constexpr (LT && PF) {
+      xk = pk[i];
+      xm = pm[i];
+    } else {
+      xk = load_at(iy, k);
+      xm = load_at(iy, m);
+    }
     if (k == 0) {  // C2R ignores the imaginary parts of X[0] and X[H]
       xk.y = T(0);
       xm.y = T(0);
@@ -473,8 +575,13 @@ __global__ __launch_bounds__(TH) void RowsInverse(RowArgs a, const Cx<T>* __rest
     buf[Lx<T>(k)] = zc(xk, xm, k);
     if (k != 0 && m != k) buf[Lx<T>(m)] = zc(xm, xk, m);
   }
+  if constexpr (LT && PF)
+    if (iy + gridDim.x < a.img_h) prefetch(iy + gridDim.x, tid);
   LdsSync();
-  Fft<T, TH, H, 0, 1, Rs...>(buf, ptw, tid);
+  if constexpr (LT)
+    FftL<TH, H, 2, 1, Rs...>(buf, td, tid);
+  else
+    Fft<T, TH, H, 0, 1, Rs...>(buf, ptw, tid);
   float* o = out + size_t(iy) * a.img_w;
   // fused peak search over the values as written (window coordinates)
   const bool peak = a.peak.partials != nullptr;
@@ -512,7 +619,8 @@ __global__ __launch_bounds__(TH) void RowsInverse(RowArgs a, const Cx<T>* __rest
       consider(x0 - a.ox + 1, v.y);
     }
     finish_peak();
-    return;
+    if constexpr (LT) LdsSync();  // the row's LDS reads before the next row's stores
+    continue;
   }
 #pragma unroll
   for (uint32_t i = 0; i < EH; ++i) {
@@ -534,51 +642,86 @@ __global__ __launch_bounds__(TH) void RowsInverse(RowArgs a, const Cx<T>* __rest
     }
   }
   finish_peak();
+  if constexpr (LT) LdsSync();
+  }
 }
 
 // real plane rows (the window's image rows, zero outside) -> spectrum rows
 // X[0..H]: X[k] = E[k] + W^k O[k], E = (Z[k] + conj Z[H-k]) / 2,
 // O = (Z[k] - conj Z[H-k]) / 2i. Rows not listed are not touched (the
 // column pass reads only listed rows).
-template <typename T, uint32_t TH, uint32_t... Rs>
+template <typename T, uint32_t TH, bool LT, uint32_t... Rs>
 __global__ __launch_bounds__(TH) void RowsForward(RowArgs a, const float* __restrict__ in,
                                                   Cx<T>* __restrict__ spec,
                                                   const Cx<T>* __restrict__ tw,
-                                                  const Cx<T>* __restrict__ ptw) {
+                                                  const Cx<T>* __restrict__ ptw,
+                                                  const Cx<double>* __restrict__ twd) {
   constexpr uint32_t H = Product<Rs...>();
   constexpr uint32_t EH = (H + TH - 1) / TH;
+  constexpr uint32_t ND1 = LT ? 2 * H / kTwdLo : 1;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   Cx<T>* buf = reinterpret_cast<Cx<T>*>(lds_raw);
-  const uint32_t tid = threadIdx.x;
+  __shared__ Cx<double> tws[LT ? ND1 + kTwdLo : 1];
+  TwdLds td{tws, tws + ND1};
+  if constexpr (LT) {
+    for (uint32_t i = threadIdx.x; i < ND1 + kTwdLo; i += TH) tws[i] = twd[i];
+    __syncthreads();
+  }
   const uint32_t n_rows = a.rows ? *a.n_rows : (a.all_rows ? a.height : a.img_h);
-  for (uint32_t r = blockIdx.x; r < n_rows; r += gridDim.x) {
-    uint32_t tid = threadIdx.x;  // opaque per row (see Columns)
-    asm volatile("" : "+v"(tid));
-    const uint32_t y = a.rows ? a.rows[r] : (a.all_rows ? r : r + a.oy);
+  const bool even = ((a.ox | a.img_w) & 1u) == 0;
+  auto row_of = [&](uint32_t r) { return a.rows ? a.rows[r] : (a.all_rows ? r : r + a.oy); };
+  // (e, o) = (x[2n], x[2n+1]) of plane row y, zero outside the window
+  auto pair_at = [&](uint32_t y, uint32_t n) {
     const int64_t iy = int64_t(y) - a.oy;
     const bool in_y = iy >= 0 && iy < a.img_h;
     const float* row = in + (in_y ? size_t(iy) * a.img_w : 0);
-    const bool even = ((a.ox | a.img_w) & 1u) == 0;
+    const uint32_t x0 = 2 * n, x1 = x0 + 1;
+    float2 v = {0.0f, 0.0f};
+    if (even) {  // (x[2n], x[2n+1]) both in or both out: one 8-B load
+      if (in_y && x0 >= a.ox && x0 < a.ox + a.img_w)
+        v = *reinterpret_cast<const float2*>(row + (x0 - a.ox));
+    } else {
+      v.x = in_y && x0 >= a.ox && x0 < a.ox + a.img_w ? row[x0 - a.ox] : 0.0f;
+      v.y = in_y && x1 >= a.ox && x1 < a.ox + a.img_w ? row[x1 - a.ox] : 0.0f;
+    }
+    return v;
+  };
+  // LT: the next row's input is loaded into registers before this row's
+  // transform and stores (see RowsInverse)
+  float2 pre[EH];
+  auto prefetch = [&](uint32_t r, uint32_t tid) {
+    const uint32_t y = row_of(r);
 #pragma unroll
     for (uint32_t i = 0; i < EH; ++i) {
       const uint32_t n = tid + i * TH;
       if (H % TH != 0 && n >= H) continue;
-      const uint32_t x0 = 2 * n, x1 = x0 + 1;
-      T e = T(0), od = T(0);
-      if (even) {  // (x[2n], x[2n+1]) both in or both out: one 8-B load
-        if (in_y && x0 >= a.ox && x0 < a.ox + a.img_w) {
-          const float2 v = *reinterpret_cast<const float2*>(row + (x0 - a.ox));
-          e = T(v.x);
-          od = T(v.y);
-        }
-      } else {
-        e = in_y && x0 >= a.ox && x0 < a.ox + a.img_w ? T(row[x0 - a.ox]) : T(0);
-        od = in_y && x1 >= a.ox && x1 < a.ox + a.img_w ? T(row[x1 - a.ox]) : T(0);
-      }
-      buf[Lx<T>(n)] = {e, od};
+      pre[i] = pair_at(y, n);
     }
+  };
+  if constexpr (LT)
+    if (blockIdx.x < n_rows) prefetch(blockIdx.x, threadIdx.x);
+  for (uint32_t r = blockIdx.x; r < n_rows; r += gridDim.x) {
+    uint32_t tid = threadIdx.x;  // opaque per row (see Columns)
+    asm volatile("" : "+v"(tid));
+    const uint32_t y = row_of(r);
+#pragma unroll
+    for (uint32_t i = 0; i < EH; ++i) {
+      const uint32_t n = tid + i * TH;
+      if (H % TH != 0 && n >= H) continue;
+      float2 v;
+      if constexpr (LT)
+        v = pre[i];
+      else
+        v = pair_at(y, n);
+      buf[Lx<T>(n)] = {T(v.x), T(v.y)};
+    }
+    if constexpr (LT)
+      if (r + gridDim.x < n_rows) prefetch(r + gridDim.x, tid);
     LdsSync();
-    Fft<T, TH, H, 0, 1, Rs...>(buf, ptw, tid);
+    if constexpr (LT)
+      FftL<TH, H, 2, 1, Rs...>(buf, td, tid);
+    else
+      Fft<T, TH, H, 0, 1, Rs...>(buf, ptw, tid);
     Cx<T>* X = spec + size_t(y) * a.ld;
     const T h = T(0.5);
     // X[k] from (Z[k], conj Z[H-k]) and X[H-k] from (Z[H-k], conj Z[k]): the
@@ -587,7 +730,12 @@ __global__ __launch_bounds__(TH) void RowsForward(RowArgs a, const float* __rest
     auto put = [&](uint32_t k, Cx<T> zk, Cx<T> zc) {
       const Cx<T> ev = {h * (zk.x + zc.x), h * (zk.y + zc.y)};
       const Cx<T> od = {h * (zk.y - zc.y), -h * (zk.x - zc.x)};  // (zk - zc) / 2i
-      const Cx<T> v = Add(ev, Mul(tw[k], od));
+      Cx<T> wk;
+      if constexpr (LT)
+        wk = ToF(TwD(td, k));
+      else
+        wk = tw[k];
+      const Cx<T> v = Add(ev, Mul(wk, od));
       // one address, one 8/16-byte store (a store per layout branch was
       // split into scalar halves)
       *(a.tiled ? spec + TileIndex(y, k, a.height) : X + k) = v;
@@ -819,13 +967,24 @@ __global__ __launch_bounds__(1024) void CompactRows(const uint8_t* __restrict__ 
         reinterpret_cast<const void*>(&ff::Columns<T, TH, PF, __VA_ARGS__>),   \
         MakeRadixList<__VA_ARGS__>()                                           \
   }
-#define RDL_FAST_ROWS(T, TH, ...)                                              \
-  FastRows {                                                                   \
-    2 * ff::Product<__VA_ARGS__>(), sizeof(T) == 8, TH,                        \
-        reinterpret_cast<const void*>(&ff::RowsInverse<T, TH, __VA_ARGS__>),   \
-        reinterpret_cast<const void*>(&ff::RowsForward<T, TH, __VA_ARGS__>),   \
-        MakeRadixList<__VA_ARGS__>()                                           \
+#define RDL_FAST_ROWS(T, TH, ...)                                                      \
+  FastRows {                                                                           \
+    2 * ff::Product<__VA_ARGS__>(), sizeof(T) == 8, TH,                                \
+        reinterpret_cast<const void*>(&ff::RowsInverse<T, TH, false, __VA_ARGS__>),    \
+        reinterpret_cast<const void*>(&ff::RowsForward<T, TH, false, __VA_ARGS__>),    \
+        MakeRadixList<__VA_ARGS__>(), RowsLt<T, TH, __VA_ARGS__>(true),                \
+        RowsLt<T, TH, __VA_ARGS__>(false)                                              \
   }
+
+// the float row kernels with LDS double twiddles (none for double)
+template <typename T, uint32_t TH, uint32_t... Rs>
+const void* RowsLt(bool inverse) {
+  if constexpr (sizeof(T) == 4)
+    return inverse ? reinterpret_cast<const void*>(&ff::RowsInverse<T, TH, true, Rs...>)
+                   : reinterpret_cast<const void*>(&ff::RowsForward<T, TH, true, Rs...>);
+  else
+    return nullptr;
+}
 
 const FastColumns* FindFastColumns(uint32_t n, bool f64) {
   static const FastColumns kPlans[] = {
@@ -1086,10 +1245,10 @@ int SlotsPerCu(rdl_session* s, const void* fn, uint32_t threads, size_t lds) {
   const auto key = std::make_tuple(fn, s->device, lds);
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
-  // (a little below the CU's LDS: the row kernels also hold a static
-  // reduction array for the fused peak search)
+  // (below the CU's LDS by the static arrays: the row kernels' reduction
+  // array for the fused peak search and the float rows' twiddle tables)
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          int(kFftLdsBytesFast - 1024)) != hipSuccess)
+                          int(kFftLdsBytesFast - 4096)) != hipSuccess)
     return -1;
   int n = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, int(threads), lds) != hipSuccess)
@@ -1161,11 +1320,26 @@ int ConvColumnsDLaunch(rdl_session* s, const FastColumns* p, const void* in, voi
   return RDL_OK;
 }
 
+namespace {
+// RDL_FFT_ROWTW=0: the float row kernels with global pass tables (comparison)
+bool RowTwiddlesInLds() {
+  static const bool on = [] {
+    const char* e = std::getenv("RDL_FFT_ROWTW");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+}  // namespace
+
 int FastRowsInverseLaunch(rdl_session* s, const FastRows* p, const void* spec, float* out,
                           const void* tw, const void* ptw, uint32_t height, uint32_t img_w, uint32_t img_h,
-                          uint32_t ox, uint32_t oy, int subtract, int tiled, const RowPeak* peak) {
+                          uint32_t ox, uint32_t oy, int subtract, int tiled, const RowPeak* peak,
+                          const void* twd) {
   const size_t lds = FastLdsBytes(p->n / 2, p->f64);
-  if (SlotsPerCu(s, p->inverse, p->threads, lds) < 0) {
+  const bool lt = p->inverse_lt && twd && RowTwiddlesInLds();
+  const void* fn = lt ? p->inverse_lt : p->inverse;
+  const int slots = SlotsPerCu(s, fn, p->threads, lds);
+  if (slots < 0) {
     SetError("fast FFT rows: occupancy query failed");
     return RDL_ERR_HIP;
   }
@@ -1180,18 +1354,22 @@ int FastRowsInverseLaunch(rdl_session* s, const FastRows* p, const void* spec, f
   a.subtract = subtract;
   a.tiled = tiled;
   if (peak) a.peak = *peak;
-  void* args[] = {&a, (void*)&spec, (void*)&out, (void*)&tw, (void*)&ptw};
-  RDL_HIP_CHECK(hipLaunchKernel(p->inverse, dim3(img_h), dim3(p->threads), args, lds,
-                                s->stream));
+  // LT kernels are persistent (rows grid-strided): one table load per workgroup
+  const uint32_t grid =
+      lt ? std::min<uint32_t>(img_h, uint32_t(s->n_cus) * uint32_t(slots)) : img_h;
+  void* args[] = {&a, (void*)&spec, (void*)&out, (void*)&tw, (void*)&ptw, (void*)&twd};
+  RDL_HIP_CHECK(hipLaunchKernel(fn, dim3(grid), dim3(p->threads), args, lds, s->stream));
   return RDL_OK;
 }
 
 int FastRowsForwardLaunch(rdl_session* s, const FastRows* p, const float* in, void* spec,
                           const void* tw, const void* ptw, uint32_t height, uint32_t img_w, uint32_t img_h,
                           uint32_t ox, uint32_t oy, const uint32_t* rows,
-                          const uint32_t* n_rows, int tiled) {
+                          const uint32_t* n_rows, int tiled, const void* twd) {
   const size_t lds = FastLdsBytes(p->n / 2, p->f64);
-  const int slots = SlotsPerCu(s, p->forward, p->threads, lds);
+  const bool lt = p->forward_lt && twd && RowTwiddlesInLds();
+  const void* fn = lt ? p->forward_lt : p->forward;
+  const int slots = SlotsPerCu(s, fn, p->threads, lds);
   if (slots < 0) {
     SetError("fast FFT rows: occupancy query failed");
     return RDL_ERR_HIP;
@@ -1211,9 +1389,25 @@ int FastRowsForwardLaunch(rdl_session* s, const FastRows* p, const float* in, vo
   if (max_rows == 0) return RDL_OK;
   const uint32_t grid =
       std::min<uint32_t>(max_rows, uint32_t(s->n_cus) * uint32_t(slots) * 2);
-  void* args[] = {&a, (void*)&in, (void*)&spec, (void*)&tw, (void*)&ptw};
-  RDL_HIP_CHECK(hipLaunchKernel(p->forward, dim3(grid), dim3(p->threads), args, lds,
-                                s->stream));
+  void* args[] = {&a, (void*)&in, (void*)&spec, (void*)&tw, (void*)&ptw, (void*)&twd};
+  RDL_HIP_CHECK(hipLaunchKernel(fn, dim3(grid), dim3(p->threads), args, lds, s->stream));
+  return RDL_OK;
+}
+
+int MakeTwiddleBase(uint32_t base, void** out) {
+  // W_base^{64 i} for i < base / 64, then W_base^i for i < 64, in double
+  std::vector<double> host;
+  auto put = [&](uint64_t e) {
+    const long double ang = -2.0L * 3.14159265358979323846264338327950288L *
+                            (long double)(e % base) / base;
+    host.push_back(double(std::cos(ang)));
+    host.push_back(double(std::sin(ang)));
+  };
+  for (uint32_t i = 0; i < base / ff::kTwdLo; ++i) put(uint64_t(i) * ff::kTwdLo);
+  for (uint32_t i = 0; i < ff::kTwdLo; ++i) put(i);
+  RDL_HIP_CHECK(hipMalloc(out, host.size() * sizeof(double)));
+  RDL_HIP_CHECK(hipMemcpy(*out, host.data(), host.size() * sizeof(double),
+                          hipMemcpyHostToDevice));
   return RDL_OK;
 }
 

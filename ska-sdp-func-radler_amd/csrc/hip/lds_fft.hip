@@ -522,6 +522,7 @@ struct rdl_conv {
   void* ptw_col = nullptr;
   void* ptw_a = nullptr;
   void* ptw_b = nullptr;
+  void* twd_row = nullptr;  // float rows: two-level double twiddles of width (MakeTwiddleBase)
 };
 
 namespace {
@@ -581,7 +582,8 @@ int LaunchRowsForward(rdl_conv* c, const float* in, uint32_t in_w, uint32_t in_h
       return RDL_ERR_UNSUPPORTED;
     }
     return rdl::FastRowsForwardLaunch(c->s, c->fast_rows, in, spec, c->tw_row, c->ptw_row,
-                                      c->height, in_w, in_h, ox, oy, nullptr, nullptr, 1);
+                                      c->height, in_w, in_h, ox, oy, nullptr, nullptr, 1,
+                                      c->twd_row);
   }
   if (c->fast_rows) {
     const size_t row_bytes = size_t(c->width / 2 + 1) * sizeof(rdl::Cx<T>);
@@ -589,8 +591,8 @@ int LaunchRowsForward(rdl_conv* c, const float* in, uint32_t in_w, uint32_t in_h
       RDL_TRY(CompactRowsFor(c, row_mask, false));
       return rdl::FastRowsForwardLaunch(c->s, c->fast_rows, in, spec, c->tw_row,
                                         c->ptw_row, c->height, in_w, in_h, ox, oy,
-                                        c->rows_list,
-                                        c->rows_list + c->height);
+                                        c->rows_list, c->rows_list + c->height, 0,
+                                        c->twd_row);
     }
     // rows outside the window are zero spectra
     char* base = static_cast<char*>(spec);
@@ -600,7 +602,8 @@ int LaunchRowsForward(rdl_conv* c, const float* in, uint32_t in_w, uint32_t in_h
                                    size_t(c->height - oy - in_h) * row_bytes,
                                    c->s->stream));
     return rdl::FastRowsForwardLaunch(c->s, c->fast_rows, in, spec, c->tw_row, c->ptw_row,
-                                      c->height, in_w, in_h, ox, oy, nullptr, nullptr);
+                                      c->height, in_w, in_h, ox, oy, nullptr, nullptr, 0,
+                                      c->twd_row);
   }
   rdl::RowArgs a{};
   a.row_mask = row_mask;
@@ -630,8 +633,8 @@ int LaunchRowsInverse(rdl_conv* c, const void* spec, float* out, uint32_t out_w,
                       uint32_t out_h, uint32_t ox, uint32_t oy, int subtract) {
   if (c->fast_rows)
     return rdl::FastRowsInverseLaunch(c->s, c->fast_rows, spec, out, c->tw_row, c->ptw_row,
-                                      c->height,
-                                      out_w, out_h, ox, oy, subtract, c->tiled ? 1 : 0);
+                                      c->height, out_w, out_h, ox, oy, subtract,
+                                      c->tiled ? 1 : 0, nullptr, c->twd_row);
   rdl::RowArgs a{};
   a.plan = c->row_plan;
   a.height = c->height;
@@ -892,6 +895,8 @@ int rdl_conv_create_ex(rdl_session* s, uint32_t width, uint32_t height, int f64,
     }
     if (c->fast_rows)
       RDL_TRY(rdl::MakePassTable(width / 2, c->fast_rows->radix, c->f64, &c->ptw_row));
+    if (c->fast_rows && c->fast_rows->inverse_lt)
+      RDL_TRY(rdl::MakeTwiddleBase(width, &c->twd_row));
     if (c->fast_cols)
       RDL_TRY(rdl::MakePassTable(height, c->fast_cols->radix, c->f64, &c->ptw_col));
     if (c->steps) {
@@ -932,7 +937,7 @@ int rdl_conv_destroy(rdl_conv* c) {
   if (c->tw_n2) (void)hipFree(c->tw_n2);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->rows_list) (void)hipFree(c->rows_list);
-  for (void* p : {c->ptw_row, c->ptw_col, c->ptw_a, c->ptw_b})
+  for (void* p : {c->ptw_row, c->ptw_col, c->ptw_a, c->ptw_b, c->twd_row})
     if (p) (void)hipFree(p);
   delete c;
   return RDL_OK;
@@ -1106,7 +1111,7 @@ int rdl_conv_rows_inverse_peak(rdl_conv* c, const void* d_spec, float* d_out,
     else
       RDL_TRY(rdl::FastRowsInverseLaunch(s, c->fast_rows, d_spec, d_out, c->tw_row,
                                          c->ptw_row, c->height, out_w, out_h, ox, oy, 0,
-                                         c->tiled ? 1 : 0, &pk));
+                                         c->tiled ? 1 : 0, &pk, c->twd_row));
   }
   return rdl::LaunchPeakFinal(s, pk.partials, std::max<uint32_t>(out_h, 1), d_out, out_w,
                               out_h, 1, d_mask != nullptr, rdl::PeakSlot(s, slot));

@@ -71,7 +71,7 @@ CONFIGS = {
     "c2": dict(kind="multiscale", size=4096, points=1000, blobs=100, threshold=5 * NOISE,
                max_scales=6, cap=20000, image_cap=7000),
     "c3": dict(kind="joined", size=4096, points=1000, blobs=100, threshold=5 * NOISE,
-               max_scales=6, cap=20000),
+               max_scales=6, cap=20000, image_cap=5000),
     "c4": dict(kind="iuwt", size=4096, points=1000, blobs=100, threshold=5 * NOISE,
                cap=24),
     "c5": dict(kind="tiled", size=16384, points=2000, blobs=200, threshold=5 * NOISE,
