@@ -9,8 +9,10 @@ const uint8_t* DeconvolutionAlgorithm::DeviceCleanMask(gpu::Session& s,
                                                        size_t height) {
   if (!settings_.clean_mask) return nullptr;
   const size_t n = width * height;
-  if (!mask_buffer_ || mask_buffer_->Bytes() < n)
+  if (!mask_buffer_ || mask_buffer_->Bytes() < n || mask_session_ != &s) {
     mask_buffer_ = std::make_shared<gpu::Buffer>(s, n);
+    mask_session_ = &s;
+  }
   // bool is one byte holding 0/1: upload as uint8
   s.H2D(mask_buffer_->Ptr(), settings_.clean_mask, n);
   return static_cast<const uint8_t*>(mask_buffer_->Ptr());
@@ -31,8 +33,9 @@ void DeconvolutionAlgorithm::PerformSpectralFit(float* values, size_t x,
 const float* DeconvolutionAlgorithm::DeviceSpectralMap(gpu::Session& s,
                                                        size_t n_images) {
   if (!spectral_fitter_) return nullptr;
-  if (spectral_map_images_ != n_images) {
+  if (spectral_map_images_ != n_images || spectral_map_session_ != &s) {
     spectral_map_images_ = n_images;
+    spectral_map_session_ = &s;
     spectral_map_.reset();
     const std::vector<float> g = ComponentFitMatrix(*spectral_fitter_, n_polarizations_);
     spectral_map_identity_ = g.empty();

@@ -148,13 +148,18 @@ class DeconvolutionAlgorithm {
     const bool* clean_mask = nullptr;
   } settings_;
   size_t iteration_number_ = 0;
+  // device copies are bound to the worker session that made them: the
+  // subimage a ParallelDeconvolution algorithm runs can move to another
+  // worker (stream, GPU) between major iterations
   std::shared_ptr<gpu::Buffer> mask_buffer_;
+  gpu::Session* mask_session_ = nullptr;
   std::shared_ptr<const schaapcommon::fitters::SpectralFitter> spectral_fitter_;
   size_t n_polarizations_ = 1;
   rdl_logpoly logpoly_{};
   bool has_logpoly_ = false;
   std::shared_ptr<gpu::Buffer> spectral_map_;
   size_t spectral_map_images_ = 0;
+  gpu::Session* spectral_map_session_ = nullptr;
   bool spectral_map_identity_ = false;
   std::shared_ptr<const std::vector<float>> rms_factor_;
   std::shared_ptr<gpu::Buffer> rms_device_;

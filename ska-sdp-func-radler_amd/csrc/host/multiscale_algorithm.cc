@@ -123,7 +123,8 @@ void MultiScaleAlgorithm::RunFullComponentFitter(ImageSet& residual_set,
         "save_source_list");
   gpu::Session& s = residual_set.Session();
   const size_t width = residual_set.Width(), height = residual_set.Height();
-  if (!transforms_ || transforms_->Width() != width || transforms_->Height() != height)
+  if (!transforms_ || !transforms_->BoundTo(s) || transforms_->Width() != width ||
+      transforms_->Height() != height)
     transforms_ = std::make_unique<MultiScaleTransforms>(s, width, height, settings_.shape);
   std::vector<float> scales;
   std::vector<std::vector<std::pair<size_t, size_t>>> lists(scale_infos_.size());
@@ -331,7 +332,9 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
   bool has_hit_threshold_in_sub_loop = false;
   size_t threshold_countdown = std::max(size_t{8}, scale_infos_.size() * 3 / 2);
 
-  if (!transforms_ || transforms_->Width() != width ||
+  // rebuilt when another worker session runs this subimage (the ranks'
+  // ownership, parallel_deconvolution.cc, changes between major iterations)
+  if (!transforms_ || !transforms_->BoundTo(session) || transforms_->Width() != width ||
       transforms_->Height() != height)
     transforms_ = std::make_unique<MultiScaleTransforms>(session, width, height,
                                                          settings_.shape);

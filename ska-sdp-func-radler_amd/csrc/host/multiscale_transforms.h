@@ -22,6 +22,10 @@ class MultiScaleTransforms {
 
   size_t Width() const { return width_; }
   size_t Height() const { return height_; }
+  /// Whether this object's kernels, plans and work planes live on `s` (an
+  /// algorithm that a different worker session runs next must rebuild them:
+  /// work queued on two streams would race).
+  bool BoundTo(const gpu::Session& s) const { return &s_ == &s; }
 
   /// The largest scale the next transforms use. Images whose sides are not
   /// FFT-friendly (even and 7-smooth, utils::CalculateGoodFFTSize) are then

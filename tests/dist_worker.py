@@ -51,6 +51,18 @@ def tiled_settings(rd, kind, w, thr, max_iter, mgain, gw, gh):
     return s
 
 
+def tiled_problem(w, gw, channels):
+    """(psf, dirty) of the distributed tiled tests: one field, or `channels`
+    joined channels of one sky (100 MHz + 10 MHz steps, spectral index -0.7,
+    a PSF per channel; tests/config_problems.joined_channels)."""
+    if channels == 1:
+        from synthetic import problem
+        return problem(w, w, 40, 4, seed=w + gw)
+    from config_problems import joined_channels
+    freqs = [100e6 + 10e6 * i for i in range(channels)]
+    return joined_channels(w, 40, 4, seed=w + gw, frequencies=freqs)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rank", type=int, required=True)
@@ -62,6 +74,8 @@ def main():
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--grid", type=int, nargs=2, default=(2, 2))
     ap.add_argument("--majors", type=int, default=2)
+    ap.add_argument("--channels", type=int, default=1,
+                    help="joined channels (tests/config_problems.joined_channels)")
     args = ap.parse_args()
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -82,14 +96,13 @@ def main():
         out["owners"] = np.array([rd.distributed.subimage_owner(i, args.world)
                                   for i in range(10)])
     else:
-        from synthetic import problem
         w = args.size
         gw, gh = args.grid
-        psf, dirty = problem(w, w, 40, 4, seed=w + gw)
+        psf, dirty = tiled_problem(w, gw, args.channels)
         thr, max_iter = 4e-3, 1500
         mgain = 0.9 if args.majors == 1 else 0.5
         s = tiled_settings(rd, args.kind, w, thr, max_iter, mgain, gw, gh)
-        run = rd.gpu.DeviceRun(s, psf, dirty, [],
+        run = rd.gpu.DeviceRun(s, psf, dirty, [1.0] * args.channels if args.channels > 1 else [],
                                2.0 * PIXEL_SCALE if args.kind == 1 else 0.0)
         run.set_communicator(comm)
         for major in range(args.majors):

@@ -11,7 +11,9 @@ CPU (gloo, world 2): the host communicator plumbing (broadcast of a host
 buffer, max) and the static ownership.
 GPU (gloo, world 2 and 3, all ranks on cuda:0): distributed tiled runs vs the
 oracle (same tiles, per-subimage traces identical, residual/model within
-2e-5 * max|dirty|) and vs each other (bit-identical on every rank).
+2e-5 * max|dirty|) and vs each other (bit-identical on every rank), for one
+field and for joined channels (4 and 8 channels, the C3 image set split by
+subimage).
 """
 import os
 import socket
@@ -91,15 +93,21 @@ def test_host_communicator_gloo_world2(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,kind,w,gw,gh", [(2, 1, 256, 2, 2), (3, 1, 320, 3, 2),
-                                                (2, 0, 192, 2, 2)])
-def test_distributed_tiled_matches_oracle_snapshot(tmp_path, world, kind, w, gw, gh):
+@pytest.mark.parametrize("world,kind,w,gw,gh,channels", [
+    (2, 1, 256, 2, 2, 1), (3, 1, 320, 3, 2, 1), (2, 0, 192, 2, 2, 1),
+    # joined channels split by subimage over the ranks
+    (2, 1, 256, 2, 2, 4), (3, 1, 256, 3, 2, 8),
+    (1, 1, 256, 3, 2, 8), (2, 1, 256, 3, 2, 8), (3, 1, 256, 3, 2, 4), (3, 1, 256, 3, 2, 1)])
+def test_distributed_tiled_matches_oracle_snapshot(tmp_path, world, kind, w, gw, gh, channels):
+    from dist_worker import tiled_problem
     majors = 2
     outs = _launch(tmp_path, world, "tiled",
                    ["--kind", str(kind), "--size", str(w), "--grid", str(gw), str(gh),
-                    "--majors", str(majors)])
+                    "--majors", str(majors), "--channels", str(channels)])
     h = w
-    psf, dirty = problem(w, h, 40, 4, seed=w + gw)
+    psf, dirty = tiled_problem(w, gw, channels)
+    if channels == 1:
+        psf, dirty = psf[None], dirty[None]
     thr, max_iter, mgain = 4e-3, 1500, 0.5
     orc = get_oracle()
     orc.set_threads(8)
@@ -109,11 +117,11 @@ def test_distributed_tiled_matches_oracle_snapshot(tmp_path, world, kind, w, gw,
         st.update(max_scales=4, beam_size_in_pixels=2.0)
     par = OracleParallel(orc, kind, gw, gh, **st)
     par.set_snapshot(True)
-    res_o, mod_o = dirty[None].copy(), np.zeros((1, h, w), np.float32)
+    res_o, mod_o = dirty.copy(), np.zeros((channels, h, w), np.float32)
     prev = 0
     tol = 2e-5 * np.abs(dirty).max()
     for major in range(majors):
-        r_o, _, _, trace_o = par.execute(res_o, mod_o, psf[None], mgain)
+        r_o, _, _, trace_o = par.execute(res_o, mod_o, psf, mgain)
         # every rank holds the same merged images and counters
         for o in outs[1:]:
             assert np.array_equal(o[f"residual{major}"], outs[0][f"residual{major}"])
@@ -131,8 +139,8 @@ def test_distributed_tiled_matches_oracle_snapshot(tmp_path, world, kind, w, gw,
         assert int(outs[0][f"iterations{major}"]) == r_o.total_iterations - prev
         prev = r_o.total_iterations
         assert bool(outs[0][f"another{major}"]) == bool(r_o.another_iteration_required)
-        assert np.abs(outs[0][f"residual{major}"].reshape(h, w) - res_o[0]).max() <= tol
-        assert np.abs(outs[0][f"model{major}"].reshape(h, w) - mod_o[0]).max() <= tol
+        assert np.abs(outs[0][f"residual{major}"].reshape(res_o.shape) - res_o).max() <= tol
+        assert np.abs(outs[0][f"model{major}"].reshape(mod_o.shape) - mod_o).max() <= tol
 
 
 @pytest.mark.gpu
