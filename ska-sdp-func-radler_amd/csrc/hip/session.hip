@@ -1,5 +1,13 @@
 // Session / runtime part of the C-ABI (rdl_hip.h "runtime" section).
+#include <dlfcn.h>
+#include <execinfo.h>
+#include <fcntl.h>
+#include <signal.h>
+#include <ucontext.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -14,6 +22,63 @@ thread_local std::string g_last_error;
 std::mutex g_registry_mutex;
 std::vector<rdl_session*> g_sessions;
 std::map<std::string, TimingEntry> g_retired;
+
+// Diagnostics for crashes outside our code (RDL_SEGV_REPORT=<file>): the
+// signal, the faulting pc with the module holding it (dladdr), a native
+// backtrace, and the process's module map (/proc/self/maps), appended to
+// <file>; then the default action runs (the process dies as it would have).
+char g_segv_path[512] = {0};
+
+void WriteAll(int fd, const char* p, size_t n) {
+  while (n > 0) {
+    const ssize_t w = write(fd, p, n);
+    if (w <= 0) return;
+    p += w;
+    n -= size_t(w);
+  }
+}
+
+void SegvReport(int sig, siginfo_t* info, void* ctx) {
+  const int fd = open(g_segv_path, O_WRONLY | O_CREAT | O_APPEND, 0644);
+  if (fd >= 0) {
+    const ucontext_t* uc = static_cast<const ucontext_t*>(ctx);
+    void* pc = reinterpret_cast<void*>(uc->uc_mcontext.gregs[REG_RIP]);
+    Dl_info d{};
+    const bool known = dladdr(pc, &d) != 0;
+    char buf[1024];
+    const int n = snprintf(
+        buf, sizeof buf, "signal %d (code %d) address %p pc %p module %s +0x%lx symbol %s\n",
+        sig, info->si_code, info->si_addr, pc, known && d.dli_fname ? d.dli_fname : "?",
+        known && d.dli_fbase ? (unsigned long)((char*)pc - (char*)d.dli_fbase) : 0ul,
+        known && d.dli_sname ? d.dli_sname : "?");
+    WriteAll(fd, buf, size_t(std::max(n, 0)));
+    void* frames[64];
+    backtrace_symbols_fd(frames, backtrace(frames, 64), fd);
+    WriteAll(fd, "--- /proc/self/maps\n", 20);
+    const int maps = open("/proc/self/maps", O_RDONLY);
+    if (maps >= 0) {
+      ssize_t r;
+      while ((r = read(maps, buf, sizeof buf)) > 0) WriteAll(fd, buf, size_t(r));
+      close(maps);
+    }
+    close(fd);
+  }
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
+void InstallSegvReport() {
+  const char* path = std::getenv("RDL_SEGV_REPORT");
+  if (!path || !path[0]) return;
+  snprintf(g_segv_path, sizeof g_segv_path, "%s", path);
+  struct sigaction sa {};
+  sa.sa_sigaction = SegvReport;
+  sa.sa_flags = SA_SIGINFO | SA_RESETHAND;
+  sigemptyset(&sa.sa_mask);
+  sigaction(SIGSEGV, &sa, nullptr);
+  sigaction(SIGBUS, &sa, nullptr);
+}
+std::once_flag g_segv_once;
 
 void Fold(std::map<std::string, TimingEntry>& into,
           const std::map<std::string, TimingEntry>& from) {
@@ -117,6 +182,7 @@ int rdl_device_count(int* count) {
 
 int rdl_session_create(int device, rdl_session** out) {
   RDL_ARG_CHECK(out, "out is NULL");
+  std::call_once(rdl::g_segv_once, rdl::InstallSegvReport);
   int n = 0;
   RDL_HIP_CHECK(hipGetDeviceCount(&n));
   RDL_ARG_CHECK(device >= 0 && device < n, "invalid device index");
