@@ -448,6 +448,15 @@ int rdl_subminor_model_rows(rdl_subminor* h, uint32_t image_index,
 int rdl_subminor_model_f64(rdl_subminor* h, uint32_t image_index,
                            double* d_dest, uint32_t dest_w, uint32_t dest_h,
                            uint32_t ox, uint32_t oy);
+/* Mode 0 of rdl_subminor_model (at offset 0,0) restricted to the rows that
+ * hold a non-zero model value: the rows y of d_dest marked d_rows[y + oy]
+ * (rdl_subminor_model_rows' mask) are zeroed and every component is stored;
+ * other rows keep their contents, which the masked correction transform
+ * (rdl_conv_rows_forward_masked) never reads. Replaces a full-plane zero fill
+ * per outer iteration. */
+int rdl_subminor_model_masked(rdl_subminor* h, uint32_t image_index, float* d_dest,
+                              uint32_t dest_w, uint32_t dest_h, const uint8_t* d_rows,
+                              uint32_t oy);
 /* Selected positions (packed y<<16|x) and per-image model values of the last
  * run, copied to host (UpdateComponentList / UpdateAutoMask inputs). */
 /* SubMinorLoop::UpdateAutoMask (cpp/algorithms/subminor_loop.cc:220-228):

@@ -51,14 +51,17 @@ struct rdl_subminor {
   uint32_t table_max = 16384;         // largest selection given a pairwise PSF table
   void* table = nullptr;              // [n_psf][n_sel][n_sel] PSF values at the
   size_t table_bytes = 0;             //   selected pixels' pairwise offsets
-  void* pos_buf = nullptr;            // single-pass selection: positions
+  void* pos_buf = nullptr;            // selected positions (sparse / single pass)
   size_t pos_bytes = 0;
-  int select_passes = 1;              // 1 single pass, 3 count + scan + scatter
+  void* local_buf = nullptr;          // sparse selection: the chunks' own lists
+  size_t local_bytes = 0;
+  int select_passes = 0;              // 0 sparse two-phase, 1 single pass, 3 count + scan + scatter
   int select_ticket = 1;              // single pass: chunk order by ticket
   uint64_t select_spin_limit = uint64_t(1) << 26;  // look-back polls before failing
   int tab = 1;                        // SubminorLoopTab where it applies (RDL_SUBMINOR_TAB=0: off)
   uint32_t tab_threads = 0;           // 0: 512 up to 2048 pixels per participant, else 1024
   uint32_t tab_target = 1024;         // pixels per participant (RDL_SUBMINOR_TAB_TARGET)
+  uint32_t tab_single = 8192;         // one workgroup up to this (RDL_SUBMINOR_TAB_SINGLE)
 };
 
 namespace rdl {
@@ -336,6 +339,77 @@ __global__ __launch_bounds__(kSpThreads) void SelSinglePass(SelArgs a, uint32_t*
     }
     o += step;
   }
+}
+
+// Sparse two-phase selection (the default): SelLocal flags each chunk's
+// pixels once (the single pass's loads and tests) and stores the chunk's
+// count and its selected positions, ascending, in the chunk's own slot of
+// `local`; SelScan turns the counts into offsets; SelPlace moves every
+// non-empty chunk's positions to its offset. No workgroup waits for another
+// (the single pass's look-back chained the chunks), and a selection is a few
+// thousand pixels, so the second pass touches a few hundred chunks.
+__global__ __launch_bounds__(kSpThreads) void SelLocal(SelArgs a, uint32_t* __restrict__ counts,
+                                                       uint32_t* __restrict__ local) {
+  __shared__ uint32_t wave_tot[kSelItems][kSpThreads / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t b = blockIdx.x;
+  const uint64_t base = uint64_t(b) * kSpChunk;
+  uint64_t ballots[kSelItems];
+  uint32_t idx[kSelItems];
+  BoxWalker bw(a, base + tid);
+  float v0[kSelItems];
+#pragma unroll
+  for (uint32_t i = 0; i < kSelItems; ++i) {
+    idx[i] = bw.b < a.box_pixels ? (a.ys + bw.y) * a.width + a.xs + bw.x : 0xffffffffu;
+    bw.Advance(a, kSpThreads);
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < kSelItems; ++i)  // every load in flight at once
+    v0[i] = a.residuals[idx[i] == 0xffffffffu ? 0u : idx[i]];
+#pragma unroll
+  for (uint32_t i = 0; i < kSelItems; ++i) {
+    const bool sel = idx[i] != 0xffffffffu && SelectedValue(a, idx[i], v0[i]);
+    ballots[i] = __ballot(sel);
+    if (lane == 0) wave_tot[i][wave] = uint32_t(__popcll(ballots[i]));
+  }
+  __syncthreads();
+  uint32_t count = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < kSelItems; ++i)
+#pragma unroll
+    for (uint32_t w = 0; w < kSpThreads / 64; ++w) count += wave_tot[i][w];
+  if (tid == 0) counts[b] = count;
+  if (count == 0) return;
+  uint32_t* out = local + base;
+  uint32_t o = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < kSelItems; ++i) {
+    uint32_t woff = 0, step = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kSpThreads / 64; ++w) {
+      woff += w < wave ? wave_tot[i][w] : 0u;
+      step += wave_tot[i][w];
+    }
+    if ((ballots[i] >> lane) & 1ull) {
+      const uint32_t before = uint32_t(__popcll(ballots[i] & ((1ull << lane) - 1ull)));
+      const uint32_t x = idx[i] % a.width, y = idx[i] / a.width;
+      out[o + woff + before] = (y << 16) | x;
+    }
+    o += step;
+  }
+}
+
+// chunk b's positions (offsets[b] .. offsets[b + 1], the last to *total)
+__global__ __launch_bounds__(256) void SelPlace(const uint32_t* __restrict__ offsets,
+                                                uint32_t n_chunks,
+                                                const uint64_t* __restrict__ total,
+                                                const uint32_t* __restrict__ local,
+                                                uint32_t* __restrict__ pos) {
+  const uint32_t b = blockIdx.x;
+  const uint32_t off = offsets[b];
+  const uint32_t end = b + 1 < n_chunks ? offsets[b + 1] : uint32_t(*total);
+  const uint32_t* src = local + uint64_t(b) * kSpChunk;
+  for (uint32_t k = threadIdx.x; off + k < end; k += 256) pos[off + k] = src[k];
 }
 
 // the selected pixels' residual values, [image][n_sel]
@@ -727,6 +801,18 @@ __global__ __launch_bounds__(256) void MarkModelRows(const uint32_t* pos,
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n_sel;
        i += uint64_t(gridDim.x) * blockDim.x)
     if (m[i] != 0.0f) rows[(pos[i] >> 16) + oy] = 1;
+}
+
+// zero the rows y of a width-wide plane whose mark rows[y + oy] is set
+__global__ __launch_bounds__(256) void ZeroMarkedRows(float* __restrict__ plane, uint32_t width,
+                                                      uint32_t height,
+                                                      const uint8_t* __restrict__ rows,
+                                                      uint32_t oy) {
+  for (uint32_t y = blockIdx.x; y < height; y += gridDim.x) {
+    if (!rows[y + oy]) continue;
+    float* row = plane + size_t(y) * width;
+    for (uint32_t x = threadIdx.x; x < width; x += 256) row[x] = 0.0f;
+  }
 }
 
 // Model update of a scale > 0 outer iteration: model += the selection's
@@ -1480,11 +1566,12 @@ __device__ __forceinline__ uint32_t XccId() {
   return uint32_t(__builtin_amdgcn_s_getreg((20) | (0 << 6) | ((4 - 1) << 11)));
 }
 
-template <int ITEMS, int THREADS>
+template <int ITEMS, int THREADS, bool NEG>
 __global__ __launch_bounds__(THREADS) void SubminorLoopTab(LoopArgs a) {
   constexpr int WAVES = THREADS / 64;
   constexpr int SLANES = WAVES <= 8 ? 8 : 16;
-  // {key hi, key lo, value bits, -}, parity double-buffered
+  // {key hi, key lo, value bits, -}, parity double-buffered (NEG: phase 1
+  // uses .x, phase 2 .y/.z of the same slots)
   __shared__ uint4 slots[2][WAVES];
   const uint32_t G = a.n_blocks;
   if (G > 1 && blockIdx.x % kTabParticipantStride != 0u) return;
@@ -1531,6 +1618,8 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTab(LoopArgs a) {
   const float* table = a.table;
   float c = 0.0f, m = 0.0f, start_abs = 0.0f, flux = 0.0f;
   uint32_t cp = 0, par = 0, epoch = 0;
+  uint32_t row_cp = 0xffffffffu;  // the component whose row pv holds
+  float pv[ITEMS];
   uint32_t pend_pos = 0;
   bool pend = false;  // a trace entry waiting for its position's load
   bool have = false, diverging = false;
@@ -1559,10 +1648,13 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTab(LoopArgs a) {
     if (have) {
       // the component's row of the pairwise table (contiguous over j): all
       // loads in flight, then the FMAs (subminor_loop.cc:93-108)
-      const float* row = table + size_t(cp) * n + base;
-      float pv[ITEMS];
+      // (a repeated component reuses the row already in registers)
+      if (cp != row_cp) {
+        const float* row = table + size_t(cp) * n + base;
 #pragma unroll
-      for (int i = 0; i < ITEMS; ++i) pv[i] = row[tid + uint32_t(i) * THREADS];
+        for (int i = 0; i < ITEMS; ++i) pv[i] = row[tid + uint32_t(i) * THREADS];
+        row_cp = cp;
+      }
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i)
         if (__float_as_uint(pv[i]) != kOutsideBits) R[i] = __builtin_fmaf(-pv[i], c, R[i]);
@@ -1576,56 +1668,114 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTab(LoopArgs a) {
       }
     }
     RDL_TPHASE(0)
-    // ---- this thread's best: the largest key, then the lowest index
-    // (MaxKey's high word; NaN 0, index 0's NaN ~0); compares and selects
-    // only, no branch per item
-    uint32_t bh = 0u, bj = 0xffffffffu, bv = __float_as_uint(R[0]);
+    uint32_t gh, gl, gv;
+    if constexpr (NEG) {
+      // ---- phase 1: the largest |R| of the thread (the float max skips
+      // NaN: their key is 0, as MaxKey's), of the wave and of the block;
+      // keys are the bits of |R| with the top bit set (-1: no value)
+      float tb = -1.0f;
 #pragma unroll
-    for (int i = 0; i < ITEMS; ++i) {
-      const float v = neg ? fabsf(R[i]) : R[i];
-      const uint32_t u = __float_as_uint(v);
-      uint32_t h = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-      const uint32_t j = base + tid + uint32_t(i) * THREADS;
-      if (v != v) h = (j == 0u && cnt > 0u) ? 0xffffffffu : 0u;
-      const bool better = h > bh;  // items ascend in j: equal keys keep the first
-      bh = better ? h : bh;
-      bj = better ? j : bj;
-      bv = better ? __float_as_uint(R[i]) : bv;
-    }
-    RDL_TPHASE(1)
-    // ---- wave winner: DPP max of the keys; the lowest index on exact ties
-    const uint32_t mh = MaxU32<64>(bh);
-    const uint64_t tie = __ballot(bh == mh);
-    int owner;
-    if ((tie & (tie - 1ull)) == 0ull) {
-      owner = __builtin_ctzll(tie);
-    } else {  // several lanes: the largest ~j among them (0: a key-0 wave)
-      const uint32_t ml = MaxU32<64>(bh == mh ? ~bj : 0u);
-      owner = FirstLane(bh == mh && ~bj == ml);
-    }
-    // a key-0 wave stands for its first pixel (lane 0's item 0, as
-    // SubminorLoopReg), whose value is lane 0's initial bv
-    const uint32_t wl = mh == 0u ? 0u : ~uint32_t(__builtin_amdgcn_readlane(int(bj), owner));
-    const uint32_t wv = uint32_t(__builtin_amdgcn_readlane(int(bv), mh == 0u ? 0 : owner));
-    if (lane == 0) slots[par][wave] = make_uint4(mh, wl, wv, 0u);
-    RDL_TPHASE(2)
-    LdsBarrier();
-    RDL_TPHASE(3)
-    // ---- block winner over the wave slots
-    const uint4 s4 = lane < uint32_t(WAVES) ? slots[par][lane] : make_uint4(0u, 0u, 0u, 0u);
-    par ^= 1u;
-    uint32_t gh = MaxU32<SLANES>(s4.x);
-    bool mine = lane < uint32_t(WAVES) && s4.x == gh;
-    uint64_t t2 = __ballot(mine);
-    int win;
-    if ((t2 & (t2 - 1ull)) == 0ull) {
-      win = __builtin_ctzll(t2);
+      for (int i = 0; i < ITEMS; ++i) tb = __builtin_fmaxf(tb, __builtin_fabsf(R[i]));
+      uint32_t key = tb >= 0.0f ? (__float_as_uint(tb) | 0x80000000u) : 0u;
+      // selection index 0 holding NaN outranks every key (MaxKey's ~0)
+      const bool j0nan = base == 0u && tid == 0u && cnt > 0u && R[0] != R[0];
+      key = j0nan ? 0xffffffffu : key;
+      const uint32_t mh = MaxU32<64>(key);
+      if (lane == 0) slots[par][wave].x = mh;
+      RDL_TPHASE(2)
+      LdsBarrier();
+      RDL_TPHASE(3)
+      gh = MaxU32<SLANES>(lane < uint32_t(WAVES) ? slots[par][lane].x : 0u);
+      // ---- phase 2: the waves holding the block's key find its lowest
+      // selection index (~j, maximised) and value; the others publish 0
+      uint32_t nj = 0u, vb = 0u;
+      if (mh == gh) {
+        if (gh == 0xffffffffu) {
+          if (j0nan) nj = 0xffffffffu, vb = __float_as_uint(R[0]);
+        } else if (gh == 0u) {
+          // no value at all: the first pixel stands for the block
+          if (tid == 0u) vb = __float_as_uint(R[0]);
+        } else if (key == gh) {
+          const float mf = __uint_as_float(gh & 0x7fffffffu);
+#pragma unroll
+          for (int i = ITEMS - 1; i >= 0; --i) {
+            const bool eq = __builtin_fabsf(R[i]) == mf;
+            nj = eq ? ~(base + tid + uint32_t(i) * THREADS) : nj;
+            vb = eq ? __float_as_uint(R[i]) : vb;
+          }
+        }
+        const uint32_t ml = MaxU32<64>(nj);
+        const int owner = FirstLane(nj == ml);
+        const uint32_t wv = uint32_t(__builtin_amdgcn_readlane(int(vb), owner));
+        if (lane == 0) {
+          slots[par][wave].y = ml;
+          slots[par][wave].z = wv;
+        }
+      } else if (lane == 0) {
+        slots[par][wave].y = 0u;
+        slots[par][wave].z = 0u;
+      }
+      LdsBarrier();
+      const uint4 s4 = lane < uint32_t(WAVES) ? slots[par][lane] : make_uint4(0u, 0u, 0u, 0u);
+      par ^= 1u;
+      gl = MaxU32<SLANES>(s4.y);
+      const int win = FirstLane(lane < uint32_t(WAVES) && s4.y == gl);
+      gv = uint32_t(__builtin_amdgcn_readlane(int(s4.z), win));
     } else {
-      const uint32_t l2 = MaxU32<SLANES>(mine ? s4.y : 0u);
-      win = FirstLane(mine && s4.y == l2);
+      // ---- this thread's best: the largest key, then the lowest index
+      // (MaxKey's high word; NaN 0, index 0's NaN ~0); compares and selects
+      // only, no branch per item
+      uint32_t bh = 0u, bj = 0xffffffffu, bv = __float_as_uint(R[0]);
+  #pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        const float v = neg ? fabsf(R[i]) : R[i];
+        const uint32_t u = __float_as_uint(v);
+        uint32_t h = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+        const uint32_t j = base + tid + uint32_t(i) * THREADS;
+        if (v != v) h = (j == 0u && cnt > 0u) ? 0xffffffffu : 0u;
+        const bool better = h > bh;  // items ascend in j: equal keys keep the first
+        bh = better ? h : bh;
+        bj = better ? j : bj;
+        bv = better ? __float_as_uint(R[i]) : bv;
+      }
+      RDL_TPHASE(1)
+      // ---- wave winner: DPP max of the keys; the lowest index on exact ties
+      const uint32_t mh = MaxU32<64>(bh);
+      const uint64_t tie = __ballot(bh == mh);
+      int owner;
+      if ((tie & (tie - 1ull)) == 0ull) {
+        owner = __builtin_ctzll(tie);
+      } else {  // several lanes: the largest ~j among them (0: a key-0 wave)
+        const uint32_t ml = MaxU32<64>(bh == mh ? ~bj : 0u);
+        owner = FirstLane(bh == mh && ~bj == ml);
+      }
+      // a key-0 wave stands for its first pixel (lane 0's item 0, as
+      // SubminorLoopReg), whose value is lane 0's initial bv
+      const uint32_t wl = mh == 0u ? 0u : ~uint32_t(__builtin_amdgcn_readlane(int(bj), owner));
+      const uint32_t wv = uint32_t(__builtin_amdgcn_readlane(int(bv), mh == 0u ? 0 : owner));
+      if (lane == 0) slots[par][wave] = make_uint4(mh, wl, wv, 0u);
+      RDL_TPHASE(2)
+      LdsBarrier();
+      RDL_TPHASE(3)
+      // ---- block winner over the wave slots
+      const uint4 s4 = lane < uint32_t(WAVES) ? slots[par][lane] : make_uint4(0u, 0u, 0u, 0u);
+      par ^= 1u;
+      uint32_t gh0 = MaxU32<SLANES>(s4.x);
+      bool mine = lane < uint32_t(WAVES) && s4.x == gh0;
+      uint64_t t2 = __ballot(mine);
+      int win;
+      if ((t2 & (t2 - 1ull)) == 0ull) {
+        win = __builtin_ctzll(t2);
+      } else {
+        const uint32_t l2 = MaxU32<SLANES>(mine ? s4.y : 0u);
+        win = FirstLane(mine && s4.y == l2);
+      }
+      const uint32_t gl0 = uint32_t(__builtin_amdgcn_readlane(int(s4.y), win));
+      const uint32_t gv0 = uint32_t(__builtin_amdgcn_readlane(int(s4.z), win));
+      gh = gh0;
+      gl = gl0;
+      gv = gv0;
     }
-    uint32_t gl = uint32_t(__builtin_amdgcn_readlane(int(s4.y), win));
-    uint32_t gv = uint32_t(__builtin_amdgcn_readlane(int(s4.z), win));
     if (G > 1) {
       // ---- exchange of the participants' winners
       ++epoch;  // 1, 2, ... (granules are zeroed per launch)
@@ -1663,8 +1813,9 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTab(LoopArgs a) {
       if (failed) break;
       // lexicographic (hi, lo) max over the participants (lanes < G)
       gh = MaxU32<64>(lane < G ? xh : 0u);
-      mine = lane < G && xh == gh;
-      t2 = __ballot(mine);
+      const bool mine = lane < G && xh == gh;
+      const uint64_t t2 = __ballot(mine);
+      int win;
       if ((t2 & (t2 - 1ull)) == 0ull) {
         win = __builtin_ctzll(t2);
       } else {
@@ -1705,11 +1856,15 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTab(LoopArgs a) {
     c = m * a.gain;
     flux += c;  // flux += m * gain (the same product)
     cp = wp;
-    // the owner adds the component (M is never -0, so the select form is exact)
+    // the owner lane adds the component (scalar branches to its wave and item)
+    {
+      const uint32_t off = wp - base;
+      if (off < cnt && (off % uint32_t(THREADS)) / 64u == wave) {
+        const uint32_t wi = off / uint32_t(THREADS);
 #pragma unroll
-    for (int i = 0; i < ITEMS; ++i) {
-      const float mi = M[i] + c;
-      M[i] = wp == base + tid + uint32_t(i) * THREADS ? mi : M[i];
+        for (int i = 0; i < ITEMS; ++i)
+          if (uint32_t(i) == wi && lane == (off & 63u)) M[i] += c;
+      }
     }
     if (tracer) {  // the load lands with the next row's (one wait for both)
       pend_pos = a.pos[wp];
@@ -1748,14 +1903,19 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTab(LoopArgs a) {
   }
 }
 
+template <int THREADS, bool NEG>
+auto TabKernel(uint32_t items) {
+  return items <= 1    ? SubminorLoopTab<1, THREADS, NEG>
+         : items <= 2  ? SubminorLoopTab<2, THREADS, NEG>
+         : items <= 4  ? SubminorLoopTab<4, THREADS, NEG>
+         : items <= 8  ? SubminorLoopTab<8, THREADS, NEG>
+         : items <= 16 ? SubminorLoopTab<16, THREADS, NEG>
+                       : SubminorLoopTab<(THREADS <= 256 ? 32 : 16), THREADS, NEG>;
+}
+
 template <int THREADS>
 int LaunchTab(const LoopArgs& a, uint32_t items, hipStream_t stream) {
-  auto k = items <= 1    ? SubminorLoopTab<1, THREADS>
-           : items <= 2  ? SubminorLoopTab<2, THREADS>
-           : items <= 4  ? SubminorLoopTab<4, THREADS>
-           : items <= 8  ? SubminorLoopTab<8, THREADS>
-           : items <= 16 ? SubminorLoopTab<(THREADS <= 256 ? 16 : 8), THREADS>
-                         : SubminorLoopTab<(THREADS <= 256 ? 32 : 8), THREADS>;
+  auto k = a.allow_negative ? TabKernel<THREADS, true>(items) : TabKernel<THREADS, false>(items);
   if (a.n_blocks > 1) {
     void* args[] = {const_cast<LoopArgs*>(&a)};
     RDL_HIP_CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k),
@@ -1899,15 +2059,18 @@ int rdl_subminor_create(rdl_session* s, rdl_subminor** out) {
     h->big_max = uint32_t(std::strtoul(e, nullptr, 10));
   if (const char* e = std::getenv("RDL_SUBMINOR_BIG_TARGET"))
     h->big_target = uint32_t(std::strtoul(e, nullptr, 10));
-  // RDL_SUBMINOR_SELECT=3: the count + scan + scatter selection
+  // RDL_SUBMINOR_SELECT=1 (2): the single-pass look-back selection (chunks
+  // in ticket / blockIdx order); 3: count + scan + scatter (comparisons)
   if (const char* e = std::getenv("RDL_SUBMINOR_SELECT")) {
     const int v = std::atoi(e);
-    h->select_passes = v == 3 ? 3 : 1;
-    h->select_ticket = v == 2 ? 0 : 1;  // 2: single pass ordered by blockIdx
+    h->select_passes = v == 3 ? 3 : v == 1 || v == 2 ? 1 : 0;
+    h->select_ticket = v == 2 ? 0 : 1;
   }
   if (const char* e = std::getenv("RDL_SUBMINOR_TAB")) h->tab = std::atoi(e);
   if (const char* e = std::getenv("RDL_SUBMINOR_TAB_TARGET"))
     h->tab_target = uint32_t(std::strtoul(e, nullptr, 10));
+  if (const char* e = std::getenv("RDL_SUBMINOR_TAB_SINGLE"))
+    h->tab_single = uint32_t(std::min<unsigned long>(std::strtoul(e, nullptr, 10), 16384));
   if (const char* e = std::getenv("RDL_SUBMINOR_TAB_THREADS"))
     h->tab_threads = uint32_t(std::strtoul(e, nullptr, 10));
   // test hook: RDL_SELECT_SPIN_LIMIT=0 makes any look-back wait fail
@@ -1926,6 +2089,7 @@ int rdl_subminor_destroy(rdl_subminor* h) {
   if (h->counts) (void)hipFree(h->counts);
   if (h->sel) (void)hipFree(h->sel);
   if (h->pos_buf) (void)hipFree(h->pos_buf);
+  if (h->local_buf) (void)hipFree(h->local_buf);
   if (h->sync) (void)hipFree(h->sync);
   if (h->table) (void)hipFree(h->table);
   delete h;
@@ -1976,14 +2140,30 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   sa.allow_negative = p->allow_negative;
   sa.rms = p->d_rms;
   const uint32_t n_chunks = std::max<uint32_t>(
-      1, rdl::DivUp(sa.box_pixels, h->select_passes == 1 ? rdl::kSpChunk : rdl::kChunk));
+      1, rdl::DivUp(sa.box_pixels, h->select_passes == 3 ? rdl::kChunk : rdl::kSpChunk));
   uint64_t* d_total = reinterpret_cast<uint64_t*>(s->d_small);
   const double sel_bytes = double(sa.box_pixels) * 4.0 * p->n_images;
   // positions of up to the whole box (single pass) or the counts (three
   // kernels: RDL_SUBMINOR_SELECT=3, for comparison)
   uint32_t* counts = nullptr;
   uint32_t* sel_failed = nullptr;  // single pass: set by a timed-out look-back
-  if (h->select_passes == 1) {
+  if (h->select_passes == 0) {
+    // counts (then offsets), the chunks' local lists, the placed positions
+    const size_t slots = size_t(n_chunks) * rdl::kSpChunk;
+    RDL_TRY(rdl::Grow(&h->counts, &h->counts_bytes,
+                      size_t(n_chunks) * sizeof(uint32_t) + 64, st));
+    RDL_TRY(rdl::Grow(&h->local_buf, &h->local_bytes, slots * sizeof(uint32_t), st));
+    RDL_TRY(rdl::Grow(&h->pos_buf, &h->pos_bytes,
+                      std::max<size_t>(sa.box_pixels, 1) * sizeof(uint32_t), st));
+    counts = static_cast<uint32_t*>(h->counts);
+    rdl::ScopedTiming t(s, "subminor_select", sel_bytes);
+    rdl::SelLocal<<<n_chunks, rdl::kSpThreads, 0, st>>>(
+        sa, counts, static_cast<uint32_t*>(h->local_buf));
+    rdl::SelScan<<<1, 1024, 0, st>>>(counts, n_chunks, d_total);
+    rdl::SelPlace<<<n_chunks, 256, 0, st>>>(counts, n_chunks, d_total,
+                                            static_cast<const uint32_t*>(h->local_buf),
+                                            static_cast<uint32_t*>(h->pos_buf));
+  } else if (h->select_passes == 1) {
     RDL_TRY(rdl::Grow(&h->counts, &h->counts_bytes,
                       size_t(n_chunks) * sizeof(uint64_t) + 64, st));
     RDL_TRY(rdl::Grow(&h->pos_buf, &h->pos_bytes,
@@ -2027,7 +2207,7 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
     return RDL_OK;
   }
   const uint32_t ni = p->n_images;
-  if (h->select_passes == 1) {
+  if (h->select_passes != 3) {
     RDL_TRY(rdl::Grow(&h->sel, &h->sel_bytes, 2 * n_sel * ni * sizeof(float) + 256, st));
     h->d_pos = static_cast<uint32_t*>(h->pos_buf);
     h->d_r = static_cast<float*>(h->sel);
@@ -2071,7 +2251,7 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   // otherwise pay a cross-workgroup exchange per component
   const uint64_t big_cap = 1024ull * (ni_t <= 2 ? 8 : 4);
   const bool want_table = (h->mode == 0 || h->mode == 6) && reg_ok && n_sel >= 2 && n_sel <= h->table_max &&
-                          uint64_t(ni / p->n_pol) * n_sel * n_sel <= (uint64_t(1) << 27);
+                          uint64_t(ni / p->n_pol) * n_sel * n_sel <= (uint64_t(1) << 28);
   // (one CU's memory pipe streams those rows: at most 8192 values per
   // iteration, so joined channels keep the grid above 8192 / N_img pixels)
   const bool table_single = want_table && n_sel <= big_cap && work <= 8192;
@@ -2171,7 +2351,7 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
     // one workgroup up to 8192 pixels (measured on MI355X: an exchange costs
     // more than the row it splits below that; tools/bench_subminor.py), then
     // participants of tab_target pixels; mode 6 always splits by tab_target
-    const uint64_t target = h->mode == 6 || n_sel > 8192
+    const uint64_t target = h->mode == 6 || n_sel > h->tab_single
                                 ? std::max<uint32_t>(h->tab_target, 256)
                                 : std::max<uint64_t>(n_sel, 1);
     tab_g = uint32_t(std::min<uint64_t>({(n_sel + target - 1) / target, 32, max_blocks}));
@@ -2181,12 +2361,12 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
                       ? h->tab_threads
                       : (tab_per <= 2048 ? 512u : 1024u);
     const uint64_t need = (tab_per + tab_threads - 1) / tab_threads;
-    const uint32_t cap = tab_threads == 256 ? 32 : 8;
+    const uint32_t cap = tab_threads == 256 ? 32 : 16;
     if (need > cap) tab_threads = 1024;
     const uint64_t need2 = (tab_per + tab_threads - 1) / tab_threads;
     tab_items = need2 <= 1 ? 1 : need2 <= 2 ? 2 : need2 <= 4 ? 4 : need2 <= 8 ? 8
                 : need2 <= 16 ? 16 : 32;
-    if (need2 > (tab_threads == 256 ? 32u : 8u)) {
+    if (need2 > (tab_threads == 256 ? 32u : 16u)) {
       rdl::SetError("table sub-minor kernel: too many pixels per participant");
       return RDL_ERR_ARG;
     }
@@ -2394,6 +2574,26 @@ int rdl_subminor_model(rdl_subminor* h, uint32_t image_index, float* d_dest,
   rdl::ScatterModel<float><<<grid, 256, 0, s->stream>>>(
       h->d_pos, h->d_m + size_t(image_index) * h->n_selected, h->n_selected,
       d_dest, dest_w, ox, oy, mode == 1);
+  RDL_HIP_CHECK(hipGetLastError());
+  return RDL_OK;
+}
+
+int rdl_subminor_model_masked(rdl_subminor* h, uint32_t image_index, float* d_dest,
+                              uint32_t dest_w, uint32_t dest_h, const uint8_t* d_rows,
+                              uint32_t oy) {
+  RDL_ARG_CHECK(h && d_dest && d_rows, "NULL argument");
+  RDL_ARG_CHECK(image_index < h->n_images || h->n_selected == 0,
+                "image index out of range");
+  RDL_ARG_CHECK(dest_w >= h->width && dest_h >= h->height, "destination too small");
+  if (h->n_selected == 0) return RDL_OK;
+  rdl_session* s = h->s;
+  rdl::ZeroMarkedRows<<<std::min<uint32_t>(dest_h, 4096), 256, 0, s->stream>>>(
+      d_dest, dest_w, dest_h, d_rows, oy);
+  RDL_HIP_CHECK(hipGetLastError());
+  const unsigned grid = std::min<uint64_t>(4096, rdl::DivUp(h->n_selected, 256));
+  rdl::ScatterModel<float><<<grid, 256, 0, s->stream>>>(
+      h->d_pos, h->d_m + size_t(image_index) * h->n_selected, h->n_selected, d_dest,
+      dest_w, 0, 0, false);
   RDL_HIP_CHECK(hipGetLastError());
   return RDL_OK;
 }

@@ -207,21 +207,27 @@ void MultiScaleAlgorithm::FindActiveScaleConvolvedMaxima(
   scale_image_valid_.assign(scale_infos_.size(), false);
   if (identity && scale_images_.size() != scale_infos_.size())
     scale_images_.assign(scale_infos_.size(), gpu::Planes());
-  image_set.GetLinearIntegrated(d_integrated);
+  // one image whose integration is the identity: the searches and the
+  // forward transform read the residual itself (no integrated copy)
+  const float* d_source = d_integrated;
+  if (identity)
+    d_source = image_set.Data(0);
+  else
+    image_set.GetLinearIntegrated(d_integrated);
   bool need_fft = false;
   for (size_t si = 0; si != scale_infos_.size(); ++si) {
     ScaleInfo& e = scale_infos_[si];
     if (!e.is_active) continue;
     if (e.scale == 0.0f) {
-      FindPeakDirect(d_integrated, si);
+      FindPeakDirect(d_source, si);
       if (report_rms)
-        gpu::Check(rdl_rms(s, d_integrated, w * h, &e.rms), "rdl_rms");
+        gpu::Check(rdl_rms(s, d_source, w * h, &e.rms), "rdl_rms");
     } else {
       need_fft = true;
     }
   }
   if (!need_fft) return;
-  transforms_->Forward(d_integrated, spectrum_->Ptr());
+  transforms_->Forward(d_source, spectrum_->Ptr());
   std::vector<size_t> pending;  // scale of each queued peak search
   if (scale_infos_.size() > RDL_PEAK_SLOTS)
     throw std::runtime_error("MultiScaleAlgorithm: too many scales");
@@ -440,7 +446,9 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
       tw = twice_cache.emplace(scale_with_peak, std::move(t)).first;
     }
     const gpu::Planes& twice = tw->second;
-    // individually convolved images (:336-354)
+    // individually convolved images (:336-354); at scale 0 the fast sub-minor
+    // loop only reads them, so it reads the residual itself
+    const bool alias_residual = settings_.fast_sub_minor_loop && info.scale == 0.0f;
     if (info.scale != 0.0f && scale_with_peak < scale_image_valid_.size() &&
         scale_image_valid_[scale_with_peak]) {
       // the residual has not changed since FindActiveScaleConvolvedMaxima
@@ -449,7 +457,7 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
       individual.SetPlanes(scale_images_[scale_with_peak]);
       scale_images_[scale_with_peak] = previous;
       scale_image_valid_[scale_with_peak] = false;
-    } else {
+    } else if (!alias_residual) {
       individual.CopyFrom(data_image);
       if (info.scale != 0.0f)
         for (size_t i = 0; i != data_image.Size(); ++i)
@@ -498,7 +506,7 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
       SubMinorLoop::RunResult r;
       {
         prof::Section prof_run("ms.subminor_run");
-        r = sub.Run(individual, twice);
+        r = sub.Run(alias_residual ? data_image : individual, twice);
       }
       for (size_t c = 0; c + 1 < xy.size(); c += 2) {
         trace_.push_back(xy[c]);

@@ -116,13 +116,17 @@ void SubMinorLoop::CorrectResidualDirtyWithSpectrum(size_t image_index,
                                     width_ * height_ * sizeof(float));
     gpu::Buffer& work = s_.Scratch(gpu::Session::kCorrectionSpectrum, fft.SpectrumBytes());
     gpu::Buffer& rows = s_.Scratch(gpu::Session::kCorrectionRows, padded_height_);
-    GetFullIndividualModel(image_index, model.F());
     // the model holds a few hundred components per outer iteration: the
-    // transform skips its empty rows (exactly zero, so nothing changes)
+    // transform skips its empty rows (exactly zero, so nothing changes), and
+    // only the rows it reads are zeroed before the components are stored
     gpu::Check(rdl_subminor_model_rows(h_, uint32_t(image_index),
                                        static_cast<uint8_t*>(rows.Ptr()),
                                        uint32_t(padded_height_), oy),
                "rdl_subminor_model_rows");
+    gpu::Check(rdl_subminor_model_masked(h_, uint32_t(image_index), model.F(),
+                                         uint32_t(width_), uint32_t(height_),
+                                         static_cast<const uint8_t*>(rows.Ptr()), oy),
+               "rdl_subminor_model_masked");
     fft.ConvolveSubtract(model.F(), width_, height_, ox, oy, d_spectrum, work.Ptr(),
                          d_residual, static_cast<const uint8_t*>(rows.Ptr()),
                          !fft.SplitColumns());

@@ -535,21 +535,31 @@ def test_subminor_loop_bit_exact(sess, orc, w, n_src, threshold_frac, mgain, max
         a.free()
 
 
-@pytest.mark.parametrize("n_target,per_participant", [
-    (300, 1 << 20), (1500, 512), (1500, 1 << 20), (5000, 256), (5000, 1024), (5000, 1 << 20),
-    (11000, 512), (11000, 4096)])
-def test_subminor_table_kernel_bit_exact(sess, orc, n_target, per_participant):
+@pytest.mark.parametrize("n_target,per_participant,neg,quantum", [
+    (300, 1 << 20, 1, 0), (1500, 512, 1, 0), (1500, 1 << 20, 1, 0), (5000, 256, 1, 0),
+    (5000, 1024, 1, 0), (5000, 1 << 20, 1, 0), (11000, 512, 1, 0), (11000, 4096, 1, 0),
+    # one 1024-thread workgroup of 16 pixels per thread, and two of 8
+    (16000, 1 << 20, 1, 0), (16000, 8192, 1, 0),
+    # positive components only (the single-key argmax)
+    (1500, 1 << 20, 0, 0), (5000, 1024, 0, 0),
+    # exact |value| ties (values on a 2^-12 grid, both signs): the lowest
+    # selection index wins, inside a thread, a wave, a workgroup and a grid
+    (3000, 1 << 20, 1, 2.0 ** -12), (3000, 512, 1, 2.0 ** -12)])
+def test_subminor_table_kernel_bit_exact(sess, orc, n_target, per_participant, neg, quantum):
     """The pairwise-table loop (rdl_subminor_set_tuning mode 6) on one
     workgroup and on grids of 2..22 participants: the threshold is set so
     that about n_target pixels are selected; trace and model values bit-exact
     against the oracle's sub-minor loop (GenericClean's Clark path)."""
     w = h = 512
     psf, dirty = synthetic(w, h, 200, 7)
-    thr = float(np.sort(np.abs(dirty).ravel())[-n_target])
+    if quantum:
+        dirty = (np.round(dirty / quantum) * quantum).astype(np.float32)
+        psf = (np.round(psf / quantum) * quantum).astype(np.float32)
+    thr = float(np.sort(np.abs(dirty if neg else np.maximum(dirty, 0)).ravel())[-n_target])
     max_iter = 1500
     res_o, mod_o = dirty[None].copy(), np.zeros((1, h, w), np.float32)
     alg = OracleAlgorithm(orc, 0, threshold=thr, max_iterations=max_iter, border_ratio=0.0,
-                          use_sub_minor=1, major_loop_gain=1.0)
+                          use_sub_minor=1, major_loop_gain=1.0, allow_negative=neg)
     r, trace_o = alg.execute(res_o, mod_o, psf[None])
     dres, dpsf = sess.array(dirty[None]), sess.array(psf[None])
     sm = C.c_void_p()
@@ -558,7 +568,7 @@ def test_subminor_table_kernel_bit_exact(sess, orc, n_target, per_participant):
     p = SubminorParams()
     p.width, p.height, p.n_images, p.n_pol = w, h, 1, 1
     p.integ = integration(1, 1, mode=0)
-    p.allow_negative, p.stop_on_negative = 1, 0
+    p.allow_negative, p.stop_on_negative = neg, 0
     p.threshold, p.gain, p.divergence_limit = np.float32(thr), 0.1, 4.0
     p.iteration_start, p.max_iterations = 0, max_iter
     out = SubminorResult()
@@ -567,7 +577,8 @@ def test_subminor_table_kernel_bit_exact(sess, orc, n_target, per_participant):
                               trace.ctypes.data_as(C.c_void_p), C.c_uint64(max_iter))
     n_it = out.iteration
     print(f"n_sel {out.n_selected}, {n_it} iterations")
-    assert abs(int(out.n_selected) - n_target) <= n_target // 10 + 5
+    if not quantum:
+        assert abs(int(out.n_selected) - n_target) <= n_target // 10 + 5
     assert n_it == r.iteration_number
     assert np.array_equal(trace[:n_it], trace_o[:n_it, :2])
     dmod = sess.array(shape=(h, w))
@@ -655,6 +666,54 @@ def test_ms_transform_any_size(orc, w, h, shape):
         assert err <= 2e-6 * np.abs(img).max() * np.sqrt(np.log2(pw * ph)), (sc, err)
 
 
+@pytest.mark.parametrize("w,h,border,frac", [(4096, 4096, 0, 0.001), (1000, 700, 13, 0.05),
+                                             (300, 200, 0, 1.0), (8192, 1024, 100, 0.0002)])
+def test_subminor_selection_modes_agree(sess, w, h, border, frac):
+    """The sparse two-phase selection (default), the single-pass look-back
+    (RDL_SUBMINOR_SELECT=1) and count + scan + scatter (=3) select the same
+    pixels in the same (box) order, with the same residual values: sparse
+    selections, a clean border, and every pixel of the box (frac 1)."""
+    import os
+    rng = np.random.default_rng(w + h)
+    img = rng.standard_normal((h, w)).astype(np.float32)
+    box = img[border:h - border, border:w - border]
+    thr = 0.0 if frac >= 1.0 else float(np.quantile(np.abs(box), 1.0 - frac))
+    psf = np.zeros((h, w), np.float32)
+    psf[h // 2, w // 2] = 1.0
+    dres, dpsf = sess.array(img), sess.array(psf)
+    got = []
+    for mode in ("0", "1", "3"):
+        os.environ["RDL_SUBMINOR_SELECT"] = mode
+        sm = C.c_void_p()
+        try:
+            sess.rdl.rdl_subminor_create(sess.h, C.byref(sm))
+        finally:
+            del os.environ["RDL_SUBMINOR_SELECT"]
+        p = SubminorParams()
+        p.width, p.height, p.n_images, p.n_pol = w, h, 1, 1
+        p.integ = integration(1, 1, mode=0)
+        p.h_border = p.v_border = border
+        p.allow_negative, p.stop_on_negative = 1, 0
+        p.threshold, p.gain, p.divergence_limit = thr, 0.1, 0.0
+        p.iteration_start, p.max_iterations = 0, 0
+        out = SubminorResult()
+        sess.rdl.rdl_subminor_run(sm, dres.vp, dpsf.vp, C.byref(p), C.byref(out), None,
+                                  C.c_uint64(0))
+        n = int(out.n_selected)
+        pos = np.zeros(max(n, 1), np.uint32)
+        mod = np.zeros(max(n, 1), np.float32)
+        sess.rdl.rdl_subminor_get(sm, pos.ctypes.data_as(C.c_void_p),
+                                  mod.ctypes.data_as(C.c_void_p), C.c_uint64(n))
+        got.append(pos[:n])
+        sess.rdl.rdl_subminor_destroy(sm)
+    ys, xs = np.nonzero(np.abs(box) >= np.float32(thr))
+    expect = ((ys + border).astype(np.uint32) << 16) | (xs + border).astype(np.uint32)
+    for g in got:
+        assert np.array_equal(g, expect)
+    for a in (dres, dpsf):
+        a.free()
+
+
 def test_subminor_selection_lookback_timeout_is_reported(sess):
     """The single-pass selection's decoupled look-back gives up after a spin
     limit (never reached in practice). With the limit forced to 0
@@ -672,11 +731,13 @@ def test_subminor_selection_lookback_timeout_is_reported(sess):
     failed = ok = 0
     for _ in range(8):
         os.environ["RDL_SELECT_SPIN_LIMIT"] = "0"
+        os.environ["RDL_SUBMINOR_SELECT"] = "1"  # the single pass (not the default)
         sm = C.c_void_p()
         try:
             sess.rdl.rdl_subminor_create(sess.h, C.byref(sm))
         finally:
             del os.environ["RDL_SELECT_SPIN_LIMIT"]
+            del os.environ["RDL_SUBMINOR_SELECT"]
         p = SubminorParams()
         p.width, p.height, p.n_images, p.n_pol = w, h, 1, 1
         p.integ = integration(1, 1, mode=0)

@@ -36,8 +36,8 @@ def main():
         sizes = (4096, 6144, 8192, 12288, 16384, 32768)
         variants = ((0, 1024), (5, 2048), (5, 3072), (5, 4096))
     if os.environ.get("RDL_BENCH_TAB"):  # the table kernel (pixels per participant)
-        sizes = (200, 400, 800, 1024, 1500, 2048, 3000, 4096, 6000, 8192, 11000)
-        variants = ((-1, 0), (6, 1024), (6, 4096), (6, 1 << 20))
+        sizes = (200, 400, 800, 1024, 1500, 2048, 3000, 4096, 6000, 8192, 11000, 16000)
+        variants = ((-1, 0), (6, 1024), (6, 4096), (6, 8192), (6, 1 << 20))
         threads = os.environ.get("RDL_SUBMINOR_TAB_THREADS", "")
     if os.environ.get("RDL_BENCH_BIG"):  # one 1024-thread workgroup vs the grid
         sizes = (1536, 2048, 3072, 4096, 6144, 8192)
