@@ -57,6 +57,7 @@ struct rdl_subminor {
   size_t local_bytes = 0;
   int select_passes = 0;              // 0 sparse two-phase, 1 single pass, 3 count + scan + scatter
   int select_ticket = 1;              // single pass: chunk order by ticket
+  int select_quad = 1;                // sparse: 16-byte loads where they apply
   uint64_t select_spin_limit = uint64_t(1) << 26;  // look-back polls before failing
   int tab = 1;                        // SubminorLoopTab where it applies (RDL_SUBMINOR_TAB=0: off)
   uint32_t tab_threads = 0;           // 0: 512 up to 2048 pixels per participant, else 1024
@@ -399,16 +400,97 @@ __global__ __launch_bounds__(kSpThreads) void SelLocal(SelArgs a, uint32_t* __re
   }
 }
 
+// SelLocal with 16-byte loads (rows whose width is a multiple of 4, one
+// image with the identity integration, no RMS weights): a workgroup takes
+// `rpb` box rows, each as `ipr` items of 512 float4 (items of a row in
+// order, rows in order: box order), so the selection costs a peak search's
+// read. A lane's 4-pixel flags are ranked across the wave from three
+// ballots of its count's bits.
+constexpr uint32_t kQuadItems = 16;
+constexpr uint32_t kQuadChunk = kSpThreads * kQuadItems * 4;  // pixel slots per chunk
+
+__global__ __launch_bounds__(kSpThreads) void SelLocalQuad(SelArgs a, uint32_t ipr, uint32_t rpb,
+                                                           uint32_t* __restrict__ counts,
+                                                           uint32_t* __restrict__ local) {
+  __shared__ uint32_t wave_tot[kQuadItems][kSpThreads / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t b = blockIdx.x;
+  const uint32_t y0 = a.ys + b * rpb;
+  const uint32_t y1 = min(a.ye, y0 + rpb);
+  const uint32_t q0 = a.xs >> 2, q1 = (a.xe + 3) >> 2;
+  const uint64_t lower = (uint64_t(1) << lane) - 1ull;
+  float4 v[kQuadItems];
+  uint32_t mk[kQuadItems];
+#pragma unroll
+  for (uint32_t i = 0; i < kQuadItems; ++i) {  // every load in flight at once
+    const uint32_t y = y0 + i / ipr, q = q0 + (i % ipr) * kSpThreads + tid;
+    const bool in = y < y1 && q < q1;
+    v[i] = in ? reinterpret_cast<const float4*>(a.residuals + size_t(y) * a.width)[q]
+              : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    mk[i] = in ? 0x01010101u : 0u;
+    if (in && a.mask) mk[i] = reinterpret_cast<const uint32_t*>(a.mask + size_t(y) * a.width)[q];
+  }
+  uint32_t m4[kQuadItems], pre[kQuadItems];
+#pragma unroll
+  for (uint32_t i = 0; i < kQuadItems; ++i) {
+    const uint32_t q = q0 + (i % ipr) * kSpThreads + tid;
+    const float vv[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+    uint32_t m = 0u;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+      const uint32_t x = 4 * q + j;
+      const float value = a.allow_negative ? fabsf(vv[j]) : vv[j];
+      const bool sel = ((mk[i] >> (8 * j)) & 0xffu) && x >= a.xs && x < a.xe &&
+                       value >= a.threshold;
+      m |= sel ? (1u << j) : 0u;
+    }
+    const uint32_t c = uint32_t(__popc(m));
+    const uint64_t b0 = __ballot(c & 1u), b1 = __ballot(c & 2u), b2 = __ballot(c & 4u);
+    pre[i] = uint32_t(__popcll(b0 & lower) + 2 * __popcll(b1 & lower) + 4 * __popcll(b2 & lower));
+    m4[i] = m;
+    if (lane == 0)
+      wave_tot[i][wave] = uint32_t(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2));
+  }
+  __syncthreads();
+  uint32_t count = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < kQuadItems; ++i)
+#pragma unroll
+    for (uint32_t w = 0; w < kSpThreads / 64; ++w) count += wave_tot[i][w];
+  if (tid == 0) counts[b] = count;
+  if (count == 0) return;
+  uint32_t* out = local + uint64_t(b) * kQuadChunk;
+  uint32_t o = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < kQuadItems; ++i) {
+    uint32_t woff = 0, step = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kSpThreads / 64; ++w) {
+      woff += w < wave ? wave_tot[i][w] : 0u;
+      step += wave_tot[i][w];
+    }
+    if (m4[i]) {
+      const uint32_t y = y0 + i / ipr, q = q0 + (i % ipr) * kSpThreads + tid;
+      uint32_t k = o + woff + pre[i];
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j)
+        if ((m4[i] >> j) & 1u) out[k++] = (y << 16) | (4 * q + j);
+    }
+    o += step;
+  }
+}
+
 // chunk b's positions (offsets[b] .. offsets[b + 1], the last to *total)
 __global__ __launch_bounds__(256) void SelPlace(const uint32_t* __restrict__ offsets,
                                                 uint32_t n_chunks,
                                                 const uint64_t* __restrict__ total,
                                                 const uint32_t* __restrict__ local,
+                                                uint32_t chunk_slots,
                                                 uint32_t* __restrict__ pos) {
   const uint32_t b = blockIdx.x;
   const uint32_t off = offsets[b];
   const uint32_t end = b + 1 < n_chunks ? offsets[b + 1] : uint32_t(*total);
-  const uint32_t* src = local + uint64_t(b) * kSpChunk;
+  const uint32_t* src = local + uint64_t(b) * chunk_slots;
   for (uint32_t k = threadIdx.x; off + k < end; k += 256) pos[off + k] = src[k];
 }
 
@@ -2065,6 +2147,7 @@ int rdl_subminor_create(rdl_session* s, rdl_subminor** out) {
     const int v = std::atoi(e);
     h->select_passes = v == 3 ? 3 : v == 1 || v == 2 ? 1 : 0;
     h->select_ticket = v == 2 ? 0 : 1;
+    h->select_quad = v == 4 ? 0 : 1;  // 4: the sparse selection's scalar loads
   }
   if (const char* e = std::getenv("RDL_SUBMINOR_TAB")) h->tab = std::atoi(e);
   if (const char* e = std::getenv("RDL_SUBMINOR_TAB_TARGET"))
@@ -2139,8 +2222,20 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   sa.threshold = p->threshold;
   sa.allow_negative = p->allow_negative;
   sa.rms = p->d_rms;
-  const uint32_t n_chunks = std::max<uint32_t>(
-      1, rdl::DivUp(sa.box_pixels, h->select_passes == 3 ? rdl::kChunk : rdl::kSpChunk));
+  // the sparse selection's 16-byte-load variant: rows of whole float4
+  // (width % 4 == 0), at most 16 items of 512 float4 per row
+  const uint32_t quads_per_row = ((sa.xe + 3) >> 2) - (sa.xs >> 2);
+  const uint32_t quad_ipr = std::max<uint32_t>(1, rdl::DivUp(quads_per_row, rdl::kSpThreads));
+  const bool quad = h->select_passes == 0 && h->select_quad && p->width % 4 == 0 &&
+                    p->integ.copy_fast_path && !p->d_rms && sa.box_pixels > 0 &&
+                    quad_ipr <= rdl::kQuadItems;
+  const uint32_t quad_rpb = rdl::kQuadItems / quad_ipr;
+  const uint32_t n_chunks =
+      quad ? rdl::DivUp(sa.ye - sa.ys, quad_rpb)
+           : std::max<uint32_t>(1, rdl::DivUp(sa.box_pixels, h->select_passes == 3
+                                                                 ? rdl::kChunk
+                                                                 : rdl::kSpChunk));
+  const uint32_t chunk_slots = quad ? rdl::kQuadChunk : rdl::kSpChunk;
   uint64_t* d_total = reinterpret_cast<uint64_t*>(s->d_small);
   const double sel_bytes = double(sa.box_pixels) * 4.0 * p->n_images;
   // positions of up to the whole box (single pass) or the counts (three
@@ -2149,7 +2244,7 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   uint32_t* sel_failed = nullptr;  // single pass: set by a timed-out look-back
   if (h->select_passes == 0) {
     // counts (then offsets), the chunks' local lists, the placed positions
-    const size_t slots = size_t(n_chunks) * rdl::kSpChunk;
+    const size_t slots = size_t(n_chunks) * chunk_slots;
     RDL_TRY(rdl::Grow(&h->counts, &h->counts_bytes,
                       size_t(n_chunks) * sizeof(uint32_t) + 64, st));
     RDL_TRY(rdl::Grow(&h->local_buf, &h->local_bytes, slots * sizeof(uint32_t), st));
@@ -2157,12 +2252,16 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
                       std::max<size_t>(sa.box_pixels, 1) * sizeof(uint32_t), st));
     counts = static_cast<uint32_t*>(h->counts);
     rdl::ScopedTiming t(s, "subminor_select", sel_bytes);
-    rdl::SelLocal<<<n_chunks, rdl::kSpThreads, 0, st>>>(
-        sa, counts, static_cast<uint32_t*>(h->local_buf));
+    if (quad)
+      rdl::SelLocalQuad<<<n_chunks, rdl::kSpThreads, 0, st>>>(
+          sa, quad_ipr, quad_rpb, counts, static_cast<uint32_t*>(h->local_buf));
+    else
+      rdl::SelLocal<<<n_chunks, rdl::kSpThreads, 0, st>>>(
+          sa, counts, static_cast<uint32_t*>(h->local_buf));
     rdl::SelScan<<<1, 1024, 0, st>>>(counts, n_chunks, d_total);
     rdl::SelPlace<<<n_chunks, 256, 0, st>>>(counts, n_chunks, d_total,
                                             static_cast<const uint32_t*>(h->local_buf),
-                                            static_cast<uint32_t*>(h->pos_buf));
+                                            chunk_slots, static_cast<uint32_t*>(h->pos_buf));
   } else if (h->select_passes == 1) {
     RDL_TRY(rdl::Grow(&h->counts, &h->counts_bytes,
                       size_t(n_chunks) * sizeof(uint64_t) + 64, st));
@@ -2357,9 +2456,11 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
     tab_g = uint32_t(std::min<uint64_t>({(n_sel + target - 1) / target, 32, max_blocks}));
     tab_g = std::max<uint32_t>(tab_g, 1);
     tab_per = (n_sel + tab_g - 1) / tab_g;
+    // measured on MI355X (tools/bench_subminor.py, RDL_BENCH_TAB): four
+    // waves up to 2048 pixels and for grid participants, eight to 8192
     tab_threads = h->tab_threads == 256 || h->tab_threads == 512 || h->tab_threads == 1024
                       ? h->tab_threads
-                      : (tab_per <= 2048 ? 512u : 1024u);
+                      : (tab_g > 1 || tab_per <= 2048 ? 256u : 512u);
     const uint64_t need = (tab_per + tab_threads - 1) / tab_threads;
     const uint32_t cap = tab_threads == 256 ? 32 : 16;
     if (need > cap) tab_threads = 1024;

@@ -666,13 +666,16 @@ def test_ms_transform_any_size(orc, w, h, shape):
         assert err <= 2e-6 * np.abs(img).max() * np.sqrt(np.log2(pw * ph)), (sc, err)
 
 
-@pytest.mark.parametrize("w,h,border,frac", [(4096, 4096, 0, 0.001), (1000, 700, 13, 0.05),
-                                             (300, 200, 0, 1.0), (8192, 1024, 100, 0.0002)])
-def test_subminor_selection_modes_agree(sess, w, h, border, frac):
-    """The sparse two-phase selection (default), the single-pass look-back
-    (RDL_SUBMINOR_SELECT=1) and count + scan + scatter (=3) select the same
-    pixels in the same (box) order, with the same residual values: sparse
-    selections, a clean border, and every pixel of the box (frac 1)."""
+@pytest.mark.parametrize("w,h,border,frac,masked", [
+    (4096, 4096, 0, 0.001, 0), (1000, 700, 13, 0.05, 0), (300, 200, 0, 1.0, 0),
+    (8192, 1024, 100, 0.0002, 0), (1000, 700, 13, 0.05, 1), (998, 301, 7, 0.3, 1),
+    (20000, 40, 3, 0.01, 0), (40000, 24, 3, 0.01, 0)])
+def test_subminor_selection_modes_agree(sess, w, h, border, frac, masked):
+    """The sparse two-phase selection (default; 16-byte loads where the width
+    is a multiple of 4, RDL_SUBMINOR_SELECT=4 forces its scalar loads), the
+    single-pass look-back (=1) and count + scan + scatter (=3) select the same
+    pixels in the same (box) order: sparse selections, a clean border, a clean
+    mask, every pixel of the box (frac 1), rows too wide for the vector path."""
     import os
     rng = np.random.default_rng(w + h)
     img = rng.standard_normal((h, w)).astype(np.float32)
@@ -681,8 +684,10 @@ def test_subminor_selection_modes_agree(sess, w, h, border, frac):
     psf = np.zeros((h, w), np.float32)
     psf[h // 2, w // 2] = 1.0
     dres, dpsf = sess.array(img), sess.array(psf)
+    mask = (rng.random((h, w)) < 0.7).astype(np.uint8) if masked else None
+    dmask = sess.array(mask, dtype=np.uint8) if masked else None
     got = []
-    for mode in ("0", "1", "3"):
+    for mode in ("0", "4", "1", "3"):
         os.environ["RDL_SUBMINOR_SELECT"] = mode
         sm = C.c_void_p()
         try:
@@ -693,6 +698,8 @@ def test_subminor_selection_modes_agree(sess, w, h, border, frac):
         p.width, p.height, p.n_images, p.n_pol = w, h, 1, 1
         p.integ = integration(1, 1, mode=0)
         p.h_border = p.v_border = border
+        if masked:
+            p.d_mask = dmask.vp
         p.allow_negative, p.stop_on_negative = 1, 0
         p.threshold, p.gain, p.divergence_limit = thr, 0.1, 0.0
         p.iteration_start, p.max_iterations = 0, 0
@@ -706,11 +713,14 @@ def test_subminor_selection_modes_agree(sess, w, h, border, frac):
                                   mod.ctypes.data_as(C.c_void_p), C.c_uint64(n))
         got.append(pos[:n])
         sess.rdl.rdl_subminor_destroy(sm)
-    ys, xs = np.nonzero(np.abs(box) >= np.float32(thr))
+    keep = np.abs(box) >= np.float32(thr)
+    if masked:
+        keep &= mask[border:h - border, border:w - border] != 0
+    ys, xs = np.nonzero(keep)
     expect = ((ys + border).astype(np.uint32) << 16) | (xs + border).astype(np.uint32)
     for g in got:
         assert np.array_equal(g, expect)
-    for a in (dres, dpsf):
+    for a in (dres, dpsf) + ((dmask,) if masked else ()):
         a.free()
 
 

@@ -37,7 +37,7 @@ def main():
         variants = ((0, 1024), (5, 2048), (5, 3072), (5, 4096))
     if os.environ.get("RDL_BENCH_TAB"):  # the table kernel (pixels per participant)
         sizes = (200, 400, 800, 1024, 1500, 2048, 3000, 4096, 6000, 8192, 11000, 16000)
-        variants = ((-1, 0), (6, 1024), (6, 4096), (6, 8192), (6, 1 << 20))
+        variants = ((-1, 0), (6, 512), (6, 1024), (6, 2048), (6, 8192), (6, 1 << 20))
         threads = os.environ.get("RDL_SUBMINOR_TAB_THREADS", "")
     if os.environ.get("RDL_BENCH_BIG"):  # one 1024-thread workgroup vs the grid
         sizes = (1536, 2048, 3072, 4096, 6144, 8192)
