@@ -279,7 +279,10 @@ def cpu_to_threshold(out_path, threads):
            "wall_clock_to_threshold_s": round(total, 2), "setup_s": round(setup, 2),
            "clean_s": round(total - setup, 2), "components": n,
            "final_peak": float(r.final_peak),
-           "reached_threshold": bool(abs(r.final_peak) <= c["threshold"] * 1.0000001),
+           "stop": "the multiscale loop's threshold countdown (multiscale_algorithm.cc:"
+                   "323-328, 378-384): it ends max(8, 1.5 x scales) sub-minor loops after "
+                   "the sub-loop threshold reaches the final threshold; final_peak is the "
+                   "last selected scale's peak, as the reference reports it",
            "components_per_s_with_setup": round(n / total, 2),
            "components_per_s_after_setup": round(n / max(total - setup, 1e-9), 2),
            "note": "oracle MultiScale (C++ restatement of the reference, std::thread, "
@@ -288,6 +291,34 @@ def cpu_to_threshold(out_path, threads):
     with open(out_path, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out), flush=True)
+
+
+def with_amdahl(rd, once):
+    """Run `once()` with the host profile's pass sections on: the wall clock
+    of the find-peak and cleaning passes over the subimages (the part that
+    N ranks split) against the whole Perform (load, split, passes, model
+    merge, store). serial_fraction f bounds the N-rank speedup at
+    1 / (f + (1 - f) / N), before load imbalance between ranks."""
+    rd.gpu.host_profile_reset()
+    rd.gpu.host_profile_enable(True)
+    try:
+        out = once()
+    finally:
+        rd.gpu.host_profile_enable(False)
+    prof = rd.gpu.host_profile()
+    total = prof.get("perform.total", (0, 0.0))[1]
+    passes = sum(prof.get(k, (0, 0.0))[1] for k in ("par.findpeak_pass", "par.clean_pass"))
+    if total <= 0.0:
+        return out, None
+    f = max(0.0, total - passes) / total
+    return out, {"perform_s": round(total, 4), "subimage_passes_s": round(passes, 4),
+                 "serial_fraction": round(f, 4),
+                 "speedup_bound": {str(n): round(1.0 / (f + (1.0 - f) / n), 2)
+                                   for n in (2, 4, 8)},
+                 "note": "passes: find-peak + cleaning over the subimages (split over "
+                         "ranks); serial: accessor load, split, model copy, store. The "
+                         "subimage merges run inside the passes (on N ranks every rank "
+                         "merges all of them), so f is a lower bound"}
 
 
 def committed_cpu_to_threshold():
@@ -337,6 +368,8 @@ def main():
     ap.add_argument("--sigma", type=float, default=5.0)
     ap.add_argument("--tiled-reference", type=int, default=1,
                     help="N = 1 fields: also time the tiled N > 1 workload on this GPU")
+    ap.add_argument("--joined-reference", type=int, default=1,
+                    help="N = 1: also time the joined-channel workload split by subimage")
     ap.add_argument("--device-resident", type=int, default=1,
                     help="also time the HBM-resident major iteration (0 = skip)")
     ap.add_argument("--cpu-outer", type=int, default=2,
@@ -457,13 +490,49 @@ def main():
         # measured before the headline: after the fields runs the subimage
         # streams of this process ran 1.3x slower (7.96 vs 6.07 s per step)
         tiled_once()
-        t_comps, t_el = tiled_once()
+        (t_comps, t_el), t_amdahl = with_amdahl(rd, tiled_once)
         tiled_ref = {"workload": (f"multiscale-{args.size}x{args.size}-{args.scales}scales"
                                   f"-tiled{args.grid}x{args.grid}"),
                      "value": round(t_comps / t_el, 2), "ms_per_step": round(1e3 * t_el, 2),
+                     "wall_clock_to_threshold_s": round(t_el, 4),
                      "components_per_step": t_comps, "pool": args.pool,
+                     "amdahl": t_amdahl,
                      "note": "the default N > 1 workload (ParallelDeconvolution subimages) "
                              "on one GPU, for the same-workload scaling curve"}
+
+    # the joined-channel workload (8 channels x 4096^2) split
+    # into grid x grid subimages on this one GPU: the N = 1 point of
+    # `--workload joined --gpus N` (N > 1 splits the subimages over ranks)
+    joined_ref = None
+    if args.joined_reference and world == 1 and workload == "fields":
+        from config_problems import joined_channels
+        jsize, jch = 4096, args.channels
+        jfreqs = [100e6 + 10e6 * i for i in range(jch)]
+        j_psf, j_dirty = joined_channels(jsize, args.points, args.blobs, SEED, jfreqs)
+        sj = settings_for(rd, jsize, args.max_iter, args.scales, threshold, args.grid, args.pool)
+        jextra = dict(n_deconvolution_groups=jch,
+                      frequencies=np.array([[f, f] for f in jfreqs], np.float64),
+                      weights=np.ones(jch, np.float64))
+
+        def joined_once():
+            arrays = (j_psf, j_dirty.copy(), np.zeros_like(j_dirty))
+            r = rd.Radler(sj, *arrays, BEAM_PX * PIXEL_SCALE, **jextra)
+            t = time.perf_counter()
+            r.perform(0)
+            return rd.gpu.total_iteration_number(r), time.perf_counter() - t
+
+        print("[bench] joined reference (warm-up + 1 step) ...", file=sys.stderr, flush=True)
+        joined_once()
+        (j_comps, j_el), j_amdahl = with_amdahl(rd, joined_once)
+        joined_ref = {"workload": (f"joined{jch}ch-multiscale-{jsize}x{jsize}-{args.scales}"
+                                   f"scales-tiled{args.grid}x{args.grid}"),
+                      "value": round(j_comps / j_el, 2), "ms_per_step": round(1e3 * j_el, 2),
+                      "wall_clock_to_threshold_s": round(j_el, 4),
+                      "components_per_step": j_comps, "pool": args.pool,
+                      "amdahl": j_amdahl,
+                      "note": "`--workload joined --gpus N` at N = 1 (the channels' image set "
+                              "split by subimage, one GPU)"}
+        del j_psf, j_dirty
 
     # C2 (4096^2) to the threshold on this GPU: the same problem as the
     # committed CPU to-threshold run (wall clock against wall clock)
@@ -671,6 +740,7 @@ def main():
                                    f"/pool{args.pool}" if split else f"fields{world}")},
         "device_resident": resident,
         "tiled_n1": tiled_ref,
+        "joined_n1": joined_ref,
         "c2_to_threshold": c2_ref,
         "roofline": roofline,
         "cpu_baseline": cpu,

@@ -36,6 +36,14 @@ void DijkstraSplitter::Divide(const float* image, float* output, size_t lo,
   auto pixel = [&](size_t u, size_t v) -> size_t {
     return kVertical ? u * width_ + v : v * width_ + u;
   };
+  // the search runs on band-local copies laid out [u][v - lo] (|pixel| and
+  // the settled costs): the frontier then walks neighbouring cache lines
+  // instead of image rows a full width apart (a horizontal band is
+  // transposed). Same pushes and pops in the same order, same result.
+  std::vector<float> weight(band * n_u);
+  std::vector<float> dist(band * n_u, std::numeric_limits<float>::max());
+  for (size_t u = 0; u != n_u; ++u)
+    for (size_t v = lo; v != hi; ++v) weight[u * band + (v - lo)] = std::fabs(image[pixel(u, v)]);
   std::vector<Node> heap_store;
   heap_store.reserve(8 * band);
   std::priority_queue<Node, std::vector<Node>, LaterFirst> open(LaterFirst(),
@@ -44,19 +52,16 @@ void DijkstraSplitter::Divide(const float* image, float* output, size_t lo,
     open.push(Node{0.0f, 0, uint16_t(v), 0, uint16_t(v)});
   // predecessor of each settled pixel (pu << 16 | pv), band-local layout
   std::vector<uint32_t> back(band * n_u);
-  for (size_t u = 0; u != n_u; ++u)
-    for (size_t v = lo; v != hi; ++v)
-      output[pixel(u, v)] = std::numeric_limits<float>::max();
   Node cur{};
   while (!open.empty()) {
     cur = open.top();
     open.pop();
     if (cur.u == n_u) break;
-    const size_t at = pixel(cur.u, cur.v);
-    const float cost = cur.cost + std::fabs(image[at]);
-    if (!(cost < output[at])) continue;
-    output[at] = cost;
-    back[(cur.v - lo) + size_t(cur.u) * band] = (uint32_t(cur.pu) << 16) | cur.pv;
+    const size_t at = size_t(cur.u) * band + (cur.v - lo);
+    const float cost = cur.cost + weight[at];
+    if (!(cost < dist[at])) continue;
+    dist[at] = cost;
+    back[at] = (uint32_t(cur.pu) << 16) | cur.pv;
     const uint16_t u = cur.u, v = cur.v;
     const uint16_t u1 = uint16_t(u + 1);
     if (v > lo) {
@@ -74,7 +79,7 @@ void DijkstraSplitter::Divide(const float* image, float* output, size_t lo,
   uint32_t pu = cur.pu, pv = cur.pv;
   for (; pu > 0;) {
     output[pixel(pu, pv)] = 1.0f;
-    const uint32_t p = back[(pv - lo) + size_t(pu) * band];
+    const uint32_t p = back[size_t(pu) * band + (pv - lo)];
     pu = p >> 16;
     pv = p & 0xffffu;
   }

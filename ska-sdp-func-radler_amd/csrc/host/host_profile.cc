@@ -1,6 +1,7 @@
 #include "host_profile.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <map>
@@ -30,13 +31,17 @@ Store& TheStore() {
 }
 }  // namespace
 
-bool Enabled() {
-  static const bool on = [] {
+std::atomic<bool>& Flag() {
+  static std::atomic<bool> on{[] {
     const char* e = std::getenv("RADLER_HOST_PROFILE");
     return e && e[0] == '1';
-  }();
+  }()};
   return on;
 }
+
+bool Enabled() { return Flag().load(std::memory_order_relaxed); }
+
+void SetEnabled(bool on) { Flag().store(on, std::memory_order_relaxed); }
 
 void Add(const char* name, uint64_t ns) {
   Store& s = TheStore();

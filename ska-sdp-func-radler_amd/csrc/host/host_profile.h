@@ -12,6 +12,8 @@
 namespace radler::prof {
 
 bool Enabled();
+/// Turns the sections on or off at run time (bench.py's reference legs).
+void SetEnabled(bool on);
 void Add(const char* name, uint64_t ns);
 struct Entry {
   std::string name;

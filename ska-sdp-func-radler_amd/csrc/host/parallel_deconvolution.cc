@@ -11,6 +11,7 @@
 #include <functional>
 #include <limits>
 #include <map>
+#include <optional>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -939,6 +940,9 @@ ParallelDeconvolutionResult ParallelDeconvolution::ExecuteParallelRun(
                   : n_workers;
   if (rank_workers > 1) EnsureWorkers(s, rank_workers);
   double start_peak = 0.0;
+  // (the passes' wall clock: the part of a major iteration that the ranks
+  // split; bench.py's Amdahl estimate)
+  std::optional<prof::Section> pass(std::in_place, "par.findpeak_pass");
   if (distributed) {
     start_peak = RunSubImagesDistributed(data_image, model_image, result_model,
                                          psf_images, psf_indices, 0.0, true);
@@ -956,6 +960,7 @@ ParallelDeconvolutionResult ParallelDeconvolution::ExecuteParallelRun(
   const double threshold = start_peak * (1.0 - major_loop_gain);
   log::Info() << "Maximum start peak over " << subimages_.size()
               << " subimages: " << start_peak << '\n';
+  pass.emplace("par.clean_pass");
   if (distributed)
     RunSubImagesDistributed(data_image, model_image, result_model, psf_images,
                             psf_indices, threshold, false);
@@ -966,6 +971,7 @@ ParallelDeconvolutionResult ParallelDeconvolution::ExecuteParallelRun(
     for (SubImage& sub : subimages_)
       RunSubImage(sub, data_image, model_image, result_model,
                   psf_images[psf_indices[sub.index]], threshold, false);
+  pass.reset();
   model_image.CopyFrom(result_model);
 
   ParallelDeconvolutionResult result;

@@ -590,6 +590,7 @@ void InitGpu(py::module& m) {
     return out;
   });
   g.def("host_profile_reset", &radler::prof::Reset);
+  g.def("host_profile_enable", &radler::prof::SetEnabled, py::arg("on"));
   g.def(
       "local_rms",
       [](FloatArray integrated, int method, double window, double beam,
