@@ -1652,8 +1652,7 @@ template <int ITEMS, int THREADS, bool NEG>
 __global__ __launch_bounds__(THREADS) void SubminorLoopTab(LoopArgs a) {
   constexpr int WAVES = THREADS / 64;
   constexpr int SLANES = WAVES <= 8 ? 8 : 16;
-  // {key hi, key lo, value bits, -}, parity double-buffered (NEG: phase 1
-  // uses .x, phase 2 .y/.z of the same slots)
+  // {key hi, key lo, value bits, -}, parity double-buffered
   __shared__ uint4 slots[2][WAVES];
   const uint32_t G = a.n_blocks;
   if (G > 1 && blockIdx.x % kTabParticipantStride != 0u) return;
@@ -1750,65 +1749,29 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTab(LoopArgs a) {
       }
     }
     RDL_TPHASE(0)
-    uint32_t gh, gl, gv;
+    // ---- this thread's best: the largest key, then the lowest index
+    // (MaxKey's high word; NaN 0, index 0's NaN ~0); compares and selects
+    // only, no branch per item
+    uint32_t bh = 0u, bj = 0xffffffffu, bv = __float_as_uint(R[0]);
     if constexpr (NEG) {
-      // ---- phase 1: the largest |R| of the thread (the float max skips
-      // NaN: their key is 0, as MaxKey's), of the wave and of the block;
-      // keys are the bits of |R| with the top bit set (-1: no value)
+      // |R| keys: the largest |R| by a float max chain (the max skips NaN,
+      // whose key is 0), then the lowest item holding it
       float tb = -1.0f;
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) tb = __builtin_fmaxf(tb, __builtin_fabsf(R[i]));
-      uint32_t key = tb >= 0.0f ? (__float_as_uint(tb) | 0x80000000u) : 0u;
-      // selection index 0 holding NaN outranks every key (MaxKey's ~0)
-      const bool j0nan = base == 0u && tid == 0u && cnt > 0u && R[0] != R[0];
-      key = j0nan ? 0xffffffffu : key;
-      const uint32_t mh = MaxU32<64>(key);
-      if (lane == 0) slots[par][wave].x = mh;
-      RDL_TPHASE(2)
-      LdsBarrier();
-      RDL_TPHASE(3)
-      gh = MaxU32<SLANES>(lane < uint32_t(WAVES) ? slots[par][lane].x : 0u);
-      // ---- phase 2: the waves holding the block's key find its lowest
-      // selection index (~j, maximised) and value; the others publish 0
-      uint32_t nj = 0u, vb = 0u;
-      if (mh == gh) {
-        if (gh == 0xffffffffu) {
-          if (j0nan) nj = 0xffffffffu, vb = __float_as_uint(R[0]);
-        } else if (gh == 0u) {
-          // no value at all: the first pixel stands for the block
-          if (tid == 0u) vb = __float_as_uint(R[0]);
-        } else if (key == gh) {
-          const float mf = __uint_as_float(gh & 0x7fffffffu);
+      bh = tb >= 0.0f ? (__float_as_uint(tb) | 0x80000000u) : 0u;
 #pragma unroll
-          for (int i = ITEMS - 1; i >= 0; --i) {
-            const bool eq = __builtin_fabsf(R[i]) == mf;
-            nj = eq ? ~(base + tid + uint32_t(i) * THREADS) : nj;
-            vb = eq ? __float_as_uint(R[i]) : vb;
-          }
-        }
-        const uint32_t ml = MaxU32<64>(nj);
-        const int owner = FirstLane(nj == ml);
-        const uint32_t wv = uint32_t(__builtin_amdgcn_readlane(int(vb), owner));
-        if (lane == 0) {
-          slots[par][wave].y = ml;
-          slots[par][wave].z = wv;
-        }
-      } else if (lane == 0) {
-        slots[par][wave].y = 0u;
-        slots[par][wave].z = 0u;
+      for (int i = ITEMS - 1; i >= 0; --i) {
+        const bool eq = __builtin_fabsf(R[i]) == tb;
+        bj = eq ? base + tid + uint32_t(i) * THREADS : bj;
+        bv = eq ? __float_as_uint(R[i]) : bv;
       }
-      LdsBarrier();
-      const uint4 s4 = lane < uint32_t(WAVES) ? slots[par][lane] : make_uint4(0u, 0u, 0u, 0u);
-      par ^= 1u;
-      gl = MaxU32<SLANES>(s4.y);
-      const int win = FirstLane(lane < uint32_t(WAVES) && s4.y == gl);
-      gv = uint32_t(__builtin_amdgcn_readlane(int(s4.z), win));
+      if (base == 0u && tid == 0u && cnt > 0u && R[0] != R[0]) {
+        bh = 0xffffffffu;  // selection index 0 holding NaN outranks every key
+        bj = 0u;
+      }
     } else {
-      // ---- this thread's best: the largest key, then the lowest index
-      // (MaxKey's high word; NaN 0, index 0's NaN ~0); compares and selects
-      // only, no branch per item
-      uint32_t bh = 0u, bj = 0xffffffffu, bv = __float_as_uint(R[0]);
-  #pragma unroll
+#pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
         const float v = neg ? fabsf(R[i]) : R[i];
         const uint32_t u = __float_as_uint(v);
@@ -1820,31 +1783,33 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTab(LoopArgs a) {
         bj = better ? j : bj;
         bv = better ? __float_as_uint(R[i]) : bv;
       }
-      RDL_TPHASE(1)
-      // ---- wave winner: DPP max of the keys; the lowest index on exact ties
-      const uint32_t mh = MaxU32<64>(bh);
-      const uint64_t tie = __ballot(bh == mh);
-      int owner;
-      if ((tie & (tie - 1ull)) == 0ull) {
-        owner = __builtin_ctzll(tie);
-      } else {  // several lanes: the largest ~j among them (0: a key-0 wave)
-        const uint32_t ml = MaxU32<64>(bh == mh ? ~bj : 0u);
-        owner = FirstLane(bh == mh && ~bj == ml);
-      }
-      // a key-0 wave stands for its first pixel (lane 0's item 0, as
-      // SubminorLoopReg), whose value is lane 0's initial bv
-      const uint32_t wl = mh == 0u ? 0u : ~uint32_t(__builtin_amdgcn_readlane(int(bj), owner));
-      const uint32_t wv = uint32_t(__builtin_amdgcn_readlane(int(bv), mh == 0u ? 0 : owner));
-      if (lane == 0) slots[par][wave] = make_uint4(mh, wl, wv, 0u);
-      RDL_TPHASE(2)
-      LdsBarrier();
-      RDL_TPHASE(3)
-      // ---- block winner over the wave slots
-      const uint4 s4 = lane < uint32_t(WAVES) ? slots[par][lane] : make_uint4(0u, 0u, 0u, 0u);
-      par ^= 1u;
-      uint32_t gh0 = MaxU32<SLANES>(s4.x);
-      bool mine = lane < uint32_t(WAVES) && s4.x == gh0;
-      uint64_t t2 = __ballot(mine);
+    }
+    RDL_TPHASE(1)
+    // ---- wave winner: DPP max of the keys; the lowest index on exact ties
+    const uint32_t mh = MaxU32<64>(bh);
+    const uint64_t tie = __ballot(bh == mh);
+    int owner;
+    if ((tie & (tie - 1ull)) == 0ull) {
+      owner = __builtin_ctzll(tie);
+    } else {  // several lanes: the largest ~j among them (0: a key-0 wave)
+      const uint32_t ml = MaxU32<64>(bh == mh ? ~bj : 0u);
+      owner = FirstLane(bh == mh && ~bj == ml);
+    }
+    // a key-0 wave stands for its first pixel (lane 0's item 0, as
+    // SubminorLoopReg), whose value is lane 0's initial bv
+    const uint32_t wl = mh == 0u ? 0u : ~uint32_t(__builtin_amdgcn_readlane(int(bj), owner));
+    const uint32_t wv = uint32_t(__builtin_amdgcn_readlane(int(bv), mh == 0u ? 0 : owner));
+    if (lane == 0) slots[par][wave] = make_uint4(mh, wl, wv, 0u);
+    RDL_TPHASE(2)
+    LdsBarrier();
+    RDL_TPHASE(3)
+    // ---- block winner over the wave slots
+    const uint4 s4 = lane < uint32_t(WAVES) ? slots[par][lane] : make_uint4(0u, 0u, 0u, 0u);
+    par ^= 1u;
+    uint32_t gh = MaxU32<SLANES>(s4.x);
+    {
+      const bool mine = lane < uint32_t(WAVES) && s4.x == gh;
+      const uint64_t t2 = __ballot(mine);
       int win;
       if ((t2 & (t2 - 1ull)) == 0ull) {
         win = __builtin_ctzll(t2);
@@ -1852,12 +1817,10 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTab(LoopArgs a) {
         const uint32_t l2 = MaxU32<SLANES>(mine ? s4.y : 0u);
         win = FirstLane(mine && s4.y == l2);
       }
-      const uint32_t gl0 = uint32_t(__builtin_amdgcn_readlane(int(s4.y), win));
-      const uint32_t gv0 = uint32_t(__builtin_amdgcn_readlane(int(s4.z), win));
-      gh = gh0;
-      gl = gl0;
-      gv = gv0;
+      owner = win;
     }
+    uint32_t gl = uint32_t(__builtin_amdgcn_readlane(int(s4.y), owner));
+    uint32_t gv = uint32_t(__builtin_amdgcn_readlane(int(s4.z), owner));
     if (G > 1) {
       // ---- exchange of the participants' winners
       ++epoch;  // 1, 2, ... (granules are zeroed per launch)
