@@ -34,7 +34,7 @@ FAMILY_KERNELS = {
     "spectrum_multiply": r"^rdl::SpectrumMultiply\(",
     "subminor_loop": r"SubminorLoop",
     "subminor_table": r"BuildPairTable",
-    "subminor_select": r"^rdl::Sel(Count|Scan|Scatter|SinglePass|Gather)\(",
+    "subminor_select": r"^rdl::Sel(Count|Scan|Scatter|SinglePass|Gather|Local|LocalQuad|Place)\(",
     "find_peak": r"^void rdl::FindPeak|^rdl::FindPeakFinal",
     "integrate": r"^rdl::IntegrateKernel\(",
     "add": r"^rdl::AddKernel\(",
@@ -46,7 +46,7 @@ FAMILY_KERNELS = {
 # over the summed launches and algorithmic bytes of both (the *_sparse
 # families count a lower bound: the skipped zero rows are not known on the host)
 GROUPS = {
-    "conv64_cols+conv64_cols_sparse": (r"rdl::ff::Columns<double",
+    "conv64_cols+conv64_cols_sparse": (r"rdl::ff::Columns(ConvD)?<(double|512u)",
                                        ("conv64_cols", "conv64_cols_sparse")),
     "conv64_rows+conv64_rows_sparse": (r"rdl::ff::Rows(Inverse|Forward)<double",
                                        ("conv64_rows", "conv64_rows_sparse")),
