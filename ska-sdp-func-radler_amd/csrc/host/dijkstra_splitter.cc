@@ -11,18 +11,75 @@ namespace radler::math {
 
 namespace {
 
-// One heap entry: the cost of the path up to the predecessor, the target and
-// the predecessor as (u, v) — u runs along the path, v across the band.
-// 12 bytes (images up to 65535 pixels a side); the heap order depends only
-// on `cost`, like the reference's Visit (dijkstra_splitter.h:24-29), so
-// equal costs pop in the same heap order as the reference's queue.
-struct Node {
-  float cost;
-  uint16_t u, v, pu, pv;
+// The open list: libstdc++'s std::priority_queue algorithm (push_heap's
+// sift-up, pop_heap's hole walk to a leaf then sift-up: bits/stl_heap.h) over
+// the comparator "later first" (a.cost > b.cost, the reference's Visit
+// order, dijkstra_splitter.h:24-29), restated on split arrays: the costs the
+// comparisons read are packed 4 bytes apart and the payload (target and
+// predecessor as (u, v), 8 bytes) moves alongside. The same comparisons and
+// moves as the reference's queue, so equal costs pop in its order.
+class OpenList {
+ public:
+  explicit OpenList(size_t reserve) {
+    cost_.reserve(reserve);
+    load_.reserve(reserve);
+  }
+  bool Empty() const { return cost_.empty(); }
+  float TopCost() const { return cost_[0]; }
+  uint64_t TopLoad() const { return load_[0]; }
+  void Push(float c, uint64_t l) {
+    cost_.push_back(c);
+    load_.push_back(l);
+    SiftUp(cost_.size() - 1, 0, c, l);
+  }
+  void Pop() {
+    const size_t last = cost_.size() - 1;
+    const float vc = cost_[last];
+    const uint64_t vl = load_[last];
+    cost_[last] = cost_[0];
+    load_[last] = load_[0];
+    // __adjust_heap(first, 0, len = last, value)
+    const size_t len = last;
+    size_t hole = 0, child = 0;
+    while (len > 0 && child < (len - 1) / 2) {
+      child = 2 * (child + 1);
+      if (cost_[child] > cost_[child - 1]) --child;  // comp(child, child - 1)
+      cost_[hole] = cost_[child];
+      load_[hole] = load_[child];
+      hole = child;
+    }
+    if (len > 0 && (len & 1) == 0 && child == (len - 2) / 2) {
+      child = 2 * (child + 1);
+      cost_[hole] = cost_[child - 1];
+      load_[hole] = load_[child - 1];
+      hole = child - 1;
+    }
+    SiftUp(hole, 0, vc, vl);
+    cost_.pop_back();
+    load_.pop_back();
+  }
+
+ private:
+  // __push_heap(first, hole, top, value): while comp(parent, value)
+  void SiftUp(size_t hole, size_t top, float c, uint64_t l) {
+    size_t parent = (hole - 1) / 2;
+    while (hole > top && cost_[parent] > c) {
+      cost_[hole] = cost_[parent];
+      load_[hole] = load_[parent];
+      hole = parent;
+      parent = (hole - 1) / 2;
+    }
+    cost_[hole] = c;
+    load_[hole] = l;
+  }
+  std::vector<float> cost_;
+  std::vector<uint64_t> load_;
 };
-struct LaterFirst {
-  bool operator()(const Node& a, const Node& b) const { return a.cost > b.cost; }
-};
+
+// payload: target (u, v) and predecessor (pu, pv), 16 bits each
+inline uint64_t Load(uint32_t u, uint32_t v, uint32_t pu, uint32_t pv) {
+  return uint64_t(u) | (uint64_t(v) << 16) | (uint64_t(pu) << 32) | (uint64_t(pv) << 48);
+}
 
 }  // namespace
 
@@ -44,39 +101,38 @@ void DijkstraSplitter::Divide(const float* image, float* output, size_t lo,
   std::vector<float> dist(band * n_u, std::numeric_limits<float>::max());
   for (size_t u = 0; u != n_u; ++u)
     for (size_t v = lo; v != hi; ++v) weight[u * band + (v - lo)] = std::fabs(image[pixel(u, v)]);
-  std::vector<Node> heap_store;
-  heap_store.reserve(8 * band);
-  std::priority_queue<Node, std::vector<Node>, LaterFirst> open(LaterFirst(),
-                                                                std::move(heap_store));
-  for (size_t v = lo; v != hi; ++v)
-    open.push(Node{0.0f, 0, uint16_t(v), 0, uint16_t(v)});
+  OpenList open(8 * band);
+  for (size_t v = lo; v != hi; ++v) open.Push(0.0f, Load(0, uint32_t(v), 0, uint32_t(v)));
   // predecessor of each settled pixel (pu << 16 | pv), band-local layout
   std::vector<uint32_t> back(band * n_u);
-  Node cur{};
-  while (!open.empty()) {
-    cur = open.top();
-    open.pop();
-    if (cur.u == n_u) break;
-    const size_t at = size_t(cur.u) * band + (cur.v - lo);
-    const float cost = cur.cost + weight[at];
+  uint32_t end_pu = 0, end_pv = 0;
+  while (!open.Empty()) {
+    const float top_cost = open.TopCost();
+    const uint64_t top = open.TopLoad();
+    open.Pop();
+    const uint32_t cu = uint32_t(top & 0xffffu), cv = uint32_t((top >> 16) & 0xffffu);
+    end_pu = uint32_t((top >> 32) & 0xffffu);
+    end_pv = uint32_t(top >> 48);
+    if (cu == n_u) break;
+    const size_t at = size_t(cu) * band + (cv - lo);
+    const float cost = top_cost + weight[at];
     if (!(cost < dist[at])) continue;
     dist[at] = cost;
-    back[at] = (uint32_t(cur.pu) << 16) | cur.pv;
-    const uint16_t u = cur.u, v = cur.v;
-    const uint16_t u1 = uint16_t(u + 1);
-    if (v > lo) {
-      open.push(Node{cost, u1, uint16_t(v - 1), u, v});
-      open.push(Node{cost, u, uint16_t(v - 1), u, v});
+    back[at] = (end_pu << 16) | end_pv;
+    const uint32_t u1 = cu + 1;
+    if (cv > lo) {
+      open.Push(cost, Load(u1, cv - 1, cu, cv));
+      open.Push(cost, Load(cu, cv - 1, cu, cv));
     }
-    open.push(Node{cost, u1, v, u, v});
-    if (v + 1u < hi) {
-      open.push(Node{cost, u1, uint16_t(v + 1), u, v});
-      open.push(Node{cost, u, uint16_t(v + 1), u, v});
+    open.Push(cost, Load(u1, cv, cu, cv));
+    if (cv + 1u < hi) {
+      open.Push(cost, Load(u1, cv + 1, cu, cv));
+      open.Push(cost, Load(cu, cv + 1, cu, cv));
     }
   }
   for (size_t u = 0; u != n_u; ++u)
     for (size_t v = lo; v != hi; ++v) output[pixel(u, v)] = 0.0f;
-  uint32_t pu = cur.pu, pv = cur.pv;
+  uint32_t pu = end_pu, pv = end_pv;
   for (; pu > 0;) {
     output[pixel(pu, pv)] = 1.0f;
     const uint32_t p = back[size_t(pu) * band + (pv - lo)];
