@@ -436,14 +436,19 @@ __global__ __launch_bounds__(TH) void ColumnsConvD(ColArgs a, const Cx<double>* 
     const Cx<double>* in_c = in + cc;
     const uint32_t k_stride = a.kern_cm ? 1u : a.ld;
     const Cx<double>* kern_c = a.kern_cm ? kern + size_t(cc) * N : kern + cc;
-    // K x s in the last forward pass's output order: rows j + r NBL
-    Cx<double> K[BL][RL];
+    // K x s in the last forward pass's output order: rows j + r NBL; held in
+    // registers from the round's start (512 threads), or read where it is
+    // multiplied (1024 threads: the registers go to the second set of waves)
+    constexpr bool KREG = TH <= 512;
+    Cx<double> K[KREG ? BL : 1][KREG ? RL : 1];
+    if constexpr (KREG) {
 #pragma unroll
-    for (uint32_t i = 0; i < BL; ++i) {
-      const uint32_t j = tid + i * TH;
-      if (NBL % TH == 0 || j < NBL)
+      for (uint32_t i = 0; i < BL; ++i) {
+        const uint32_t j = tid + i * TH;
+        if (NBL % TH == 0 || j < NBL)
 #pragma unroll
-        for (uint32_t r = 0; r < RL; ++r) K[i][r] = kern_c[(j + r * NBL) * k_stride];
+          for (uint32_t r = 0; r < RL; ++r) K[i][r] = kern_c[(j + r * NBL) * k_stride];
+      }
     }
     // forward pass 1: straight from global memory through the row bitmap
     auto load = [&](uint32_t y) {
@@ -453,7 +458,12 @@ __global__ __launch_bounds__(TH) void ColumnsConvD(ColArgs a, const Cx<double>* 
     CPass<TH, N, R1, 1, 1, 0>(buf, t1, t2, tid, load,
                               [&](uint32_t, uint32_t, uint32_t y, Cx<double> v) { buf[y] = v; });
     auto mulk = [&](uint32_t i, uint32_t r, uint32_t y, Cx<double> v) {
-      buf[y] = Conj(Scale(Mul(v, K[i][r]), s));
+      Cx<double> k;
+      if constexpr (KREG)
+        k = K[i][r];
+      else
+        k = kern_c[(tid + i * TH + r * NBL) * k_stride];
+      buf[y] = Conj(Scale(Mul(v, k), s));
     };
     CFwdTail<TH, N, R1, decltype(mulk), Rs...>(buf, t1, t2, tid, mulk);
     // inverse = conj(forward(conj(X K s))); the last pass stores row-major
@@ -1190,11 +1200,24 @@ const FastColumns* FindConvColumnsD(uint32_t n) {
       RDL_CONV_D(512, 5, 3, 5, 8, 8),        // 4800
       RDL_CONV_D(512, 5, 5, 5, 5, 8),        // 5000
   };
-  static const bool off = [] {
+  // 1024-thread plans of the large sizes (one column's 145 KiB of LDS per
+  // CU: twice the waves cover the passes' LDS and memory waits; 9072:
+  // 779 -> 661 us, tools/bench_fftk.py f64); RDL_FFT_CONVD=512 keeps the
+  // 512-thread plans, =0 disables the engine
+  static const FastColumns kPlans1024[] = {
+      RDL_CONV_D(1024, 7, 9, 9, 4, 4),        // 9072
+      RDL_CONV_D(1024, 9, 4, 4, 4, 4, 4),     // 9216
+      RDL_CONV_D(1024, 7, 3, 7, 4, 4, 4),     // 9408
+      RDL_CONV_D(1024, 7, 5, 3, 5, 3, 3, 2),  // 9450
+  };
+  static const int mode = [] {
     const char* e = std::getenv("RDL_FFT_CONVD");
-    return e && e[0] == '0';
+    return !e ? 2 : e[0] == '0' ? 0 : std::atoi(e) == 512 ? 1 : 2;
   }();
-  if (off) return nullptr;
+  if (mode == 0) return nullptr;
+  if (mode == 2)
+    for (const FastColumns& p : kPlans1024)
+      if (p.n == n) return &p;
   for (const FastColumns& p : kPlans)
     if (p.n == n) return &p;
   return nullptr;
