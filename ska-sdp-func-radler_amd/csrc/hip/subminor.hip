@@ -1581,8 +1581,7 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopReg(LoopArgs a) {
         for (int i = 0; i < ITEMS; ++i)
           if (i == wi)
 #pragma unroll
-            for (int k = 0; k < NI; ++k)
-              if (k < n_img) M[i][k] += c[k];
+            for (int k = 0; k < NI; ++k) M[i][k] += c[k];
       }
     }
     if (blockIdx.x == 0 && tid == 0 && a.trace) {
@@ -1948,6 +1947,386 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTab(LoopArgs a) {
   }
 }
 
+// RegIntegration's RDL_INTEGRATE_LINEAR branch alone (SubminorLoopTabN's
+// integrations): the same operations in the same order
+template <int NI>
+struct LinearIntegration {
+  uint32_t incl = 0;
+  float w[NI];
+  float factor = 1.0f;
+  __device__ void Init(const rdl_integration& g) {
+    factor = g.factor;
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+      w[k] = uint32_t(k) < g.n_images ? g.weights[k] : 0.0f;
+      if (uint32_t(k) < g.n_images && w[k] != 0.0f && ((g.pol_mask >> (uint32_t(k) % g.n_pol)) & 1u))
+        incl |= 1u << k;
+    }
+  }
+  __device__ float operator()(const float (&v)[NI]) const {
+    float acc = 0.0f;
+    bool first = true;
+#pragma unroll
+    for (int k = 0; k < NI; ++k)
+      if ((incl >> k) & 1u) {
+        acc = first ? v[k] * w[k] : __builtin_fmaf(v[k], w[k], acc);
+        first = false;
+      }
+    return first ? 0.0f : acc * factor;
+  }
+};
+
+// ------------------------------------------------- pairwise-table loop, N_img
+// SubminorLoopTabN: SubminorLoopTab for joined images (NI = 2..8 images of
+// one polarization, each with its own PSF, the linear integration; no RMS
+// factor, spectral map or log-polynomial fit). Per iteration the component's table row of
+// every PSF (FMAs into the register-resident images), the integrated value
+// per pixel, the key argmax as SubminorLoopTab's (|integrated| max chain with
+// allow_negative), the wave winner's image values through its LDS slot, and
+// for G > 1 participants (one XCD, as SubminorLoopTab) records of 3 + N_img
+// epoch-tagged granules. The same operations in the same order as
+// SubminorLoopReg: traces and model values are identical.
+template <int NI, int ITEMS, int THREADS, bool NEG>
+__global__ __launch_bounds__(THREADS) void SubminorLoopTabN(LoopArgs a) {
+  constexpr int WAVES = THREADS / 64;
+  constexpr int SLANES = WAVES <= 8 ? 8 : 16;
+  constexpr uint32_t REC = 3 + NI;
+  __shared__ uint4 slots[2][WAVES];     // {key hi, key lo, integrated bits, -}
+  __shared__ float slotv[2][WAVES][NI];  // the wave winner's image values
+  const uint32_t G = a.n_blocks;
+  if (G > 1 && blockIdx.x % kTabParticipantStride != 0u) return;
+  const uint32_t rank = G > 1 ? blockIdx.x / kTabParticipantStride : 0u;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t n = uint32_t(a.n_sel), per = a.per_block;
+  const uint32_t base = rank * per;
+  const uint32_t cnt = base >= n ? 0u : min(per, n - base);
+  const bool neg = a.allow_negative != 0;
+  LinearIntegration<NI> ri;
+  ri.Init(a.integ);
+  // uniform values kept in VGPRs (one wave per SIMD leaves them free; as
+  // SGPRs they spilled): weights, factor, and below the component values
+#pragma unroll
+  for (int k = 0; k < NI; ++k) asm volatile("" : "+v"(ri.w[k]));
+  asm volatile("" : "+v"(ri.factor));
+  uint64_t* gran = reinterpret_cast<uint64_t*>(a.records);
+  uint64_t* recs = gran + G;
+  float R[ITEMS][NI], M[ITEMS][NI];
+#pragma unroll
+  for (int i = 0; i < ITEMS; ++i) {
+    const uint32_t j = tid + uint32_t(i) * THREADS;
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+      // beyond the slice: NaN (never a winner; see the padded table)
+      R[i][k] = j < cnt ? a.r[size_t(k) * n + base + j] : __int_as_float(0x7fc00000);
+      M[i][k] = 0.0f;
+    }
+  }
+  bool fast = true;
+  bool failed = false;
+  if (G > 1) {
+    if (tid == 0)
+      __hip_atomic_store(gran + rank, (uint64_t(1) << 32) | XccId(), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t xcc = 0u;
+    for (uint64_t spins = 0; !failed; ++spins) {
+      uint64_t v = 0;
+      if (lane < G)
+        v = __hip_atomic_load(gran + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__all(lane >= G || (v >> 32) == 1u)) {
+        xcc = uint32_t(v);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      failed = spins > (uint64_t(1) << 24);
+    }
+    const uint32_t x0 = uint32_t(__builtin_amdgcn_readlane(int(xcc), 0));
+    fast = __all(lane >= G || xcc == x0);
+  }
+  const size_t sq = size_t(n) * n;
+  float c[NI];
+#pragma unroll
+  for (int k = 0; k < NI; ++k) c[k] = 0.0f;
+  float m = 0.0f, start_abs = 0.0f, flux = 0.0f;
+  uint32_t cp = 0, par = 0, epoch = 0;
+  uint32_t row_cp = 0xffffffffu;
+  float pv[ITEMS][NI];
+  uint32_t pend_pos = 0;
+  bool pend = false, have = false, diverging = false;
+  uint64_t iteration = a.iteration_start;
+  const bool tracer = rank == 0 && tid == 0 && a.trace;
+  const uint32_t thr_bits = __float_as_uint(a.threshold) & 0x7fffffffu;
+  const uint32_t thr_mode = a.threshold != a.threshold        ? 0u
+                            : (__float_as_uint(a.threshold) >> 31) && thr_bits ? 1u
+                                                                                : 2u;
+  uint32_t lim_mode = 0u, lim_bits = 0u;
+  const bool stop_neg = a.stop_on_negative != 0;
+  uint64_t remaining =
+      a.max_iterations > a.iteration_start ? a.max_iterations - a.iteration_start : 0u;
+  while (!failed) {
+    if (have) {
+      // the component's row of every PSF (contiguous over j)
+      if (cp != row_cp) {
+#pragma unroll
+        for (int q = 0; q < NI; ++q) {
+          const float* row = a.table + size_t(q) * sq + size_t(cp) * n + base;
+#pragma unroll
+          for (int i = 0; i < ITEMS; ++i) pv[i][q] = row[tid + uint32_t(i) * THREADS];
+        }
+        row_cp = cp;
+      }
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        const bool in = __float_as_uint(pv[i][0]) != kOutsideBits;
+#pragma unroll
+        for (int k = 0; k < NI; ++k) {
+          const float t = __builtin_fmaf(-pv[i][k], c[k], R[i][k]);
+          R[i][k] = in ? t : R[i][k];
+        }
+      }
+      if (pend) {
+        const uint64_t t = iteration - a.iteration_start;
+        if (t < a.trace_cap) {
+          a.trace[2 * t] = pend_pos & 0xffffu;
+          a.trace[2 * t + 1] = pend_pos >> 16;
+        }
+        pend = false;
+      }
+    }
+    // ---- integrated values and this thread's best (as SubminorLoopTab)
+    float iv[ITEMS];
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) iv[i] = ri(R[i]);
+    uint32_t bh = 0u, bj = 0xffffffffu, bv = __float_as_uint(iv[0]), li = 0u;
+    if constexpr (NEG) {
+      float tb = -1.0f;
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) tb = __builtin_fmaxf(tb, __builtin_fabsf(iv[i]));
+      bh = tb >= 0.0f ? (__float_as_uint(tb) | 0x80000000u) : 0u;
+#pragma unroll
+      for (int i = ITEMS - 1; i >= 0; --i) {
+        const bool eq = __builtin_fabsf(iv[i]) == tb;
+        bj = eq ? base + tid + uint32_t(i) * THREADS : bj;
+        bv = eq ? __float_as_uint(iv[i]) : bv;
+        li = eq ? uint32_t(i) : li;
+      }
+      if (base == 0u && tid == 0u && cnt > 0u && iv[0] != iv[0]) {
+        bh = 0xffffffffu;
+        bj = 0u;
+        li = 0u;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        const float v = neg ? fabsf(iv[i]) : iv[i];
+        const uint32_t u = __float_as_uint(v);
+        uint32_t h = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+        const uint32_t j = base + tid + uint32_t(i) * THREADS;
+        if (v != v) h = (j == 0u && cnt > 0u) ? 0xffffffffu : 0u;
+        const bool better = h > bh;
+        bh = better ? h : bh;
+        bj = better ? j : bj;
+        bv = better ? __float_as_uint(iv[i]) : bv;
+        li = better ? uint32_t(i) : li;
+      }
+    }
+    // ---- wave winner and its image values
+    const uint32_t mh = MaxU32<64>(bh);
+    const uint64_t tie = __ballot(bh == mh);
+    int owner;
+    if (mh == 0u) {
+      owner = 0;  // a key-0 wave stands for lane 0's item 0
+    } else if ((tie & (tie - 1ull)) == 0ull) {
+      owner = __builtin_ctzll(tie);
+    } else {
+      const uint32_t ml = MaxU32<64>(bh == mh ? ~bj : 0u);
+      owner = FirstLane(bh == mh && ~bj == ml);
+    }
+    const uint32_t wl = mh == 0u ? 0u : ~uint32_t(__builtin_amdgcn_readlane(int(bj), owner));
+    const uint32_t wv = uint32_t(__builtin_amdgcn_readlane(int(bv), owner));
+    if (lane == 0) slots[par][wave] = make_uint4(mh, wl, wv, 0u);
+    // the owner lane stores its candidate's image values (a key-0 wave: lane
+    // 0's item 0, li = 0)
+    if (int(lane) == owner) {
+      float v[NI];
+#pragma unroll
+      for (int k = 0; k < NI; ++k) v[k] = R[0][k];
+#pragma unroll
+      for (int i = 1; i < ITEMS; ++i)
+#pragma unroll
+        for (int k = 0; k < NI; ++k) v[k] = li == uint32_t(i) ? R[i][k] : v[k];
+#pragma unroll
+      for (int k = 0; k < NI; ++k) slotv[par][wave][k] = v[k];
+    }
+    LdsBarrier();
+    // ---- block winner over the wave slots
+    const uint4 s4 = lane < uint32_t(WAVES) ? slots[par][lane] : make_uint4(0u, 0u, 0u, 0u);
+    uint32_t gh = MaxU32<SLANES>(s4.x);
+    {
+      const bool mine = lane < uint32_t(WAVES) && s4.x == gh;
+      const uint64_t t2 = __ballot(mine);
+      if ((t2 & (t2 - 1ull)) == 0ull) {
+        owner = __builtin_ctzll(t2);
+      } else {
+        const uint32_t l2 = MaxU32<SLANES>(mine ? s4.y : 0u);
+        owner = FirstLane(mine && s4.y == l2);
+      }
+    }
+    uint32_t gl = uint32_t(__builtin_amdgcn_readlane(int(s4.y), owner));
+    uint32_t gv = uint32_t(__builtin_amdgcn_readlane(int(s4.z), owner));
+    float wr[NI];
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+      wr[k] = slotv[par][owner][k];
+      asm volatile("" : "+v"(wr[k]));
+    }
+    par ^= 1u;
+    if (G > 1) {
+      ++epoch;
+      uint64_t* mine_rec = recs + (size_t(epoch & 1u) * G + rank) * REC;
+      if (wave == 0 && lane < REC) {
+        uint32_t w = lane == 0 ? gh : lane == 1 ? gl : gv;
+#pragma unroll
+        for (int k = 0; k < NI; ++k)
+          if (lane == 3u + uint32_t(k)) w = __float_as_uint(wr[k]);
+        const uint64_t g = (uint64_t(epoch) << 32) | w;
+        if (fast)
+          __hip_atomic_store(mine_rec + lane, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        else
+          __hip_atomic_store(mine_rec + lane, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      uint32_t xr[REC];
+#pragma unroll
+      for (uint32_t w = 0; w < REC; ++w) xr[w] = 0u;
+      for (uint64_t spins = 0;; ++spins) {
+        bool ok = true;
+        if (lane < G) {
+          const uint64_t* rr = recs + (size_t(epoch & 1u) * G + lane) * REC;
+#pragma unroll
+          for (uint32_t w = 0; w < REC; ++w) {
+            const uint64_t g = __hip_atomic_load(rr + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok = ok && uint32_t(g >> 32) == epoch;
+            xr[w] = uint32_t(g);
+          }
+        }
+        if (__all(ok)) break;
+        if (spins > (uint64_t(1) << 26)) {
+          failed = true;
+          break;
+        }
+      }
+      if (failed) break;
+      gh = MaxU32<64>(lane < G ? xr[0] : 0u);
+      const bool mine = lane < G && xr[0] == gh;
+      const uint64_t t2 = __ballot(mine);
+      int win;
+      if ((t2 & (t2 - 1ull)) == 0ull) {
+        win = __builtin_ctzll(t2);
+      } else {
+        const uint32_t l2 = MaxU32<64>(mine ? xr[1] : 0u);
+        win = FirstLane(mine && xr[1] == l2);
+      }
+      gl = uint32_t(__builtin_amdgcn_readlane(int(xr[1]), win));
+      gv = uint32_t(__builtin_amdgcn_readlane(int(xr[2]), win));
+#pragma unroll
+      for (int k = 0; k < NI; ++k)
+        wr[k] = __uint_as_float(uint32_t(__builtin_amdgcn_readlane(int(xr[3 + k]), win)));
+    }
+    // ---- decisions (as SubminorLoopTab, on the integrated value's bits)
+    const bool none = gh == 0u || (gh == 0xffffffffu && gl == 0xffffffffu);
+    const uint32_t wp = none ? 0u : 0xffffffffu - gl;
+    m = __uint_as_float(gv);
+    const uint32_t ab = gv & 0x7fffffffu;
+    const bool is_nan = ab > 0x7f800000u;
+    if (!have) {
+      start_abs = __uint_as_float(ab);
+      if (a.divergence_limit != 0.0f) {
+        const float lim = start_abs * a.divergence_limit;
+        lim_bits = __float_as_uint(lim) & 0x7fffffffu;
+        lim_mode = lim != lim ? 0u : ((__float_as_uint(lim) >> 31) && lim_bits) ? 1u : 2u;
+      }
+    } else {
+      diverging = lim_mode == 1u ? !is_nan : lim_mode == 2u ? (!is_nan && ab > lim_bits) : false;
+      ++iteration;
+      --remaining;
+    }
+    const bool above = thr_mode == 1u ? !is_nan : thr_mode == 2u ? (!is_nan && ab > thr_bits)
+                                                               : false;
+    const bool non_negative = !is_nan && ((gv >> 31) == 0u || gv == 0x80000000u);
+    const bool go = above && remaining != 0u && (!stop_neg || non_negative) && !diverging;
+    if (!go) break;
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+      c[k] = wr[k] * a.gain;
+      asm volatile("" : "+v"(c[k]));
+    }
+    flux += m * a.gain;
+    cp = wp;
+    {
+      const uint32_t off = wp - base;
+      if (off < cnt && (off % uint32_t(THREADS)) / 64u == wave) {
+        const uint32_t oi = off / uint32_t(THREADS);
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i)
+          if (uint32_t(i) == oi && lane == (off & 63u))
+#pragma unroll
+            for (int k = 0; k < NI; ++k) M[i][k] += c[k];
+      }
+    }
+    if (tracer) {
+      pend_pos = a.pos[wp];
+      pend = true;
+    }
+    have = true;
+  }
+  if (pend) {
+    const uint64_t t = iteration - a.iteration_start;
+    if (t < a.trace_cap) {
+      a.trace[2 * t] = pend_pos & 0xffffu;
+      a.trace[2 * t + 1] = pend_pos >> 16;
+    }
+  }
+  if (failed) {
+    if (tid == 0) StoreSc1(&a.result[8], 1u);
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < ITEMS; ++i) {
+    const uint32_t j = tid + uint32_t(i) * THREADS;
+    if (j < cnt)
+#pragma unroll
+      for (int k = 0; k < NI; ++k) a.m[size_t(k) * n + base + j] = M[i][k];
+  }
+  if (rank == 0 && tid == 0) {
+    LoopResult* r = reinterpret_cast<LoopResult*>(a.result);
+    r->iteration = iteration;
+    r->peak = m;
+    r->diverging = diverging ? 1 : 0;
+    r->flux = flux;
+  }
+}
+
+template <int NI, bool NEG>
+auto TabNKernel(uint32_t items) {
+  return items <= 1   ? SubminorLoopTabN<NI, 1, 256, NEG>
+         : items <= 2 ? SubminorLoopTabN<NI, 2, 256, NEG>
+                      : SubminorLoopTabN<NI, 4, 256, NEG>;
+}
+
+template <int NI>
+int LaunchTabN(const LoopArgs& a, uint32_t items, hipStream_t stream) {
+  auto k = a.allow_negative ? TabNKernel<NI, true>(items) : TabNKernel<NI, false>(items);
+  if (a.n_blocks > 1) {
+    void* args[] = {const_cast<LoopArgs*>(&a)};
+    RDL_HIP_CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k),
+                                             dim3(a.n_blocks * kTabParticipantStride),
+                                             dim3(256), args, 0, stream));
+  } else {
+    k<<<1, 256, 0, stream>>>(a);
+    RDL_HIP_CHECK(hipGetLastError());
+  }
+  return RDL_OK;
+}
+
 template <int THREADS, bool NEG>
 auto TabKernel(uint32_t items) {
   return items <= 1    ? SubminorLoopTab<1, THREADS, NEG>
@@ -2102,6 +2481,8 @@ int rdl_subminor_create(rdl_session* s, rdl_subminor** out) {
     h->wave_max = uint32_t(std::strtoul(e, nullptr, 10));
   if (const char* e = std::getenv("RDL_SUBMINOR_BIG_MAX"))
     h->big_max = uint32_t(std::strtoul(e, nullptr, 10));
+  if (const char* e = std::getenv("RDL_SUBMINOR_TARGET"))  // pixels x images per workgroup
+    h->target_per_block = uint32_t(std::strtoul(e, nullptr, 10));
   if (const char* e = std::getenv("RDL_SUBMINOR_BIG_TARGET"))
     h->big_target = uint32_t(std::strtoul(e, nullptr, 10));
   // RDL_SUBMINOR_SELECT=1 (2): the single-pass look-back selection (chunks
@@ -2407,6 +2788,29 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
     rdl::SetError("table sub-minor kernel does not apply to this selection");
     return RDL_ERR_ARG;
   }
+  // joined images (2..8, no RMS / spectral / log-polynomial fit):
+  // SubminorLoopTabN, participants of up to 1024 pixels (a row of every PSF
+  // per pixel: 1024 x 8 PSFs is the 32 KiB an iteration of one workgroup
+  // streams), at most 32 (one XCD)
+  const bool tabn_shape = want_table && ni > 1 && ni <= 8 && !p->d_rms && !p->d_spectral &&
+                          !lpfit && h->tab && h->mode == 0 && !use_wave &&
+                          p->integ.mode == RDL_INTEGRATE_LINEAR && !p->integ.copy_fast_path &&
+                          p->n_pol == 1;
+  uint32_t tabn_g = 0, tabn_items = 0;
+  if (tabn_shape) {
+    const uint64_t target = std::max<uint64_t>(256, 8192 / std::max<uint32_t>(ni / p->n_pol, 1));
+    const uint64_t tgt = std::min<uint64_t>(target, 1024);
+    const uint64_t gg = (n_sel + tgt - 1) / tgt;
+    if (gg <= std::min<uint32_t>(32, max_blocks)) {
+      tabn_g = uint32_t(std::max<uint64_t>(gg, 1));
+      const uint64_t pp = (n_sel + tabn_g - 1) / tabn_g;
+      const uint64_t need = (pp + 255) / 256;
+      tabn_items = need <= 1 ? 1 : need <= 2 ? 2 : 4;
+      g = tabn_g;
+      per = pp;
+    }
+  }
+  const bool use_tabn = tabn_g > 0;
   uint32_t tab_g = 1, tab_threads = 512, tab_items = 1;
   uint64_t tab_per = n_sel;
   if (use_tab) {
@@ -2468,7 +2872,8 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   la.prof = s->trace_subminor_phases ? 1 : 0;
   const uint64_t n_trace = (h_trace && trace_cap) ? trace_cap : 0;
   const size_t rec_bytes =
-      use_tab   ? (size_t(7) * g * sizeof(uint64_t) + 15) / 16 * 16
+      use_tab    ? (size_t(7) * g * sizeof(uint64_t) + 15) / 16 * 16
+      : use_tabn ? ((size_t(1) + 2 * (3 + ni)) * g * sizeof(uint64_t) + 15) / 16 * 16
       : use_reg ? (size_t(2) * g * (3 + ni_t) * sizeof(uint64_t) + 15) / 16 * 16
                 : size_t(2) * g * la.rec_words * sizeof(uint32_t);
   const size_t sync_need = 256 + 256 + rec_bytes + n_trace * 8;
@@ -2480,10 +2885,10 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   la.trace = n_trace ? reinterpret_cast<uint32_t*>(sb + 512 + rec_bytes) : nullptr;
   la.trace_cap = n_trace;
   // zero counter, result and (register kernel) the epoch-tagged granules
-  RDL_HIP_CHECK(hipMemsetAsync(sb, 0, (use_reg || use_tab) ? 512 + rec_bytes : 512, st));
+  RDL_HIP_CHECK(hipMemsetAsync(sb, 0, (use_reg || use_tab || use_tabn) ? 512 + rec_bytes : 512, st));
   la.table = nullptr;
   const uint32_t n_psf = ni / p->n_pol;
-  if ((use_reg || use_tab) && want_table) {
+  if ((use_reg || use_tab || use_tabn) && want_table) {
     // (+ 32 KiB: the table loop reads whole workgroup-sized slices of a row)
     const size_t table_bytes = size_t(n_psf) * n_sel * n_sel * sizeof(float) + (32 << 10);
     RDL_TRY(rdl::Grow(&h->table, &h->table_bytes, table_bytes, st));
@@ -2509,6 +2914,16 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
         RDL_TRY(rdl::LaunchTab<512>(la, tab_items, st));
       else
         RDL_TRY(rdl::LaunchTab<1024>(la, tab_items, st));
+    } else if (use_tabn) {
+      switch (ni) {
+        case 2: RDL_TRY(rdl::LaunchTabN<2>(la, tabn_items, st)); break;
+        case 3: RDL_TRY(rdl::LaunchTabN<3>(la, tabn_items, st)); break;
+        case 4: RDL_TRY(rdl::LaunchTabN<4>(la, tabn_items, st)); break;
+        case 5: RDL_TRY(rdl::LaunchTabN<5>(la, tabn_items, st)); break;
+        case 6: RDL_TRY(rdl::LaunchTabN<6>(la, tabn_items, st)); break;
+        case 7: RDL_TRY(rdl::LaunchTabN<7>(la, tabn_items, st)); break;
+        default: RDL_TRY(rdl::LaunchTabN<8>(la, tabn_items, st)); break;
+      }
     } else if (use_big) {
       const uint64_t bi = (per + 1023) / 1024;
       const uint32_t bitems = bi <= 1 ? 1 : bi <= 2 ? 2 : bi <= 4 ? 4 : 8;
@@ -2585,8 +3000,9 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
                  "[subminor] n_sel=%llu g=%u kind=%d threads=%d table=%d iters=%llu us=%.1f "
                  "gather=%llu integ=%llu wred=%llu bar=%llu xchg=%llu dec=%llu\n",
                  (unsigned long long)n_sel, g,
-                 use_tab ? 30 + int(tab_items) : use_reg ? 10 + int(items) : int(use_lds),
-                 use_tab ? int(tab_threads)
+                 use_tab ? 30 + int(tab_items) : use_tabn ? 50 + int(tabn_items)
+                 : use_reg ? 10 + int(items) : int(use_lds),
+                 use_tab ? int(tab_threads) : use_tabn ? 256
                  : use_wave ? 64 : use_big ? 1024 : use_reg ? int(rdl::kRegThreads) : 512,
                  la.table ? 1 : 0,
                  (unsigned long long)(res.iteration - p->iteration_start),

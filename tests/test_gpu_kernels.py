@@ -666,6 +666,55 @@ def test_ms_transform_any_size(orc, w, h, shape):
         assert err <= 2e-6 * np.abs(img).max() * np.sqrt(np.log2(pw * ph)), (sc, err)
 
 
+@pytest.mark.parametrize("n_ch,n_target,neg", [
+    (2, 300, 1), (2, 2500, 1), (4, 1500, 1), (8, 600, 1), (8, 3000, 1), (8, 5000, 1),
+    (3, 1500, 0), (8, 2000, 0)])
+def test_subminor_joined_table_kernel_bit_exact(sess, orc, n_ch, n_target, neg):
+    """The joined-image table loop (SubminorLoopTabN: 2..8 images, linear
+    integration, one workgroup up to 1024 pixels, then XCD-local participants
+    of <= 1024): trace and model values bit-exact against the oracle's Clark
+    sub-minor loop over the same joined image set."""
+    w = h = 512
+    psf, dirty = synthetic(w, h, 200, 7)
+    dirties = np.stack([dirty * np.float32(1.0 + 0.15 * k) + np.float32(1e-3 * k) *
+                        np.roll(dirty, 3 * k, axis=1) for k in range(n_ch)]).astype(np.float32)
+    psfs = np.stack([np.roll(psf, k, axis=0) * np.float32(1.0 - 0.02 * k)
+                     for k in range(n_ch)]).astype(np.float32)
+    integ = orc.integrate(dirties)
+    val = np.abs(integ) if neg else np.maximum(integ, 0)
+    thr = float(np.sort(val.ravel())[-n_target])
+    max_iter = 1200
+    res_o, mod_o = dirties.copy(), np.zeros((n_ch, h, w), np.float32)
+    alg = OracleAlgorithm(orc, 0, threshold=thr, max_iterations=max_iter, border_ratio=0.0,
+                          use_sub_minor=1, major_loop_gain=1.0, allow_negative=neg)
+    r, trace_o = alg.execute(res_o, mod_o, psfs)
+    dres, dpsf = sess.array(dirties), sess.array(psfs)
+    sm = C.c_void_p()
+    sess.rdl.rdl_subminor_create(sess.h, C.byref(sm))
+    p = SubminorParams()
+    p.width, p.height, p.n_images, p.n_pol = w, h, n_ch, 1
+    p.integ = integration(n_ch, 1, mode=0)
+    p.allow_negative, p.stop_on_negative = neg, 0
+    p.threshold, p.gain, p.divergence_limit = np.float32(thr), 0.1, 4.0
+    p.iteration_start, p.max_iterations = 0, max_iter
+    out = SubminorResult()
+    trace = np.zeros((max_iter, 2), np.uint32)
+    sess.rdl.rdl_subminor_run(sm, dres.vp, dpsf.vp, C.byref(p), C.byref(out),
+                              trace.ctypes.data_as(C.c_void_p), C.c_uint64(max_iter))
+    n_it = out.iteration
+    print(f"n_sel {out.n_selected}, {n_it} iterations")
+    assert n_it == r.iteration_number
+    assert np.array_equal(trace[:n_it], trace_o[:n_it, :2])
+    for k in range(n_ch):
+        dmod = sess.array(shape=(h, w))
+        sess.rdl.rdl_subminor_model(sm, k, dmod.vp, w, h, 0, 0, 0)
+        assert np.array_equal(bits(dmod.get()), bits(mod_o[k])), k
+        dmod.free()
+    sess.rdl.rdl_subminor_destroy(sm)
+    for a in (dres, dpsf):
+        a.free()
+
+
 @pytest.mark.parametrize("w,h,border,frac,masked", [
     (4096, 4096, 0, 0.001, 0), (1000, 700, 13, 0.05, 0), (300, 200, 0, 1.0, 0),
     (8192, 1024, 100, 0.0002, 0), (1000, 700, 13, 0.05, 1), (998, 301, 7, 0.3, 1),
