@@ -55,6 +55,8 @@ struct rdl_subminor {
   size_t pos_bytes = 0;
   void* local_buf = nullptr;          // sparse selection: the chunks' own lists
   size_t local_bytes = 0;
+  void* stamp_mark = nullptr;         // shape-model stamping: tiles a stamp reaches
+  size_t stamp_mark_bytes = 0;
   int select_passes = 0;              // 0 sparse two-phase, 1 single pass, 3 count + scan + scatter
   int select_ticket = 1;              // single pass: chunk order by ticket
   int select_quad = 1;                // sparse: 16-byte loads where they apply
@@ -915,10 +917,54 @@ __device__ __forceinline__ uint32_t WrapDist(int32_t d, uint32_t size) {
   return uint32_t(d);
 }
 
+// the tiles some component's n x n stamp reaches (circularly, as the
+// stamping's hit test): a conservative byte map, so a tile no stamp reaches
+// skips its walk over the selection
+__device__ __forceinline__ void TileSpan(int32_t lo, int32_t hi, uint32_t size,
+                                         uint32_t (&a)[2], uint32_t (&b)[2], int& k) {
+  // [lo, hi] (hi - lo < size) as tile ranges, split where it wraps
+  k = 0;
+  if (lo < 0) {
+    a[k] = uint32_t(lo + int32_t(size)) / kStampTile;
+    b[k++] = (size - 1) / kStampTile;
+    lo = 0;
+  }
+  if (hi >= int32_t(size)) {
+    a[k] = 0;
+    b[k++] = uint32_t(hi - int32_t(size)) / kStampTile;
+    hi = int32_t(size) - 1;
+  }
+  a[k] = uint32_t(lo) / kStampTile;
+  b[k++] = uint32_t(hi) / kStampTile;
+}
+
+__global__ __launch_bounds__(256) void MarkStampTiles(const uint32_t* __restrict__ pos,
+                                                      const float* __restrict__ m,
+                                                      uint64_t n_sel, uint32_t n,
+                                                      uint32_t width, uint32_t height,
+                                                      uint32_t tiles_x,
+                                                      uint8_t* __restrict__ mark) {
+  const int32_t h = int32_t(n / 2);
+  for (uint64_t c = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; c < n_sel;
+       c += uint64_t(gridDim.x) * blockDim.x) {
+    if (m[c] == 0.0f) continue;
+    const int32_t xc = int32_t(pos[c] & 0xffffu), yc = int32_t(pos[c] >> 16);
+    uint32_t xa[2], xb[2], ya[2], yb[2];
+    int nx, ny;
+    TileSpan(xc - h, xc + h, width, xa, xb, nx);
+    TileSpan(yc - h, yc + h, height, ya, yb, ny);
+    for (int i = 0; i < ny; ++i)
+      for (uint32_t ty = ya[i]; ty <= yb[i]; ++ty)
+        for (int j = 0; j < nx; ++j)
+          for (uint32_t tx = xa[j]; tx <= xb[j]; ++tx) mark[ty * tiles_x + tx] = 1;
+  }
+}
+
 __global__ __launch_bounds__(kStampThreads) void StampShapeModel(
     const uint32_t* __restrict__ pos, const float* __restrict__ m, uint64_t n_sel,
     const float* __restrict__ kern, uint32_t n, float* __restrict__ model,
-    uint32_t width, uint32_t height, uint32_t tiles_x) {
+    uint32_t width, uint32_t height, uint32_t tiles_x, const uint8_t* __restrict__ mark) {
+  if (!mark[blockIdx.x]) return;
   __shared__ uint32_t list[kStampThreads];
   __shared__ uint32_t wave_count[kStampThreads / 64];
   __shared__ uint32_t n_list;
@@ -1726,15 +1772,10 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTab(LoopArgs a) {
   }
   while (!failed) {
     if (have) {
-      // the component's row of the pairwise table (contiguous over j): all
-      // loads in flight, then the FMAs (subminor_loop.cc:93-108)
-      // (a repeated component reuses the row already in registers)
-      if (cp != row_cp) {
-        const float* row = table + size_t(cp) * n + base;
-#pragma unroll
-        for (int i = 0; i < ITEMS; ++i) pv[i] = row[tid + uint32_t(i) * THREADS];
-        row_cp = cp;
-      }
+      // the component's row of the pairwise table (contiguous over j), issued
+      // before the previous iteration's decisions (a repeated component
+      // reuses the row already in registers); the FMAs (subminor_loop.cc:
+      // 93-108)
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i)
         if (__float_as_uint(pv[i]) != kOutsideBits) R[i] = __builtin_fmaf(-pv[i], c, R[i]);
@@ -1875,6 +1916,14 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTab(LoopArgs a) {
     // integer order of the bits; NaN never passes a comparison)
     const bool none = gh == 0u || (gh == 0xffffffffu && gl == 0xffffffffu);
     const uint32_t wp = none ? 0u : 0xffffffffu - gl;
+    // the winner's table row: in flight while the decisions run (a row the
+    // loop then does not use is only read; wp < n_sel always)
+    if (wp != row_cp) {
+      const float* row = table + size_t(wp) * n + base;
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) pv[i] = row[tid + uint32_t(i) * THREADS];
+      row_cp = wp;
+    }
     m = __uint_as_float(gv);
     const uint32_t ab = gv & 0x7fffffffu;
     const bool is_nan = ab > 0x7f800000u;
@@ -2064,16 +2113,8 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTabN(LoopArgs a) {
       a.max_iterations > a.iteration_start ? a.max_iterations - a.iteration_start : 0u;
   while (!failed) {
     if (have) {
-      // the component's row of every PSF (contiguous over j)
-      if (cp != row_cp) {
-#pragma unroll
-        for (int q = 0; q < NI; ++q) {
-          const float* row = a.table + size_t(q) * sq + size_t(cp) * n + base;
-#pragma unroll
-          for (int i = 0; i < ITEMS; ++i) pv[i][q] = row[tid + uint32_t(i) * THREADS];
-        }
-        row_cp = cp;
-      }
+      // the component's row of every PSF (contiguous over j), issued before
+      // the previous iteration's decisions
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
         const bool in = __float_as_uint(pv[i][0]) != kOutsideBits;
@@ -2234,6 +2275,15 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTabN(LoopArgs a) {
     // ---- decisions (as SubminorLoopTab, on the integrated value's bits)
     const bool none = gh == 0u || (gh == 0xffffffffu && gl == 0xffffffffu);
     const uint32_t wp = none ? 0u : 0xffffffffu - gl;
+    if (wp != row_cp) {
+#pragma unroll
+      for (int q = 0; q < NI; ++q) {
+        const float* row = a.table + size_t(q) * sq + size_t(wp) * n + base;
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) pv[i][q] = row[tid + uint32_t(i) * THREADS];
+      }
+      row_cp = wp;
+    }
     m = __uint_as_float(gv);
     const uint32_t ab = gv & 0x7fffffffu;
     const bool is_nan = ab > 0x7f800000u;
@@ -2517,6 +2567,7 @@ int rdl_subminor_destroy(rdl_subminor* h) {
   if (h->sel) (void)hipFree(h->sel);
   if (h->pos_buf) (void)hipFree(h->pos_buf);
   if (h->local_buf) (void)hipFree(h->local_buf);
+  if (h->stamp_mark) (void)hipFree(h->stamp_mark);
   if (h->sync) (void)hipFree(h->sync);
   if (h->table) (void)hipFree(h->table);
   delete h;
@@ -3095,9 +3146,16 @@ int rdl_subminor_add_shape_model(rdl_subminor* h, uint32_t image_index,
     // algorithmic bytes: the selection read per tile is cached; count the
     // model read-modify-write of the whole plane
     rdl::ScopedTiming t(s, "stamp_model", 8.0 * double(width) * height);
+    const size_t n_tiles = size_t(tiles_x) * tiles_y;
+    RDL_TRY(rdl::Grow(&h->stamp_mark, &h->stamp_mark_bytes, n_tiles, s->stream));
+    uint8_t* mark = static_cast<uint8_t*>(h->stamp_mark);
+    RDL_HIP_CHECK(hipMemsetAsync(mark, 0, n_tiles, s->stream));
+    const float* mi = h->d_m + size_t(image_index) * h->n_selected;
+    rdl::MarkStampTiles<<<unsigned(std::min<uint64_t>(1024, rdl::DivUp(h->n_selected, 256))),
+                          256, 0, s->stream>>>(h->d_pos, mi, h->n_selected, n, width, height,
+                                               tiles_x, mark);
     rdl::StampShapeModel<<<tiles_x * tiles_y, rdl::kStampThreads, 0, s->stream>>>(
-        h->d_pos, h->d_m + size_t(image_index) * h->n_selected, h->n_selected,
-        d_kernel, n, d_model, width, height, tiles_x);
+        h->d_pos, mi, h->n_selected, d_kernel, n, d_model, width, height, tiles_x, mark);
   }
   RDL_HIP_CHECK(hipGetLastError());
   return RDL_OK;

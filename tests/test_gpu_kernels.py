@@ -666,6 +666,53 @@ def test_ms_transform_any_size(orc, w, h, shape):
         assert err <= 2e-6 * np.abs(img).max() * np.sqrt(np.log2(pw * ph)), (sc, err)
 
 
+@pytest.mark.parametrize("w,h,n", [(300, 200, 33), (256, 256, 129), (1000, 130, 65), (130, 97, 97)])
+def test_subminor_shape_model_stamp(sess, w, h, n):
+    """rdl_subminor_add_shape_model (the scale > 0 model update): every
+    selected component's n x n stamp added circularly, each pixel summing the
+    components in selection order — against the same sums in numpy float32
+    (partial edge tiles, stamps wrapping both edges, tiles no stamp reaches)."""
+    rng = np.random.default_rng(w + n)
+    psf, dirty = synthetic(w, h, 40, 3)
+    dirty = dirty.astype(np.float32)
+    dres, dpsf = sess.array(dirty[None]), sess.array(psf[None])
+    sm = C.c_void_p()
+    sess.rdl.rdl_subminor_create(sess.h, C.byref(sm))
+    p = SubminorParams()
+    p.width, p.height, p.n_images, p.n_pol = w, h, 1, 1
+    p.integ = integration(1, 1, mode=0)
+    p.allow_negative, p.stop_on_negative = 1, 0
+    p.threshold = float(np.sort(np.abs(dirty).ravel())[-400])
+    p.gain, p.divergence_limit = 0.1, 0.0
+    p.iteration_start, p.max_iterations = 0, 300
+    out = SubminorResult()
+    sess.rdl.rdl_subminor_run(sm, dres.vp, dpsf.vp, C.byref(p), C.byref(out), None,
+                              C.c_uint64(0))
+    n_sel = int(out.n_selected)
+    pos = np.zeros(n_sel, np.uint32)
+    mod = np.zeros(n_sel, np.float32)
+    sess.rdl.rdl_subminor_get(sm, pos.ctypes.data_as(C.c_void_p),
+                              mod.ctypes.data_as(C.c_void_p), C.c_uint64(n_sel))
+    kern = rng.random((n, n)).astype(np.float32)
+    dk = sess.array(kern)
+    dmodel = sess.array(np.zeros((h, w), np.float32))
+    sess.rdl.rdl_subminor_add_shape_model(sm, 0, dk.vp, n, dmodel.vp, w, h)
+    acc = np.zeros((h, w), np.float32)
+    hh = n // 2
+    for p_, v in zip(pos, mod):
+        if v == 0.0:
+            continue
+        xc, yc = int(p_ & 0xffff), int(p_ >> 16)
+        ys = (np.arange(-hh, hh + 1) + yc) % h
+        xs = (np.arange(-hh, hh + 1) + xc) % w
+        acc[np.ix_(ys, xs)] += np.float32(v) * kern
+    assert (mod != 0).sum() > 10
+    assert np.array_equal(dmodel.get(), acc)
+    sess.rdl.rdl_subminor_destroy(sm)
+    for a in (dres, dpsf, dk, dmodel):
+        a.free()
+
+
 @pytest.mark.parametrize("n_ch,n_target,neg", [
     (2, 300, 1), (2, 2500, 1), (4, 1500, 1), (8, 600, 1), (8, 3000, 1), (8, 5000, 1),
     (3, 1500, 0), (8, 2000, 0)])
