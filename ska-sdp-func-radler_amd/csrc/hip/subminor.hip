@@ -2745,7 +2745,8 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   // otherwise pay a cross-workgroup exchange per component
   const uint64_t big_cap = 1024ull * (ni_t <= 2 ? 8 : 4);
   const bool want_table = (h->mode == 0 || h->mode == 6) && reg_ok && n_sel >= 2 && n_sel <= h->table_max &&
-                          uint64_t(ni / p->n_pol) * n_sel * n_sel <= (uint64_t(1) << 28);
+                          uint64_t(ni / p->n_pol) * n_sel * n_sel <=
+                              (uint64_t(1) << (ni > 1 ? 29 : 28));  // 1 / 2 GiB
   // (one CU's memory pipe streams those rows: at most 8192 values per
   // iteration, so joined channels keep the grid above 8192 / N_img pixels)
   const bool table_single = want_table && n_sel <= big_cap && work <= 8192;
