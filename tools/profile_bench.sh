@@ -7,7 +7,7 @@
 set -e
 TAG=${1:-bench}
 shift || true
-ARGS=${*:---cpu-outer 0 --tiled-reference 0 --c2-reference 0}
+ARGS=${*:---cpu-outer 0 --tiled-reference 0 --joined-reference 0 --c2-reference 0}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
