@@ -408,7 +408,7 @@ __global__ __launch_bounds__(kSpThreads) void SelLocal(SelArgs a, uint32_t* __re
 // order, rows in order: box order), so the selection costs a peak search's
 // read. A lane's 4-pixel flags are ranked across the wave from three
 // ballots of its count's bits.
-constexpr uint32_t kQuadItems = 16;
+constexpr uint32_t kQuadItems = 8;
 constexpr uint32_t kQuadChunk = kSpThreads * kQuadItems * 4;  // pixel slots per chunk
 
 __global__ __launch_bounds__(kSpThreads) void SelLocalQuad(SelArgs a, uint32_t ipr, uint32_t rpb,
@@ -433,6 +433,7 @@ __global__ __launch_bounds__(kSpThreads) void SelLocalQuad(SelArgs a, uint32_t i
     if (in && a.mask) mk[i] = reinterpret_cast<const uint32_t*>(a.mask + size_t(y) * a.width)[q];
   }
   uint32_t m4[kQuadItems], pre[kQuadItems];
+  uint32_t any_m = 0u;
 #pragma unroll
   for (uint32_t i = 0; i < kQuadItems; ++i) {
     const uint32_t q = q0 + (i % ipr) * kSpThreads + tid;
@@ -446,12 +447,25 @@ __global__ __launch_bounds__(kSpThreads) void SelLocalQuad(SelArgs a, uint32_t i
                        value >= a.threshold;
       m |= sel ? (1u << j) : 0u;
     }
-    const uint32_t c = uint32_t(__popc(m));
-    const uint64_t b0 = __ballot(c & 1u), b1 = __ballot(c & 2u), b2 = __ballot(c & 4u);
-    pre[i] = uint32_t(__popcll(b0 & lower) + 2 * __popcll(b1 & lower) + 4 * __popcll(b2 & lower));
     m4[i] = m;
-    if (lane == 0)
-      wave_tot[i][wave] = uint32_t(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2));
+    any_m |= m;
+  }
+  // a selection is sparse: most waves select nothing and skip the ranking
+  if (__any(any_m != 0u)) {
+#pragma unroll
+    for (uint32_t i = 0; i < kQuadItems; ++i) {
+      const uint32_t c = uint32_t(__popc(m4[i]));
+      const uint64_t b0 = __ballot(c & 1u), b1 = __ballot(c & 2u), b2 = __ballot(c & 4u);
+      pre[i] = uint32_t(__popcll(b0 & lower) + 2 * __popcll(b1 & lower) + 4 * __popcll(b2 & lower));
+      if (lane == 0)
+        wave_tot[i][wave] = uint32_t(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2));
+    }
+  } else {
+#pragma unroll
+    for (uint32_t i = 0; i < kQuadItems; ++i) {
+      pre[i] = 0u;
+      if (lane == 0) wave_tot[i][wave] = 0u;
+    }
   }
   __syncthreads();
   uint32_t count = 0;
