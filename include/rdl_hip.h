@@ -47,6 +47,20 @@ int rdl_session_destroy(rdl_session* s);
 int rdl_session_sync(rdl_session* s);
 /* hipStream_t of the session, for callers that record events on it. */
 void* rdl_session_stream(rdl_session* s);
+/* Two launch lanes on one session, for independent chains that overlap on
+ * the device (the per-scale inverse transforms + peak searches of
+ * FindActiveScaleConvolvedMaxima, multiscale_algorithm.cc:578-634 of the
+ * reference, which runs them on threads). rdl_session_fork orders a second
+ * stream after everything issued so far; rdl_session_lane(s, 1) sends the
+ * following launches there (0: back to the session's stream);
+ * rdl_session_join orders the session's stream after the second lane and
+ * selects lane 0. Launchers that keep scratch (the four-step column
+ * scratch) keep one per lane; fused peak searches keep one partials area
+ * per peak slot. rdl_malloc / rdl_free (stream-ordered on lane 0) must not
+ * be called while lane 1 is selected. */
+int rdl_session_fork(rdl_session* s);
+int rdl_session_lane(rdl_session* s, int lane);
+int rdl_session_join(rdl_session* s);
 /* Make the session's device current for the calling host thread (worker
  * threads of the subimage pool call this once before allocating). */
 int rdl_session_bind(rdl_session* s);

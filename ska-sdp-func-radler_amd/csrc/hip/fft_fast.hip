@@ -1377,9 +1377,18 @@ int FastRowsInverseLaunch(rdl_session* s, const FastRows* p, const void* spec, f
   a.subtract = subtract;
   a.tiled = tiled;
   if (peak) a.peak = *peak;
-  // LT kernels are persistent (rows grid-strided): one table load per workgroup
+  // LT kernels are persistent (rows grid-strided): one table load per workgroup.
+  // A session with a second lane keeps one slot per CU free for the other
+  // lane's column passes (8192^2 bench: 762.8 -> 757.3 ms per step; 770.9
+  // with one lane), RDL_ROWS_PER_CU sets the cap
+  static const int cap_env = [] {
+    const char* e = std::getenv("RDL_ROWS_PER_CU");
+    return e ? std::atoi(e) : 0;
+  }();
+  const int cap = cap_env > 0 ? cap_env : (s->aux && slots >= 4 ? slots - 1 : slots);
+  const uint32_t per_cu = uint32_t(cap < slots ? cap : slots);
   const uint32_t grid =
-      lt ? std::min<uint32_t>(img_h, uint32_t(s->n_cus) * uint32_t(slots)) : img_h;
+      lt ? std::min<uint32_t>(img_h, uint32_t(s->n_cus) * per_cu) : img_h;
   void* args[] = {&a, (void*)&spec, (void*)&out, (void*)&tw, (void*)&ptw, (void*)&twd};
   RDL_HIP_CHECK(hipLaunchKernel(fn, dim3(grid), dim3(p->threads), args, lds, s->stream));
   return RDL_OK;

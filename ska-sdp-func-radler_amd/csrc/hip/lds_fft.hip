@@ -506,8 +506,10 @@ struct rdl_conv {
   void* tw_n1 = nullptr;
   void* tw_n2 = nullptr;
   uint32_t split_cols = 0;
-  void* scratch = nullptr;  // spectrum-sized, for the out-of-place B passes
-  size_t scratch_bytes = 0;
+  // spectrum-sized, for the out-of-place B passes; one per session lane
+  void* scratch_lane[2] = {nullptr, nullptr};
+  void* scratch = nullptr;  // the current lane's (set by EnsureSplitScratch)
+  size_t scratch_bytes[2] = {0, 0};
   // compile-time-planned kernels (fft_fast.hip) where the size has a plan
   const rdl::FastColumns* fast_cols = nullptr;
   const rdl::FastColumns* conv_cols = nullptr;  // float64 mode-1 columns (ColumnsConvD)
@@ -774,15 +776,19 @@ int LaunchSplit(rdl_conv* c, bool pass_b, int mode, const void* in, void* out,
 }
 
 int EnsureSplitScratch(rdl_conv* c, size_t bytes) {
-  if (c->scratch_bytes >= bytes) return RDL_OK;
+  const int l = c->s->lane;
+  c->scratch = c->scratch_lane[l];
+  if (c->scratch_bytes[l] >= bytes) return RDL_OK;
   if (c->scratch) {
-    RDL_HIP_CHECK(hipStreamSynchronize(c->s->stream));
+    RDL_HIP_CHECK(hipStreamSynchronize(c->s->home));
+    if (c->s->aux) RDL_HIP_CHECK(hipStreamSynchronize(c->s->aux));
     RDL_HIP_CHECK(hipFree(c->scratch));
-    c->scratch = nullptr;
-    c->scratch_bytes = 0;
+    c->scratch = c->scratch_lane[l] = nullptr;
+    c->scratch_bytes[l] = 0;
   }
   RDL_HIP_CHECK(hipMalloc(&c->scratch, bytes));
-  c->scratch_bytes = bytes;
+  c->scratch_lane[l] = c->scratch;
+  c->scratch_bytes[l] = bytes;
   return RDL_OK;
 }
 
@@ -935,7 +941,8 @@ int rdl_conv_destroy(rdl_conv* c) {
   if (c->tw_col) (void)hipFree(c->tw_col);
   if (c->tw_n1) (void)hipFree(c->tw_n1);
   if (c->tw_n2) (void)hipFree(c->tw_n2);
-  if (c->scratch) (void)hipFree(c->scratch);
+  for (void* p : c->scratch_lane)
+    if (p) (void)hipFree(p);
   if (c->rows_list) (void)hipFree(c->rows_list);
   for (void* p : {c->ptw_row, c->ptw_col, c->ptw_a, c->ptw_b, c->twd_row})
     if (p) (void)hipFree(p);
@@ -1101,8 +1108,11 @@ int rdl_conv_rows_inverse_peak(rdl_conv* c, const void* d_spec, float* d_out,
   if (pk.ye > out_h) pk.ye = out_h;
   pk.mask = d_mask;
   pk.allow_negative = allow_negative;
-  RDL_TRY(s->EnsureScratch(s->partials, std::max<size_t>(out_h, 1) * sizeof(uint64_t)));
-  pk.partials = static_cast<uint64_t*>(s->partials.ptr);
+  // one partials area per peak slot: the scales' searches may run on two
+  // session lanes at once
+  const size_t rows = std::max<size_t>(out_h, 1);
+  RDL_TRY(s->EnsureScratch(s->partials, RDL_PEAK_SLOTS * rows * sizeof(uint64_t)));
+  pk.partials = static_cast<uint64_t*>(s->partials.ptr) + slot * rows;
   {
     rdl::ScopedTiming t(s, "conv_rows",
                         SpectrumBytes(c) + double(out_w) * out_h * 4.0);

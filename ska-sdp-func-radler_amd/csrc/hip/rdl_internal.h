@@ -60,7 +60,13 @@ struct Scratch {
 
 struct rdl_session {
   int device = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;  // the current lane's stream (launchers use this)
+  // two-lane chains (rdl_session_fork / _lane / _join): `home` is the
+  // session's own stream, `aux` the second lane's; `lane` selects `stream`
+  hipStream_t home = nullptr;
+  hipStream_t aux = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  int lane = 0;
   int n_cus = 256;
   uint32_t coop_limit = 0;       // cap on cooperative grids (0: n_cus)
   bool timing = false;

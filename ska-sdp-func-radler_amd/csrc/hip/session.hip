@@ -143,7 +143,8 @@ int rdl_session::CollectTimings() {
 int rdl_session::EnsureScratch(rdl::Scratch& s, size_t bytes) {
   if (s.bytes >= bytes) return RDL_OK;
   if (s.ptr) {
-    RDL_HIP_CHECK(hipStreamSynchronize(stream));
+    RDL_HIP_CHECK(hipStreamSynchronize(home));
+    if (aux) RDL_HIP_CHECK(hipStreamSynchronize(aux));
     RDL_HIP_CHECK(hipFree(s.ptr));
     s.ptr = nullptr;
     s.bytes = 0;
@@ -198,6 +199,7 @@ int rdl_session_create(int device, rdl_session** out) {
   auto s = std::make_unique<rdl_session>();
   s->device = device;
   RDL_HIP_CHECK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+  s->home = s->stream;
   hipDeviceProp_t prop;
   RDL_HIP_CHECK(hipGetDeviceProperties(&prop, device));
   s->n_cus = prop.multiProcessorCount;
@@ -228,7 +230,8 @@ int rdl_session::FlushCache() {
     cache_bytes = 0;
   }
   if (blocks.empty()) return RDL_OK;
-  RDL_HIP_CHECK(hipStreamSynchronize(stream));
+  RDL_HIP_CHECK(hipStreamSynchronize(home));
+  if (aux) RDL_HIP_CHECK(hipStreamSynchronize(aux));
   for (auto& [bytes, p] : blocks) RDL_HIP_CHECK(hipFree(p));
   return RDL_OK;
 }
@@ -236,6 +239,9 @@ int rdl_session::FlushCache() {
 int rdl_session_destroy(rdl_session* s) {
   if (!s) return RDL_OK;
   (void)hipSetDevice(s->device);
+  if (s->aux) (void)hipStreamSynchronize(s->aux);
+  s->stream = s->home;
+  s->lane = 0;
   (void)hipStreamSynchronize(s->stream);
   (void)s->FlushCache();
   {
@@ -259,8 +265,43 @@ int rdl_session_destroy(rdl_session* s) {
   if (s->d_small) (void)hipFree(s->d_small);
   if (s->h_small) (void)hipHostFree(s->h_small);
   if (s->comm) rdl_comm_destroy(s);
-  (void)hipStreamDestroy(s->stream);
+  if (s->aux) (void)hipStreamDestroy(s->aux);
+  if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);
+  if (s->ev_join) (void)hipEventDestroy(s->ev_join);
+  (void)hipStreamDestroy(s->home);
   delete s;
+  return RDL_OK;
+}
+
+int rdl_session_fork(rdl_session* s) {
+  RDL_ARG_CHECK(s, "session is NULL");
+  RDL_ARG_CHECK(s->lane == 0, "fork from lane 1");
+  if (!s->aux) {
+    RDL_HIP_CHECK(hipSetDevice(s->device));
+    RDL_HIP_CHECK(hipStreamCreateWithFlags(&s->aux, hipStreamNonBlocking));
+    RDL_HIP_CHECK(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
+    RDL_HIP_CHECK(hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming));
+  }
+  RDL_HIP_CHECK(hipEventRecord(s->ev_fork, s->home));
+  RDL_HIP_CHECK(hipStreamWaitEvent(s->aux, s->ev_fork, 0));
+  return RDL_OK;
+}
+
+int rdl_session_lane(rdl_session* s, int lane) {
+  RDL_ARG_CHECK(s, "session is NULL");
+  RDL_ARG_CHECK(lane == 0 || (lane == 1 && s->aux), "lane 1 needs rdl_session_fork");
+  s->lane = lane;
+  s->stream = lane ? s->aux : s->home;
+  return RDL_OK;
+}
+
+int rdl_session_join(rdl_session* s) {
+  RDL_ARG_CHECK(s, "session is NULL");
+  s->lane = 0;
+  s->stream = s->home;
+  if (!s->aux) return RDL_OK;
+  RDL_HIP_CHECK(hipEventRecord(s->ev_join, s->aux));
+  RDL_HIP_CHECK(hipStreamWaitEvent(s->home, s->ev_join, 0));
   return RDL_OK;
 }
 

@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <set>
 #include <stdexcept>
@@ -18,6 +19,24 @@
 namespace radler::algorithms {
 
 using multiscale::MultiScaleTransforms;
+
+namespace {
+// RDL_SCALE_LANES=1: the scales' inverse transforms on one stream (default 2;
+// read per major iteration, so a test can compare both in one process)
+int ScaleLanes() {
+  const char* e = std::getenv("RDL_SCALE_LANES");
+  return e && e[0] == '1' ? 1 : 2;
+}
+
+// joins the session's second lane if a scope exits while it is selected
+struct LaneJoin {
+  rdl_session* s;
+  bool& forked;
+  ~LaneJoin() {
+    if (forked) (void)rdl_session_join(s);
+  }
+};
+}  // namespace
 
 void InitializeScales(std::vector<MultiScaleAlgorithm::ScaleInfo>& scales,
                       double beam_size_in_pixels, size_t min_width_height,
@@ -231,6 +250,37 @@ void MultiScaleAlgorithm::FindActiveScaleConvolvedMaxima(
   std::vector<size_t> pending;  // scale of each queued peak search
   if (scale_infos_.size() > RDL_PEAK_SLOTS)
     throw std::runtime_error("MultiScaleAlgorithm: too many scales");
+  // The scales' inverse transforms + fused peak searches are independent
+  // (the reference runs them on threads, threaded_deconvolution_tools.cc):
+  // with a kept image per scale they alternate over two session lanes, so
+  // one scale's latency-bound row pass overlaps the next one's column
+  // passes. Every buffer a lane writes is its own (work spectrum, four-step
+  // scratch, peak partials slot, scale image); the kernel spectra and the
+  // scale images are made before the fork (no allocation on lane 1).
+  const bool fused_search = !report_rms && !RmsFactorImage();
+  bool forked = false;
+  if (identity && fused_search && spectrum_work2_) {
+    size_t n_fft = 0;
+    for (size_t si = 0; si != scale_infos_.size(); ++si) {
+      const ScaleInfo& e = scale_infos_[si];
+      if (!e.is_active || e.scale == 0.0f) continue;
+      transforms_->KernelSpectrum(e.scale);
+      ++n_fft;
+    }
+    if (n_fft > 1) {
+      for (size_t si = 0; si != scale_infos_.size(); ++si) {
+        const ScaleInfo& e = scale_infos_[si];
+        if (!e.is_active || e.scale == 0.0f) continue;
+        gpu::Planes& kept = scale_images_[si];
+        if (!kept.buffer || kept.width != w || kept.height != h)
+          kept = gpu::Planes::Make(*session_, w, h, 1);
+      }
+      gpu::Check(rdl_session_fork(s), "rdl_session_fork");
+      forked = true;
+    }
+  }
+  LaneJoin lane_join{s, forked};
+  int lane = 0;
   for (size_t si = 0; si != scale_infos_.size(); ++si) {
     ScaleInfo& e = scale_infos_[si];
     if (!e.is_active || e.scale == 0.0f) continue;
@@ -247,9 +297,23 @@ void MultiScaleAlgorithm::FindActiveScaleConvolvedMaxima(
         std::max<size_t>(size_t(std::round(w * CleanBorderRatio())), border_scale));
     const uint32_t yb = uint32_t(
         std::max<size_t>(size_t(std::round(h * CleanBorderRatio())), border_scale));
+    if (forked) {
+      gpu::Check(rdl_session_lane(s, lane), "rdl_session_lane");
+      void* work = lane ? spectrum_work2_->Ptr() : spectrum_work_->Ptr();
+      if (transforms_->ConvolveSpectrumPeak(spectrum_->Ptr(), e.scale, work, d_conv, xb, yb,
+                                            AllowNegativeComponents(), MaskFor(si),
+                                            uint32_t(pending.size()))) {
+        pending.push_back(si);
+        lane ^= 1;
+        continue;
+      }
+      // no fused kernels for this size (nothing was issued): lane 0 from here
+      forked = false;
+      gpu::Check(rdl_session_join(s), "rdl_session_join");
+    }
     // the peak search fused into the inverse row pass where it can be (the
     // RMS-weighted search reads a weighted copy, so it stays separate)
-    if (!report_rms && !RmsFactorImage() &&
+    if (fused_search &&
         transforms_->ConvolveSpectrumPeak(spectrum_->Ptr(), e.scale, spectrum_work_->Ptr(),
                                           d_conv, xb, yb, AllowNegativeComponents(),
                                           MaskFor(si), uint32_t(pending.size()))) {
@@ -267,6 +331,10 @@ void MultiScaleAlgorithm::FindActiveScaleConvolvedMaxima(
                                      uint32_t(pending.size())),
                "rdl_find_peak_enqueue");
     pending.push_back(si);
+  }
+  if (forked) {
+    forked = false;
+    gpu::Check(rdl_session_join(s), "rdl_session_join");
   }
   std::vector<rdl_peak> peaks(pending.size());
   gpu::Check(rdl_find_peak_collect(s, uint32_t(pending.size()), peaks.data()),
@@ -355,6 +423,10 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
   const size_t spectrum_bytes = transforms_->SpectrumBytes();
   spectrum_ = std::make_shared<gpu::Buffer>(session, spectrum_bytes);
   spectrum_work_ = std::make_shared<gpu::Buffer>(session, spectrum_bytes);
+  spectrum_work2_.reset();
+  if (ScaleLanes() > 1 && data_image.Size() == 1 &&
+      data_image.Integration(false).copy_fast_path)
+    spectrum_work2_ = std::make_shared<gpu::Buffer>(session, spectrum_bytes);
 
   // ConvolvePsfs (:29-88): convolved[psf][scale]
   const size_t n_psf = data_image.PsfCount();

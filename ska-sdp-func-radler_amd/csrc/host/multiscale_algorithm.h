@@ -115,6 +115,9 @@ class MultiScaleAlgorithm final : public DeconvolutionAlgorithm {
   /// unnormalized / factor at the peak (:736-743), the value itself without
   float Normalized(float value, size_t x, size_t y, size_t w) const;
   std::shared_ptr<gpu::Buffer> spectrum_, spectrum_work_;
+  // the second session lane's work spectrum (FindActiveScaleConvolvedMaxima
+  // alternates the scales' fused inverse transforms over two lanes)
+  std::shared_ptr<gpu::Buffer> spectrum_work2_;
   // One image with the identity integration (ImageSet copy fast path): the
   // integrated image IS the residual, so the scale-convolved images that
   // FindActiveScaleConvolvedMaxima computes are the next outer iteration's

@@ -88,6 +88,28 @@ def test_multiscale_restore_is_repeatable():
         assert np.array_equal(x, y)
 
 
+@pytest.mark.parametrize("w,max_iter", [(256, 1500), (4096, 3000)])
+def test_multiscale_scale_lanes_identical(w, max_iter, monkeypatch):
+    """The scales' inverse transforms + fused peak searches on two session
+    lanes (rdl_session_fork/_lane/_join, per-lane four-step scratch at 4096^2,
+    per-slot peak partials) give bit-identical traces and images to one lane
+    (RDL_SCALE_LANES=1)."""
+    h = w
+    psf, dirty = problem(w, h, 40, 4, seed=w + 1)
+    out = []
+    for lanes in ("1", "2"):
+        monkeypatch.setenv("RDL_SCALE_LANES", lanes)
+        s = gpu_settings(w, h, 1e-3, max_iter, 6)
+        run = rd.gpu.DeviceRun(s, psf, dirty, [], 2.0 * PIXEL_SCALE)
+        r = run.execute()
+        out.append((r["iterations"], run.trace(), run.residual(), run.model()))
+    (i1, t1, r1, m1), (i2, t2, r2, m2) = out
+    assert i1 == i2 and i1 > 100
+    assert np.array_equal(t1, t2)
+    assert np.array_equal(r1, r2)
+    assert np.array_equal(m1, m2)
+
+
 JOINED_CASES = [
     # w, n_channels, weights, max_scales, fast
     (128, 2, None, 4, True),
