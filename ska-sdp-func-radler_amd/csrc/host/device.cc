@@ -348,7 +348,10 @@ std::shared_ptr<Session> Session::Worker(int device, size_t index) {
   static auto* workers = new std::map<std::pair<int, size_t>, std::shared_ptr<Session>>();
   std::lock_guard<std::mutex> lock(mutex);
   auto& w = (*workers)[{device, index}];
-  if (!w) w = std::make_shared<Session>(device);
+  if (!w) {
+    w = std::make_shared<Session>(device);
+    w->worker_ = true;
+  }
   return w;
 }
 

@@ -130,6 +130,9 @@ class Session {
   Session& operator=(const Session&) = delete;
   rdl_session* Handle() const { return s_; }
   int Device() const { return device_; }
+  /// A subimage pool's worker (Session::Worker): its streams already run
+  /// concurrently with the pool's other workers.
+  bool IsWorker() const { return worker_; }
   Fft& GetFft(size_t width, size_t height, bool f64 = false);
   void Sync();
   /// Make this session's device current for the calling thread.
@@ -174,6 +177,7 @@ class Session {
  private:
   rdl_session* s_ = nullptr;
   int device_;
+  bool worker_ = false;
   std::map<std::tuple<size_t, size_t, bool>, std::unique_ptr<Fft>> ffts_;
   Buffer scratch_[kNumScratch];
   rdl_subminor* subminor_ = nullptr;

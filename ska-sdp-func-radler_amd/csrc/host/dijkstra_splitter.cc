@@ -1,10 +1,13 @@
 #include "dijkstra_splitter.h"
 
 #include <algorithm>
+#include <atomic>
+#include <cstring>
 #include <cmath>
 #include <cstdint>
 #include <limits>
 #include <queue>
+#include <cstdlib>
 #include <stdexcept>
 
 namespace radler::math {
@@ -81,14 +84,192 @@ inline uint64_t Load(uint32_t u, uint32_t v, uint32_t pu, uint32_t pv) {
   return uint64_t(u) | (uint64_t(v) << 16) | (uint64_t(pu) << 32) | (uint64_t(pv) << 48);
 }
 
+
+// The radix heap of a monotone search (keys never below the last popped one):
+// non-negative float keys compare as their bit patterns, bucket b holds the
+// keys whose highest bit differing from the last popped key is bit b - 1.
+// Items are (key << 32 | payload) words. Pops come in key order; equal keys
+// in no particular order.
+class RadixQueue {
+ public:
+  bool Empty() const { return size_ == 0; }
+  void Push(uint64_t item) {
+    bucket_[Bucket(uint32_t(item >> 32))].push_back(item);
+    ++size_;
+  }
+  uint64_t Pop() {  // the queue must not be empty
+    if (bucket_[0].empty()) {
+      size_t b = 1;
+      while (bucket_[b].empty()) ++b;
+      uint64_t lowest = UINT64_MAX;
+      for (uint64_t it : bucket_[b]) lowest = std::min(lowest, it);
+      last_ = uint32_t(lowest >> 32);
+      for (uint64_t it : bucket_[b]) bucket_[Bucket(uint32_t(it >> 32))].push_back(it);
+      bucket_[b].clear();
+    }
+    const uint64_t item = bucket_[0].back();
+    bucket_[0].pop_back();
+    --size_;
+    return item;
+  }
+
+ private:
+  size_t Bucket(uint32_t key) const {
+    return key == last_ ? 0 : size_t(32 - __builtin_clz(key ^ last_));
+  }
+  std::vector<uint64_t> bucket_[33];
+  uint32_t last_ = 0;
+  size_t size_ = 0;
+};
+
+inline uint32_t KeyBits(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  return u;
+}
+inline float KeyFloat(uint32_t u) {
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+
+std::atomic<uint64_t> g_fast_divides{0}, g_exact_divides{0};
+
+// The reference's search visits pixels in key order (the key of an entry is
+// its predecessor's path cost) and keeps, per pixel, the predecessor of the
+// first entry popped; only entries with EQUAL keys to the same pixel pop in
+// an order that depends on the heap's history. This search settles the same
+// pixels at the same costs in key order with any tie order (a radix heap),
+// and marks every pixel that a second entry reaches with its settling key.
+// The divider it traces is the reference's when no pixel whose predecessor
+// the trace reads is marked, none was settled at the final key, and no other
+// last-row pixel ends at the final cost: then every predecessor on the path
+// and the end pixel are the unique minimum, whatever the pop order among
+// equal keys. Returns false (output untouched) otherwise.
+template <bool kVertical>
+bool DivideByKeyOrder(const float* image, float* output, size_t width, size_t height,
+                      size_t lo, size_t hi) {
+  const size_t n_u = kVertical ? height : width;
+  const size_t band = hi - lo;
+  auto pixel = [&](size_t u, size_t v) -> size_t {
+    return kVertical ? u * width + v : v * width + u;
+  };
+  const float unset = std::numeric_limits<float>::max();
+  std::vector<float> weight(band * n_u), dist(band * n_u, unset), key_of(band * n_u);
+  std::vector<uint32_t> back(band * n_u);
+  std::vector<uint8_t> tied(band * n_u, 0);
+  for (size_t u = 0; u != n_u; ++u)
+    for (size_t v = lo; v != hi; ++v) weight[u * band + (v - lo)] = std::fabs(image[pixel(u, v)]);
+  // payload: the target (u << vbits | v - lo) << 3 | the step from its
+  // predecessor (kStep*), 32 bits (else the exact search runs)
+  unsigned vbits = 1, ubits = 1;
+  while ((size_t(1) << vbits) < band) ++vbits;
+  while ((size_t(1) << ubits) <= n_u) ++ubits;
+  if (ubits + vbits + 3 > 32) return false;
+  const uint32_t vmask = (1u << vbits) - 1;
+  constexpr int kStepU[6] = {1, 0, 1, 1, 0, 0};  // target - predecessor
+  constexpr int kStepV[6] = {-1, -1, 0, 1, 1, 0};  // step 5: a start pixel
+  RadixQueue open;
+  auto push = [&](uint32_t key, uint32_t u, uint32_t v, unsigned step) {
+    const size_t at = size_t(u) * band + (v - lo);
+    if (u != n_u && dist[at] != unset) {  // settled: its entry would be dropped
+      if (KeyBits(key_of[at]) == key) tied[at] = 1;
+      return;
+    }
+    open.Push((uint64_t(key) << 32) | (((u << vbits) | (v - uint32_t(lo))) << 3) | step);
+  };
+  for (size_t v = lo; v != hi; ++v) push(0u, 0, uint32_t(v), 5);
+  uint32_t end_key = 0, end_pu = 0, end_pv = 0;
+  bool ended = false;
+  while (!open.Empty()) {
+    const uint64_t top = open.Pop();
+    const uint32_t key = uint32_t(top >> 32);
+    if (ended && key != end_key) break;  // drained the final key
+    const unsigned step = unsigned(top & 7);
+    const uint32_t cu = uint32_t(top) >> (3 + vbits);
+    const uint32_t cv = ((uint32_t(top) >> 3) & vmask) + uint32_t(lo);
+    const size_t at = size_t(cu) * band + (cv - lo);
+    const uint32_t pu = cu - kStepU[step], pv = cv - kStepV[step];
+    if (cu == n_u) {
+      if (!ended) {
+        ended = true;
+        end_key = key;
+        end_pu = pu;
+        end_pv = pv;
+      }
+      continue;
+    }
+    if (dist[at] != unset) {
+      if (KeyBits(key_of[at]) == key) tied[at] = 1;
+      continue;
+    }
+    const float cost = KeyFloat(key) + weight[at];
+    if (!(cost < unset)) continue;  // NaN / inf: never settles (as there)
+    dist[at] = cost;
+    key_of[at] = KeyFloat(key);
+    back[at] = (pu << 16) | pv;
+    const uint32_t c = KeyBits(cost), u1 = cu + 1;
+    if (cv > lo) {
+      push(c, u1, cv - 1, 0);
+      push(c, cu, cv - 1, 1);
+    }
+    push(c, u1, cv, 2);
+    if (cv + 1u < hi) {
+      push(c, u1, cv + 1, 3);
+      push(c, cu, cv + 1, 4);
+    }
+  }
+  if (!ended) return false;
+  // another last-row pixel at the final cost: the end is a tie
+  const size_t last = (n_u - 1) * band;
+  for (size_t v = 0; v != band; ++v)
+    if (v + lo != end_pv && KeyBits(dist[last + v]) == end_key) return false;
+  for (uint32_t pu = end_pu, pv = end_pv; pu > 0;) {
+    const size_t at = size_t(pu) * band + (pv - lo);
+    if (tied[at] || KeyBits(key_of[at]) >= end_key) return false;
+    pu = back[at] >> 16;
+    pv = back[at] & 0xffffu;
+  }
+  for (size_t u = 0; u != n_u; ++u)
+    for (size_t v = lo; v != hi; ++v) output[pixel(u, v)] = 0.0f;
+  uint32_t pu = end_pu, pv = end_pv;
+  for (; pu > 0;) {
+    output[pixel(pu, pv)] = 1.0f;
+    const uint32_t p = back[size_t(pu) * band + (pv - lo)];
+    pu = p >> 16;
+    pv = p & 0xffffu;
+  }
+  output[pixel(0, pv)] = 1.0f;
+  return true;
+}
+
 }  // namespace
+
+DivideStats DijkstraSplitter::Stats() {
+  return {g_fast_divides.load(), g_exact_divides.load()};
+}
 
 template <bool kVertical>
 void DijkstraSplitter::Divide(const float* image, float* output, size_t lo,
                               size_t hi) const {
-  const size_t n_u = kVertical ? height_ : width_;  // path length axis
   if (width_ >= 65535 || height_ >= 65535)
     throw std::runtime_error("DijkstraSplitter: image side of 65535 pixels or more");
+  static const bool exact_only = [] {
+    const char* e = std::getenv("RDL_SPLIT_EXACT");
+    return e && e[0] == '1';
+  }();
+  if (!exact_only && DivideByKeyOrder<kVertical>(image, output, width_, height_, lo, hi)) {
+    ++g_fast_divides;
+    return;
+  }
+  ++g_exact_divides;
+  DivideExact<kVertical>(image, output, lo, hi);
+}
+
+template <bool kVertical>
+void DijkstraSplitter::DivideExact(const float* image, float* output, size_t lo,
+                                   size_t hi) const {
+  const size_t n_u = kVertical ? height_ : width_;  // path length axis
   const size_t band = hi - lo;
   auto pixel = [&](size_t u, size_t v) -> size_t {
     return kVertical ? u * width_ + v : v * width_ + u;

@@ -9,9 +9,18 @@
 
 namespace radler::math {
 
+/// Divider searches so far (process-wide): settled by the key-order search
+/// with a unique minimum path, or run through the reference's heap order.
+struct DivideStats {
+  unsigned long long key_order, exact;
+};
+
 class DijkstraSplitter {
  public:
   DijkstraSplitter(size_t width, size_t height) : width_(width), height_(height) {}
+
+  /// Process-wide counts of the two divider searches (see Divide).
+  static DivideStats Stats();
 
   /// Shortest top-to-bottom path of sum |image| inside columns [x1, x2);
   /// output (a width x height plane) gets 1 on the path, 0 elsewhere in the
@@ -43,8 +52,14 @@ class DijkstraSplitter {
                        size_t& subheight) const;
 
  private:
+  /// Divider search: the key-order search (a radix heap) when its path is
+  /// provably the reference's (no tie decides it), else DivideExact.
+  /// RDL_SPLIT_EXACT=1 always runs DivideExact.
   template <bool kVertical>
   void Divide(const float* image, float* output, size_t lo, size_t hi) const;
+  /// The reference's search with its binary heap's exact pop order.
+  template <bool kVertical>
+  void DivideExact(const float* image, float* output, size_t lo, size_t hi) const;
 
   size_t width_, height_;
 };

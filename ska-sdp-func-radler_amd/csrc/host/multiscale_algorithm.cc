@@ -424,7 +424,10 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
   spectrum_ = std::make_shared<gpu::Buffer>(session, spectrum_bytes);
   spectrum_work_ = std::make_shared<gpu::Buffer>(session, spectrum_bytes);
   spectrum_work2_.reset();
-  if (ScaleLanes() > 1 && data_image.Size() == 1 &&
+  // the second lane only on a main session: a subimage pool's workers
+  // already keep up to 16 streams busy, and a lane pair per worker adds
+  // a spectrum buffer and fork/join events to every small subimage
+  if (ScaleLanes() > 1 && !session.IsWorker() && data_image.Size() == 1 &&
       data_image.Integration(false).copy_fast_path)
     spectrum_work2_ = std::make_shared<gpu::Buffer>(session, spectrum_bytes);
 

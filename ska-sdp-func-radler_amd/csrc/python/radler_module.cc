@@ -473,6 +473,10 @@ void InitTiling(py::module& m) {
     if (image.ndim() != 2) throw std::runtime_error("image must be 2-D");
     return radler::math::DijkstraSplitter(image.shape(1), image.shape(0));
   };
+  t.def("divide_stats", [] {
+    const radler::math::DivideStats st = radler::math::DijkstraSplitter::Stats();
+    return py::make_tuple(st.key_order, st.exact);
+  }, "(key-order searches, exact heap-order searches) run by this process");
   t.def("divide_vertically", [splitter](const F32& image, F32& output, size_t x1,
                                         size_t x2) {
     splitter(image).DivideVertically(image.data(), output.mutable_data(), x1, x2);

@@ -18,7 +18,7 @@ from synthetic import problem
 PIXEL_SCALE = 1.0 / 3600.0 * np.pi / 180.0
 
 GEOMETRY_CASES = [(256, 256, 3, 2, 1), (200, 160, 2, 2, 2), (301, 257, 4, 3, 3),
-                  (128, 512, 2, 4, 4), (512, 512, 8, 8, 5)]
+                  (128, 512, 2, 4, 4), (512, 512, 8, 8, 5), (2048, 1536, 4, 3, 6)]
 
 
 @pytest.mark.parametrize("w,h,gw,gh,seed", GEOMETRY_CASES)
@@ -44,6 +44,40 @@ def test_splitter_flat_image_is_deterministic():
     img = np.ones((96, 128), np.float32)
     assert all(np.array_equal(a, b) for a, b in
                zip(rd.tiling.make_subimages(img, 3, 3), make_subimages(get_oracle(), img, 3, 3)))
+
+
+def _divide_counts():
+    return np.array(rd.tiling.divide_stats(), np.int64)
+
+
+@pytest.mark.parametrize("kind", ["noise", "quantized", "zeros", "nan"])
+def test_splitter_key_order_search_matches_oracle(kind):
+    """The dividers come from the key-order search (radix heap) when no tie
+    decides the path, else from the reference's heap order; either way the
+    geometry is the oracle's (whose search is the reference's heap). Noisy
+    images take the key-order search; tie-heavy ones fall back."""
+    rng = np.random.default_rng(11)
+    _, img = problem(768, 640, 60, 6, seed=12)
+    if kind == "quantized":  # few distinct values: equal path costs everywhere
+        img = np.round(img / (np.abs(img).max() * 0.05)).astype(np.float32)
+    elif kind == "zeros":
+        img = img.copy()
+        img[:, ::3] = 0.0
+        img[100:300] = 0.0
+    elif kind == "nan":
+        img = img.copy()
+        img[rng.integers(0, 640, 50), rng.integers(0, 768, 50)] = np.nan
+    before = _divide_counts()
+    boxes, labels = rd.tiling.make_subimages(img, 4, 3)
+    used = _divide_counts() - before
+    assert used.sum() == (4 - 1) + (3 - 1)
+    boxes_o, labels_o = make_subimages(get_oracle(), img, 4, 3)
+    assert np.array_equal(boxes, boxes_o)
+    assert np.array_equal(labels, labels_o)
+    if kind in ("noise", "nan"):
+        assert used[0] == used.sum()  # no tie on any divider
+    if kind == "quantized":
+        assert used[1] > 0
 
 
 def _settings(kind, w, thr, max_iter, mgain, gw, gh, threads):
