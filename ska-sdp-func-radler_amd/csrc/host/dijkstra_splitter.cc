@@ -6,6 +6,7 @@
 #include <cmath>
 #include <cstdint>
 #include <limits>
+#include <memory>
 #include <queue>
 #include <cstdlib>
 #include <stdexcept>
@@ -155,68 +156,66 @@ bool DivideByKeyOrder(const float* image, float* output, size_t width, size_t he
     return kVertical ? u * width + v : v * width + u;
   };
   const float unset = std::numeric_limits<float>::max();
-  std::vector<float> weight(band * n_u), dist(band * n_u, unset), key_of(band * n_u);
-  std::vector<uint32_t> back(band * n_u);
+  // key_of and back are written when a pixel settles, before any read
+  std::unique_ptr<float[]> weight(new float[band * n_u]), key_of(new float[band * n_u]);
+  std::unique_ptr<uint32_t[]> back(new uint32_t[band * n_u]);
+  std::vector<float> dist(band * n_u, unset);
   std::vector<uint8_t> tied(band * n_u, 0);
   for (size_t u = 0; u != n_u; ++u)
     for (size_t v = lo; v != hi; ++v) weight[u * band + (v - lo)] = std::fabs(image[pixel(u, v)]);
-  // payload: the target (u << vbits | v - lo) << 3 | the step from its
-  // predecessor (kStep*), 32 bits (else the exact search runs)
+  // The queue holds settled pixels, keyed by their cost: popping one at key
+  // k pops, in the reference's terms, its (up to five) entries of key k;
+  // every entry of a smaller key has been popped, so a target still
+  // unsettled settles at k, and a settled one reached at its own settling
+  // key is a tie. Payload: the pixel as u << vbits | v - lo.
   unsigned vbits = 1, ubits = 1;
   while ((size_t(1) << vbits) < band) ++vbits;
   while ((size_t(1) << ubits) <= n_u) ++ubits;
-  if (ubits + vbits + 3 > 32) return false;
+  if (ubits + vbits > 32) return false;
   const uint32_t vmask = (1u << vbits) - 1;
-  constexpr int kStepU[6] = {1, 0, 1, 1, 0, 0};  // target - predecessor
-  constexpr int kStepV[6] = {-1, -1, 0, 1, 1, 0};  // step 5: a start pixel
   RadixQueue open;
-  auto push = [&](uint32_t key, uint32_t u, uint32_t v, unsigned step) {
+  // settle (u, v) from (pu, pv) at key k, or mark the tie
+  auto reach = [&](uint32_t k, uint32_t u, uint32_t v, uint32_t pu, uint32_t pv) {
     const size_t at = size_t(u) * band + (v - lo);
-    if (u != n_u && dist[at] != unset) {  // settled: its entry would be dropped
-      if (KeyBits(key_of[at]) == key) tied[at] = 1;
+    if (dist[at] != unset) {
+      if (KeyBits(key_of[at]) == k) tied[at] = 1;
       return;
     }
-    open.Push((uint64_t(key) << 32) | (((u << vbits) | (v - uint32_t(lo))) << 3) | step);
+    const float cost = KeyFloat(k) + weight[at];
+    if (!(cost < unset)) return;  // NaN / inf: never settles (as there)
+    dist[at] = cost;
+    key_of[at] = KeyFloat(k);
+    back[at] = (pu << 16) | pv;
+    open.Push((uint64_t(KeyBits(cost)) << 32) | (u << vbits) | (v - uint32_t(lo)));
   };
-  for (size_t v = lo; v != hi; ++v) push(0u, 0, uint32_t(v), 5);
+  for (size_t v = lo; v != hi; ++v) reach(0u, 0, uint32_t(v), 0, uint32_t(v));
   uint32_t end_key = 0, end_pu = 0, end_pv = 0;
   bool ended = false;
   while (!open.Empty()) {
     const uint64_t top = open.Pop();
-    const uint32_t key = uint32_t(top >> 32);
-    if (ended && key != end_key) break;  // drained the final key
-    const unsigned step = unsigned(top & 7);
-    const uint32_t cu = uint32_t(top) >> (3 + vbits);
-    const uint32_t cv = ((uint32_t(top) >> 3) & vmask) + uint32_t(lo);
-    const size_t at = size_t(cu) * band + (cv - lo);
-    const uint32_t pu = cu - kStepU[step], pv = cv - kStepV[step];
-    if (cu == n_u) {
+    const uint32_t k = uint32_t(top >> 32);
+    if (ended && k != end_key) break;  // drained the final key
+    const uint32_t cu = uint32_t(top) >> vbits, cv = (uint32_t(top) & vmask) + uint32_t(lo);
+    const uint32_t u1 = cu + 1;
+    if (u1 == n_u) {  // its entries past the last row end the search
       if (!ended) {
         ended = true;
-        end_key = key;
-        end_pu = pu;
-        end_pv = pv;
+        end_key = k;
+        end_pu = cu;
+        end_pv = cv;
       }
+      if (cv > lo) reach(k, cu, cv - 1, cu, cv);
+      if (cv + 1u < hi) reach(k, cu, cv + 1, cu, cv);
       continue;
     }
-    if (dist[at] != unset) {
-      if (KeyBits(key_of[at]) == key) tied[at] = 1;
-      continue;
-    }
-    const float cost = KeyFloat(key) + weight[at];
-    if (!(cost < unset)) continue;  // NaN / inf: never settles (as there)
-    dist[at] = cost;
-    key_of[at] = KeyFloat(key);
-    back[at] = (pu << 16) | pv;
-    const uint32_t c = KeyBits(cost), u1 = cu + 1;
     if (cv > lo) {
-      push(c, u1, cv - 1, 0);
-      push(c, cu, cv - 1, 1);
+      reach(k, u1, cv - 1, cu, cv);
+      reach(k, cu, cv - 1, cu, cv);
     }
-    push(c, u1, cv, 2);
+    reach(k, u1, cv, cu, cv);
     if (cv + 1u < hi) {
-      push(c, u1, cv + 1, 3);
-      push(c, cu, cv + 1, 4);
+      reach(k, u1, cv + 1, cu, cv);
+      reach(k, cu, cv + 1, cu, cv);
     }
   }
   if (!ended) return false;
