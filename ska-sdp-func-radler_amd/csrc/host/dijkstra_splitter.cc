@@ -10,6 +10,7 @@
 #include <queue>
 #include <cstdlib>
 #include <stdexcept>
+#include <thread>
 
 namespace radler::math {
 
@@ -149,7 +150,7 @@ std::atomic<uint64_t> g_fast_divides{0}, g_exact_divides{0};
 // equal keys. Returns false (output untouched) otherwise.
 template <bool kVertical>
 bool DivideByKeyOrder(const float* image, float* output, size_t width, size_t height,
-                      size_t lo, size_t hi) {
+                      size_t lo, size_t hi, std::atomic<int>* race) {
   const size_t n_u = kVertical ? height : width;
   const size_t band = hi - lo;
   auto pixel = [&](size_t u, size_t v) -> size_t {
@@ -229,6 +230,10 @@ bool DivideByKeyOrder(const float* image, float* output, size_t width, size_t he
     pu = back[at] >> 16;
     pv = back[at] & 0xffffu;
   }
+  // racing the exact search: the first to claim the band writes it (the
+  // two dividers are then identical)
+  int running = 0;
+  if (race && !race->compare_exchange_strong(running, 1)) return true;
   for (size_t u = 0; u != n_u; ++u)
     for (size_t v = lo; v != hi; ++v) output[pixel(u, v)] = 0.0f;
   uint32_t pu = end_pu, pv = end_pv;
@@ -257,17 +262,51 @@ void DijkstraSplitter::Divide(const float* image, float* output, size_t lo,
     const char* e = std::getenv("RDL_SPLIT_EXACT");
     return e && e[0] == '1';
   }();
-  if (!exact_only && DivideByKeyOrder<kVertical>(image, output, width_, height_, lo, hi)) {
-    ++g_fast_divides;
+  static const bool race_on = [] {
+    const char* e = std::getenv("RDL_SPLIT_RACE");
+    return !(e && e[0] == '0');
+  }();
+  if (exact_only) {
+    ++g_exact_divides;
+    DivideExact<kVertical>(image, output, lo, hi, nullptr);
     return;
   }
-  ++g_exact_divides;
-  DivideExact<kVertical>(image, output, lo, hi);
+  if (!race_on) {
+    if (DivideByKeyOrder<kVertical>(image, output, width_, height_, lo, hi, nullptr)) {
+      ++g_fast_divides;
+      return;
+    }
+    ++g_exact_divides;
+    DivideExact<kVertical>(image, output, lo, hi, nullptr);
+    return;
+  }
+  // Race: the exact search runs on its own thread from the start; a
+  // key-order result (about a fifth of its time) cancels it, else it
+  // finishes. The divider costs max(key order, exact) at worst instead of
+  // their sum.
+  std::atomic<int> race{0};  // 0 running, 1 key order wrote, 2 exact wrote
+  std::exception_ptr exact_error;
+  std::thread exact([&] {
+    try {
+      DivideExact<kVertical>(image, output, lo, hi, &race);
+    } catch (...) {
+      exact_error = std::current_exception();
+    }
+  });
+  bool fast = false;
+  try {
+    fast = DivideByKeyOrder<kVertical>(image, output, width_, height_, lo, hi, &race);
+  } catch (...) {
+    fast = false;  // the exact search still decides
+  }
+  exact.join();
+  if (!fast && exact_error) std::rethrow_exception(exact_error);
+  ++(fast ? g_fast_divides : g_exact_divides);
 }
 
 template <bool kVertical>
 void DijkstraSplitter::DivideExact(const float* image, float* output, size_t lo,
-                                   size_t hi) const {
+                                   size_t hi, std::atomic<int>* race) const {
   const size_t n_u = kVertical ? height_ : width_;  // path length axis
   const size_t band = hi - lo;
   auto pixel = [&](size_t u, size_t v) -> size_t {
@@ -286,7 +325,11 @@ void DijkstraSplitter::DivideExact(const float* image, float* output, size_t lo,
   // predecessor of each settled pixel (pu << 16 | pv), band-local layout
   std::vector<uint32_t> back(band * n_u);
   uint32_t end_pu = 0, end_pv = 0;
-  while (!open.Empty()) {
+  for (uint32_t poll = 0; !open.Empty();) {
+    if (race && ++poll == 0x10000u) {  // cancelled by a key-order result
+      poll = 0;
+      if (race->load(std::memory_order_relaxed) == 1) return;
+    }
     const float top_cost = open.TopCost();
     const uint64_t top = open.TopLoad();
     open.Pop();
@@ -310,6 +353,8 @@ void DijkstraSplitter::DivideExact(const float* image, float* output, size_t lo,
       open.Push(cost, Load(cu, cv + 1, cu, cv));
     }
   }
+  int running = 0;
+  if (race && !race->compare_exchange_strong(running, 2)) return;
   for (size_t u = 0; u != n_u; ++u)
     for (size_t v = lo; v != hi; ++v) output[pixel(u, v)] = 0.0f;
   uint32_t pu = end_pu, pv = end_pv;

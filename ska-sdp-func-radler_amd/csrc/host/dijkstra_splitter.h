@@ -4,6 +4,7 @@
 // data-parallel); the image comes from the device once per major iteration.
 #pragma once
 
+#include <atomic>
 #include <cstddef>
 #include <vector>
 
@@ -53,13 +54,17 @@ class DijkstraSplitter {
 
  private:
   /// Divider search: the key-order search (a radix heap) when its path is
-  /// provably the reference's (no tie decides it), else DivideExact.
+  /// provably the reference's (no tie decides it), else DivideExact; the two
+  /// race on two threads (RDL_SPLIT_RACE=0: one after the other).
   /// RDL_SPLIT_EXACT=1 always runs DivideExact.
   template <bool kVertical>
   void Divide(const float* image, float* output, size_t lo, size_t hi) const;
-  /// The reference's search with its binary heap's exact pop order.
+  /// The reference's search with its binary heap's exact pop order. With
+  /// `race`, it returns without writing once a key-order result claimed the
+  /// band (race == 1), and claims it (race = 2) before writing.
   template <bool kVertical>
-  void DivideExact(const float* image, float* output, size_t lo, size_t hi) const;
+  void DivideExact(const float* image, float* output, size_t lo, size_t hi,
+                   std::atomic<int>* race) const;
 
   size_t width_, height_;
 };
