@@ -19,6 +19,13 @@ Workloads (--workload):
           SURVEY.md C5) shared by the ranks: find-peak pass, one RCCL
           allreduce(max) of the start peak, owner broadcasts of the subimage
           results (strong scaling; N > 1 default, 8192^2 8 x 8)
+  joined  the C3 image set (8 channels x 4096^2); at N > 1 split into
+          subimages shared by the ranks like `tiled`
+
+At N = 1 the line also carries: tiled_n1 / joined_n1 (the split workloads
+and the unsplit C3 run on this GPU), c2_to_threshold, and cpu_baseline with a
+live to-threshold run of a smaller problem on the CPU and the GPU
+(`--to-threshold-live`, default t2k: 2048^2).
 
 Multi-GPU: one process per GPU. `--gpus N` without a launcher re-launches
 itself under torch.distributed.run (before anything touches the GPU); under a
@@ -232,20 +239,19 @@ def cpu_baseline(psf, dirty, max_scales, threshold, threads, outer_all, outer_si
                           f"({runs[1]['components']} components)" if len(runs) > 1 else ""))}
 
 
-def cpu_to_threshold(out_path, threads):
+def cpu_to_threshold(name, threads):
     """The CPU baseline to the threshold (north_star's wall-clock-to-threshold
-    beside the CPU): the oracle's MultiScale major iteration on the C2
-    configuration (tests/config_problems.py: 4096^2, 6 scales, 1000 points +
-    100 blobs, threshold 5 sigma, no component cap), setup (scale-convolved
-    PSFs, first peak search) included and also reported alone. Runs on the
-    host only (no GPU call) and writes one JSON object to `out_path`; bench.py
-    reads the committed copy (profiles/r*_cpu_c2_to_threshold.json) into the
-    line beside the GPU's live run of the same problem (`c2_to_threshold`)."""
+    beside the CPU): the oracle's MultiScale major iteration on the
+    configuration `name` of tests/config_problems.py (c2: 4096^2, 1000 points
+    + 100 blobs; t2k: 2048^2, 250 points + 25 blobs; 6 scales, threshold
+    5 sigma, no component cap), setup (scale-convolved PSFs, first peak
+    search) included and also reported alone. Host only (no GPU call); a
+    heartbeat on stderr covers the silent native call."""
     import threading
     import config_problems as cp
     from oracle_lib import OracleAlgorithm, get_oracle
-    psfs, dirty = cp.problem("c2")
-    c = cp.CONFIGS["c2"]
+    psfs, dirty = cp.problem(name)
+    c = cp.CONFIGS[name]
     orc = get_oracle()
     orc.set_threads(threads)
     res, mod = dirty.copy(), np.zeros_like(dirty)
@@ -258,7 +264,7 @@ def cpu_to_threshold(out_path, threads):
     def heartbeat():
         t = time.perf_counter()
         while not done.wait(30.0):
-            print(f"[cpu_to_threshold] running {time.perf_counter() - t:.0f} s",
+            print(f"[cpu_to_threshold] {name}: running {time.perf_counter() - t:.0f} s",
                   file=sys.stderr, flush=True)
 
     hb = threading.Thread(target=heartbeat, daemon=True)
@@ -272,25 +278,44 @@ def cpu_to_threshold(out_path, threads):
     total = time.perf_counter() - t0
     setup = alg.setup_seconds()
     n = int(r.iteration_number)
-    out = {"workload": "c2: multiscale 4096x4096, 6 scales, 1000 points + 100 blobs, "
-                       "threshold 5 sigma (tests/config_problems.py)",
-           "kind": "port", "threads": threads, "cpu_model": cpu_model(),
-           "affinity_cores": affinity_cores(),
-           "wall_clock_to_threshold_s": round(total, 2), "setup_s": round(setup, 2),
-           "clean_s": round(total - setup, 2), "components": n,
-           "final_peak": float(r.final_peak),
-           "stop": "the multiscale loop's threshold countdown (multiscale_algorithm.cc:"
-                   "323-328, 378-384): it ends max(8, 1.5 x scales) sub-minor loops after "
-                   "the sub-loop threshold reaches the final threshold; final_peak is the "
-                   "last selected scale's peak, as the reference reports it",
-           "components_per_s_with_setup": round(n / total, 2),
-           "components_per_s_after_setup": round(n / max(total - setup, 1e-9), 2),
-           "note": "oracle MultiScale (C++ restatement of the reference, std::thread, "
-                   "float64 FFT; the reference uses FFTW float), one major iteration "
-                   "(major_loop_gain 1) to the threshold"}
-    with open(out_path, "w") as f:
-        json.dump(out, f, indent=1)
-    print(json.dumps(out), flush=True)
+    size = c["size"]
+    return {"workload": (f"{name}: multiscale {size}x{size}, {c['max_scales']} scales, "
+                         f"{c['points']} points + {c['blobs']} blobs, threshold 5 sigma "
+                         f"(tests/config_problems.py)"),
+            "kind": "port", "threads": threads, "cpu_model": cpu_model(),
+            "affinity_cores": affinity_cores(),
+            "wall_clock_to_threshold_s": round(total, 3), "setup_s": round(setup, 3),
+            "clean_s": round(total - setup, 3), "components": n,
+            "final_peak": float(r.final_peak),
+            "stop": "the multiscale loop's threshold countdown (multiscale_algorithm.cc:"
+                    "323-328, 378-384): it ends max(8, 1.5 x scales) sub-minor loops after "
+                    "the sub-loop threshold reaches the final threshold; final_peak is the "
+                    "last selected scale's peak, as the reference reports it",
+            "components_per_s_with_setup": round(n / total, 2),
+            "components_per_s_after_setup": round(n / max(total - setup, 1e-9), 2),
+            "note": "oracle MultiScale (C++ restatement of the reference, std::thread, "
+                    "float64 FFT; the reference uses FFTW float), one major iteration "
+                    "(major_loop_gain 1) to the threshold"}
+
+
+def gpu_to_threshold(rd, name):
+    """The same problem to the threshold through Radler.perform on this GPU
+    (accessor load + major iteration + store; warm-up + one timed run).
+    Returns (components, seconds)."""
+    import config_problems as cp
+    c = cp.CONFIGS[name]
+    psfs, dirty = cp.problem(name)
+    st = settings_for(rd, c["size"], 10 ** 9, c["max_scales"], c["threshold"], 1, 1)
+
+    def once():
+        arrays = (psfs[0], dirty[0].copy(), np.zeros_like(dirty[0]))
+        r = rd.Radler(st, *arrays, cp.BEAM_PX * cp.PIXEL_SCALE)
+        t = time.perf_counter()
+        r.perform(0)
+        return rd.gpu.total_iteration_number(r), time.perf_counter() - t
+
+    once()
+    return once()
 
 
 def with_amdahl(rd, once):
@@ -369,7 +394,8 @@ def main():
     ap.add_argument("--tiled-reference", type=int, default=1,
                     help="N = 1 fields: also time the tiled N > 1 workload on this GPU")
     ap.add_argument("--joined-reference", type=int, default=1,
-                    help="N = 1: also time the joined-channel workload split by subimage")
+                    help="N = 1: also time the joined-channel workload, unsplit (the C3 "
+                         "computation) and split by subimage (the N > 1 partitioning)")
     ap.add_argument("--device-resident", type=int, default=1,
                     help="also time the HBM-resident major iteration (0 = skip)")
     ap.add_argument("--cpu-outer", type=int, default=2,
@@ -386,6 +412,10 @@ def main():
                     help="N = 1 fields: also time Radler.perform to the threshold on the C2 "
                          "configuration (4096^2), the workload of the committed CPU "
                          "to-threshold run")
+    ap.add_argument("--to-threshold-live", default="t2k",
+                    help="N = 1 fields: a tests/config_problems.py problem run to the "
+                         "threshold by the GPU and by the CPU oracle in this job "
+                         "(cpu_baseline.to_threshold; 'none' = skip)")
     ap.add_argument("--cpu-to-threshold", metavar="OUT_JSON",
                     help="host only: run the CPU oracle to the threshold on C2 (setup "
                          "included), write the JSON and exit")
@@ -396,7 +426,10 @@ def main():
     args = ap.parse_args()
 
     if args.cpu_to_threshold:
-        cpu_to_threshold(args.cpu_to_threshold, args.cpu_threads or cpu_share())
+        out = cpu_to_threshold("c2", args.cpu_threads or cpu_share())
+        with open(args.cpu_to_threshold, "w") as f:
+            json.dump(out, f, indent=1)
+        print(json.dumps(out), flush=True)
         return
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(relaunch(args))
@@ -514,14 +547,21 @@ def main():
                       frequencies=np.array([[f, f] for f in jfreqs], np.float64),
                       weights=np.ones(jch, np.float64))
 
-        def joined_once():
+        def joined_once(settings=sj):
             arrays = (j_psf, j_dirty.copy(), np.zeros_like(j_dirty))
-            r = rd.Radler(sj, *arrays, BEAM_PX * PIXEL_SCALE, **jextra)
+            r = rd.Radler(settings, *arrays, BEAM_PX * PIXEL_SCALE, **jextra)
             t = time.perf_counter()
             r.perform(0)
             return rd.gpu.total_iteration_number(r), time.perf_counter() - t
 
-        print("[bench] joined reference (warm-up + 1 step) ...", file=sys.stderr, flush=True)
+        # unsplit: the C3 computation itself (one image set, one GPU)
+        su = settings_for(rd, jsize, args.max_iter, args.scales, threshold, 1, 1)
+        print("[bench] joined reference, unsplit (warm-up + 1 step) ...", file=sys.stderr,
+              flush=True)
+        joined_once(su)
+        u_comps, u_el = joined_once(su)
+        print("[bench] joined reference, split (warm-up + 1 step) ...", file=sys.stderr,
+              flush=True)
         joined_once()
         (j_comps, j_el), j_amdahl = with_amdahl(rd, joined_once)
         joined_ref = {"workload": (f"joined{jch}ch-multiscale-{jsize}x{jsize}-{args.scales}"
@@ -530,35 +570,39 @@ def main():
                       "wall_clock_to_threshold_s": round(j_el, 4),
                       "components_per_step": j_comps, "pool": args.pool,
                       "amdahl": j_amdahl,
-                      "note": "`--workload joined --gpus N` at N = 1 (the channels' image set "
-                              "split by subimage, one GPU)"}
+                      "unsplit": {"workload": (f"joined{jch}ch-multiscale-{jsize}x{jsize}-"
+                                               f"{args.scales}scales"),
+                                  "value": round(u_comps / u_el, 2),
+                                  "wall_clock_to_threshold_s": round(u_el, 4),
+                                  "components_per_step": u_comps,
+                                  "note": "SURVEY.md C3 as one image set on one GPU: the "
+                                          "joined N = 1 point of the C3 computation"},
+                      "note": "`--workload joined --gpus N` at N = 1: the channels' image set "
+                              "split into grid x grid subimages (the partitioning N > 1 "
+                              "shares over ranks, DESIGN.md §6), a different problem from "
+                              "the unsplit C3 run in `unsplit`"}
         del j_psf, j_dirty
 
     # C2 (4096^2) to the threshold on this GPU: the same problem as the
     # committed CPU to-threshold run (wall clock against wall clock)
     c2_ref = None
     if args.c2_reference and world == 1 and workload == "fields":
-        import config_problems as cp
-        c2 = cp.CONFIGS["c2"]
-        c2_psf, c2_dirty = cp.problem("c2")
-        sc = settings_for(rd, c2["size"], 10 ** 9, c2["max_scales"], c2["threshold"], 1, 1)
-
-        def c2_once():
-            arrays = (c2_psf[0], c2_dirty[0].copy(), np.zeros_like(c2_dirty[0]))
-            r = rd.Radler(sc, *arrays, cp.BEAM_PX * cp.PIXEL_SCALE)
-            t = time.perf_counter()
-            r.perform(0)
-            return rd.gpu.total_iteration_number(r), time.perf_counter() - t
-
         print("[bench] C2 4096^2 to threshold (warm-up + 1 step) ...", file=sys.stderr,
               flush=True)
-        c2_once()
-        c_comps, c_el = c2_once()
+        c_comps, c_el = gpu_to_threshold(rd, "c2")
         c2_ref = {"workload": "c2: multiscale 4096x4096, 6 scales (tests/config_problems.py)",
                   "wall_clock_to_threshold_s": round(c_el, 4), "components": c_comps,
                   "value": round(c_comps / c_el, 2),
                   "step": "Radler.perform (accessor load + major iteration + store)"}
-        del c2_psf, c2_dirty
+
+    # the live CPU-vs-GPU to-threshold problem, GPU side (the CPU side runs
+    # after the timed region, with cpu_baseline)
+    live_tt = None
+    if (args.to_threshold_live != "none" and args.cpu_outer > 0 and world == 1
+            and workload == "fields"):
+        print(f"[bench] {args.to_threshold_live} to threshold on the GPU (warm-up + 1) ...",
+              file=sys.stderr, flush=True)
+        live_tt = gpu_to_threshold(rd, args.to_threshold_live)
 
     # Per-launch HIP events cost time (in the gridded runs, with 16 streams of
     # small kernels, 15-35 % of a step), so every family is timed on the last
@@ -713,14 +757,31 @@ def main():
             "threads = OMP_NUM_THREADS, the job's CPU share on the pool's one-GPU boxes "
             "(16); the affinity mask lists all of the machine's cores, which other jobs "
             "share, so they are not used")
-        tt = committed_cpu_to_threshold()
-        if tt is not None:
-            if c2_ref is not None:
-                tt["gpu_wall_clock_to_threshold_s"] = c2_ref["wall_clock_to_threshold_s"]
-                tt["gpu_components"] = c2_ref["components"]
-                tt["speedup_wall_clock"] = round(
-                    tt["wall_clock_to_threshold_s"] / c2_ref["wall_clock_to_threshold_s"], 1)
+        if live_tt is not None:
+            # measured live, in this job: the oracle on the same problem and
+            # threads as above, to the threshold, against the GPU's run of it
+            print(f"[cpu_baseline] {args.to_threshold_live} to threshold on {threads} "
+                  f"threads ...", file=sys.stderr, flush=True)
+            tt = cpu_to_threshold(args.to_threshold_live, threads)
+            g_comps, g_el = live_tt
+            tt.update({"measured": "live, this job",
+                       "gpu_wall_clock_to_threshold_s": round(g_el, 4),
+                       "gpu_components": g_comps,
+                       "gpu_components_per_s": round(g_comps / g_el, 2),
+                       "speedup_wall_clock": round(tt["wall_clock_to_threshold_s"] / g_el, 1),
+                       "speedup_wall_clock_after_cpu_setup": round(tt["clean_s"] / g_el, 1)})
             cpu["to_threshold"] = tt
+        ref = committed_cpu_to_threshold()
+        if ref is not None:
+            # the larger C2 (4096^2) CPU run, committed from an earlier job on
+            # the same kind of box; the GPU side is this job's c2_to_threshold
+            if c2_ref is not None:
+                ref["gpu_wall_clock_to_threshold_s"] = c2_ref["wall_clock_to_threshold_s"]
+                ref["gpu_components"] = c2_ref["components"]
+                ref["speedup_wall_clock"] = round(
+                    ref["wall_clock_to_threshold_s"] / c2_ref["wall_clock_to_threshold_s"], 1)
+            ref["measured"] = "committed file (not this job)"
+            cpu["to_threshold_c2_committed"] = ref
 
     grid = f"-tiled{args.grid}x{args.grid}" if split else ""
     chans = f"joined{args.channels}ch-" if joined else ""
@@ -748,7 +809,12 @@ def main():
                    "channels": args.channels if joined else 1,
                    "fields_per_gpu": 0 if split else 1,
                    "parallelism": (f"subimages{args.grid * args.grid}/ranks{world}"
-                                   f"/pool{args.pool}" if split else f"fields{world}")},
+                                   f"/pool{args.pool}" if split else f"fields{world}"),
+                   **({"problem": ("the joined image set split into grid x grid subimages "
+                                   "shared by the ranks (ParallelDeconvolution over the "
+                                   "channels' set): at N > 1 this solves the tiled problem, "
+                                   "not the unsplit C3 run (joined_n1.unsplit of the N = 1 "
+                                   "line)")} if joined and split else {})},
         "device_resident": resident,
         "tiled_n1": tiled_ref,
         "joined_n1": joined_ref,

@@ -1437,7 +1437,7 @@ int MakeTwiddleBase(uint32_t base, void** out) {
   };
   for (uint32_t i = 0; i < base / ff::kTwdLo; ++i) put(uint64_t(i) * ff::kTwdLo);
   for (uint32_t i = 0; i < ff::kTwdLo; ++i) put(i);
-  RDL_HIP_CHECK(hipMalloc(out, host.size() * sizeof(double)));
+  RDL_HIP_CHECK(rdl::DevMalloc(out, host.size() * sizeof(double)));
   RDL_HIP_CHECK(hipMemcpy(*out, host.data(), host.size() * sizeof(double),
                           hipMemcpyHostToDevice));
   return RDL_OK;
@@ -1492,7 +1492,7 @@ int MakePassTable(uint32_t n, const RadixList& radix, bool f64, void** out) {
       std::memcpy(&host[i * 8], v, 8);
     }
   }
-  RDL_HIP_CHECK(hipMalloc(out, host.size()));
+  RDL_HIP_CHECK(rdl::DevMalloc(out, host.size()));
   RDL_HIP_CHECK(hipMemcpy(*out, host.data(), host.size(), hipMemcpyHostToDevice));
   return RDL_OK;
 }

@@ -232,7 +232,7 @@ static int CreateFft(rdl_session* s, uint32_t width, uint32_t height, bool f64,
   RDL_FFT_CHECK(rocfft_plan_get_work_buffer_size(f->fwd, &w1));
   RDL_FFT_CHECK(rocfft_plan_get_work_buffer_size(f->inv, &w2));
   f->work_bytes = std::max(w1, w2);
-  if (f->work_bytes) RDL_HIP_CHECK(hipMalloc(&f->work, f->work_bytes));
+  if (f->work_bytes) RDL_HIP_CHECK(rdl::DevMalloc(&f->work, f->work_bytes));
   RDL_FFT_CHECK(rocfft_execution_info_create(&f->info_fwd));
   RDL_FFT_CHECK(rocfft_execution_info_create(&f->info_inv));
   RDL_FFT_CHECK(rocfft_execution_info_set_stream(f->info_fwd, s->stream));
@@ -277,7 +277,7 @@ int rdl_fft_destroy(rdl_fft* f) {
   if (f->inv) rocfft_plan_destroy(f->inv);
   if (f->info_fwd) rocfft_execution_info_destroy(f->info_fwd);
   if (f->info_inv) rocfft_execution_info_destroy(f->info_inv);
-  if (f->work) (void)hipFree(f->work);
+  if (f->work) (void)rdl::DevFree(f->work);
   delete f;
   return RDL_OK;
 }

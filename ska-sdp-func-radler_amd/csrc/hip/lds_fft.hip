@@ -556,7 +556,7 @@ int MakePlan(rdl_conv* c, uint32_t n, bool f64, rdl::LdsPlan* plan, void** tw) {
       std::memcpy(&host[k * esz], v, 8);
     }
   }
-  RDL_HIP_CHECK(hipMalloc(tw, host.size()));
+  RDL_HIP_CHECK(rdl::DevMalloc(tw, host.size()));
   RDL_HIP_CHECK(hipMemcpy(*tw, host.data(), host.size(), hipMemcpyHostToDevice));
   plan->tw = *tw;
   (void)c;
@@ -568,7 +568,7 @@ int MakePlan(rdl_conv* c, uint32_t n, bool f64, rdl::LdsPlan* plan, void** tw) {
 int CompactRowsFor(rdl_conv* c, const uint8_t* row_mask, bool reuse) {
   if (reuse && c->rows_list_mask == row_mask) return RDL_OK;
   if (!c->rows_list)
-    RDL_HIP_CHECK(hipMalloc(&c->rows_list, (size_t(c->height) + 1) * sizeof(uint32_t)));
+    RDL_HIP_CHECK(rdl::DevMalloc(&c->rows_list, (size_t(c->height) + 1) * sizeof(uint32_t)));
   RDL_TRY(rdl::FastCompactRows(c->s, row_mask, c->height, c->rows_list,
                                c->rows_list + c->height));
   c->rows_list_mask = row_mask;
@@ -782,11 +782,11 @@ int EnsureSplitScratch(rdl_conv* c, size_t bytes) {
   if (c->scratch) {
     RDL_HIP_CHECK(hipStreamSynchronize(c->s->home));
     if (c->s->aux) RDL_HIP_CHECK(hipStreamSynchronize(c->s->aux));
-    RDL_HIP_CHECK(hipFree(c->scratch));
+    RDL_HIP_CHECK(rdl::DevFree(c->scratch));
     c->scratch = c->scratch_lane[l] = nullptr;
     c->scratch_bytes[l] = 0;
   }
-  RDL_HIP_CHECK(hipMalloc(&c->scratch, bytes));
+  RDL_HIP_CHECK(rdl::DevMalloc(&c->scratch, bytes));
   c->scratch_lane[l] = c->scratch;
   c->scratch_bytes[l] = bytes;
   return RDL_OK;
@@ -937,15 +937,15 @@ int rdl_conv_create_ex(rdl_session* s, uint32_t width, uint32_t height, int f64,
 int rdl_conv_destroy(rdl_conv* c) {
   if (!c) return RDL_OK;
   (void)hipStreamSynchronize(c->s->stream);
-  if (c->tw_row) (void)hipFree(c->tw_row);
-  if (c->tw_col) (void)hipFree(c->tw_col);
-  if (c->tw_n1) (void)hipFree(c->tw_n1);
-  if (c->tw_n2) (void)hipFree(c->tw_n2);
+  if (c->tw_row) (void)rdl::DevFree(c->tw_row);
+  if (c->tw_col) (void)rdl::DevFree(c->tw_col);
+  if (c->tw_n1) (void)rdl::DevFree(c->tw_n1);
+  if (c->tw_n2) (void)rdl::DevFree(c->tw_n2);
   for (void* p : c->scratch_lane)
-    if (p) (void)hipFree(p);
-  if (c->rows_list) (void)hipFree(c->rows_list);
+    if (p) (void)rdl::DevFree(p);
+  if (c->rows_list) (void)rdl::DevFree(c->rows_list);
   for (void* p : {c->ptw_row, c->ptw_col, c->ptw_a, c->ptw_b, c->twd_row})
-    if (p) (void)hipFree(p);
+    if (p) (void)rdl::DevFree(p);
   delete c;
   return RDL_OK;
 }

@@ -56,6 +56,34 @@ struct Scratch {
   size_t bytes = 0;
 };
 
+// Live-block registry for the RDL_SEGV_REPORT crash report: every device
+// block (hipMalloc) and pinned host block (hipHostMalloc) this library holds,
+// in a fixed lock-free table the signal handler can read (session.hip).
+// kind: 'd' device, 'h' pinned host.
+void TrackBlock(const void* p, size_t bytes, char kind);
+void UntrackBlock(const void* p);
+
+template <typename T>
+hipError_t DevMalloc(T** p, size_t bytes) {
+  const hipError_t e = hipMalloc(reinterpret_cast<void**>(p), bytes);
+  if (e == hipSuccess) TrackBlock(*p, bytes, 'd');
+  return e;
+}
+inline hipError_t DevFree(void* p) {
+  UntrackBlock(p);
+  return hipFree(p);
+}
+template <typename T>
+hipError_t HostMalloc(T** p, size_t bytes) {
+  const hipError_t e = hipHostMalloc(reinterpret_cast<void**>(p), bytes, hipHostMallocDefault);
+  if (e == hipSuccess) TrackBlock(*p, bytes, 'h');
+  return e;
+}
+inline hipError_t HostFree(void* p) {
+  UntrackBlock(p);
+  return hipHostFree(p);
+}
+
 }  // namespace rdl
 
 struct rdl_session {

@@ -25,9 +25,26 @@ std::map<std::string, TimingEntry> g_retired;
 
 // Diagnostics for crashes outside our code (RDL_SEGV_REPORT=<file>): the
 // signal, the faulting pc with the module holding it (dladdr), a native
-// backtrace, and the process's module map (/proc/self/maps), appended to
-// <file>; then the default action runs (the process dies as it would have).
+// backtrace, every live block of this library (device and pinned host, with
+// the block holding or nearest to the fault address), and the process's whole
+// module map (/proc/self/maps), appended to <file>; then the default action
+// runs (the process dies as it would have). Only async-signal-safe calls
+// after the first line (open/write/read/close; the integer formatting is our
+// own); dladdr and backtrace are warmed up when the handler is installed.
 char g_segv_path[512] = {0};
+
+// Live-block registry: open addressing over a fixed table, one CAS per
+// insert, a relaxed store per removal; readers (the handler) take whatever is
+// there. Full table: the block is simply not listed.
+constexpr size_t kBlockSlots = 8192;
+struct BlockSlot {
+  std::atomic<uintptr_t> base{0};
+  std::atomic<size_t> bytes{0};
+  std::atomic<char> kind{0};
+};
+BlockSlot g_blocks[kBlockSlots];
+
+size_t SlotOf(uintptr_t p) { return size_t((p >> 12) * 0x9E3779B97F4A7C15ull >> 51) % kBlockSlots; }
 
 void WriteAll(int fd, const char* p, size_t n) {
   while (n > 0) {
@@ -37,26 +54,117 @@ void WriteAll(int fd, const char* p, size_t n) {
     n -= size_t(w);
   }
 }
+void WriteStr(int fd, const char* p) { WriteAll(fd, p, strlen(p)); }
+void WriteHex(int fd, uintptr_t v) {
+  char b[19] = "0x";
+  int n = 2;
+  for (int sh = 60; sh >= 0; sh -= 4) {
+    const unsigned d = unsigned(v >> sh) & 15u;
+    if (n > 2 || d || sh == 0) b[n++] = char(d < 10 ? '0' + d : 'a' + d - 10);
+  }
+  WriteAll(fd, b, size_t(n));
+}
+void WriteDec(int fd, uint64_t v) {
+  char b[21];
+  int n = 20;
+  b[n] = 0;
+  do {
+    b[--n] = char('0' + v % 10);
+    v /= 10;
+  } while (v);
+  WriteAll(fd, b + n, size_t(20 - n));
+}
+
+void WriteBlocks(int fd, uintptr_t fault) {
+  WriteStr(fd, "--- live blocks of librdl_hip (kind base bytes end)\n");
+  uintptr_t best_base = 0, best_end = 0;
+  uintptr_t best_dist = ~uintptr_t(0);
+  char best_kind = 0;
+  uint64_t n = 0, dev = 0, host = 0;
+  for (size_t i = 0; i != kBlockSlots; ++i) {
+    const uintptr_t b = g_blocks[i].base.load(std::memory_order_relaxed);
+    if (!b) continue;
+    const size_t bytes = g_blocks[i].bytes.load(std::memory_order_relaxed);
+    const char k = g_blocks[i].kind.load(std::memory_order_relaxed);
+    const uintptr_t e = b + bytes;
+    ++n;
+    (k == 'h' ? host : dev) += bytes;
+    char kb[3] = {k ? k : '?', ' ', 0};
+    WriteStr(fd, kb);
+    WriteHex(fd, b);
+    WriteStr(fd, " ");
+    WriteDec(fd, bytes);
+    WriteStr(fd, " ");
+    WriteHex(fd, e);
+    WriteStr(fd, "\n");
+    const uintptr_t d = fault < b ? b - fault : fault >= e ? fault - e + 1 : 0;
+    if (d < best_dist) {
+      best_dist = d;
+      best_base = b;
+      best_end = e;
+      best_kind = k;
+    }
+  }
+  WriteStr(fd, "blocks ");
+  WriteDec(fd, n);
+  WriteStr(fd, ", device bytes ");
+  WriteDec(fd, dev);
+  WriteStr(fd, ", pinned host bytes ");
+  WriteDec(fd, host);
+  WriteStr(fd, "\nfault address ");
+  WriteHex(fd, fault);
+  if (best_dist == ~uintptr_t(0)) {
+    WriteStr(fd, ": no live block\n");
+    return;
+  }
+  WriteStr(fd, best_dist == 0 ? ": INSIDE " : ": nearest ");
+  char kb[2] = {best_kind ? best_kind : '?', 0};
+  WriteStr(fd, kb);
+  WriteStr(fd, " block ");
+  WriteHex(fd, best_base);
+  WriteStr(fd, "..");
+  WriteHex(fd, best_end);
+  if (best_dist) {
+    WriteStr(fd, " at distance ");
+    WriteDec(fd, best_dist);
+  }
+  WriteStr(fd, "\n");
+}
 
 void SegvReport(int sig, siginfo_t* info, void* ctx) {
   const int fd = open(g_segv_path, O_WRONLY | O_CREAT | O_APPEND, 0644);
   if (fd >= 0) {
+    void* pc = nullptr;
+#if defined(__x86_64__)
     const ucontext_t* uc = static_cast<const ucontext_t*>(ctx);
-    void* pc = reinterpret_cast<void*>(uc->uc_mcontext.gregs[REG_RIP]);
+    pc = reinterpret_cast<void*>(uc->uc_mcontext.gregs[REG_RIP]);
+#else
+    (void)ctx;
+#endif
     Dl_info d{};
-    const bool known = dladdr(pc, &d) != 0;
-    char buf[1024];
-    const int n = snprintf(
-        buf, sizeof buf, "signal %d (code %d) address %p pc %p module %s +0x%lx symbol %s\n",
-        sig, info->si_code, info->si_addr, pc, known && d.dli_fname ? d.dli_fname : "?",
-        known && d.dli_fbase ? (unsigned long)((char*)pc - (char*)d.dli_fbase) : 0ul,
-        known && d.dli_sname ? d.dli_sname : "?");
-    WriteAll(fd, buf, size_t(std::max(n, 0)));
+    const bool known = pc && dladdr(pc, &d) != 0;
+    WriteStr(fd, "signal ");
+    WriteDec(fd, uint64_t(sig));
+    WriteStr(fd, " (code ");
+    WriteDec(fd, uint64_t(uint32_t(info->si_code)));
+    WriteStr(fd, ") address ");
+    WriteHex(fd, reinterpret_cast<uintptr_t>(info->si_addr));
+    WriteStr(fd, " pc ");
+    WriteHex(fd, reinterpret_cast<uintptr_t>(pc));
+    WriteStr(fd, " module ");
+    WriteStr(fd, known && d.dli_fname ? d.dli_fname : "?");
+    WriteStr(fd, " +");
+    WriteHex(fd, known && d.dli_fbase ? uintptr_t((char*)pc - (char*)d.dli_fbase) : 0);
+    WriteStr(fd, " symbol ");
+    WriteStr(fd, known && d.dli_sname ? d.dli_sname : "?");
+    WriteStr(fd, "\n");
     void* frames[64];
     backtrace_symbols_fd(frames, backtrace(frames, 64), fd);
-    WriteAll(fd, "--- /proc/self/maps\n", 20);
+    WriteBlocks(fd, reinterpret_cast<uintptr_t>(info->si_addr));
+    WriteStr(fd, "--- /proc/self/maps\n");
     const int maps = open("/proc/self/maps", O_RDONLY);
     if (maps >= 0) {
+      char buf[4096];
       ssize_t r;
       while ((r = read(maps, buf, sizeof buf)) > 0) WriteAll(fd, buf, size_t(r));
       close(maps);
@@ -71,6 +179,11 @@ void InstallSegvReport() {
   const char* path = std::getenv("RDL_SEGV_REPORT");
   if (!path || !path[0]) return;
   snprintf(g_segv_path, sizeof g_segv_path, "%s", path);
+  // load libgcc's unwinder and resolve dladdr now, not inside the handler
+  void* frames[4];
+  (void)backtrace(frames, 4);
+  Dl_info d{};
+  (void)dladdr(reinterpret_cast<void*>(&InstallSegvReport), &d);
   struct sigaction sa {};
   sa.sa_sigaction = SegvReport;
   sa.sa_flags = SA_SIGINFO | SA_RESETHAND;
@@ -93,6 +206,32 @@ void Fold(std::map<std::string, TimingEntry>& into,
 std::atomic<bool> g_timing_all{false};
 char g_timing_family[64] = {0};
 void SetError(const std::string& msg) { g_last_error = msg; }
+
+void TrackBlock(const void* p, size_t bytes, char kind) {
+  const uintptr_t b = reinterpret_cast<uintptr_t>(p);
+  if (!b) return;
+  for (size_t i = 0, k = SlotOf(b); i != kBlockSlots; ++i, k = (k + 1) % kBlockSlots) {
+    uintptr_t empty = 0;
+    if (g_blocks[k].base.load(std::memory_order_relaxed) == 0 &&
+        g_blocks[k].base.compare_exchange_strong(empty, b, std::memory_order_relaxed)) {
+      g_blocks[k].bytes.store(bytes, std::memory_order_relaxed);
+      g_blocks[k].kind.store(kind, std::memory_order_relaxed);
+      return;
+    }
+  }
+}
+
+void UntrackBlock(const void* p) {
+  const uintptr_t b = reinterpret_cast<uintptr_t>(p);
+  if (!b) return;
+  for (size_t i = 0, k = SlotOf(b); i != kBlockSlots; ++i, k = (k + 1) % kBlockSlots)
+    if (g_blocks[k].base.load(std::memory_order_relaxed) == b) {
+      g_blocks[k].bytes.store(0, std::memory_order_relaxed);
+      g_blocks[k].kind.store(0, std::memory_order_relaxed);
+      g_blocks[k].base.store(0, std::memory_order_relaxed);
+      return;
+    }
+}
 }  // namespace rdl
 
 hipEvent_t rdl_session::GetEvent() {
@@ -145,11 +284,11 @@ int rdl_session::EnsureScratch(rdl::Scratch& s, size_t bytes) {
   if (s.ptr) {
     RDL_HIP_CHECK(hipStreamSynchronize(home));
     if (aux) RDL_HIP_CHECK(hipStreamSynchronize(aux));
-    RDL_HIP_CHECK(hipFree(s.ptr));
+    RDL_HIP_CHECK(rdl::DevFree(s.ptr));
     s.ptr = nullptr;
     s.bytes = 0;
   }
-  RDL_HIP_CHECK(hipMalloc(&s.ptr, bytes));
+  RDL_HIP_CHECK(rdl::DevMalloc(&s.ptr, bytes));
   s.bytes = bytes;
   if (poison) RDL_HIP_CHECK(hipMemsetAsync(s.ptr, 0xff, bytes, stream));
   return RDL_OK;
@@ -157,14 +296,23 @@ int rdl_session::EnsureScratch(rdl::Scratch& s, size_t bytes) {
 
 namespace rdl {
 int FlushDeviceCaches(int device) {
-  std::vector<rdl_session*> same;
-  {
-    const std::lock_guard<std::mutex> lock(g_registry_mutex);
-    for (rdl_session* o : g_sessions)
-      if (o->device == device) same.push_back(o);
+  // Under the registry lock (rdl_session_destroy takes it before deleting a
+  // session, so no session listed here can go away meanwhile): take every
+  // cached block of the device's sessions, wait for the whole device once
+  // (no other session's streams are touched: one may be forking its second
+  // lane concurrently), then free them. The caller has made `device` current.
+  std::vector<void*> blocks;
+  const std::lock_guard<std::mutex> lock(g_registry_mutex);
+  for (rdl_session* o : g_sessions) {
+    if (o->device != device) continue;
+    const std::lock_guard<std::mutex> clock(o->cache_mutex);
+    for (auto& [bytes, p] : o->cache_free) blocks.push_back(p);
+    o->cache_free.clear();
+    o->cache_bytes = 0;
   }
-  // sessions are only destroyed by their owners, never while they allocate
-  for (rdl_session* o : same) RDL_TRY(o->FlushCache());
+  if (blocks.empty()) return RDL_OK;
+  RDL_HIP_CHECK(hipDeviceSynchronize());
+  for (void* p : blocks) RDL_HIP_CHECK(rdl::DevFree(p));
   return RDL_OK;
 }
 }  // namespace rdl
@@ -212,8 +360,8 @@ int rdl_session_create(int device, rdl_session** out) {
   const char* cache = std::getenv("RDL_ALLOC_CACHE");
   s->cache_on = !(cache && cache[0] == '0');
   s->trace_subminor_phases = trace && trace[0] == '1';  // 2: timing only
-  RDL_HIP_CHECK(hipMalloc(&s->d_small, 1 << 16));
-  RDL_HIP_CHECK(hipHostMalloc(&s->h_small, 1 << 16, hipHostMallocDefault));
+  RDL_HIP_CHECK(rdl::DevMalloc(&s->d_small, 1 << 16));
+  RDL_HIP_CHECK(rdl::HostMalloc(&s->h_small, 1 << 16));
   {
     const std::lock_guard<std::mutex> lock(rdl::g_registry_mutex);
     rdl::g_sessions.push_back(s.get());
@@ -232,7 +380,7 @@ int rdl_session::FlushCache() {
   if (blocks.empty()) return RDL_OK;
   RDL_HIP_CHECK(hipStreamSynchronize(home));
   if (aux) RDL_HIP_CHECK(hipStreamSynchronize(aux));
-  for (auto& [bytes, p] : blocks) RDL_HIP_CHECK(hipFree(p));
+  for (auto& [bytes, p] : blocks) RDL_HIP_CHECK(rdl::DevFree(p));
   return RDL_OK;
 }
 
@@ -257,13 +405,13 @@ int rdl_session_destroy(rdl_session* s) {
       (void)hipEventDestroy(b);
     }
   for (hipEvent_t e : s->event_pool) (void)hipEventDestroy(e);
-  if (s->partials.ptr) (void)hipFree(s->partials.ptr);
-  if (s->radix.ptr) (void)hipFree(s->radix.ptr);
-  if (s->kernel.ptr) (void)hipFree(s->kernel.ptr);
-  if (s->loop_state.ptr) (void)hipFree(s->loop_state.ptr);
-  if (s->iuwt.ptr) (void)hipFree(s->iuwt.ptr);
-  if (s->d_small) (void)hipFree(s->d_small);
-  if (s->h_small) (void)hipHostFree(s->h_small);
+  if (s->partials.ptr) (void)rdl::DevFree(s->partials.ptr);
+  if (s->radix.ptr) (void)rdl::DevFree(s->radix.ptr);
+  if (s->kernel.ptr) (void)rdl::DevFree(s->kernel.ptr);
+  if (s->loop_state.ptr) (void)rdl::DevFree(s->loop_state.ptr);
+  if (s->iuwt.ptr) (void)rdl::DevFree(s->iuwt.ptr);
+  if (s->d_small) (void)rdl::DevFree(s->d_small);
+  if (s->h_small) (void)rdl::HostFree(s->h_small);
   if (s->comm) rdl_comm_destroy(s);
   if (s->aux) (void)hipStreamDestroy(s->aux);
   if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);
@@ -345,13 +493,13 @@ int rdl_malloc(rdl_session* s, size_t bytes, void** d_out) {
     int prev = 0;
     RDL_HIP_CHECK(hipGetDevice(&prev));
     if (prev != s->device) RDL_HIP_CHECK(hipSetDevice(s->device));
-    hipError_t e = hipMalloc(d_out, bytes);
+    hipError_t e = rdl::DevMalloc(d_out, bytes);
     if (e == hipErrorOutOfMemory) {
       // give back every cached block on this device (the main session's and
       // every worker's: a pool's sessions live for the process), then retry
       (void)hipGetLastError();
       RDL_TRY(rdl::FlushDeviceCaches(s->device));
-      e = hipMalloc(d_out, bytes);
+      e = rdl::DevMalloc(d_out, bytes);
     }
     if (prev != s->device) (void)hipSetDevice(prev);
     RDL_HIP_CHECK(e);
@@ -388,7 +536,7 @@ int rdl_free(rdl_session* s, void* d_ptr) {
     }
   }
   RDL_HIP_CHECK(hipStreamSynchronize(s->stream));
-  RDL_HIP_CHECK(hipFree(d_ptr));
+  RDL_HIP_CHECK(rdl::DevFree(d_ptr));
   return RDL_OK;
 }
 
@@ -415,12 +563,12 @@ int rdl_memcpy_d2h(rdl_session* s, void* h_dst, const void* d_src,
 int rdl_host_alloc(size_t bytes, void** h_out) {
   RDL_ARG_CHECK(h_out, "NULL argument");
   *h_out = nullptr;
-  RDL_HIP_CHECK(hipHostMalloc(h_out, std::max<size_t>(bytes, 64), hipHostMallocDefault));
+  RDL_HIP_CHECK(rdl::HostMalloc(h_out, std::max<size_t>(bytes, 64)));
   return RDL_OK;
 }
 
 int rdl_host_free(void* h_ptr) {
-  if (h_ptr) RDL_HIP_CHECK(hipHostFree(h_ptr));
+  if (h_ptr) RDL_HIP_CHECK(rdl::HostFree(h_ptr));
   return RDL_OK;
 }
 

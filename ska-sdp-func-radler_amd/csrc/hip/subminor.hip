@@ -549,6 +549,13 @@ struct LoopArgs {
   const float* table;     // pairwise PSF table (BuildPairTable) or nullptr
   rdl_logpoly lp;         // log-polynomial fit (has_lp; SubminorLoop only)
   int32_t has_lp;
+  // table loops on a grid: launched blocks per participant (the participants
+  // are blocks 0, S, 2S, ...: S = 8 puts them on one XCD under round-robin
+  // dispatch; a pooled session whose share of the GPU is below 8 blocks per
+  // participant launches S = 1), and 1 to exchange through agent-scope
+  // stores even when every participant is on one XCD (RDL_SUBMINOR_EXCHANGE=agent)
+  uint32_t part_stride;
+  int32_t agent_exchange;
 };
 
 struct LoopResult {
@@ -1700,7 +1707,18 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopReg(LoopArgs a) {
 //
 // Same operations in the same order, same argmax order and tie rules as the
 // generic kernels: traces and model values are identical.
-constexpr uint32_t kTabParticipantStride = 8;  // blocks per participant
+constexpr uint32_t kTabParticipantStride = 8;  // blocks per participant (LoopArgs::part_stride)
+
+// The "fast" exchange below publishes records with workgroup-scope stores
+// that the other participants poll with agent-scope (L1-bypassing) loads:
+// visible to them only because gfx950's vector L1 is write-through, so every
+// store reaches the XCD's L2 the participants share (checked at run time:
+// all participants on one XCC). A target whose L1 could hold such stores
+// needs the agent-scope form, which RDL_SUBMINOR_EXCHANGE=agent selects (and
+// tests/test_gpu_kernels.py compares with the fast one).
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "subminor.hip: the workgroup-scope exchange relies on gfx950's write-through vector L1"
+#endif
 
 __device__ __forceinline__ uint32_t XccId() {
   // HW_REG_XCC_ID (hwreg 20), bits [3:0]
@@ -1714,8 +1732,8 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTab(LoopArgs a) {
   // {key hi, key lo, value bits, -}, parity double-buffered
   __shared__ uint4 slots[2][WAVES];
   const uint32_t G = a.n_blocks;
-  if (G > 1 && blockIdx.x % kTabParticipantStride != 0u) return;
-  const uint32_t rank = G > 1 ? blockIdx.x / kTabParticipantStride : 0u;
+  if (G > 1 && blockIdx.x % a.part_stride != 0u) return;
+  const uint32_t rank = G > 1 ? blockIdx.x / a.part_stride : 0u;
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const uint32_t n = uint32_t(a.n_sel), per = a.per_block;
   const uint32_t base = rank * per;
@@ -1753,7 +1771,7 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTab(LoopArgs a) {
       failed = spins > (uint64_t(1) << 24);
     }
     const uint32_t x0 = uint32_t(__builtin_amdgcn_readlane(int(xcc), 0));
-    fast = __all(lane >= G || xcc == x0);
+    fast = __all(lane >= G || xcc == x0) && !a.agent_exchange;
   }
   const float* table = a.table;
   float c = 0.0f, m = 0.0f, start_abs = 0.0f, flux = 0.0f;
@@ -2057,8 +2075,8 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTabN(LoopArgs a) {
   __shared__ uint4 slots[2][WAVES];     // {key hi, key lo, integrated bits, -}
   __shared__ float slotv[2][WAVES][NI];  // the wave winner's image values
   const uint32_t G = a.n_blocks;
-  if (G > 1 && blockIdx.x % kTabParticipantStride != 0u) return;
-  const uint32_t rank = G > 1 ? blockIdx.x / kTabParticipantStride : 0u;
+  if (G > 1 && blockIdx.x % a.part_stride != 0u) return;
+  const uint32_t rank = G > 1 ? blockIdx.x / a.part_stride : 0u;
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const uint32_t n = uint32_t(a.n_sel), per = a.per_block;
   const uint32_t base = rank * per;
@@ -2103,7 +2121,7 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTabN(LoopArgs a) {
       failed = spins > (uint64_t(1) << 24);
     }
     const uint32_t x0 = uint32_t(__builtin_amdgcn_readlane(int(xcc), 0));
-    fast = __all(lane >= G || xcc == x0);
+    fast = __all(lane >= G || xcc == x0) && !a.agent_exchange;
   }
   const size_t sq = size_t(n) * n;
   float c[NI];
@@ -2382,7 +2400,7 @@ int LaunchTabN(const LoopArgs& a, uint32_t items, hipStream_t stream) {
   if (a.n_blocks > 1) {
     void* args[] = {const_cast<LoopArgs*>(&a)};
     RDL_HIP_CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k),
-                                             dim3(a.n_blocks * kTabParticipantStride),
+                                             dim3(a.n_blocks * a.part_stride),
                                              dim3(256), args, 0, stream));
   } else {
     k<<<1, 256, 0, stream>>>(a);
@@ -2407,7 +2425,7 @@ int LaunchTab(const LoopArgs& a, uint32_t items, hipStream_t stream) {
   if (a.n_blocks > 1) {
     void* args[] = {const_cast<LoopArgs*>(&a)};
     RDL_HIP_CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k),
-                                             dim3(a.n_blocks * kTabParticipantStride),
+                                             dim3(a.n_blocks * a.part_stride),
                                              dim3(THREADS), args, 0, stream));
   } else {
     k<<<1, THREADS, 0, stream>>>(a);
@@ -2504,11 +2522,11 @@ int Grow(void** p, size_t* have, size_t need, hipStream_t stream) {
   if (*have >= need) return RDL_OK;
   if (*p) {
     RDL_HIP_CHECK(hipStreamSynchronize(stream));
-    RDL_HIP_CHECK(hipFree(*p));
+    RDL_HIP_CHECK(rdl::DevFree(*p));
     *p = nullptr;
     *have = 0;
   }
-  RDL_HIP_CHECK(hipMalloc(p, need));
+  RDL_HIP_CHECK(rdl::DevMalloc(p, need));
   *have = need;
   return RDL_OK;
 }
@@ -2577,13 +2595,13 @@ int rdl_subminor_create(rdl_session* s, rdl_subminor** out) {
 int rdl_subminor_destroy(rdl_subminor* h) {
   if (!h) return RDL_OK;
   (void)hipStreamSynchronize(h->s->stream);
-  if (h->counts) (void)hipFree(h->counts);
-  if (h->sel) (void)hipFree(h->sel);
-  if (h->pos_buf) (void)hipFree(h->pos_buf);
-  if (h->local_buf) (void)hipFree(h->local_buf);
-  if (h->stamp_mark) (void)hipFree(h->stamp_mark);
-  if (h->sync) (void)hipFree(h->sync);
-  if (h->table) (void)hipFree(h->table);
+  if (h->counts) (void)rdl::DevFree(h->counts);
+  if (h->sel) (void)rdl::DevFree(h->sel);
+  if (h->pos_buf) (void)rdl::DevFree(h->pos_buf);
+  if (h->local_buf) (void)rdl::DevFree(h->local_buf);
+  if (h->stamp_mark) (void)rdl::DevFree(h->stamp_mark);
+  if (h->sync) (void)rdl::DevFree(h->sync);
+  if (h->table) (void)rdl::DevFree(h->table);
   delete h;
   return RDL_OK;
 }
@@ -2936,6 +2954,17 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   la.stop_on_negative = p->stop_on_negative;
   la.use_lds = use_lds ? 1 : 0;
   la.prof = s->trace_subminor_phases ? 1 : 0;
+  // a pooled session (coop_limit: its share of the CUs) launches only as
+  // many blocks as its share; the participants then spread over XCDs and
+  // exchange through agent-scope stores (the kernel sees the XCC ids)
+  la.part_stride = rdl::kTabParticipantStride;
+  if ((use_tab || use_tabn) && g > 1 && s->coop_limit &&
+      uint64_t(g) * rdl::kTabParticipantStride > s->coop_limit)
+    la.part_stride = 1;
+  {
+    const char* e = std::getenv("RDL_SUBMINOR_EXCHANGE");  // read per run (tests toggle it)
+    la.agent_exchange = e && std::strcmp(e, "agent") == 0 ? 1 : 0;
+  }
   const uint64_t n_trace = (h_trace && trace_cap) ? trace_cap : 0;
   const size_t rec_bytes =
       use_tab    ? (size_t(7) * g * sizeof(uint64_t) + 15) / 16 * 16

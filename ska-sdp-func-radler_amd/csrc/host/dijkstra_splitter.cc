@@ -10,6 +10,7 @@
 #include <queue>
 #include <cstdlib>
 #include <stdexcept>
+#include <system_error>
 #include <thread>
 
 namespace radler::math {
@@ -286,13 +287,25 @@ void DijkstraSplitter::Divide(const float* image, float* output, size_t lo,
   // their sum.
   std::atomic<int> race{0};  // 0 running, 1 key order wrote, 2 exact wrote
   std::exception_ptr exact_error;
-  std::thread exact([&] {
-    try {
-      DivideExact<kVertical>(image, output, lo, hi, &race);
-    } catch (...) {
-      exact_error = std::current_exception();
+  std::thread exact;
+  try {
+    exact = std::thread([&] {
+      try {
+        DivideExact<kVertical>(image, output, lo, hi, &race);
+      } catch (...) {
+        exact_error = std::current_exception();
+      }
+    });
+  } catch (const std::system_error&) {
+    // no thread to be had: the two searches in turn
+    if (DivideByKeyOrder<kVertical>(image, output, width_, height_, lo, hi, nullptr)) {
+      ++g_fast_divides;
+      return;
     }
-  });
+    ++g_exact_divides;
+    DivideExact<kVertical>(image, output, lo, hi, nullptr);
+    return;
+  }
   bool fast = false;
   try {
     fast = DivideByKeyOrder<kVertical>(image, output, width_, height_, lo, hi, &race);
@@ -300,8 +313,14 @@ void DijkstraSplitter::Divide(const float* image, float* output, size_t lo,
     fast = false;  // the exact search still decides
   }
   exact.join();
-  if (!fast && exact_error) std::rethrow_exception(exact_error);
-  ++(fast ? g_fast_divides : g_exact_divides);
+  // the search that claimed the band wrote it (DivideByKeyOrder also returns
+  // true when it lost the claim to an exact result)
+  const int writer = race.load();
+  if (writer != 1 && exact_error) std::rethrow_exception(exact_error);
+  if (writer == 0)
+    throw std::logic_error("DijkstraSplitter: neither divider search wrote the band");
+  ++(writer == 1 ? g_fast_divides : g_exact_divides);
+  (void)fast;
 }
 
 template <bool kVertical>
@@ -326,7 +345,7 @@ void DijkstraSplitter::DivideExact(const float* image, float* output, size_t lo,
   std::vector<uint32_t> back(band * n_u);
   uint32_t end_pu = 0, end_pv = 0;
   for (uint32_t poll = 0; !open.Empty();) {
-    if (race && ++poll == 0x10000u) {  // cancelled by a key-order result
+    if (race && ++poll == 0x1000u) {  // cancelled by a key-order result
       poll = 0;
       if (race->load(std::memory_order_relaxed) == 1) return;
     }

@@ -9,6 +9,8 @@ container clean bit-identical images.
     C3  joined-channel multiscale, 8 channels x 4096^2
     C4  IUWT, 4096^2
     C5  parallel-deconvolution tiling, 16384^2 multiscale, 8x8 subimages
+    H8K the bench's headline workload: multiscale 8192^2, 6 scales, 2000
+        points + 200 blobs (bench.make_problem(8192, SEED, 2000, 200))
 """
 import hashlib
 
@@ -64,18 +66,30 @@ def joined_channels(size, n_points, n_blobs, seed=SEED, frequencies=C3_FREQUENCI
 # model are stored as the image checkpoint: it stops before the first
 # decision the float32-vs-float64 rounding could flip on the GPU (the full
 # trace's first divergence, tests/test_configs_gpu.py), so the images are
-# comparable pixel for pixel.
+# comparable pixel for pixel. C2 / C3 sit just below the GPU's measured first
+# divergence (7 259 / 17 026 components, round 3); "near_tie" = the fixture's
+# first oracle near-tie, which the GPU must reach identically in any case.
 CONFIGS = {
     "c1": dict(kind="hogbom", size=1024, points=200, blobs=20, threshold=0.0,
                max_iterations=1000),
     "c2": dict(kind="multiscale", size=4096, points=1000, blobs=100, threshold=5 * NOISE,
                max_scales=6, cap=20000, image_cap=7000),
     "c3": dict(kind="joined", size=4096, points=1000, blobs=100, threshold=5 * NOISE,
-               max_scales=6, cap=20000, image_cap=5000),
+               max_scales=6, cap=20000, image_cap=17000),
     "c4": dict(kind="iuwt", size=4096, points=1000, blobs=100, threshold=5 * NOISE,
                cap=24),
     "c5": dict(kind="tiled", size=16384, points=2000, blobs=200, threshold=5 * NOISE,
-               max_scales=6, grid=8, cap=200),
+               max_scales=6, grid=8, cap=2000),
+    # bench.py's headline (BASELINE metric) workload, capped: the trace up to
+    # and past the first near-tie, the image checkpoint AT the first near-tie
+    # (make_config_golden.py: image_cap "near_tie")
+    "h8k": dict(kind="multiscale", size=8192, points=2000, blobs=200, threshold=5 * NOISE,
+                max_scales=6, cap=16000, image_cap="near_tie"),
+    # bench.py's live CPU-vs-GPU wall-clock-to-threshold leg: C2's sky density
+    # on 2048^2, small enough for the CPU oracle to reach the threshold inside
+    # the default bench run (no fixture: both sides run it in the same job)
+    "t2k": dict(kind="multiscale", size=2048, points=250, blobs=25, threshold=5 * NOISE,
+                max_scales=6),
 }
 
 

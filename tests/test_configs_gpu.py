@@ -41,8 +41,12 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 # way (the oracle's margins put C2's one observed divergence at 1.55e-7)
 RTOL = 1e-6
 # residual / model agreement (x max|dirty|) when the traces are identical:
-# FFT rounding of the residual corrections and scale-convolved PSFs
-IMG_TOL = 2e-5
+# FFT rounding of the residual corrections and scale-convolved PSFs. Round 3
+# measured at most 2.6e-8 x max|dirty| (C2 checkpoint; C3 1.5e-8, C5 1.1e-8),
+# so 1e-6 leaves ~40x headroom and still catches a 1e-5-sized regression
+IMG_TOL = 1e-6
+# IUWT (C4): measured 1.6e-7 x max|dirty| after 24 steps (round 3)
+IUWT_IMG_TOL = 1e-5
 
 
 def fixture(name):
@@ -194,7 +198,35 @@ def _multiscale(name):
 @pytest.mark.gpu
 def test_c2_multiscale_4096_trace():
     c = _multiscale("c2")
-    assert c.matched >= 7000
+    # the fixture's image checkpoint sits below the GPU's measured first
+    # divergence (round 3: 7 259), so the trace must reach it identically
+    assert c.matched >= int(fixture("c2")["ck_iterations"])
+
+
+@pytest.mark.gpu
+def test_h8k_headline_multiscale_8192_trace():
+    """bench.py's headline workload (the BASELINE metric's 8192^2 multiscale
+    sky: bench.make_problem(8192, SEED, 2000, 200), 6 scales, 5 sigma, the
+    bench's Settings) capped at the fixture's 16 000 components: the trace
+    tie-aware against the oracle past its first near-tie, and the residual /
+    model at the checkpoint placed at that first near-tie."""
+    c = _multiscale("h8k")
+    assert c.matched >= int(fixture("h8k")["ck_iterations"])
+
+
+def test_h8k_inputs_are_the_bench_inputs():
+    """The h8k problem is bench.py's generator with bench.py's seed and sky
+    (checked at a small size on the CPU; at 8192^2 the fixture's SHA-256
+    pins the regenerated inputs before the GPU test runs)."""
+    import bench
+    c = cp.CONFIGS["h8k"]
+    assert (c["size"], c["points"], c["blobs"], c["max_scales"]) == (8192, 2000, 200, 6)
+    assert (cp.SEED, cp.NOISE, cp.BEAM_PX, cp.PIXEL_SCALE) == (
+        bench.SEED, bench.NOISE, bench.BEAM_PX, bench.PIXEL_SCALE)
+    assert c["threshold"] == 5.0 * bench.NOISE
+    psf_b, dirty_b = bench.make_problem(256, bench.SEED, 40, 4)
+    psf_c, dirty_c = cp.single_field(256, 40, 4)
+    assert np.array_equal(psf_b, psf_c) and np.array_equal(dirty_b, dirty_c)
 
 
 @pytest.mark.gpu
@@ -260,7 +292,7 @@ def test_c4_iuwt_4096_steps():
         assert (bool(g[0]), g[1], g[2], g[3], g[4], g[5], g[6]) == (
             bool(o["succeeded"]), o["scale"], o["x"], o["y"], o["end_scale"],
             o["min_scale"], o["area"]), (g, o)
-    tol = 1e-4 * float(fx["dirty_absmax"])
+    tol = IUWT_IMG_TOL * float(fx["dirty_absmax"])
     check_samples(fx, run.residual().reshape(dirty.shape),
                   run.model().reshape(dirty.shape), tol)
 

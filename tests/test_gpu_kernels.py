@@ -550,6 +550,30 @@ def test_subminor_table_kernel_bit_exact(sess, orc, n_target, per_participant, n
     workgroup and on grids of 2..22 participants: the threshold is set so
     that about n_target pixels are selected; trace and model values bit-exact
     against the oracle's sub-minor loop (GenericClean's Clark path)."""
+    _table_kernel_case(sess, orc, n_target, per_participant, neg, quantum)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("exchange,sharing", [("agent", 0), (None, 16), ("agent", 16)])
+@pytest.mark.parametrize("quantum", [0, 2.0 ** -12])
+def test_subminor_table_grid_exchange_forms(sess, orc, exchange, sharing, quantum, monkeypatch):
+    """The grid table loop's participant exchange in its other forms, against
+    the oracle like the default (fast: workgroup-scope stores, every
+    participant on one XCD): agent-scope stores (RDL_SUBMINOR_EXCHANGE=agent),
+    and a pooled session's share of the GPU (rdl_session_set_concurrency 16:
+    16 blocks for ~10 participants, so one launched block per participant,
+    spread over the XCDs, which makes the kernel pick agent-scope stores)."""
+    if exchange:
+        monkeypatch.setenv("RDL_SUBMINOR_EXCHANGE", exchange)
+    if sharing:
+        sess.rdl.rdl_session_set_concurrency(sess.h, sharing)
+    try:
+        _table_kernel_case(sess, orc, 5000, 512, 1, quantum)
+    finally:
+        sess.rdl.rdl_session_set_concurrency(sess.h, 1)
+
+
+def _table_kernel_case(sess, orc, n_target, per_participant, neg, quantum):
     w = h = 512
     psf, dirty = synthetic(w, h, 200, 7)
     if quantum:
