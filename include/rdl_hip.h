@@ -592,6 +592,35 @@ int rdl_conv_columns_layout(rdl_conv* c, const void* d_in, void* d_out,
 #define RDL_CONV_FAST_TILED 4
 int rdl_conv_fast(const rdl_conv* c);
 
+/* Several scale convolutions of ONE float plane (FindActiveScaleConvolvedMaxima
+ * -> ThreadedDeconvolutionTools::FindMultiScalePeak, which convolves the same
+ * integrated image with every active scale's kernel: multiscale_algorithm.cc:
+ * 578-634, threaded_deconvolution_tools.cc:52-107, each a
+ * MultiScaleTransforms::Transform, multiscale_transforms.cc:9-21), for plans
+ * with RDL_CONV_FAST_TILED only (RDL_ERR_UNSUPPORTED otherwise):
+ *   rdl_conv_forward_half: the row transforms of the plane (as
+ *     rdl_conv_rows_forward) and the first column step, into d_half
+ *     (rdl_conv_spectrum_bytes);
+ *   rdl_conv_real_kernel: the scale kernel's spectrum: h_shape is the n x n
+ *     shape function (MakeShapeFunction, n odd, symmetric in x and y) placed
+ *     as PrepareSmallConvolutionKernel; such a kernel's spectrum is real and
+ *     even, evaluated here in double and stored as float in the tiled layout
+ *     (rdl_conv_real_kernel_bytes);
+ *   rdl_conv_scales: for i < n_scales (<= 8): the rest of the forward column
+ *     transform, x d_kernels[i] x scale, and the inner inverse column step,
+ *     into d_outs[i] (spectrum-sized, distinct from d_half);
+ *   rdl_conv_scale_finish: the outer inverse column step: d_in (one of
+ *     d_outs) -> d_out (!= d_in), the column-inverted spectrum that
+ *     rdl_conv_rows_inverse(_peak) turns into the convolved image.
+ * The forward spectrum itself is never stored. */
+size_t rdl_conv_real_kernel_bytes(const rdl_conv* c);
+int rdl_conv_real_kernel(rdl_conv* c, const float* h_shape, uint32_t n, void* d_kernel);
+int rdl_conv_forward_half(rdl_conv* c, const float* d_in, uint32_t in_w, uint32_t in_h,
+                          uint32_t ox, uint32_t oy, void* d_half);
+int rdl_conv_scales(rdl_conv* c, const void* d_half, uint32_t n_scales,
+                    const void* const* d_kernels, void* const* d_outs, double scale);
+int rdl_conv_scale_finish(rdl_conv* c, const void* d_in, void* d_out);
+
 /* dst = a * b * scale, complex, n_complex elements. */
 int rdl_spectrum_multiply(rdl_session* s, void* d_dst, const void* d_a,
                           const void* d_b, size_t n_complex, float scale);

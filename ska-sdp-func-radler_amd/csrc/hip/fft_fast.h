@@ -56,6 +56,8 @@ struct FastSteps {
   const void* step_a;
   const void* step_b;
   RadixList radix_a, radix_b;  // of the length-n1 / length-n2 transforms
+  const void* step_b_scales;   // ff::ColStepBScales (forward B, x K_s, inner inverse)
+  const void* step_a_inv;      // ff::ColStepAInv (outer inverse step)
 };
 
 /* The pass table of a length-n transform with these radices (ff::Pass):
@@ -71,6 +73,22 @@ const FastSteps* FindFastSteps(uint32_t n);
 int FastStepLaunch(rdl_session* s, const FastSteps* p, bool pass_b, const void* in,
                    void* out, const void* kern, const void* tw, const void* ptw,
                    uint32_t n_cols, int inverse, float scale);
+/* Several scale convolutions from one forward half (A pass output `in`):
+ * per scale s, the forward B DFT, x kerns[s] (real, float tiles) x scale,
+ * the inner inverse DFT and its twiddle into outs[s] (ff::ColStepBScales);
+ * then per scale FastStepAInvLaunch -> the natural-order column inverse.
+ * tw: the length-n table W_n^k. At most 8 scales per launch. */
+int FastScalesLaunch(rdl_session* s, const FastSteps* p, const void* in, const void* tw,
+                     const void* ptw_b, uint32_t n_cols, uint32_t n_scales,
+                     const float* const* kerns, void* const* outs, float scale);
+int FastStepAInvLaunch(rdl_session* s, const FastSteps* p, const void* in, void* out,
+                       const void* ptw_a, uint32_t n_cols);
+/* cos(2 pi j / n), j < n, double (long double on the host) */
+int MakeCosTable(uint32_t n, void** out);
+/* the real spectrum of a symmetric n x n kernel (n odd) placed at the origin
+ * of a w x h plane, float, tiled; a_scratch: (n / 2 + 1) x (w / 2 + 1) doubles */
+int RealKernelLaunch(rdl_session* s, const float* shape, uint32_t n, uint32_t w, uint32_t h,
+                     const void* cos_w, const void* cos_h, void* a_scratch, float* out);
 /* tiled spectrum size in complex elements for a plane of `width` x `height` */
 inline size_t TiledComplexCount(uint32_t width, uint32_t height) {
   return size_t((width / 2 + 1 + 15) / 16) * 16 * height;

@@ -937,6 +937,203 @@ __global__ __launch_bounds__(TH) void ColStepB(StepArgs a, const Cx<float>* __re
   }
 }
 
+// ------------------------------- several scales from one forward half
+// The scale convolutions of one image (FindMultiScalePeak: every active
+// scale's kernel times the same forward spectrum) without the forward
+// spectrum ever reaching HBM. After A (forward), T[k1 N2 + n2] holds, per k1,
+// the inputs of the length-N2 DFTs whose outputs are X[k1 + N1 k2]. The
+// inverse of Y = X K s is conj(z), z = DFT(conj Y); with k = k1 + N1 k2 and
+// m = m2 + N2 m1:
+//   z[m2 + N2 m1] = sum_k1 W_N1^(m1 k1) W_N^(m2 k1) sum_k2 conj Y[k1 + N1 k2] W_N2^(m2 k2),
+// so a workgroup holding one k1 group runs the forward B DFT, multiplies by
+// each scale's (real, even) kernel, runs the inner inverse DFT over k2 and
+// the twiddle W_N^(m2 k1) in LDS, and writes U_s[k1 N2 + m2] (B*, below);
+// ColStepAInv then runs the outer DFT over k1 per m2 and stores conj(z) in
+// natural order. Per scale that is one write + one read + one write of the
+// spectrum (against read X + K, write, read, write for A(x K) + B), and the
+// forward B pass is gone.
+constexpr uint32_t kMaxScaleOuts = 8;
+struct ScalesArgs {
+  uint32_t n_tiles;
+  uint32_t n_scales;
+  float scale;                          // 1 / (W H)
+  const float* kern[kMaxScaleOuts];     // real kernel spectra, float tiles (16 per row)
+  Cx<float>* out[kMaxScaleOuts];        // U_s, the tiled spectrum layout
+};
+
+// B*: workgroup = (tile, GB consecutive k1). ptw: the length-N2 pass table;
+// tw: the length-N table W_N^e.
+template <uint32_t TH, uint32_t N1, uint32_t N2, uint32_t GB, uint32_t... R2>
+__global__ __launch_bounds__(TH) void ColStepBScales(ScalesArgs a,
+                                                     const Cx<float>* __restrict__ in,
+                                                     const Cx<float>* __restrict__ tw,
+                                                     const Cx<float>* __restrict__ ptw) {
+  constexpr uint32_t S = N2 + 1;
+  constexpr uint32_t N = N1 * N2;
+  constexpr uint32_t COUNT = kTile * GB;
+  constexpr uint32_t EL = COUNT * N2;
+  constexpr uint32_t E = (EL + TH - 1) / TH;
+  constexpr uint32_t NT = TableSize<1, R2...>();
+  __shared__ Cx<float> buf[COUNT * S];
+  __shared__ Cx<float> wt[NT > 0 ? NT : 1];
+  __shared__ Cx<float> wb[GB * N2];  // W_N^{m2 k1} of this workgroup's k1
+  const uint32_t tid = threadIdx.x;
+  const uint32_t tile = blockIdx.x / (N1 / GB);
+  const uint32_t k1_0 = (blockIdx.x % (N1 / GB)) * GB;
+  const size_t base = size_t(tile) * N * kTile;
+  for (uint32_t i = tid; i < NT; i += TH) wt[i] = ptw[i];
+  for (uint32_t i = tid; i < GB * N2; i += TH) {
+    const uint32_t g = i / N2, m2 = i % N2;
+    wb[i] = tw[(m2 * (k1_0 + g)) % N];
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < E; ++i) {
+    const uint32_t idx = tid + i * TH;
+    if (EL % TH != 0 && idx >= EL) continue;
+    const uint32_t col = idx % kTile, q = idx / kTile;
+    const uint32_t n2 = q % N2, g = q / N2;  // rows k1 N2 .. k1 N2 + N2 - 1: contiguous
+    buf[(g * kTile + col) * S + n2] = in[base + size_t((k1_0 + g) * N2 + n2) * kTile + col];
+  }
+  LdsSync();
+  BFft<float, TH, N2, COUNT, S, 0, 1, R2...>(buf, wt, tid);
+  // X[k1 + N1 k2] into registers: (col, g, k2), GB adjacent rows per k2
+  Cx<float> X[E];
+#pragma unroll
+  for (uint32_t i = 0; i < E; ++i) {
+    const uint32_t idx = tid + i * TH;
+    if (EL % TH != 0 && idx >= EL) continue;
+    const uint32_t col = idx % kTile, q = idx / kTile;
+    const uint32_t g = q % GB, k2 = q / GB;
+    X[i] = buf[(g * kTile + col) * S + k2];
+  }
+  for (uint32_t sc = 0; sc < a.n_scales; ++sc) {
+    // opaque per scale (see Columns): the per-element addresses are
+    // recomputed, not hoisted out of the loop into registers
+    uint32_t tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const float* __restrict__ kern = a.kern[sc];
+    LdsSync();  // every read of buf (X, or the previous scale's stores) done
+#pragma unroll
+    for (uint32_t i = 0; i < E; ++i) {
+      const uint32_t idx = tid + i * TH;
+      if (EL % TH != 0 && idx >= EL) continue;
+      const uint32_t col = idx % kTile, q = idx / kTile;
+      const uint32_t g = q % GB, k2 = q / GB;
+      const float k = kern[(size_t(tile) * N + k1_0 + g + N1 * k2) * kTile + col];
+      // conj(X K s), K real: the complex product's terms with Im K = 0
+      const Cx<float> v = {(X[i].x * k) * a.scale, -((X[i].y * k) * a.scale)};
+      buf[(g * kTile + col) * S + k2] = v;
+    }
+    LdsSync();
+    BFft<float, TH, N2, COUNT, S, 0, 1, R2...>(buf, wt, tid);
+    Cx<float>* __restrict__ out = a.out[sc];
+#pragma unroll
+    for (uint32_t i = 0; i < E; ++i) {
+      const uint32_t idx = tid + i * TH;
+      if (EL % TH != 0 && idx >= EL) continue;
+      const uint32_t col = idx % kTile, q = idx / kTile;
+      const uint32_t m2 = q % N2, g = q / N2;  // rows k1 N2 + m2: contiguous
+      out[base + size_t((k1_0 + g) * N2 + m2) * kTile + col] =
+          Mul(buf[(g * kTile + col) * S + m2], wb[g * N2 + m2]);
+    }
+  }
+}
+
+// The outer inverse step: workgroup = (tile, GA consecutive m2): the length-N1
+// DFTs over k1 of U[k1 N2 + m2], conj(z) to row m2 + N2 m1 (natural order).
+template <uint32_t TH, uint32_t N1, uint32_t N2, uint32_t GA, uint32_t... R1>
+__global__ __launch_bounds__(TH) void ColStepAInv(StepArgs a, const Cx<float>* __restrict__ in,
+                                                  Cx<float>* __restrict__ out,
+                                                  const Cx<float>* __restrict__ ptw) {
+  constexpr uint32_t N = N1 * N2;
+  constexpr uint32_t S = N1 + 1;
+  constexpr uint32_t COUNT = kTile * GA;
+  constexpr uint32_t EL = COUNT * N1;
+  constexpr uint32_t E = (EL + TH - 1) / TH;
+  constexpr uint32_t NT = TableSize<1, R1...>();
+  __shared__ Cx<float> buf[COUNT * S];
+  __shared__ Cx<float> wt[NT > 0 ? NT : 1];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t tile = blockIdx.x / (N2 / GA);
+  const uint32_t m2_0 = (blockIdx.x % (N2 / GA)) * GA;
+  const size_t base = size_t(tile) * N * kTile;
+  for (uint32_t i = tid; i < NT; i += TH) wt[i] = ptw[i];
+#pragma unroll
+  for (uint32_t i = 0; i < E; ++i) {
+    const uint32_t idx = tid + i * TH;
+    if (EL % TH != 0 && idx >= EL) continue;
+    const uint32_t col = idx % kTile, q = idx / kTile;
+    const uint32_t g = q % GA, k1 = q / GA;  // rows k1 N2 + m2_0 ..: GA contiguous
+    buf[(g * kTile + col) * S + k1] = in[base + size_t(k1 * N2 + m2_0 + g) * kTile + col];
+  }
+  LdsSync();
+  BFft<float, TH, N1, COUNT, S, 0, 1, R1...>(buf, wt, tid);
+#pragma unroll
+  for (uint32_t i = 0; i < E; ++i) {
+    const uint32_t idx = tid + i * TH;
+    if (EL % TH != 0 && idx >= EL) continue;
+    const uint32_t col = idx % kTile, q = idx / kTile;
+    const uint32_t g = q % GA, m1 = q / GA;  // rows m2 + N2 m1: GA adjacent per m1
+    out[base + size_t(m2_0 + g + N2 * m1) * kTile + col] =
+        Conj(buf[(g * kTile + col) * S + m1]);
+  }
+  (void)a;
+}
+
+// The real, even spectrum of a symmetric small kernel placed as
+// PrepareSmallConvolutionKernel (centre at (0, 0), wrapped): with k even in
+// x and y, K(u, v) = sum_y cos(2 pi v y / H) sum_x k(x, y) cos(2 pi u x / W),
+// evaluated in double from cosine tables (cos_w[j] = cos(2 pi j / W), long
+// double on the host, angles reduced exactly: (u x) mod W), rounded to float
+// once. Stage 1: A[y][u] = k(0, y) + 2 sum_{x=1..r} k(x, y) cos(2 pi u x / W)
+// for the kernel rows y = 0..r.
+__global__ __launch_bounds__(256) void RealKernelRows(const float* __restrict__ shape,
+                                                      uint32_t n, uint32_t w, uint32_t nu,
+                                                      const double* __restrict__ cos_w,
+                                                      double* __restrict__ a_out) {
+  const uint32_t u = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t y = blockIdx.y;  // 0 .. r
+  const uint32_t r = n / 2;
+  if (u >= nu) return;
+  const float* row = shape + size_t(r + y) * n + r;  // k(x, y) = row[x], x >= 0
+  double acc = 0.0;
+  uint32_t e = 0;  // (u x) mod w
+  for (uint32_t x = 1; x <= r; ++x) {
+    e += u;
+    if (e >= w) e -= w;
+    acc += double(row[x]) * cos_w[e];
+  }
+  a_out[size_t(y) * nu + u] = double(row[0]) + 2.0 * acc;
+}
+
+// Stage 2: K(u, v) = A[0][u] + 2 sum_{y=1..r} A[y][u] cos(2 pi v y / H), float,
+// tiled (16 columns per row, tile after tile; columns >= nu zero).
+__global__ __launch_bounds__(256) void RealKernelCols(const double* __restrict__ a_in,
+                                                      uint32_t r, uint32_t h, uint32_t nu,
+                                                      uint32_t n_tiles,
+                                                      const double* __restrict__ cos_h,
+                                                      float* __restrict__ out) {
+  const size_t i = size_t(blockIdx.x) * 256 + threadIdx.x;
+  const size_t total = size_t(n_tiles) * h * kTile;
+  if (i >= total) return;
+  const uint32_t col = uint32_t(i % kTile);
+  const uint32_t v = uint32_t((i / kTile) % h);
+  const uint32_t tile = uint32_t(i / (size_t(kTile) * h));
+  const uint32_t u = tile * kTile + col;
+  if (u >= nu) {
+    out[i] = 0.0f;
+    return;
+  }
+  double acc = 0.0;
+  uint32_t e = 0;  // (v y) mod h
+  for (uint32_t y = 1; y <= r; ++y) {
+    e += v;
+    if (e >= h) e -= h;
+    acc += a_in[size_t(y) * nu + u] * cos_h[e];
+  }
+  out[i] = float(a_in[u] + 2.0 * acc);
+}
+
 // row mask (one byte per plane row) -> ascending list of the non-zero rows
 __global__ __launch_bounds__(1024) void CompactRows(const uint8_t* __restrict__ mask,
                                                     uint32_t n, uint32_t* __restrict__ rows,
@@ -1234,7 +1431,9 @@ size_t ConvColumnsDLdsBytes(uint32_t n) {
     N1 * N2, N1, N2, GA, GB, 256,                                                  \
         reinterpret_cast<const void*>(&ff::ColStepA<256, N1, N2, GA, RA>),         \
         reinterpret_cast<const void*>(&ff::ColStepB<256, N1, N2, GB, RB>),         \
-        MakeRadixList<RA>(), MakeRadixList<RB>()                                   \
+        MakeRadixList<RA>(), MakeRadixList<RB>(),                                  \
+        reinterpret_cast<const void*>(&ff::ColStepBScales<256, N1, N2, GB, RB>),   \
+        reinterpret_cast<const void*>(&ff::ColStepAInv<256, N1, N2, GA, RA>)       \
   }
 #define RDL_R(...) __VA_ARGS__
 
@@ -1461,6 +1660,67 @@ int FastStepLaunch(rdl_session* s, const FastSteps* p, bool pass_b, const void* 
     RDL_HIP_CHECK(hipLaunchKernel(p->step_a, dim3(grid), dim3(p->threads), args, 0,
                                   s->stream));
   }
+  return RDL_OK;
+}
+
+int FastScalesLaunch(rdl_session* s, const FastSteps* p, const void* in, const void* tw,
+                     const void* ptw_b, uint32_t n_cols, uint32_t n_scales,
+                     const float* const* kerns, void* const* outs, float scale) {
+  if (n_scales == 0) return RDL_OK;
+  if (n_scales > ff::kMaxScaleOuts) {
+    SetError("scale convolutions: at most 8 scales per launch");
+    return RDL_ERR_ARG;
+  }
+  ff::ScalesArgs a{};
+  a.n_tiles = (n_cols + ff::kTile - 1) / ff::kTile;
+  a.n_scales = n_scales;
+  a.scale = scale;
+  for (uint32_t i = 0; i < n_scales; ++i) {
+    a.kern[i] = kerns[i];
+    a.out[i] = static_cast<Cx<float>*>(outs[i]);
+  }
+  const uint32_t grid = a.n_tiles * (p->n1 / p->gb);
+  void* args[] = {&a, (void*)&in, (void*)&tw, (void*)&ptw_b};
+  RDL_HIP_CHECK(hipLaunchKernel(p->step_b_scales, dim3(grid), dim3(p->threads), args, 0,
+                                s->stream));
+  return RDL_OK;
+}
+
+int FastStepAInvLaunch(rdl_session* s, const FastSteps* p, const void* in, void* out,
+                       const void* ptw_a, uint32_t n_cols) {
+  ff::StepArgs a{};
+  a.n_tiles = (n_cols + ff::kTile - 1) / ff::kTile;
+  const uint32_t grid = a.n_tiles * (p->n2 / p->ga);
+  void* args[] = {&a, (void*)&in, (void*)&out, (void*)&ptw_a};
+  RDL_HIP_CHECK(hipLaunchKernel(p->step_a_inv, dim3(grid), dim3(p->threads), args, 0,
+                                s->stream));
+  return RDL_OK;
+}
+
+int MakeCosTable(uint32_t n, void** out) {
+  std::vector<double> host(n);
+  for (uint32_t j = 0; j < n; ++j)
+    host[j] = double(std::cos(2.0L * 3.14159265358979323846264338327950288L *
+                              (long double)j / n));
+  RDL_HIP_CHECK(rdl::DevMalloc(out, host.size() * sizeof(double)));
+  RDL_HIP_CHECK(hipMemcpy(*out, host.data(), host.size() * sizeof(double),
+                          hipMemcpyHostToDevice));
+  return RDL_OK;
+}
+
+int RealKernelLaunch(rdl_session* s, const float* shape, uint32_t n, uint32_t w, uint32_t h,
+                     const void* cos_w, const void* cos_h, void* a_scratch, float* out) {
+  const uint32_t nu = w / 2 + 1;
+  const uint32_t r = n / 2;
+  const uint32_t n_tiles = (nu + ff::kTile - 1) / ff::kTile;
+  ff::RealKernelRows<<<dim3((nu + 255) / 256, r + 1), 256, 0, s->stream>>>(
+      shape, n, w, nu, static_cast<const double*>(cos_w), static_cast<double*>(a_scratch));
+  RDL_HIP_CHECK(hipGetLastError());
+  const size_t total = size_t(n_tiles) * h * ff::kTile;
+  ff::RealKernelCols<<<dim3(uint32_t((total + 255) / 256)), 256, 0, s->stream>>>(
+      static_cast<const double*>(a_scratch), r, h, nu, n_tiles,
+      static_cast<const double*>(cos_h), out);
+  RDL_HIP_CHECK(hipGetLastError());
   return RDL_OK;
 }
 

@@ -525,6 +525,10 @@ struct rdl_conv {
   void* ptw_a = nullptr;
   void* ptw_b = nullptr;
   void* twd_row = nullptr;  // float rows: two-level double twiddles of width (MakeTwiddleBase)
+  // rdl_conv_real_kernel: cosine tables of width and height, stage-1 scratch
+  void* cos_w = nullptr;
+  void* cos_h = nullptr;
+  rdl::Scratch real_a;
 };
 
 namespace {
@@ -944,7 +948,8 @@ int rdl_conv_destroy(rdl_conv* c) {
   for (void* p : c->scratch_lane)
     if (p) (void)rdl::DevFree(p);
   if (c->rows_list) (void)rdl::DevFree(c->rows_list);
-  for (void* p : {c->ptw_row, c->ptw_col, c->ptw_a, c->ptw_b, c->twd_row})
+  for (void* p : {c->ptw_row, c->ptw_col, c->ptw_a, c->ptw_b, c->twd_row, c->cos_w, c->cos_h,
+                  c->real_a.ptr})
     if (p) (void)rdl::DevFree(p);
   delete c;
   return RDL_OK;
@@ -1130,6 +1135,85 @@ int rdl_conv_rows_inverse_peak(rdl_conv* c, const void* d_spec, float* d_out,
 int rdl_conv_forward(rdl_conv* c, const float* d_in, void* d_spec) {
   RDL_TRY(rdl_conv_rows_forward(c, d_in, c->width, c->height, 0, 0, d_spec));
   return rdl_conv_columns(c, d_spec, d_spec, nullptr, 0, 1.0);
+}
+
+size_t rdl_conv_real_kernel_bytes(const rdl_conv* c) {
+  return c && c->tiled ? rdl::TiledComplexCount(c->width, c->height) * sizeof(float) : 0;
+}
+
+int rdl_conv_real_kernel(rdl_conv* c, const float* h_shape, uint32_t n, void* d_kernel) {
+  RDL_ARG_CHECK(c && h_shape && d_kernel, "NULL argument");
+  if (!c->tiled) {
+    rdl::SetError("rdl_conv_real_kernel: needs a four-step (tiled) float plan");
+    return RDL_ERR_UNSUPPORTED;
+  }
+  RDL_ARG_CHECK(n % 2 == 1 && n <= c->width && n <= c->height,
+                "kernel side must be odd and fit the plane");
+  for (uint32_t y = 0; y < n; ++y)  // the evaluation assumes the symmetry
+    for (uint32_t x = 0; x < n; ++x) {
+      const float v = h_shape[x + y * n];
+      RDL_ARG_CHECK(v == h_shape[(n - 1 - x) + y * n] && v == h_shape[x + (n - 1 - y) * n],
+                    "rdl_conv_real_kernel: the kernel is not symmetric in x and y");
+    }
+  rdl_session* s = c->s;
+  if (!c->cos_w) RDL_TRY(rdl::MakeCosTable(c->width, &c->cos_w));
+  if (!c->cos_h) RDL_TRY(rdl::MakeCosTable(c->height, &c->cos_h));
+  const size_t shape_bytes = size_t(n) * n * sizeof(float);
+  RDL_TRY(s->EnsureScratch(s->kernel, shape_bytes));
+  RDL_HIP_CHECK(hipMemcpyAsync(s->kernel.ptr, h_shape, shape_bytes, hipMemcpyHostToDevice,
+                               s->stream));
+  RDL_TRY(s->EnsureScratch(c->real_a, size_t(n / 2 + 1) * (c->width / 2 + 1) * sizeof(double)));
+  RDL_TRY(rdl::RealKernelLaunch(s, static_cast<const float*>(s->kernel.ptr), n, c->width,
+                                c->height, c->cos_w, c->cos_h, c->real_a.ptr,
+                                static_cast<float*>(d_kernel)));
+  // the shape scratch is host-written next time: finish with it first
+  RDL_HIP_CHECK(hipStreamSynchronize(s->stream));
+  return RDL_OK;
+}
+
+int rdl_conv_forward_half(rdl_conv* c, const float* d_in, uint32_t in_w, uint32_t in_h,
+                          uint32_t ox, uint32_t oy, void* d_half) {
+  RDL_ARG_CHECK(c && d_in && d_half, "NULL argument");
+  if (!c->tiled) {
+    rdl::SetError("rdl_conv_forward_half: needs a four-step (tiled) float plan");
+    return RDL_ERR_UNSUPPORTED;
+  }
+  const double sb = SpectrumBytes(c);
+  // rows into the lane's scratch, A from there into d_half (A is not
+  // in-place safe: rows n2 + N2 n1 -> k1 N2 + n2)
+  RDL_TRY(EnsureSplitScratch(c, size_t(sb)));
+  void* rows = c->scratch;
+  RDL_TRY(rdl_conv_rows_forward(c, d_in, in_w, in_h, ox, oy, rows));
+  rdl::ScopedTiming t(c->s, "conv_cols", 2.0 * sb);
+  return rdl::FastStepLaunch(c->s, c->steps, false, rows, d_half, nullptr, c->tw_col, c->ptw_a,
+                             c->width / 2 + 1, 0, 1.0f);
+}
+
+int rdl_conv_scales(rdl_conv* c, const void* d_half, uint32_t n_scales,
+                    const void* const* d_kernels, void* const* d_outs, double scale) {
+  RDL_ARG_CHECK(c && d_half && (n_scales == 0 || (d_kernels && d_outs)), "NULL argument");
+  if (!c->tiled) {
+    rdl::SetError("rdl_conv_scales: needs a four-step (tiled) float plan");
+    return RDL_ERR_UNSUPPORTED;
+  }
+  for (uint32_t i = 0; i < n_scales; ++i)
+    RDL_ARG_CHECK(d_kernels[i] && d_outs[i] && d_outs[i] != d_half, "bad kernel / output");
+  const double sb = SpectrumBytes(c);
+  // the half read once; per scale a real kernel (half a spectrum) and a write
+  rdl::ScopedTiming t(c->s, "conv_cols", sb + n_scales * 1.5 * sb);
+  return rdl::FastScalesLaunch(c->s, c->steps, d_half, c->tw_col, c->ptw_b, c->width / 2 + 1,
+                               n_scales, reinterpret_cast<const float* const*>(d_kernels),
+                               d_outs, float(scale));
+}
+
+int rdl_conv_scale_finish(rdl_conv* c, const void* d_in, void* d_out) {
+  RDL_ARG_CHECK(c && d_in && d_out && d_in != d_out, "NULL or aliased argument");
+  if (!c->tiled) {
+    rdl::SetError("rdl_conv_scale_finish: needs a four-step (tiled) float plan");
+    return RDL_ERR_UNSUPPORTED;
+  }
+  rdl::ScopedTiming t(c->s, "conv_cols", 2.0 * SpectrumBytes(c));
+  return rdl::FastStepAInvLaunch(c->s, c->steps, d_in, d_out, c->ptw_a, c->width / 2 + 1);
 }
 
 }  // extern "C"

@@ -206,6 +206,41 @@ bool Fft::ConvolveWindow(const float* d_plane, const void* d_kernel_spectrum, fl
   return true;
 }
 
+bool Fft::FusedScales() const {
+  return conv_ && !f64_ && (rdl_conv_fast(conv_) & RDL_CONV_FAST_TILED) &&
+         (rdl_conv_fast(conv_) & RDL_CONV_FAST_ROWS);
+}
+
+size_t Fft::RealKernelBytes() const { return conv_ ? rdl_conv_real_kernel_bytes(conv_) : 0; }
+
+void Fft::RealKernel(const float* h_shape, size_t n, void* d_kernel) {
+  Check(rdl_conv_real_kernel(conv_, h_shape, uint32_t(n), d_kernel), "rdl_conv_real_kernel");
+}
+
+void Fft::ForwardHalf(const float* d_in, void* d_half) {
+  Check(rdl_conv_forward_half(conv_, d_in, uint32_t(width_), uint32_t(height_), 0, 0, d_half),
+        "rdl_conv_forward_half");
+}
+
+void Fft::Scales(const void* d_half, const std::vector<const void*>& d_kernels,
+                 const std::vector<void*>& d_outs) {
+  const double norm = 1.0 / (double(width_) * double(height_));
+  Check(rdl_conv_scales(conv_, d_half, uint32_t(d_kernels.size()), d_kernels.data(),
+                        d_outs.data(), double(float(norm))),
+        "rdl_conv_scales");
+}
+
+void Fft::ScaleFinishWindowPeak(const void* d_u, void* d_work, float* d_out, size_t out_w,
+                                size_t out_h, size_t ox, size_t oy, uint32_t h_border,
+                                uint32_t v_border, bool allow_negative,
+                                const uint8_t* d_mask, uint32_t slot) {
+  Check(rdl_conv_scale_finish(conv_, d_u, d_work), "rdl_conv_scale_finish");
+  Check(rdl_conv_rows_inverse_peak(conv_, d_work, d_out, uint32_t(out_w), uint32_t(out_h),
+                                   uint32_t(ox), uint32_t(oy), h_border, v_border,
+                                   allow_negative ? 1 : 0, d_mask, slot),
+        "rdl_conv_rows_inverse_peak");
+}
+
 void Fft::ForwardColumnMajor(const float* d_in, void* d_spectrum) {
   if (!conv_) throw std::logic_error("Fft::ForwardColumnMajor needs the LDS engine");
   Check(rdl_conv_rows_forward(conv_, d_in, uint32_t(width_), uint32_t(height_), 0, 0,

@@ -98,6 +98,22 @@ class Fft {
   /// LDS engine only: forward spectrum stored column by column (column k at
   /// k * height), the layout the column pass reads contiguously.
   void ForwardColumnMajor(const float* d_in, void* d_spectrum);
+  /// Four-step (tiled) float plans: several scale convolutions of one image
+  /// from one forward half (rdl_conv_forward_half / _real_kernel / _scales /
+  /// _scale_finish; the forward spectrum is never stored).
+  bool FusedScales() const;
+  size_t RealKernelBytes() const;
+  /// the real spectrum of a symmetric n x n kernel placed at the origin
+  void RealKernel(const float* h_shape, size_t n, void* d_kernel);
+  void ForwardHalf(const float* d_in, void* d_half);
+  void Scales(const void* d_half, const std::vector<const void*>& d_kernels,
+              const std::vector<void*>& d_outs);
+  /// one scale's outer inverse step and the inverse rows with the fused peak
+  /// search, writing the out_w x out_h window at (ox, oy)
+  void ScaleFinishWindowPeak(const void* d_u, void* d_work, float* d_out, size_t out_w,
+                             size_t out_h, size_t ox, size_t oy, uint32_t h_border,
+                             uint32_t v_border, bool allow_negative, const uint8_t* d_mask,
+                             uint32_t slot);
   bool UsesLds() const { return conv_ != nullptr; }
   /// LDS engine with compile-time-planned columns: Forward() stores spectra
   /// column by column, which Convolve / ConvolveSpectrum then expect.

@@ -28,6 +28,14 @@ int ScaleLanes() {
   return e && e[0] == '1' ? 1 : 2;
 }
 
+// RDL_FUSED_SCALES=0: the scales' convolutions through the forward spectrum
+// and one two-pass column inverse each instead of the fused multi-scale
+// launch (read per call, for comparisons)
+bool FusedScalesOn() {
+  const char* e = std::getenv("RDL_FUSED_SCALES");
+  return !(e && e[0] == '0');
+}
+
 // joins the session's second lane if a scope exits while it is selected
 struct LaneJoin {
   rdl_session* s;
@@ -246,10 +254,15 @@ void MultiScaleAlgorithm::FindActiveScaleConvolvedMaxima(
     }
   }
   if (!need_fft) return;
-  transforms_->Forward(d_source, spectrum_->Ptr());
-  std::vector<size_t> pending;  // scale of each queued peak search
   if (scale_infos_.size() > RDL_PEAK_SLOTS)
     throw std::runtime_error("MultiScaleAlgorithm: too many scales");
+  const bool fused_search = !report_rms && !RmsFactorImage();
+  if (fused_search && FusedScalesOn() && transforms_->Fused()) {
+    FindMaximaFused(d_source, identity);
+    return;
+  }
+  transforms_->Forward(d_source, spectrum_->Ptr());
+  std::vector<size_t> pending;  // scale of each queued peak search
   // The scales' inverse transforms + fused peak searches are independent
   // (the reference runs them on threads, threaded_deconvolution_tools.cc):
   // with a kept image per scale they alternate over two session lanes, so
@@ -257,7 +270,6 @@ void MultiScaleAlgorithm::FindActiveScaleConvolvedMaxima(
   // passes. Every buffer a lane writes is its own (work spectrum, four-step
   // scratch, peak partials slot, scale image); the kernel spectra and the
   // scale images are made before the fork (no allocation on lane 1).
-  const bool fused_search = !report_rms && !RmsFactorImage();
   bool forked = false;
   if (identity && fused_search && spectrum_work2_) {
     size_t n_fft = 0;
@@ -349,6 +361,78 @@ void MultiScaleAlgorithm::FindActiveScaleConvolvedMaxima(
   }
 }
 
+void MultiScaleAlgorithm::FindMaximaFused(const float* d_source, bool identity) {
+  // The same searches as below, with the scales' convolutions made from ONE
+  // forward half by one launch (rdl_conv_scales: the forward spectrum never
+  // reaches HBM, the scale kernels are real), then per scale the outer
+  // inverse step and the inverse rows with the fused peak search,
+  // alternating over two lanes as below.
+  rdl_session* s = session_->Handle();
+  const size_t w = transforms_->Width(), h = transforms_->Height();
+  std::vector<size_t> idx;
+  std::vector<float> scales;
+  for (size_t si = 0; si != scale_infos_.size(); ++si) {
+    const ScaleInfo& e = scale_infos_[si];
+    if (!e.is_active || e.scale == 0.0f) continue;
+    idx.push_back(si);
+    scales.push_back(e.scale);
+  }
+  // every buffer and kernel spectrum before any fork (no allocation on lane 1)
+  const size_t sb = transforms_->SpectrumBytes();
+  while (scale_u_.size() < idx.size())
+    scale_u_.push_back(std::make_shared<gpu::Buffer>(*session_, sb));
+  std::vector<void*> outs;
+  for (size_t k = 0; k != idx.size(); ++k) outs.push_back(scale_u_[k]->Ptr());
+  for (float sc : scales) transforms_->RealKernelSpectrum(sc);
+  std::vector<float*> conv(idx.size(), scratch_->F());
+  if (identity)
+    for (size_t k = 0; k != idx.size(); ++k) {
+      gpu::Planes& kept = scale_images_[idx[k]];
+      if (!kept.buffer || kept.width != w || kept.height != h)
+        kept = gpu::Planes::Make(*session_, w, h, 1);
+      conv[k] = kept.Base();
+      scale_image_valid_[idx[k]] = true;
+    }
+  transforms_->ForwardHalf(d_source, spectrum_->Ptr());
+  transforms_->Scales(spectrum_->Ptr(), scales, outs);
+  // two lanes only with one image per scale (identity: kept images)
+  bool forked = false;
+  if (identity && idx.size() > 1 && spectrum_work2_) {
+    gpu::Check(rdl_session_fork(s), "rdl_session_fork");
+    forked = true;
+  }
+  LaneJoin lane_join{s, forked};
+  int lane = 0;
+  for (size_t k = 0; k != idx.size(); ++k) {
+    const ScaleInfo& e = scale_infos_[idx[k]];
+    const size_t border_scale = size_t(std::ceil(e.scale * 0.5));
+    const uint32_t xb = uint32_t(
+        std::max<size_t>(size_t(std::round(w * CleanBorderRatio())), border_scale));
+    const uint32_t yb = uint32_t(
+        std::max<size_t>(size_t(std::round(h * CleanBorderRatio())), border_scale));
+    if (forked) gpu::Check(rdl_session_lane(s, lane), "rdl_session_lane");
+    void* work = lane ? spectrum_work2_->Ptr() : spectrum_work_->Ptr();
+    transforms_->FinishPeak(outs[k], e.scale, work, conv[k], xb, yb, AllowNegativeComponents(),
+                            MaskFor(idx[k]), uint32_t(k));
+    if (forked) lane ^= 1;
+  }
+  if (forked) {
+    forked = false;
+    gpu::Check(rdl_session_join(s), "rdl_session_join");
+  }
+  std::vector<rdl_peak> peaks(idx.size());
+  gpu::Check(rdl_find_peak_collect(s, uint32_t(idx.size()), peaks.data()),
+             "rdl_find_peak_collect");
+  for (size_t k = 0; k != idx.size(); ++k) {
+    ScaleInfo& e = scale_infos_[idx[k]];
+    const rdl_peak& p = peaks[k];
+    e.max_normalized_image_value = p.found ? Normalized(p.value, p.x, p.y, w) : 0.0f;
+    e.max_unnormalized_image_value = p.found ? p.value : 0.0f;
+    e.max_image_value_x = p.x;
+    e.max_image_value_y = p.y;
+  }
+}
+
 void MultiScaleAlgorithm::ActivateScales(size_t last) {  // :636-656
   for (size_t i = 0; i != scale_infos_.size(); ++i) {
     const bool activate =
@@ -424,6 +508,7 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
   spectrum_ = std::make_shared<gpu::Buffer>(session, spectrum_bytes);
   spectrum_work_ = std::make_shared<gpu::Buffer>(session, spectrum_bytes);
   spectrum_work2_.reset();
+  scale_u_.clear();
   // the second lane only on a main session: a subimage pool's workers
   // already keep up to 16 streams busy, and a lane pair per worker adds
   // a spectrum buffer and fork/join events to every small subimage

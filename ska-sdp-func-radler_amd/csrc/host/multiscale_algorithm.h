@@ -111,6 +111,8 @@ class MultiScaleAlgorithm final : public DeconvolutionAlgorithm {
   std::shared_ptr<gpu::Buffer> scratch_;  // W x H
   std::shared_ptr<gpu::Buffer> rms_scratch_;  // W x H: image x RMS factor
   /// d_image, or d_image x the RMS factor (multiscale_algorithm.cc:707-713)
+  /// FindActiveScaleConvolvedMaxima through the fused multi-scale launch
+  void FindMaximaFused(const float* d_source, bool identity);
   const float* PeakSearchInput(const float* d_image, size_t w, size_t h);
   /// unnormalized / factor at the peak (:736-743), the value itself without
   float Normalized(float value, size_t x, size_t y, size_t w) const;
@@ -118,6 +120,9 @@ class MultiScaleAlgorithm final : public DeconvolutionAlgorithm {
   // the second session lane's work spectrum (FindActiveScaleConvolvedMaxima
   // alternates the scales' fused inverse transforms over two lanes)
   std::shared_ptr<gpu::Buffer> spectrum_work2_;
+  // the fused multi-scale path (MultiScaleTransforms::Fused): one inner
+  // inverse spectrum per active scale, made by one launch
+  std::vector<std::shared_ptr<gpu::Buffer>> scale_u_;
   // One image with the identity integration (ImageSet copy fast path): the
   // integrated image IS the residual, so the scale-convolved images that
   // FindActiveScaleConvolvedMaxima computes are the next outer iteration's

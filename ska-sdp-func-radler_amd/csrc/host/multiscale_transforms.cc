@@ -142,6 +142,7 @@ void MultiScaleTransforms::Plan(size_t radius) {
   ph_ = ph;
   fft_ = &s_.GetFft(pw_, ph_);
   spectra_.clear();
+  real_spectra_.clear();
   plane_.reset();
 }
 
@@ -257,6 +258,57 @@ bool MultiScaleTransforms::ConvolveSpectrumPeak(const void* d_spectrum, float sc
   return fft_->ConvolveSpectrumWindowPeak(d_spectrum, kernel, d_work, d_out, width_, height_,
                                           radius_, radius_, h_border, v_border,
                                           allow_negative, d_mask, slot);
+}
+
+bool MultiScaleTransforms::Fused() { return TheFft().FusedScales(); }
+
+const void* MultiScaleTransforms::RealKernelSpectrum(float scale) {
+  TheFft();
+  if (Extended() && KernelRadius(scale) > radius_) Plan(KernelRadius(scale));
+  auto it = real_spectra_.find(scale);
+  if (it != real_spectra_.end()) return it->second->Ptr();
+  size_t n;
+  const std::vector<float> k =
+      MakeShapeFunction(scale, n, std::min(width_, height_), shape_);
+  auto spectrum = std::make_shared<gpu::Buffer>(s_, fft_->RealKernelBytes());
+  fft_->RealKernel(k.data(), n, spectrum->Ptr());
+  real_spectra_[scale] = spectrum;
+  return spectrum->Ptr();
+}
+
+void MultiScaleTransforms::ForwardHalf(const float* d_image, void* d_half) {
+  TheFft();
+  if (!Extended()) {
+    fft_->ForwardHalf(d_image, d_half);
+    return;
+  }
+  float* plane = Plane();
+  gpu::Check(rdl_periodic_extend(s_.Handle(), plane, uint32_t(pw_), uint32_t(ph_),
+                                 d_image, uint32_t(width_), uint32_t(height_),
+                                 uint32_t(radius_), uint32_t(radius_)),
+             "rdl_periodic_extend");
+  fft_->ForwardHalf(plane, d_half);
+}
+
+void MultiScaleTransforms::Scales(const void* d_half, const std::vector<float>& scales,
+                                  const std::vector<void*>& d_outs) {
+  std::vector<const void*> kernels;
+  for (float sc : scales) {
+    if (Extended() && KernelRadius(sc) > radius_)
+      throw std::logic_error("Scales: scale larger than the planned margin");
+    kernels.push_back(RealKernelSpectrum(sc));
+  }
+  fft_->Scales(d_half, kernels, d_outs);
+}
+
+void MultiScaleTransforms::FinishPeak(const void* d_u, float scale, void* d_work, float* d_out,
+                                      uint32_t h_border, uint32_t v_border,
+                                      bool allow_negative, const uint8_t* d_mask,
+                                      uint32_t slot) {
+  (void)scale;
+  const size_t ox = Extended() ? radius_ : 0, oy = Extended() ? radius_ : 0;
+  fft_->ScaleFinishWindowPeak(d_u, d_work, d_out, width_, height_, ox, oy, h_border, v_border,
+                              allow_negative, d_mask, slot);
 }
 
 }  // namespace radler::algorithms::multiscale

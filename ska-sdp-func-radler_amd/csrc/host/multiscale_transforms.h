@@ -59,6 +59,19 @@ class MultiScaleTransforms {
                             uint32_t h_border, uint32_t v_border, bool allow_negative,
                             const uint8_t* d_mask, uint32_t slot);
 
+  /// The fused multi-scale path (Fft::FusedScales) for this plane: the
+  /// forward half of an image (periodically extended where the plane is),
+  /// the scales' real kernel spectra (cached), every listed scale's inner
+  /// inverse into d_outs (spectrum-sized each), and per scale the outer
+  /// inverse + inverse rows with the fused peak search into the W x H d_out.
+  bool Fused();
+  const void* RealKernelSpectrum(float scale);
+  void ForwardHalf(const float* d_image, void* d_half);
+  void Scales(const void* d_half, const std::vector<float>& scales,
+              const std::vector<void*>& d_outs);
+  void FinishPeak(const void* d_u, float scale, void* d_work, float* d_out, uint32_t h_border,
+                  uint32_t v_border, bool allow_negative, const uint8_t* d_mask, uint32_t slot);
+
   // multiscale_transforms.h:41-195
   static std::vector<float> MakeShapeFunction(float scale, size_t& n,
                                               size_t max_n, Shape shape);
@@ -82,6 +95,7 @@ class MultiScaleTransforms {
   gpu::Fft* fft_;
   std::shared_ptr<gpu::Buffer> plane_;
   std::map<float, std::shared_ptr<gpu::Buffer>> spectra_;
+  std::map<float, std::shared_ptr<gpu::Buffer>> real_spectra_;  // RealKernelSpectrum
   std::map<float, std::pair<std::shared_ptr<gpu::Buffer>, size_t>> shapes_;
 };
 
