@@ -572,6 +572,14 @@ int rdl_conv_columns_ex(rdl_conv* c, const void* d_in, void* d_out,
                         const void* d_kernel, int mode, double scale,
                         const uint8_t* d_row_mask, int kernel_layout,
                         int out_layout);
+/* rdl_conv_columns_ex mode 1 (row-major output) where only the output rows
+ * [out_row0, out_row0 + out_rows) are needed (the inverse row pass of a
+ * padded convolution reads the image window's rows only: Image::Trim,
+ * subminor_loop.cc:213-215): the float64 convolution-column plans leave the
+ * other rows unwritten; every other plan writes them all. */
+int rdl_conv_columns_window(rdl_conv* c, const void* d_in, void* d_out,
+                            const void* d_kernel, double scale, const uint8_t* d_row_mask,
+                            int kernel_layout, uint32_t out_row0, uint32_t out_rows);
 /* As rdl_conv_columns_ex with the input layout too (in_layout
  * RDL_CONV_COL_MAJOR: a mode-2 spectrum stored as columns). Every layout
  * combination needs the compile-time-planned column kernels

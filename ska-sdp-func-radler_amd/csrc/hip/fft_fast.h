@@ -134,7 +134,8 @@ const FastColumns* FindConvColumnsD(uint32_t n);
 int ConvColumnsDLaunch(rdl_session* s, const FastColumns* p, const void* in, void* out,
                        const void* kern, const void* tw, uint32_t n_cols, int kern_cm,
                        int out_cm, const uint32_t* rows, const uint32_t* n_rows, uint32_t row0,
-                       uint32_t row_n, double scale);
+                       uint32_t row_n, double scale, uint32_t out_row0 = 0,
+                       uint32_t out_row_n = 0xffffffffu);
 /* ascending list of the rows whose mask byte is non-zero, and its length */
 int FastCompactRows(rdl_session* s, const uint8_t* mask, uint32_t n, uint32_t* rows,
                     uint32_t* count);

@@ -195,6 +195,9 @@ struct ColArgs {
   uint32_t row0, row_n;
   uint32_t per_xcd;   // columns each XCD takes per round (grid / 8)
   double scale;
+  // ColumnsConvD: output rows outside [out_row0, out_row0 + out_row_n) are
+  // not written (the inverse row pass reads the output window's rows only)
+  uint32_t out_row0, out_row_n;
 };
 
 // PF: the kernel column is loaded into registers before the forward
@@ -468,7 +471,8 @@ __global__ __launch_bounds__(TH) void ColumnsConvD(ColArgs a, const Cx<double>* 
     CFwdTail<TH, N, R1, decltype(mulk), Rs...>(buf, t1, t2, tid, mulk);
     // inverse = conj(forward(conj(X K s))); the last pass stores row-major
     auto store = [&](uint32_t, uint32_t, uint32_t y, Cx<double> v) {
-      if (active) out[a.out_cm ? size_t(c) * N + y : size_t(y) * a.ld + c] = Conj(v);
+      if (active && y - a.out_row0 < a.out_row_n)
+        out[a.out_cm ? size_t(c) * N + y : size_t(y) * a.ld + c] = Conj(v);
     };
     // (its LDS reads end in a barrier, before the next round's first stores)
     CInv<TH, N, 1, decltype(store), R1, Rs...>(buf, t1, t2, tid, store);
@@ -1515,7 +1519,7 @@ int FastColumnsLaunch(rdl_session* s, const FastColumns* p, const void* in, void
 int ConvColumnsDLaunch(rdl_session* s, const FastColumns* p, const void* in, void* out,
                        const void* kern, const void* tw, uint32_t n_cols, int kern_cm,
                        int out_cm, const uint32_t* rows, const uint32_t* n_rows, uint32_t row0,
-                       uint32_t row_n, double scale) {
+                       uint32_t row_n, double scale, uint32_t out_row0, uint32_t out_row_n) {
   const size_t lds = ConvColumnsDLdsBytes(p->n);
   const int slots = SlotsPerCu(s, p->kernel, p->threads, lds);
   if (slots < 0) {
@@ -1533,6 +1537,8 @@ int ConvColumnsDLaunch(rdl_session* s, const FastColumns* p, const void* in, voi
   a.row0 = rows ? 0u : row0;
   a.row_n = rows ? p->n : row_n;
   a.scale = scale;
+  a.out_row0 = out_row0;
+  a.out_row_n = out_row_n;
   const uint32_t want = std::min<uint32_t>(n_cols, uint32_t(s->n_cus) * uint32_t(slots));
   a.per_xcd = std::max<uint32_t>(1, (want + 7) / 8);
   const uint32_t grid = 8 * a.per_xcd;

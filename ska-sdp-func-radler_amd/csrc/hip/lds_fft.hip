@@ -666,7 +666,8 @@ int LaunchRowsInverse(rdl_conv* c, const void* spec, float* out, uint32_t out_w,
 template <typename T>
 int LaunchColumns(rdl_conv* c, const void* in, void* out, const void* kern,
                   int mode, double scale, const uint8_t* row_mask, int kern_cm,
-                  int out_cm, int in_cm = 0) {
+                  int out_cm, int in_cm = 0, uint32_t out_row0 = 0,
+                  uint32_t out_rows = 0xffffffffu) {
   if (c->tiled) {
     // four-step passes through the conv's scratch (tiled spectra; the
     // layout flags do not apply)
@@ -702,7 +703,7 @@ int LaunchColumns(rdl_conv* c, const void* in, void* out, const void* kern,
     if (c->conv_cols && mode == 1 && !in_cm && (!out_cm || in != out))
       return rdl::ConvColumnsDLaunch(c->s, c->conv_cols, in, out, kern, c->tw_col,
                                      c->width / 2 + 1, kern_cm, out_cm, rows, n_rows, 0,
-                                     c->height, scale);
+                                     c->height, scale, out_row0, out_rows);
     return rdl::FastColumnsLaunch(c->s, c->fast_cols, in, out, kern, c->ptw_col,
                                   c->width / 2 + 1, uint32_t(mode), in_cm, out_cm, kern_cm,
                                   rows, n_rows, 0, c->height, scale);
@@ -1030,6 +1031,33 @@ int rdl_conv_columns_ex(rdl_conv* c, const void* d_in, void* d_out,
                                            d_row_mask, kcm, ocm)
                 : LaunchColumnsAny<float>(c, d_in, d_out, d_kernel, mode, scale,
                                           d_row_mask, kcm, ocm);
+}
+
+int rdl_conv_columns_window(rdl_conv* c, const void* d_in, void* d_out,
+                            const void* d_kernel, double scale, const uint8_t* d_row_mask,
+                            int kernel_layout, uint32_t out_row0, uint32_t out_rows) {
+  RDL_ARG_CHECK(c && d_in && d_out && d_kernel, "NULL argument");
+  RDL_ARG_CHECK(uint64_t(out_row0) + out_rows <= c->height, "output rows outside the plane");
+  RDL_ARG_CHECK(kernel_layout == RDL_CONV_ROW_MAJOR || kernel_layout == RDL_CONV_COL_MAJOR,
+                "bad kernel layout");
+  if (!c->f64 || !c->conv_cols || c->split)
+    return rdl_conv_columns_ex(c, d_in, d_out, d_kernel, 1, scale, d_row_mask, kernel_layout,
+                               RDL_CONV_ROW_MAJOR);
+  const double sb = SpectrumBytes(c);
+  const double win = sb * double(out_rows) / double(c->height);
+  const char* fam = d_row_mask ? "conv64_cols_sparse" : "conv64_cols";
+  rdl::ScopedTiming t(c->s, fam, d_row_mask ? sb + win : 2.0 * sb + win);
+  const uint32_t* rows = nullptr;
+  const uint32_t* n_rows = nullptr;
+  if (d_row_mask) {
+    RDL_TRY(CompactRowsFor(c, d_row_mask, true));
+    rows = c->rows_list;
+    n_rows = c->rows_list + c->height;
+    c->rows_list_mask = nullptr;  // the mask's contents may change next time
+  }
+  return rdl::ConvColumnsDLaunch(c->s, c->conv_cols, d_in, d_out, d_kernel, c->tw_col,
+                                 c->width / 2 + 1, kernel_layout == RDL_CONV_COL_MAJOR, 0, rows,
+                                 n_rows, 0, c->height, scale, out_row0, out_rows);
 }
 
 int rdl_conv_columns_layout(rdl_conv* c, const void* d_in, void* d_out,

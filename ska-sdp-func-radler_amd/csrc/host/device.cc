@@ -266,11 +266,12 @@ void Fft::ConvolveSubtract(const float* d_image, size_t img_w, size_t img_h,
     Check(rdl_conv_rows_forward(conv_, d_image, uint32_t(img_w), uint32_t(img_h),
                                 uint32_t(ox), uint32_t(oy), d_work),
           "rdl_conv_rows_forward");
-  Check(rdl_conv_columns_ex(conv_, d_work, d_work, d_kernel_spectrum, 1,
-                            f64_ ? norm : double(float(norm)), d_row_mask,
-                            kernel_col_major ? RDL_CONV_COL_MAJOR : RDL_CONV_ROW_MAJOR,
-                            RDL_CONV_ROW_MAJOR),
-        "rdl_conv_columns_ex");
+  // only the window's rows of the column output are read back
+  Check(rdl_conv_columns_window(conv_, d_work, d_work, d_kernel_spectrum,
+                                f64_ ? norm : double(float(norm)), d_row_mask,
+                                kernel_col_major ? RDL_CONV_COL_MAJOR : RDL_CONV_ROW_MAJOR,
+                                uint32_t(oy), uint32_t(img_h)),
+        "rdl_conv_columns_window");
   Check(rdl_conv_rows_inverse(conv_, d_work, d_residual, uint32_t(img_w),
                               uint32_t(img_h), uint32_t(ox), uint32_t(oy), 1),
         "rdl_conv_rows_inverse");

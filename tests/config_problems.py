@@ -68,7 +68,9 @@ def joined_channels(size, n_points, n_blobs, seed=SEED, frequencies=C3_FREQUENCI
 # trace's first divergence, tests/test_configs_gpu.py), so the images are
 # comparable pixel for pixel. C2 / C3 sit just below the GPU's measured first
 # divergence (7 259 / 17 026 components, round 3); "near_tie" = the fixture's
-# first oracle near-tie, which the GPU must reach identically in any case.
+# first oracle near-tie, which the GPU must reach identically in any case;
+# `image_cap2` a second, deeper checkpoint below the GPU's measured first
+# divergence (h8k: 2 488, an exact tie in the oracle, round 4).
 CONFIGS = {
     "c1": dict(kind="hogbom", size=1024, points=200, blobs=20, threshold=0.0,
                max_iterations=1000),
@@ -84,7 +86,7 @@ CONFIGS = {
     # and past the first near-tie, the image checkpoint AT the first near-tie
     # (make_config_golden.py: image_cap "near_tie")
     "h8k": dict(kind="multiscale", size=8192, points=2000, blobs=200, threshold=5 * NOISE,
-                max_scales=6, cap=16000, image_cap="near_tie"),
+                max_scales=6, cap=16000, image_cap="near_tie", image_cap2=2400),
     # bench.py's live CPU-vs-GPU wall-clock-to-threshold leg: C2's sky density
     # on 2048^2, small enough for the CPU oracle to reach the threshold inside
     # the default bench run (no fixture: both sides run it in the same job)

@@ -99,6 +99,8 @@ def make(name):
     np.savez_compressed(path, **out)
     if "image_cap" in c:
         checkpoint(name)
+    if "image_cap2" in c:
+        checkpoint(name, "image_cap2", "ck2_")
 
 
 RTOL = 1e-6  # tests/test_configs_gpu.py
@@ -114,11 +116,12 @@ def first_near_tie(fx, rtol=RTOL):
     return int(near[0]) if len(near) else len(fx["trace"])
 
 
-def checkpoint(name):
-    """Add the image checkpoint (`ck_*` keys) to an existing fixture: the
-    oracle rerun with max_iterations = image_cap from the same inputs; its
-    trace is the full run's prefix (checked here). image_cap "near_tie" puts
-    the checkpoint at the fixture's first near-tie."""
+def checkpoint(name, key="image_cap", prefix="ck_"):
+    """Add the image checkpoint (`ck_*` keys; `ck2_*` for image_cap2) to an
+    existing fixture: the oracle rerun with max_iterations = image_cap from
+    the same inputs; its trace is the full run's prefix (checked here).
+    image_cap "near_tie" puts the checkpoint at the fixture's first
+    near-tie."""
     c = cp.CONFIGS[name]
     path = os.path.join(HERE, f"config_{name}.npz")
     out = dict(np.load(path))
@@ -128,7 +131,7 @@ def checkpoint(name):
     orc.set_threads(os.cpu_count() or 8)
     res, mod = dirty.copy(), np.zeros_like(dirty)
     st = settings(c)
-    cap = c["image_cap"]
+    cap = c[key]
     if cap == "near_tie":
         cap = first_near_tie(out)
     st["max_iterations"] = cap
@@ -139,9 +142,9 @@ def checkpoint(name):
     assert n == r.iteration_number == cap, (n, r.iteration_number)
     assert np.array_equal(trace, out["trace"][:n]), "checkpoint trace is not the full prefix"
     print(f"{name}: checkpoint at {n} components, oracle {time.time() - t0:.1f} s", flush=True)
-    out["ck_iterations"] = np.int64(n)
-    out.update({f"ck_{k}": v for k, v in image_summary("residual", res).items()})
-    out.update({f"ck_{k}": v for k, v in image_summary("model", mod).items()})
+    out[f"{prefix}iterations"] = np.int64(n)
+    out.update({f"{prefix}{k}": v for k, v in image_summary("residual", res).items()})
+    out.update({f"{prefix}{k}": v for k, v in image_summary("model", mod).items()})
     np.savez_compressed(path, **out)
 
 
@@ -150,6 +153,11 @@ if __name__ == "__main__":
     if args[:1] == ["--checkpoint"]:
         for name in args[1:]:
             checkpoint(name)
+    elif args[:1] == ["--checkpoint2"]:
+        for name in args[1:]:
+            checkpoint(name, "image_cap2", "ck2_")
     else:
-        for name in args or list(cp.CONFIGS):
+        # (t2k is bench.py's live to-threshold problem: no fixture)
+        for name in args or [n for n, c in cp.CONFIGS.items()
+                             if "cap" in c or "max_iterations" in c]:
             make(name)

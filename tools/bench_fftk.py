@@ -7,7 +7,8 @@ them (HIP-event times from the C-ABI's timing families):
        sparse model (ROWS non-zero rows), columns with the column-major PSF
        spectrum, rows inverse subtracting into the window
 
-    python tools/bench_fftk.py [reps] [case ...]     cases: f32 f64 f64_4096 f32_4096
+    python tools/bench_fftk.py [reps] [case ...]
+    cases: f32 f32_4096 f64 f64_window f64_colout f64_dense f64_4096
 
 Prints one line per family: average us per launch and the algorithmic GB/s
 (bytes as the C-ABI counts them).
@@ -69,7 +70,7 @@ def f32_case(s, n, reps):
         x.free()
 
 
-def f64_case(s, pn, n, reps, n_rows=300, out_layout=ROW_MAJOR, dense=False):
+def f64_case(s, pn, n, reps, n_rows=300, out_layout=ROW_MAJOR, dense=False, window=False):
     rng = np.random.default_rng(2)
     ox = oy = (pn - n) // 2
     psf = np.zeros((n, n), np.float32)
@@ -95,13 +96,20 @@ def f64_case(s, pn, n, reps, n_rows=300, out_layout=ROW_MAJOR, dense=False):
     timings(s)
     for _ in range(reps):
         s.rdl.rdl_conv_rows_forward_masked(c, dmod.vp, n, n, ox, oy, work.vp, dmask.vp)
-        s.rdl.rdl_conv_columns_ex(c, work.vp, work.vp if out_layout == ROW_MAJOR else out2.vp,
-                                  kspec.vp, 1, C.c_double(1.0 / (pn * pn)),
-                                  None if dense else dmask.vp, COL_MAJOR, out_layout)
+        if window:  # only the window's rows stored (rdl_conv_columns_window)
+            s.rdl.rdl_conv_columns_window(c, work.vp, work.vp, kspec.vp,
+                                          C.c_double(1.0 / (pn * pn)), dmask.vp, COL_MAJOR,
+                                          oy, n)
+        else:
+            s.rdl.rdl_conv_columns_ex(c, work.vp,
+                                      work.vp if out_layout == ROW_MAJOR else out2.vp,
+                                      kspec.vp, 1, C.c_double(1.0 / (pn * pn)),
+                                      None if dense else dmask.vp, COL_MAJOR, out_layout)
         if out_layout == ROW_MAJOR:
             s.rdl.rdl_conv_rows_inverse(c, work.vp, dres.vp, n, n, ox, oy, 1)
     s.sync()
-    tag = "col-major out" if out_layout != ROW_MAJOR else "dense" if dense else "correction"
+    tag = ("col-major out" if out_layout != ROW_MAJOR else "dense" if dense else
+           "window" if window else "correction")
     report(f"f64 {pn} {tag}", timings(s))
     s.rdl.rdl_conv_destroy(c)
     for x in (dpsf, dmod, dres, dmask, kspec, work, out2):
@@ -123,6 +131,8 @@ def main():
             f32_case(s, 4096, reps)
         elif case == "f64":
             f64_case(s, 9072, 8192, reps)
+        elif case == "f64_window":
+            f64_case(s, 9072, 8192, reps, window=True)
         elif case == "f64_colout":
             f64_case(s, 9072, 8192, reps, out_layout=COL_MAJOR)
         elif case == "f64_dense":
