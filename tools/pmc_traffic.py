@@ -39,14 +39,14 @@ FAMILY_KERNELS = {
     "integrate": r"^rdl::IntegrateKernel\(",
     "add": r"^rdl::AddKernel\(",
     # the LDS FFT engine: float32 scale convolutions (four-step columns)
-    "conv_cols": r"rdl::ff::(ColStepA|ColStepB|Columns<float)",
+    "conv_cols": r"rdl::ff::(ColStepA|ColStepB|ColStepBScales|ColStepAInv|Columns<float)",
     "conv_rows": r"rdl::ff::Rows(Inverse|Forward)<float",
 }
 # families whose kernels are shared with a sibling family: measured together,
 # over the summed launches and algorithmic bytes of both (the *_sparse
 # families count a lower bound: the skipped zero rows are not known on the host)
 GROUPS = {
-    "conv64_cols+conv64_cols_sparse": (r"rdl::ff::Columns(ConvD)?<(double|512u)",
+    "conv64_cols+conv64_cols_sparse": (r"rdl::ff::Columns(ConvD)?<(double|512u|1024u)",
                                        ("conv64_cols", "conv64_cols_sparse")),
     "conv64_rows+conv64_rows_sparse": (r"rdl::ff::Rows(Inverse|Forward)<double",
                                        ("conv64_rows", "conv64_rows_sparse")),
