@@ -6,6 +6,18 @@
 
 namespace rdl {
 
+// complex double -> complex float (the float kernel spectra of
+// rdl_conv_columns_window)
+__global__ __launch_bounds__(256) void NarrowComplexKernel(float2* __restrict__ dst,
+                                                           const double2* __restrict__ src,
+                                                           size_t n) {
+  for (size_t i = size_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += size_t(gridDim.x) * 256) {
+    const double2 v = src[i];
+    dst[i] = make_float2(float(v.x), float(v.y));
+  }
+}
+
+
 __global__ __launch_bounds__(256) void IntegrateKernel(rdl_integration g,
                                                        const float* images,
                                                        size_t n, float* dest) {
@@ -207,6 +219,16 @@ int rdl_box(rdl_session* s, float* d_dst, uint32_t dst_w, uint32_t dst_x,
   rdl::BoxKernel<<<unsigned(std::min<size_t>(16384, (total + 255) / 256)), 256, 0,
                    s->stream>>>(d_dst, dst_w, dst_x, dst_y, d_src, src_w, src_x,
                                 src_y, w, h, d_mask, op);
+  RDL_HIP_CHECK(hipGetLastError());
+  return RDL_OK;
+}
+
+int rdl_complex_narrow(rdl_session* s, void* d_dst, const void* d_src, size_t n_complex) {
+  RDL_ARG_CHECK(s && d_dst && d_src, "NULL argument");
+  if (n_complex == 0) return RDL_OK;
+  rdl::NarrowComplexKernel<<<unsigned(std::min<size_t>(16384, (n_complex + 255) / 256)), 256, 0,
+                             s->stream>>>(static_cast<float2*>(d_dst),
+                                          static_cast<const double2*>(d_src), n_complex);
   RDL_HIP_CHECK(hipGetLastError());
   return RDL_OK;
 }

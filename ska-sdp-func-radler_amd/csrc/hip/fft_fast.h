@@ -37,6 +37,7 @@ struct FastColumns {
   uint32_t threads;
   const void* kernel;
   RadixList radix;
+  const void* kernel_kf = nullptr;  // ColumnsConvD reading a float kernel spectrum
 };
 struct FastRows {
   uint32_t n;  // full row length (2 x the half-length transform)
@@ -135,7 +136,7 @@ int ConvColumnsDLaunch(rdl_session* s, const FastColumns* p, const void* in, voi
                        const void* kern, const void* tw, uint32_t n_cols, int kern_cm,
                        int out_cm, const uint32_t* rows, const uint32_t* n_rows, uint32_t row0,
                        uint32_t row_n, double scale, uint32_t out_row0 = 0,
-                       uint32_t out_row_n = 0xffffffffu);
+                       uint32_t out_row_n = 0xffffffffu, bool kernel_f32 = false);
 /* ascending list of the rows whose mask byte is non-zero, and its length */
 int FastCompactRows(rdl_session* s, const uint8_t* mask, uint32_t n, uint32_t* rows,
                     uint32_t* count);

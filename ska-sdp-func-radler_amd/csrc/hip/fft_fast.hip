@@ -25,6 +25,7 @@
 #include <map>
 #include <mutex>
 #include <tuple>
+#include <type_traits>
 #include <vector>
 
 #include "fft_dft.h"
@@ -181,6 +182,113 @@ template <uint32_t TH, uint32_t N, uint32_t SC, uint32_t NS, uint32_t R, uint32_
 __device__ __forceinline__ void FftL(Cx<float>* buf, const TwdLds& td, uint32_t tid) {
   PassL<TH, N, R, NS, SC>(buf, td, tid);
   if constexpr (sizeof...(Rest) > 0) FftL<TH, N, SC, NS * R, Rest...>(buf, td, tid);
+}
+
+// The same transform with its pass twiddles computed ONCE per workgroup (the
+// persistent row kernels transform many rows, and a thread's butterflies
+// are the same in every row): PassL's float values (double recurrence, each
+// power rounded once), kept in registers for a last pass with one butterfly
+// per thread and in a small LDS table [q NS + k] for every other pass with
+// twiddles. Same values, same arithmetic: bit-identical to FftL, without
+// its per-row double math (the row kernels' largest VALU cost).
+template <uint32_t NS, uint32_t R, uint32_t... Rest>
+constexpr uint32_t CachedTableSize(uint32_t th, uint32_t n) {
+  // entries of the LDS tables: every pass with NS > 1 except a last pass
+  // with one butterfly per thread (registers)
+  const bool last = sizeof...(Rest) == 0;
+  const bool regs = last && (n / R + th - 1) / th == 1;
+  const uint32_t here = (NS > 1 && !regs) ? NS * (R - 1) : 0;
+  if constexpr (sizeof...(Rest) > 0)
+    return here + CachedTableSize<NS * R, Rest...>(th, n);
+  else
+    return here;
+}
+
+template <uint32_t... Rs>
+constexpr uint32_t LastRadix() {
+  constexpr uint32_t r[] = {Rs...};
+  return r[sizeof...(Rs) - 1];
+}
+
+template <uint32_t TH, uint32_t N, uint32_t SC, uint32_t NS, uint32_t R, uint32_t... Rest>
+__device__ __forceinline__ void InitTwiddles(const TwdLds& td, Cx<float>* table, uint32_t off,
+                                             Cx<float>* last, uint32_t tid) {
+  constexpr uint32_t NB = N / R;
+  constexpr bool kLast = sizeof...(Rest) == 0;
+  constexpr bool kRegs = kLast && (NB + TH - 1) / TH == 1;
+  if constexpr (NS > 1) {
+    if constexpr (kRegs) {
+      const uint32_t k = tid % NS;
+      const Cx<double> w = TwD(td, k * (N / (NS * R)) * SC);
+      Cx<double> wr = w;
+      last[0] = ToF(wr);
+#pragma unroll
+      for (uint32_t r = 2; r < R; ++r) {
+        wr = Mul(wr, w);
+        last[r - 1] = ToF(wr);
+      }
+    } else {
+      for (uint32_t k = tid; k < NS; k += TH) {
+        const Cx<double> w = TwD(td, k * (N / (NS * R)) * SC);
+        Cx<double> wr = w;
+        table[off + k] = ToF(wr);
+        for (uint32_t r = 2; r < R; ++r) {
+          wr = Mul(wr, w);
+          table[off + (r - 1) * NS + k] = ToF(wr);
+        }
+      }
+    }
+  }
+  if constexpr (!kLast)
+    InitTwiddles<TH, N, SC, NS * R, Rest...>(td, table,
+                                             off + ((NS > 1 && !kRegs) ? NS * (R - 1) : 0), last,
+                                             tid);
+}
+
+template <uint32_t TH, uint32_t N, uint32_t R, uint32_t NS, bool kLast>
+__device__ __forceinline__ void PassC(Cx<float>* buf, const Cx<float>* table, uint32_t off,
+                                      const Cx<float>* last, uint32_t tid) {
+  constexpr uint32_t NB = N / R;
+  constexpr uint32_t BPT = (NB + TH - 1) / TH;
+  constexpr bool kRegs = kLast && BPT == 1;
+  Cx<float> v[BPT][R];
+#pragma unroll
+  for (uint32_t i = 0; i < BPT; ++i) {
+    const uint32_t j = tid + i * TH;
+    if (NB % TH == 0 || j < NB) {
+#pragma unroll
+      for (uint32_t r = 0; r < R; ++r) v[i][r] = buf[Lx<float>(j + r * NB)];
+    }
+  }
+  LdsSync();
+#pragma unroll
+  for (uint32_t i = 0; i < BPT; ++i) {
+    const uint32_t j = tid + i * TH;
+    if (NB % TH == 0 || j < NB) {
+      const uint32_t k = j % NS;
+      if constexpr (NS > 1) {
+#pragma unroll
+        for (uint32_t r = 1; r < R; ++r)
+          v[i][r] = Mul(v[i][r], kRegs ? last[r - 1] : table[off + (r - 1) * NS + k]);
+      }
+      Dft<float, int(R)>::Run(v[i]);
+      const uint32_t d = (j / NS) * NS * R + k;
+#pragma unroll
+      for (uint32_t r = 0; r < R; ++r) buf[Lx<float>(d + r * NS)] = v[i][r];
+    }
+  }
+  LdsSync();
+}
+
+template <uint32_t TH, uint32_t N, uint32_t NS, uint32_t R, uint32_t... Rest>
+__device__ __forceinline__ void FftC(Cx<float>* buf, const Cx<float>* table, uint32_t off,
+                                     const Cx<float>* last, uint32_t tid) {
+  constexpr bool kLast = sizeof...(Rest) == 0;
+  constexpr bool kRegs = kLast && (N / R + TH - 1) / TH == 1;
+  PassC<TH, N, R, NS, kLast>(buf, table, off, last, tid);
+  if constexpr (!kLast)
+    FftC<TH, N, NS * R, Rest...>(buf, table, off + ((NS > 1 && !kRegs) ? NS * (R - 1) : 0),
+                                 last, tid);
 }
 
 // ------------------------------------------------------------- columns
@@ -397,11 +505,14 @@ constexpr uint32_t LastOf() {
   return r[sizeof...(Rs) - 1];
 }
 
-template <uint32_t TH, uint32_t R1, uint32_t... Rs>
+// KF: the kernel spectrum stored as float complex (half the bytes of the
+// pass's largest read), widened to double where it is multiplied
+template <uint32_t TH, bool KF, uint32_t R1, uint32_t... Rs>
 __global__ __launch_bounds__(TH) void ColumnsConvD(ColArgs a, const Cx<double>* __restrict__ in,
-                                                   Cx<double>* out,
-                                                   const Cx<double>* __restrict__ kern,
+                                                   Cx<double>* out, const void* __restrict__ kern_v,
                                                    const Cx<double>* __restrict__ tw) {
+  using KT = std::conditional_t<KF, Cx<float>, Cx<double>>;
+  const KT* __restrict__ kern = static_cast<const KT*>(kern_v);
   constexpr uint32_t N = R1 * Product<Rs...>();
   constexpr uint32_t RL = LastOf<R1, Rs...>();
   constexpr uint32_t NBL = N / RL;  // last pass: butterflies, = its span
@@ -438,12 +549,17 @@ __global__ __launch_bounds__(TH) void ColumnsConvD(ColArgs a, const Cx<double>* 
     const uint32_t cc = active ? c : 0u;
     const Cx<double>* in_c = in + cc;
     const uint32_t k_stride = a.kern_cm ? 1u : a.ld;
-    const Cx<double>* kern_c = a.kern_cm ? kern + size_t(cc) * N : kern + cc;
+    const KT* kern_c = a.kern_cm ? kern + size_t(cc) * N : kern + cc;
+    auto kload = [&](uint32_t y) {
+      const KT k = kern_c[y * k_stride];
+      return Cx<double>{double(k.x), double(k.y)};
+    };
     // K x s in the last forward pass's output order: rows j + r NBL; held in
     // registers from the round's start (512 threads), or read where it is
     // multiplied (1024 threads: the registers go to the second set of waves)
-    constexpr bool KREG = TH <= 512;
-    Cx<double> K[KREG ? BL : 1][KREG ? RL : 1];
+    // (a float kernel fits registers at 1 024 threads too: half the VGPRs)
+    constexpr bool KREG = TH <= 512 || KF;
+    KT K[KREG ? BL : 1][KREG ? RL : 1];
     if constexpr (KREG) {
 #pragma unroll
       for (uint32_t i = 0; i < BL; ++i) {
@@ -463,9 +579,9 @@ __global__ __launch_bounds__(TH) void ColumnsConvD(ColArgs a, const Cx<double>* 
     auto mulk = [&](uint32_t i, uint32_t r, uint32_t y, Cx<double> v) {
       Cx<double> k;
       if constexpr (KREG)
-        k = K[i][r];
+        k = Cx<double>{double(K[i][r].x), double(K[i][r].y)};
       else
-        k = kern_c[(tid + i * TH + r * NBL) * k_stride];
+        k = kload(tid + i * TH + r * NBL);
       buf[y] = Conj(Scale(Mul(v, k), s));
     };
     CFwdTail<TH, N, R1, decltype(mulk), Rs...>(buf, t1, t2, tid, mulk);
@@ -527,8 +643,14 @@ __global__ __launch_bounds__(TH) void RowsInverse(RowArgs a, const Cx<T>* __rest
   __shared__ uint64_t red[TH / 64];  // fused peak search
   __shared__ Cx<double> tws[LT ? ND1 + kTwdLo : 1];
   TwdLds td{tws, tws + ND1};
+  // LT: the pass twiddles, made once per workgroup (FftC)
+  constexpr uint32_t NCT = LT ? CachedTableSize<1, Rs...>(TH, H) : 0;
+  __shared__ Cx<float> ctab[NCT > 0 ? NCT : 1];
+  Cx<float> clast[LT ? LastRadix<Rs...>() - 1 : 1];
   if constexpr (LT) {
     for (uint32_t i = threadIdx.x; i < ND1 + kTwdLo; i += TH) tws[i] = twd[i];
+    __syncthreads();
+    InitTwiddles<TH, H, 2, 1, Rs...>(td, ctab, 0, clast, threadIdx.x);
     __syncthreads();
   }
   // bins in pairs (k, H - k): every spectrum element is read once
@@ -593,23 +715,36 @@ __global__ __launch_bounds__(TH) void RowsInverse(RowArgs a, const Cx<T>* __rest
     if (iy + gridDim.x < a.img_h) prefetch(iy + gridDim.x, tid);
   LdsSync();
   if constexpr (LT)
-    FftL<TH, H, 2, 1, Rs...>(buf, td, tid);
+    FftC<TH, H, 1, Rs...>(buf, ctab, 0, clast, tid);
   else
     Fft<T, TH, H, 0, 1, Rs...>(buf, ptw, tid);
   float* o = out + size_t(iy) * a.img_w;
-  // fused peak search over the values as written (window coordinates)
+  // fused peak search over the values as written (window coordinates): per
+  // thread the largest PeakKey value word (0: none qualifies) and its first
+  // x, in 32-bit compares (a thread visits its x in ascending order, so the
+  // strict > keeps the first of equal values, as PeakKey's index word does);
+  // one 64-bit key per thread at the end of the row
   const bool peak = a.peak.partials != nullptr;
   const bool peak_row = peak && iy >= a.peak.ys && iy < a.peak.ye;
-  uint64_t best = 0;
+  const uint32_t pxs = a.peak.xs, pxn = a.peak.xe - a.peak.xs;
+  const uint8_t* mrow = a.peak.mask ? a.peak.mask + size_t(iy) * a.img_w : nullptr;
+  const uint32_t sign_mask = a.peak.allow_negative != 0 ? 0x7fffffffu : 0xffffffffu;
+  uint32_t best_u = 0u, best_x = 0u;
   auto consider = [&](uint32_t x, float v) {
-    if (peak_row && x >= a.peak.xs && x < a.peak.xe &&
-        (!a.peak.mask || a.peak.mask[size_t(iy) * a.img_w + x])) {
-      const uint64_t k = PeakKey(v, a.peak.allow_negative != 0, iy * a.img_w + x);
-      best = k > best ? k : best;
-    }
+    if (!peak_row) return;
+    const uint32_t u = __float_as_uint(v) & sign_mask;
+    const bool q = u > 0x00800000u && u <= 0x7f800000u && x - pxs < pxn &&
+                   (!mrow || mrow[x]);
+    const uint32_t uq = q ? u : 0u;
+    const bool better = uq > best_u;
+    best_u = better ? uq : best_u;
+    best_x = better ? x : best_x;
   };
   auto finish_peak = [&]() {
     if (!peak) return;
+    uint64_t best = best_u ? ((uint64_t(best_u) << 32) |
+                              uint64_t(0xffffffffu - (iy * a.img_w + best_x)))
+                           : 0ull;
     best = BlockMaxU64(best, red);
     if (tid == 0) a.peak.partials[iy] = best;
   };
@@ -677,6 +812,8 @@ __global__ __launch_bounds__(TH) void RowsForward(RowArgs a, const float* __rest
   Cx<T>* buf = reinterpret_cast<Cx<T>*>(lds_raw);
   __shared__ Cx<double> tws[LT ? ND1 + kTwdLo : 1];
   TwdLds td{tws, tws + ND1};
+  // (the per-row twiddle math stays: with the next row's input prefetched in
+  // registers, FftC's cached last-pass twiddles would cost a wave per SIMD)
   if constexpr (LT) {
     for (uint32_t i = threadIdx.x; i < ND1 + kTwdLo; i += TH) tws[i] = twd[i];
     __syncthreads();
@@ -1386,8 +1523,9 @@ const FastRows* FindFastRows(uint32_t n, bool f64) {
 #define RDL_CONV_D(TH, ...)                                                    \
   FastColumns {                                                                \
     ff::Product<__VA_ARGS__>(), true, TH,                                      \
-        reinterpret_cast<const void*>(&ff::ColumnsConvD<TH, __VA_ARGS__>),     \
-        MakeRadixList<__VA_ARGS__>()                                           \
+        reinterpret_cast<const void*>(&ff::ColumnsConvD<TH, false, __VA_ARGS__>), \
+        MakeRadixList<__VA_ARGS__>(),                                          \
+        reinterpret_cast<const void*>(&ff::ColumnsConvD<TH, true, __VA_ARGS__>)  \
   }
 const FastColumns* FindConvColumnsD(uint32_t n) {
   static const FastColumns kPlans[] = {
@@ -1519,9 +1657,15 @@ int FastColumnsLaunch(rdl_session* s, const FastColumns* p, const void* in, void
 int ConvColumnsDLaunch(rdl_session* s, const FastColumns* p, const void* in, void* out,
                        const void* kern, const void* tw, uint32_t n_cols, int kern_cm,
                        int out_cm, const uint32_t* rows, const uint32_t* n_rows, uint32_t row0,
-                       uint32_t row_n, double scale, uint32_t out_row0, uint32_t out_row_n) {
+                       uint32_t row_n, double scale, uint32_t out_row0, uint32_t out_row_n,
+                       bool kernel_f32) {
   const size_t lds = ConvColumnsDLdsBytes(p->n);
-  const int slots = SlotsPerCu(s, p->kernel, p->threads, lds);
+  const void* fn = kernel_f32 ? p->kernel_kf : p->kernel;
+  if (!fn) {
+    SetError("float64 correction columns: no float-kernel plan");
+    return RDL_ERR_UNSUPPORTED;
+  }
+  const int slots = SlotsPerCu(s, fn, p->threads, lds);
   if (slots < 0) {
     SetError("float64 correction columns: occupancy query failed");
     return RDL_ERR_HIP;
@@ -1543,8 +1687,7 @@ int ConvColumnsDLaunch(rdl_session* s, const FastColumns* p, const void* in, voi
   a.per_xcd = std::max<uint32_t>(1, (want + 7) / 8);
   const uint32_t grid = 8 * a.per_xcd;
   void* args[] = {&a, (void*)&in, (void*)&out, (void*)&kern, (void*)&tw};
-  RDL_HIP_CHECK(hipLaunchKernel(p->kernel, dim3(grid), dim3(p->threads), args, lds,
-                                s->stream));
+  RDL_HIP_CHECK(hipLaunchKernel(fn, dim3(grid), dim3(p->threads), args, lds, s->stream));
   return RDL_OK;
 }
 

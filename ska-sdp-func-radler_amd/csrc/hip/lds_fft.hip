@@ -1035,18 +1035,22 @@ int rdl_conv_columns_ex(rdl_conv* c, const void* d_in, void* d_out,
 
 int rdl_conv_columns_window(rdl_conv* c, const void* d_in, void* d_out,
                             const void* d_kernel, double scale, const uint8_t* d_row_mask,
-                            int kernel_layout, uint32_t out_row0, uint32_t out_rows) {
+                            int kernel_layout, uint32_t out_row0, uint32_t out_rows,
+                            int kernel_f32) {
   RDL_ARG_CHECK(c && d_in && d_out && d_kernel, "NULL argument");
   RDL_ARG_CHECK(uint64_t(out_row0) + out_rows <= c->height, "output rows outside the plane");
   RDL_ARG_CHECK(kernel_layout == RDL_CONV_ROW_MAJOR || kernel_layout == RDL_CONV_COL_MAJOR,
                 "bad kernel layout");
-  if (!c->f64 || !c->conv_cols || c->split)
+  const bool convd = c->f64 && c->conv_cols && !c->split;
+  RDL_ARG_CHECK(!kernel_f32 || convd, "a float kernel needs a float64 convolution-column plan");
+  if (!convd)
     return rdl_conv_columns_ex(c, d_in, d_out, d_kernel, 1, scale, d_row_mask, kernel_layout,
                                RDL_CONV_ROW_MAJOR);
   const double sb = SpectrumBytes(c);
   const double win = sb * double(out_rows) / double(c->height);
+  const double kb = kernel_f32 ? 0.5 * sb : sb;
   const char* fam = d_row_mask ? "conv64_cols_sparse" : "conv64_cols";
-  rdl::ScopedTiming t(c->s, fam, d_row_mask ? sb + win : 2.0 * sb + win);
+  rdl::ScopedTiming t(c->s, fam, d_row_mask ? kb + win : kb + sb + win);
   const uint32_t* rows = nullptr;
   const uint32_t* n_rows = nullptr;
   if (d_row_mask) {
@@ -1057,7 +1061,8 @@ int rdl_conv_columns_window(rdl_conv* c, const void* d_in, void* d_out,
   }
   return rdl::ConvColumnsDLaunch(c->s, c->conv_cols, d_in, d_out, d_kernel, c->tw_col,
                                  c->width / 2 + 1, kernel_layout == RDL_CONV_COL_MAJOR, 0, rows,
-                                 n_rows, 0, c->height, scale, out_row0, out_rows);
+                                 n_rows, 0, c->height, scale, out_row0, out_rows,
+                                 kernel_f32 != 0);
 }
 
 int rdl_conv_columns_layout(rdl_conv* c, const void* d_in, void* d_out,
@@ -1212,7 +1217,12 @@ int rdl_conv_forward_half(rdl_conv* c, const float* d_in, uint32_t in_w, uint32_
   RDL_TRY(EnsureSplitScratch(c, size_t(sb)));
   void* rows = c->scratch;
   RDL_TRY(rdl_conv_rows_forward(c, d_in, in_w, in_h, ox, oy, rows));
-  rdl::ScopedTiming t(c->s, "conv_cols", 2.0 * sb);
+  // algorithmic bytes (the one-pass minimum of the column work, counted per
+  // iteration as 2 sb for the forward columns + 2.5 sb per scale: spectrum
+  // read, real kernel read, result write), attributed to the three launches
+  // as A 1 sb, B* 1 + 1.5 sb per scale, A* 1 sb; the four-step passes move
+  // 2, 1 + 1.5 per scale and 2 (the intermediates): PMC shows the ratio
+  rdl::ScopedTiming t(c->s, "conv_cols", sb);
   return rdl::FastStepLaunch(c->s, c->steps, false, rows, d_half, nullptr, c->tw_col, c->ptw_a,
                              c->width / 2 + 1, 0, 1.0f);
 }
@@ -1227,7 +1237,8 @@ int rdl_conv_scales(rdl_conv* c, const void* d_half, uint32_t n_scales,
   for (uint32_t i = 0; i < n_scales; ++i)
     RDL_ARG_CHECK(d_kernels[i] && d_outs[i] && d_outs[i] != d_half, "bad kernel / output");
   const double sb = SpectrumBytes(c);
-  // the half read once; per scale a real kernel (half a spectrum) and a write
+  // algorithmic (see rdl_conv_forward_half): the forward columns' write, and
+  // per scale the spectrum and real-kernel reads
   rdl::ScopedTiming t(c->s, "conv_cols", sb + n_scales * 1.5 * sb);
   return rdl::FastScalesLaunch(c->s, c->steps, d_half, c->tw_col, c->ptw_b, c->width / 2 + 1,
                                n_scales, reinterpret_cast<const float* const*>(d_kernels),
@@ -1240,7 +1251,8 @@ int rdl_conv_scale_finish(rdl_conv* c, const void* d_in, void* d_out) {
     rdl::SetError("rdl_conv_scale_finish: needs a four-step (tiled) float plan");
     return RDL_ERR_UNSUPPORTED;
   }
-  rdl::ScopedTiming t(c->s, "conv_cols", 2.0 * SpectrumBytes(c));
+  // algorithmic (see rdl_conv_forward_half): the scale's result write
+  rdl::ScopedTiming t(c->s, "conv_cols", SpectrumBytes(c));
   return rdl::FastStepAInvLaunch(c->s, c->steps, d_in, d_out, c->ptw_a, c->width / 2 + 1);
 }
 

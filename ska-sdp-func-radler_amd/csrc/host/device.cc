@@ -254,7 +254,8 @@ void Fft::ForwardColumnMajor(const float* d_in, void* d_spectrum) {
 void Fft::ConvolveSubtract(const float* d_image, size_t img_w, size_t img_h,
                            size_t ox, size_t oy, const void* d_kernel_spectrum,
                            void* d_work, float* d_residual,
-                           const uint8_t* d_row_mask, bool kernel_col_major) {
+                           const uint8_t* d_row_mask, bool kernel_col_major,
+                           bool kernel_f32) {
   if (!conv_) throw std::logic_error("Fft::ConvolveSubtract needs the LDS engine");
   const double norm = 1.0 / (double(width_) * double(height_));
   if (d_row_mask)
@@ -270,7 +271,7 @@ void Fft::ConvolveSubtract(const float* d_image, size_t img_w, size_t img_h,
   Check(rdl_conv_columns_window(conv_, d_work, d_work, d_kernel_spectrum,
                                 f64_ ? norm : double(float(norm)), d_row_mask,
                                 kernel_col_major ? RDL_CONV_COL_MAJOR : RDL_CONV_ROW_MAJOR,
-                                uint32_t(oy), uint32_t(img_h)),
+                                uint32_t(oy), uint32_t(img_h), kernel_f32 ? 1 : 0),
         "rdl_conv_columns_window");
   Check(rdl_conv_rows_inverse(conv_, d_work, d_residual, uint32_t(img_w),
                               uint32_t(img_h), uint32_t(ox), uint32_t(oy), 1),

@@ -94,7 +94,7 @@ class Fft {
                         size_t ox, size_t oy, const void* d_kernel_spectrum,
                         void* d_work, float* d_residual,
                         const uint8_t* d_row_mask = nullptr,
-                        bool kernel_col_major = false);
+                        bool kernel_col_major = false, bool kernel_f32 = false);
   /// LDS engine only: forward spectrum stored column by column (column k at
   /// k * height), the layout the column pass reads contiguously.
   void ForwardColumnMajor(const float* d_in, void* d_spectrum);

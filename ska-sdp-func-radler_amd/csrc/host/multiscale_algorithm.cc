@@ -692,7 +692,7 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
         auto pc = padded_cache.find(key);
         if (pc == padded_cache.end())
           pc = padded_cache
-                   .emplace(key, SubMinorLoop::MakePaddedPsfSpectrum(
+                   .emplace(key, SubMinorLoop::MakeCorrectionPsfSpectrum(
                                      session, convolved[psf_index].Plane(scale_with_peak),
                                      width, height, conv_w, conv_h))
                    .first;

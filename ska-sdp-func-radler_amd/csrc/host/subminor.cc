@@ -1,5 +1,8 @@
 #include "subminor.h"
 
+#include <cstdlib>
+#include <string>
+
 #include <stdexcept>
 
 namespace radler::algorithms {
@@ -91,14 +94,32 @@ std::shared_ptr<gpu::Buffer> SubMinorLoop::MakePaddedPsfSpectrum(
   return spectrum;
 }
 
+bool SubMinorLoop::CorrectionKernelF32() {
+  const char* e = std::getenv("RDL_CORR_KERNEL");
+  return e && std::string(e) == "f32";
+}
+
+std::shared_ptr<gpu::Buffer> SubMinorLoop::MakeCorrectionPsfSpectrum(
+    gpu::Session& s, const float* d_psf, size_t width, size_t height, size_t pw, size_t ph) {
+  auto spectrum = MakePaddedPsfSpectrum(s, d_psf, width, height, pw, ph);
+  gpu::Fft& fft = s.GetFft(pw, ph, true);
+  if (!CorrectionKernelF32() || !fft.UsesLds() || fft.SplitColumns()) return spectrum;
+  const size_t n = fft.SpectrumBytes() / 16;
+  auto narrow = std::make_shared<gpu::Buffer>(s, n * 8);
+  gpu::Check(rdl_complex_narrow(s.Handle(), narrow->Ptr(), spectrum->Ptr(), n),
+             "rdl_complex_narrow");
+  s.Sync();
+  return narrow;
+}
+
 void SubMinorLoop::CorrectResidualDirty(size_t image_index, float* d_residual,
                                         const float* d_psf, size_t psf_key) {
   auto it = psf_spectra_.find(psf_key);
   if (it == psf_spectra_.end())
     it = psf_spectra_
-             .emplace(psf_key, MakePaddedPsfSpectrum(s_, d_psf, width_, height_,
-                                                     padded_width_,
-                                                     padded_height_))
+             .emplace(psf_key, MakeCorrectionPsfSpectrum(s_, d_psf, width_, height_,
+                                                         padded_width_,
+                                                         padded_height_))
              .first;
   CorrectResidualDirtyWithSpectrum(image_index, d_residual, it->second->Ptr());
 }
@@ -129,7 +150,7 @@ void SubMinorLoop::CorrectResidualDirtyWithSpectrum(size_t image_index,
                "rdl_subminor_model_masked");
     fft.ConvolveSubtract(model.F(), width_, height_, ox, oy, d_spectrum, work.Ptr(),
                          d_residual, static_cast<const uint8_t*>(rows.Ptr()),
-                         !fft.SplitColumns());
+                         !fft.SplitColumns(), CorrectionKernelF32() && !fft.SplitColumns());
     return;
   }
   gpu::Buffer& padded_ = s_.Scratch(gpu::Session::kCorrectionSpectrum,

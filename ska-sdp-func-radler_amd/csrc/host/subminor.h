@@ -68,6 +68,14 @@ class SubMinorLoop {
   static std::shared_ptr<gpu::Buffer> MakePaddedPsfSpectrum(
       gpu::Session& s, const float* d_psf, size_t width, size_t height,
       size_t padded_width, size_t padded_height);
+  /// The padded PSF spectrum as CorrectResidualDirty(WithSpectrum) reads it:
+  /// MakePaddedPsfSpectrum's float64 spectrum, or its float narrowing when
+  /// CorrectionKernelF32() (RDL_CORR_KERNEL=f32) and the LDS engine runs the
+  /// correction.
+  static std::shared_ptr<gpu::Buffer> MakeCorrectionPsfSpectrum(
+      gpu::Session& s, const float* d_psf, size_t width, size_t height,
+      size_t padded_width, size_t padded_height);
+  static bool CorrectionKernelF32();
 
   /// GetFullIndividualModel (subminor_loop.cc:186-193) into a zeroed W x H.
   void GetFullIndividualModel(size_t image_index, float* d_dest);
