@@ -579,7 +579,13 @@ int rdl_conv_columns_ex(rdl_conv* c, const void* d_in, void* d_out,
  * other rows unwritten; every other plan writes them all. */
 int rdl_conv_columns_window(rdl_conv* c, const void* d_in, void* d_out,
                             const void* d_kernel, double scale, const uint8_t* d_row_mask,
-                            int kernel_layout, uint32_t out_row0, uint32_t out_rows);
+                            int kernel_layout, uint32_t out_row0, uint32_t out_rows,
+                            int kernel_f32);
+/* kernel_f32 (float64 convolution-column plans only): d_kernel holds the
+ * kernel spectrum as float complex (rdl_complex_narrow of the float64 one),
+ * widened to double where it is multiplied. */
+/* d_dst[i] = (float complex) d_src[i], i < n_complex (double complex in). */
+int rdl_complex_narrow(rdl_session* s, void* d_dst, const void* d_src, size_t n_complex);
 /* As rdl_conv_columns_ex with the input layout too (in_layout
  * RDL_CONV_COL_MAJOR: a mode-2 spectrum stored as columns). Every layout
  * combination needs the compile-time-planned column kernels
@@ -598,6 +604,9 @@ int rdl_conv_columns_layout(rdl_conv* c, const void* d_in, void* d_out,
  * ((k / 16) * height + y) * 16 + k % 16; rdl_conv_spectrum_bytes covers the
  * padded last tile) and the layout arguments do not apply. */
 #define RDL_CONV_FAST_TILED 4
+/* float64 plans whose convolution columns run ff::ColumnsConvD (the only
+ * ones rdl_conv_columns_window's kernel_f32 applies to) */
+#define RDL_CONV_FAST_CONVD 8
 int rdl_conv_fast(const rdl_conv* c);
 
 /* Several scale convolutions of ONE float plane (FindActiveScaleConvolvedMaxima

@@ -1609,14 +1609,25 @@ int SlotsPerCu(rdl_session* s, const void* fn, uint32_t threads, size_t lds) {
   const auto key = std::make_tuple(fn, s->device, lds);
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
-  // (below the CU's LDS by the static arrays: the row kernels' reduction
-  // array for the fused peak search and the float rows' twiddle tables)
-  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          int(kFftLdsBytesFast - 4096)) != hipSuccess)
+  // (below the CU's LDS by the kernel's static arrays: the row kernels'
+  // reduction array for the fused peak search and the float rows' twiddle
+  // tables)
+  hipFuncAttributes attr{};
+  if (hipFuncGetAttributes(&attr, fn) != hipSuccess) {
+    (void)hipGetLastError();
     return -1;
+  }
+  if (attr.sharedSizeBytes >= kFftLdsBytesFast ||
+      hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          int(kFftLdsBytesFast - attr.sharedSizeBytes)) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, int(threads), lds) != hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, int(threads), lds) != hipSuccess) {
+    (void)hipGetLastError();
     return -1;
+  }
   cache[key] = std::max(n, 1);
   return cache[key];
 }

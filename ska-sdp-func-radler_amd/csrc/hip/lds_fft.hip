@@ -1103,7 +1103,8 @@ int rdl_conv_columns_layout(rdl_conv* c, const void* d_in, void* d_out,
 int rdl_conv_fast(const rdl_conv* c) {
   if (!c) return 0;
   return (c->fast_cols ? RDL_CONV_FAST_COLUMNS : 0) | (c->fast_rows ? RDL_CONV_FAST_ROWS : 0) |
-         (c->tiled ? RDL_CONV_FAST_TILED : 0);
+         (c->tiled ? RDL_CONV_FAST_TILED : 0) |
+         (c->f64 && c->conv_cols && !c->split ? RDL_CONV_FAST_CONVD : 0);
 }
 
 int rdl_conv_rows_inverse(rdl_conv* c, const void* d_spec, float* d_out,

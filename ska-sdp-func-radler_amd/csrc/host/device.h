@@ -122,6 +122,8 @@ class Fft {
   /// LDS engine with the split (four-step) column passes: spectra are read
   /// row-major, so ForwardColumnMajor is not used.
   bool SplitColumns() const { return conv_ && rdl_conv_columns_split(conv_); }
+  /// float64 convolution columns by ff::ColumnsConvD (float kernels allowed)
+  bool ConvColumnsD() const { return conv_ && (rdl_conv_fast(conv_) & RDL_CONV_FAST_CONVD); }
   /// Double-precision rocFFT plan only.
   void Forward64(const double* d_in, void* d_spectrum);
   void Convolve64(double* d_image, const void* d_kernel_spectrum);

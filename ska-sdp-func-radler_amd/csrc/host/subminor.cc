@@ -103,7 +103,7 @@ std::shared_ptr<gpu::Buffer> SubMinorLoop::MakeCorrectionPsfSpectrum(
     gpu::Session& s, const float* d_psf, size_t width, size_t height, size_t pw, size_t ph) {
   auto spectrum = MakePaddedPsfSpectrum(s, d_psf, width, height, pw, ph);
   gpu::Fft& fft = s.GetFft(pw, ph, true);
-  if (!CorrectionKernelF32() || !fft.UsesLds() || fft.SplitColumns()) return spectrum;
+  if (!CorrectionKernelF32() || !fft.ConvColumnsD()) return spectrum;
   const size_t n = fft.SpectrumBytes() / 16;
   auto narrow = std::make_shared<gpu::Buffer>(s, n * 8);
   gpu::Check(rdl_complex_narrow(s.Handle(), narrow->Ptr(), spectrum->Ptr(), n),
@@ -150,7 +150,7 @@ void SubMinorLoop::CorrectResidualDirtyWithSpectrum(size_t image_index,
                "rdl_subminor_model_masked");
     fft.ConvolveSubtract(model.F(), width_, height_, ox, oy, d_spectrum, work.Ptr(),
                          d_residual, static_cast<const uint8_t*>(rows.Ptr()),
-                         !fft.SplitColumns(), CorrectionKernelF32() && !fft.SplitColumns());
+                         !fft.SplitColumns(), CorrectionKernelF32() && fft.ConvColumnsD());
     return;
   }
   gpu::Buffer& padded_ = s_.Scratch(gpu::Session::kCorrectionSpectrum,
