@@ -48,6 +48,8 @@ struct FastRows {
   RadixList radix;  // of the half-length transform
   const void* inverse_lt;  // float: LDS double twiddles, persistent (else nullptr)
   const void* forward_lt;
+  const void* inverse_dma;  // float: ff::RowsInverseDma (else nullptr)
+  size_t inverse_dma_lds;   // its dynamic LDS bytes (all of its LDS)
 };
 
 /* float four-step column passes (column tiles of 16, see ff::TileIndex) */

@@ -557,8 +557,10 @@ __global__ __launch_bounds__(TH) void ColumnsConvD(ColArgs a, const Cx<double>* 
     // K x s in the last forward pass's output order: rows j + r NBL; held in
     // registers from the round's start (512 threads), or read where it is
     // multiplied (1024 threads: the registers go to the second set of waves)
-    // (a float kernel fits registers at 1 024 threads too: half the VGPRs)
-    constexpr bool KREG = TH <= 512 || KF;
+    // (register K before the forward transform costs more than it hides:
+    // the first pass's input loads then wait for it in order, vmcnt; with a
+    // float K at 1 024 threads: 623 -> 668 us per 9072^2 pass)
+    constexpr bool KREG = TH <= 512;
     KT K[KREG ? BL : 1][KREG ? RL : 1];
     if constexpr (KREG) {
 #pragma unroll
@@ -793,6 +795,157 @@ __global__ __launch_bounds__(TH) void RowsInverse(RowArgs a, const Cx<T>* __rest
   finish_peak();
   if constexpr (LT) LdsSync();
   }
+}
+
+// One 16-byte-per-lane LDS-DMA load (global_load_lds_dwordx4): lane i's 16 B
+// land at LDS byte `lds` + 16 i (lds wave-uniform, through m0). In inline asm
+// so the compiler does not treat it as an LDS write of unknown extent (see
+// RowsInverseDma); the caller retires it with its own s_waitcnt vmcnt and a
+// barrier before any wave reads those bytes.
+__device__ __forceinline__ void DmaLoad16(const void* g, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(g), "s"(lds)
+      : "memory");
+}
+
+// RowsInverse (float, tiled spectrum, write mode, even window) with the next
+// row's spectrum fetched by LDS-DMA while this row is transformed and
+// stored. The persistent row kernel above keeps one row per workgroup in
+// flight only while that workgroup loads it (a third of its time at three
+// workgroups per CU: ~3 TB/s); here every workgroup always has its next row
+// in flight (global_load_lds_dwordx4: a wave instruction moves 8 tiles x
+// 128 B, lane-linear into `raw`, no VGPRs), and the FFT runs in its own LDS
+// buffer. The DMA is retired by a counted vmcnt (the 16 output stores per
+// wave issued after it may stay in flight) and a barrier; every other
+// synchronisation is LDS-only, so nothing drains it early. Same arithmetic
+// as RowsInverse<float, TH, true> (FftC, zc, the fused peak search).
+template <uint32_t TH, uint32_t... Rs>
+__global__ __launch_bounds__(TH) void RowsInverseDma(RowArgs a, const Cx<float>* __restrict__ spec,
+                                                     float* __restrict__ out,
+                                                     const Cx<double>* __restrict__ twd) {
+  constexpr uint32_t H = Product<Rs...>();
+  constexpr uint32_t EH = H / TH;
+  static_assert(H % TH == 0 && (EH == 16 || EH == 8), "vmcnt counts of 8 or 16 stores");
+  constexpr uint32_t WAVES = TH / 64;
+  constexpr uint32_t ND1 = 2 * H / kTwdLo;
+  constexpr uint32_t NT = (H + 1 + kTile - 1) / kTile;  // spectrum tiles per row
+  constexpr uint32_t NI = (NT + 7) / 8;                 // DMA wave instructions per row
+  typedef __attribute__((address_space(3))) void* LdsPtr;
+  // The DMA target is its own __shared__ object; the transform, tables and
+  // reduction live in the dynamic array (RowsDmaLdsBytes). The DMA is issued
+  // by inline asm (DmaLoad16): hipcc cannot tell which LDS bytes a
+  // global_load_lds writes and, for its builtin, waits vmcnt(0) before the
+  // next LDS read whatever the arrays, which drained the prefetch at once.
+  __shared__ __attribute__((aligned(16))) Cx<float> raw[NI * 8 * kTile];
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  constexpr uint32_t NCT = CachedTableSize<1, Rs...>(TH, H);
+  Cx<float>* buf = reinterpret_cast<Cx<float>*>(lds_raw);             // the transform
+  Cx<double>* tws = reinterpret_cast<Cx<double>*>(buf + (H + (H >> kFastPadShift)));
+  Cx<float>* ctab = reinterpret_cast<Cx<float>*>(tws + ND1 + kTwdLo);
+  uint64_t* red = reinterpret_cast<uint64_t*>(ctab + (NCT > 0 ? (NCT + 1) / 2 * 2 : 2));
+  TwdLds td{tws, tws + ND1};
+  Cx<float> clast[LastRadix<Rs...>() - 1];
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  auto issue = [&](uint32_t iy) {
+    const size_t y = size_t(iy) + a.oy;
+    for (uint32_t j = wave; j < NI; j += WAVES) {
+      const uint32_t t = j * 8 + lane / 8;
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(
+          uint32_t(uintptr_t((LdsPtr)(raw + j * 8 * kTile))));
+      if (t < NT) DmaLoad16(spec + (size_t(t) * a.height + y) * kTile + (lane % 8) * 2, dst);
+    }
+  };
+  if (blockIdx.x < a.img_h) issue(blockIdx.x);
+  for (uint32_t i = threadIdx.x; i < ND1 + kTwdLo; i += TH) tws[i] = twd[i];
+  LdsSync();
+  InitTwiddles<TH, H, 2, 1, Rs...>(td, ctab, 0, clast, threadIdx.x);
+  constexpr uint32_t NP = H / 2 + 1;
+  constexpr uint32_t EP = (NP + TH - 1) / TH;
+  bool first = true;
+  for (uint32_t iy = blockIdx.x; iy < a.img_h; iy += gridDim.x) {
+    uint32_t tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));  // opaque per row (see Columns)
+    // this row's DMA (issued a row ago) landed; the previous row's EH stores
+    // per wave, issued after it, may still be in flight
+    if (first)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (EH == 16)
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    first = false;
+    LdsSync();
+    auto zc = [&](Cx<float> xk, Cx<float> xm, uint32_t k) {
+      const Cx<float> sum = {xk.x + xm.x, xk.y - xm.y};
+      const Cx<float> dif = {xk.x - xm.x, xk.y + xm.y};
+      const Cx<float> wk = ToF(TwD(td, k));
+      const Cx<float> t = Mul(Conj(wk), dif);
+      return Cx<float>{sum.x - t.y, -(sum.y + t.x)};
+    };
+#pragma unroll
+    for (uint32_t i = 0; i < EP; ++i) {
+      const uint32_t k = tid + i * TH;
+      if (NP % TH != 0 && k >= NP) continue;
+      const uint32_t m = H - k;
+      Cx<float> xk = raw[k], xm = raw[m];
+      if (k == 0) {  // C2R ignores the imaginary parts of X[0] and X[H]
+        xk.y = 0.0f;
+        xm.y = 0.0f;
+      }
+      buf[Lx<float>(k)] = zc(xk, xm, k);
+      if (k != 0 && m != k) buf[Lx<float>(m)] = zc(xm, xk, m);
+    }
+    LdsSync();  // raw is read: the next row's DMA may overwrite it
+    if (iy + gridDim.x < a.img_h) issue(iy + gridDim.x);
+    FftC<TH, H, 1, Rs...>(buf, ctab, 0, clast, tid);
+    float* o = out + size_t(iy) * a.img_w;
+    const bool peak = a.peak.partials != nullptr;
+    const bool peak_row = peak && iy >= a.peak.ys && iy < a.peak.ye;
+    const uint32_t pxs = a.peak.xs, pxn = a.peak.xe - a.peak.xs;
+    const uint8_t* mrow = a.peak.mask ? a.peak.mask + size_t(iy) * a.img_w : nullptr;
+    const uint32_t sign_mask = a.peak.allow_negative != 0 ? 0x7fffffffu : 0xffffffffu;
+    uint32_t best_u = 0u, best_x = 0u;
+    auto consider = [&](uint32_t x, float v) {
+      if (!peak_row) return;
+      const uint32_t u = __float_as_uint(v) & sign_mask;
+      const bool q = u > 0x00800000u && u <= 0x7f800000u && x - pxs < pxn &&
+                     (!mrow || mrow[x]);
+      const uint32_t uq = q ? u : 0u;
+      const bool better = uq > best_u;
+      best_u = better ? uq : best_u;
+      best_x = better ? x : best_x;
+    };
+    // the whole plane row is the window (the launcher's condition): every
+    // thread stores EH float2, in ascending x
+#pragma unroll
+    for (uint32_t i = 0; i < EH; ++i) {
+      const uint32_t n = tid + i * TH;
+      const Cx<float> z = buf[Lx<float>(n)];
+      const float2 v = {z.x, -z.y};
+      reinterpret_cast<float2*>(o)[n] = v;
+      consider(2 * n, v.x);
+      consider(2 * n + 1, v.y);
+    }
+    if (peak) {
+      uint64_t best = best_u ? ((uint64_t(best_u) << 32) |
+                                uint64_t(0xffffffffu - (iy * a.img_w + best_x)))
+                             : 0ull;
+      best = WaveMaxU64(best);
+      if (lane == 0) red[wave] = best;
+      LdsSync();
+      if (tid < 64) {
+        uint64_t w = lane < WAVES ? red[lane] : 0ull;
+        w = WaveMaxU64(w);
+        if (tid == 0) a.peak.partials[iy] = w;
+      }
+    }
+    LdsSync();  // the row's LDS reads (buf, red) before the next row's writes
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // real plane rows (the window's image rows, zero outside) -> spectrum rows
@@ -1321,8 +1474,38 @@ __global__ __launch_bounds__(1024) void CompactRows(const uint8_t* __restrict__ 
         reinterpret_cast<const void*>(&ff::RowsInverse<T, TH, false, __VA_ARGS__>),    \
         reinterpret_cast<const void*>(&ff::RowsForward<T, TH, false, __VA_ARGS__>),    \
         MakeRadixList<__VA_ARGS__>(), RowsLt<T, TH, __VA_ARGS__>(true),                \
-        RowsLt<T, TH, __VA_ARGS__>(false)                                              \
+        RowsLt<T, TH, __VA_ARGS__>(false), RowsDma<T, TH, __VA_ARGS__>(),             \
+        RowsDmaLds<T, TH, __VA_ARGS__>()                                               \
   }
+
+// the LDS-DMA inverse rows (float, 8 or 16 output pairs per thread) and
+// their one dynamic LDS array (RowsInverseDma's layout)
+template <uint32_t TH, uint32_t... Rs>
+constexpr size_t RowsDmaLdsBytes() {
+  constexpr uint32_t H = ff::Product<Rs...>();
+  constexpr uint32_t NT = (H + 1 + ff::kTile - 1) / ff::kTile;
+  constexpr uint32_t NI = (NT + 7) / 8;
+  constexpr uint32_t NCT = ff::CachedTableSize<1, Rs...>(TH, H);
+  (void)NI;  // (the DMA target is a static array of the kernel)
+  return size_t(H + (H >> kFastPadShift)) * 8 +
+         size_t(2 * H / ff::kTwdLo + ff::kTwdLo) * 16 + size_t(NCT > 0 ? (NCT + 1) / 2 * 2 : 2) * 8 +
+         size_t(TH / 64) * 8;
+}
+template <typename T, uint32_t TH, uint32_t... Rs>
+size_t RowsDmaLds() {
+  if constexpr (sizeof(T) == 4)
+    return RowsDmaLdsBytes<TH, Rs...>();
+  else
+    return 0;
+}
+template <typename T, uint32_t TH, uint32_t... Rs>
+const void* RowsDma() {
+  constexpr uint32_t H = ff::Product<Rs...>();
+  if constexpr (sizeof(T) == 4 && H % TH == 0 && (H / TH == 16 || H / TH == 8))
+    return reinterpret_cast<const void*>(&ff::RowsInverseDma<TH, Rs...>);
+  else
+    return nullptr;
+}
 
 // the float row kernels with LDS double twiddles (none for double)
 template <typename T, uint32_t TH, uint32_t... Rs>
@@ -1717,6 +1900,36 @@ int FastRowsInverseLaunch(rdl_session* s, const FastRows* p, const void* spec, f
                           const void* tw, const void* ptw, uint32_t height, uint32_t img_w, uint32_t img_h,
                           uint32_t ox, uint32_t oy, int subtract, int tiled, const RowPeak* peak,
                           const void* twd) {
+  // the LDS-DMA kernel: a tiled float spectrum written whole into the
+  // window (RDL_ROWS_DMA=0: the persistent row kernel)
+  static const bool dma_on = [] {
+    const char* e = std::getenv("RDL_ROWS_DMA");
+    return !(e && e[0] == '0');
+  }();
+  const uint32_t half = p->n / 2;
+  if (dma_on && p->inverse_dma && twd && RowTwiddlesInLds() && tiled && !subtract && ox == 0 && img_w == p->n &&
+      img_h > 0) {
+    const size_t lds = p->inverse_dma_lds;
+    const int slots = SlotsPerCu(s, p->inverse_dma, p->threads, lds);
+    if (slots < 0) {
+      SetError("fast FFT rows (DMA): occupancy query failed");
+      return RDL_ERR_HIP;
+    }
+    ff::RowArgs a{};
+    a.height = height;
+    a.ld = half + 1;
+    a.img_w = img_w;
+    a.img_h = img_h;
+    a.ox = ox;
+    a.oy = oy;
+    a.tiled = 1;
+    if (peak) a.peak = *peak;
+    const uint32_t grid = std::min<uint32_t>(img_h, uint32_t(s->n_cus) * uint32_t(slots));
+    void* args[] = {&a, (void*)&spec, (void*)&out, (void*)&twd};
+    RDL_HIP_CHECK(hipLaunchKernel(p->inverse_dma, dim3(grid), dim3(p->threads), args, lds,
+                                  s->stream));
+    return RDL_OK;
+  }
   const size_t lds = FastLdsBytes(p->n / 2, p->f64);
   const bool lt = p->inverse_lt && twd && RowTwiddlesInLds();
   const void* fn = lt ? p->inverse_lt : p->inverse;
