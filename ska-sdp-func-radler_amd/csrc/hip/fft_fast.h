@@ -49,7 +49,9 @@ struct FastRows {
   const void* inverse_lt;  // float: LDS double twiddles, persistent (else nullptr)
   const void* forward_lt;
   const void* inverse_dma;  // float: ff::RowsInverseDma (else nullptr)
-  size_t inverse_dma_lds;   // its dynamic LDS bytes (all of its LDS)
+  size_t inverse_dma_lds;   // its dynamic LDS bytes
+  const void* forward_dma;  // float: ff::RowsForwardDma (else nullptr)
+  size_t forward_dma_lds;
 };
 
 /* float four-step column passes (column tiles of 16, see ff::TileIndex) */

@@ -1059,6 +1059,90 @@ __global__ __launch_bounds__(TH) void RowsForward(RowArgs a, const float* __rest
   }
 }
 
+// RowsForward (float, whole plane rows -> tiled spectrum) with the next
+// image row fetched by LDS-DMA (DmaLoad16: a wave instruction moves 256
+// contiguous floats) while this row is transformed and stored, and the pass
+// twiddles made once per workgroup (FftC; the register prefetch of the
+// persistent kernel left no room for them). The vmcnt count: every wave
+// issues at least 2 (EP - 1) >= 16 spectrum stores after the DMA. Same
+// arithmetic as RowsForward<float, TH, true>.
+template <uint32_t TH, uint32_t... Rs>
+__global__ __launch_bounds__(TH) void RowsForwardDma(RowArgs a, const float* __restrict__ in,
+                                                     Cx<float>* __restrict__ spec,
+                                                     const Cx<double>* __restrict__ twd) {
+  constexpr uint32_t H = Product<Rs...>();
+  constexpr uint32_t EH = H / TH;
+  constexpr uint32_t NP = H / 2 + 1;
+  constexpr uint32_t EP = (NP + TH - 1) / TH;
+  static_assert(H % TH == 0 && (EH == 16 || EH == 8) && 2 * (EP - 1) >= EH,
+                "vmcnt counts of 8 or 16 stores");
+  constexpr uint32_t WAVES = TH / 64;
+  constexpr uint32_t ND1 = 2 * H / kTwdLo;
+  constexpr uint32_t NI = 2 * H / 256;  // DMA wave instructions per row (256 floats each)
+  typedef __attribute__((address_space(3))) void* LdsPtr;
+  __shared__ __attribute__((aligned(16))) float raw[2 * H];  // the DMA target (see RowsInverseDma)
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  constexpr uint32_t NCT = CachedTableSize<1, Rs...>(TH, H);
+  Cx<float>* buf = reinterpret_cast<Cx<float>*>(lds_raw);
+  Cx<double>* tws = reinterpret_cast<Cx<double>*>(buf + (H + (H >> kFastPadShift)));
+  Cx<float>* ctab = reinterpret_cast<Cx<float>*>(tws + ND1 + kTwdLo);
+  TwdLds td{tws, tws + ND1};
+  Cx<float> clast[LastRadix<Rs...>() - 1];
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  auto issue = [&](uint32_t y) {
+    const float* row = in + size_t(y) * a.img_w;
+    for (uint32_t j = wave; j < NI; j += WAVES) {
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(
+          uint32_t(uintptr_t((LdsPtr)(raw + j * 256))));
+      DmaLoad16(row + j * 256 + lane * 4, dst);
+    }
+  };
+  for (uint32_t i = threadIdx.x; i < ND1 + kTwdLo; i += TH) tws[i] = twd[i];
+  if (blockIdx.x < a.height) issue(blockIdx.x);
+  LdsSync();
+  InitTwiddles<TH, H, 2, 1, Rs...>(td, ctab, 0, clast, threadIdx.x);
+  bool first = true;
+  for (uint32_t y = blockIdx.x; y < a.height; y += gridDim.x) {
+    uint32_t tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));  // opaque per row (see Columns)
+    if (first)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (EH == 16)
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    first = false;
+    LdsSync();
+#pragma unroll
+    for (uint32_t i = 0; i < EH; ++i) {
+      const uint32_t n = tid + i * TH;
+      const float2 v = reinterpret_cast<const float2*>(raw)[n];
+      buf[Lx<float>(n)] = {v.x, v.y};
+    }
+    LdsSync();  // raw is read: the next row's DMA may overwrite it
+    if (y + gridDim.x < a.height) issue(y + gridDim.x);
+    FftC<TH, H, 1, Rs...>(buf, ctab, 0, clast, tid);
+    const float h = 0.5f;
+    auto put = [&](uint32_t k, Cx<float> zk, Cx<float> zc) {
+      const Cx<float> ev = {h * (zk.x + zc.x), h * (zk.y + zc.y)};
+      const Cx<float> od = {h * (zk.y - zc.y), -h * (zk.x - zc.x)};  // (zk - zc) / 2i
+      const Cx<float> wk = ToF(TwD(td, k));
+      spec[TileIndex(y, k, a.height)] = Add(ev, Mul(wk, od));
+    };
+#pragma unroll
+    for (uint32_t i = 0; i < EP; ++i) {
+      const uint32_t k = tid + i * TH;
+      if (NP % TH != 0 && k >= NP) continue;
+      const Cx<float> zlo = buf[Lx<float>(k)];
+      const Cx<float> zhi = k == 0 ? zlo : buf[Lx<float>(H - k)];
+      put(k, zlo, Conj(zhi));
+      if (H - k != k) put(H - k, zhi, Conj(zlo));
+    }
+    LdsSync();
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // ------------------------------------------- four-step column passes
 // A column transform of length N = N1 * N2 (float, tiled layout) as two
 // passes that each move whole 128-B lines (the one-pass column kernel reads
@@ -1475,7 +1559,8 @@ __global__ __launch_bounds__(1024) void CompactRows(const uint8_t* __restrict__ 
         reinterpret_cast<const void*>(&ff::RowsForward<T, TH, false, __VA_ARGS__>),    \
         MakeRadixList<__VA_ARGS__>(), RowsLt<T, TH, __VA_ARGS__>(true),                \
         RowsLt<T, TH, __VA_ARGS__>(false), RowsDma<T, TH, __VA_ARGS__>(),             \
-        RowsDmaLds<T, TH, __VA_ARGS__>()                                               \
+        RowsDmaLds<T, TH, __VA_ARGS__>(), RowsFwdDma<T, TH, __VA_ARGS__>(),             \
+        RowsFwdDmaLds<T, TH, __VA_ARGS__>()                                            \
   }
 
 // the LDS-DMA inverse rows (float, 8 or 16 output pairs per thread) and
@@ -1495,6 +1580,31 @@ template <typename T, uint32_t TH, uint32_t... Rs>
 size_t RowsDmaLds() {
   if constexpr (sizeof(T) == 4)
     return RowsDmaLdsBytes<TH, Rs...>();
+  else
+    return 0;
+}
+template <uint32_t TH, uint32_t... Rs>
+constexpr size_t RowsFwdDmaLdsBytes() {
+  constexpr uint32_t H = ff::Product<Rs...>();
+  constexpr uint32_t NCT = ff::CachedTableSize<1, Rs...>(TH, H);
+  return size_t(H + (H >> kFastPadShift)) * 8 + size_t(2 * H / ff::kTwdLo + ff::kTwdLo) * 16 +
+         size_t(NCT > 0 ? NCT : 1) * 8;
+}
+template <typename T, uint32_t TH, uint32_t... Rs>
+const void* RowsFwdDma() {
+  constexpr uint32_t H = ff::Product<Rs...>();
+  constexpr uint32_t NP = H / 2 + 1;
+  constexpr uint32_t EP = (NP + TH - 1) / TH;
+  if constexpr (sizeof(T) == 4 && H % TH == 0 && (H / TH == 16 || H / TH == 8) &&
+                2 * (EP - 1) >= H / TH)
+    return reinterpret_cast<const void*>(&ff::RowsForwardDma<TH, Rs...>);
+  else
+    return nullptr;
+}
+template <typename T, uint32_t TH, uint32_t... Rs>
+size_t RowsFwdDmaLds() {
+  if constexpr (sizeof(T) == 4)
+    return RowsFwdDmaLdsBytes<TH, Rs...>();
   else
     return 0;
 }
@@ -1970,6 +2080,33 @@ int FastRowsForwardLaunch(rdl_session* s, const FastRows* p, const float* in, vo
                           const void* tw, const void* ptw, uint32_t height, uint32_t img_w, uint32_t img_h,
                           uint32_t ox, uint32_t oy, const uint32_t* rows,
                           const uint32_t* n_rows, int tiled, const void* twd) {
+  // the LDS-DMA kernel: a whole float plane into a tiled spectrum
+  // (RDL_ROWS_DMA=0: the persistent row kernel)
+  static const bool dma_on = [] {
+    const char* e = std::getenv("RDL_ROWS_DMA");
+    return !(e && e[0] == '0');
+  }();
+  if (dma_on && p->forward_dma && twd && RowTwiddlesInLds() && tiled && !rows && ox == 0 &&
+      oy == 0 && img_w == p->n && img_h == height && height > 0) {
+    const size_t lds = p->forward_dma_lds;
+    const int slots = SlotsPerCu(s, p->forward_dma, p->threads, lds);
+    if (slots < 0) {
+      SetError("fast FFT rows (DMA): occupancy query failed");
+      return RDL_ERR_HIP;
+    }
+    ff::RowArgs a{};
+    a.height = height;
+    a.ld = p->n / 2 + 1;
+    a.img_w = img_w;
+    a.img_h = img_h;
+    a.tiled = 1;
+    a.all_rows = 1;
+    const uint32_t grid = std::min<uint32_t>(height, uint32_t(s->n_cus) * uint32_t(slots));
+    void* args[] = {&a, (void*)&in, (void*)&spec, (void*)&twd};
+    RDL_HIP_CHECK(hipLaunchKernel(p->forward_dma, dim3(grid), dim3(p->threads), args, lds,
+                                  s->stream));
+    return RDL_OK;
+  }
   const size_t lds = FastLdsBytes(p->n / 2, p->f64);
   const bool lt = p->forward_lt && twd && RowTwiddlesInLds();
   const void* fn = lt ? p->forward_lt : p->forward;

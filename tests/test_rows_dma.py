@@ -1,7 +1,7 @@
-"""The LDS-DMA inverse rows (ff::RowsInverseDma: the next row's tiled
-spectrum fetched by global_load_lds while this row is transformed) against
-the persistent row kernel they replace (RDL_ROWS_DMA=0): the same
-arithmetic, so the images are bit-identical and the fused peak searches
+"""The LDS-DMA row kernels (ff::RowsInverseDma / RowsForwardDma: the next
+row fetched by global_load_lds while this row is transformed) against the
+persistent row kernels they replace (RDL_ROWS_DMA=0): the same arithmetic,
+so the spectra and images are bit-identical and the fused peak searches
 return the same peaks. The switch is read once per process, so each side
 runs in its own process (one at a time)."""
 import os
@@ -35,8 +35,9 @@ img[h // 2, w // 2] = -55.0
 di = s.array(img)
 spec = s.array(shape=(nb // 8,), dtype=np.complex64)
 work = s.array(shape=(nb // 8,), dtype=np.complex64)
+s.rdl.rdl_conv_rows_forward(c, di.vp, w, h, 0, 0, spec.vp)
+res = {"rows_spectrum": spec.get()}
 s.rdl.rdl_conv_forward(c, di.vp, spec.vp)
-res = {}
 for neg in (0, 1):
     out = s.array(shape=(h, w))
     s.rdl.rdl_memcpy_d2d(s.h, work.vp, spec.vp, C.c_size_t(nb))
@@ -64,6 +65,8 @@ def run_side(tmp_path, w, h, dma):
 def test_rows_dma_bit_identical(tmp_path, w, h):
     a = run_side(tmp_path, w, h, True)
     b = run_side(tmp_path, w, h, False)
+    # the forward rows (RowsForwardDma) of the whole plane
+    assert np.array_equal(a["rows_spectrum"].view(np.uint32), b["rows_spectrum"].view(np.uint32))
     for neg in (0, 1):
         ia, ib = a[f"img{neg}"], b[f"img{neg}"]
         assert np.array_equal(ia.view(np.uint32), ib.view(np.uint32)), neg
