@@ -82,6 +82,71 @@ class OpenList {
   std::vector<uint64_t> load_;
 };
 
+// The same heap on one array of 8-byte items (cost bits << 32 | payload):
+// the comparisons read only the cost half, so equal costs pop exactly as in
+// OpenList (the pushed costs are finite and non-negative, where the float
+// order and the bit order agree), and a comparison and its move touch one
+// cache line instead of two. The pop's walk to a leaf takes two levels a
+// round with the grandchildren prefetched.
+class PackedOpenList {
+ public:
+  explicit PackedOpenList(size_t reserve) : item_(std::max<size_t>(reserve, 64)) {}
+  bool Empty() const { return n_ == 0; }
+  uint64_t Top() const { return item_[0]; }
+  void Push(uint64_t x) {
+    if (n_ == item_.size()) item_.resize(2 * n_);
+    uint64_t* a = item_.data();
+    size_t hole = n_++;
+    const uint32_t c = Key(x);
+    while (hole > 0) {  // __push_heap
+      const size_t parent = (hole - 1) / 2;
+      if (!(Key(a[parent]) > c)) break;
+      a[hole] = a[parent];
+      hole = parent;
+    }
+    a[hole] = x;
+  }
+  void Pop() {
+    const size_t len = --n_;
+    uint64_t* a = item_.data();
+    const uint64_t v = a[len];
+    size_t hole = 0, child = 0;
+    if (len > 2) {  // __adjust_heap: the hole walks to a leaf
+      const size_t lim = (len - 1) / 2;
+      while (child < lim) {
+        const size_t c0 = 2 * child + 1;
+        __builtin_prefetch(a + 2 * c0 + 1);
+        child = c0 + 1 - (Key(a[c0 + 1]) > Key(a[c0]));
+        a[hole] = a[child];
+        hole = child;
+        if (!(child < lim)) break;
+        const size_t d0 = 2 * child + 1;
+        child = d0 + 1 - (Key(a[d0 + 1]) > Key(a[d0]));
+        a[hole] = a[child];
+        hole = child;
+      }
+    }
+    if (len > 0 && (len & 1) == 0 && child == (len - 2) / 2) {
+      child = 2 * child + 2;
+      a[hole] = a[child - 1];
+      hole = child - 1;
+    }
+    const uint32_t c = Key(v);
+    while (hole > 0) {  // __push_heap of the former last item
+      const size_t parent = (hole - 1) / 2;
+      if (!(Key(a[parent]) > c)) break;
+      a[hole] = a[parent];
+      hole = parent;
+    }
+    a[hole] = v;
+  }
+
+ private:
+  static uint32_t Key(uint64_t x) { return uint32_t(x >> 32); }
+  std::vector<uint64_t> item_;
+  size_t n_ = 0;
+};
+
 // payload: target (u, v) and predecessor (pu, pv), 16 bits each
 inline uint64_t Load(uint32_t u, uint32_t v, uint32_t pu, uint32_t pv) {
   return uint64_t(u) | (uint64_t(v) << 16) | (uint64_t(pu) << 32) | (uint64_t(pv) << 48);
@@ -248,6 +313,92 @@ bool DivideByKeyOrder(const float* image, float* output, size_t width, size_t he
   return true;
 }
 
+// The reference's search (dijkstra_splitter.cc:34-86 / :88-142) with its
+// heap's exact pop order, on PackedOpenList. An entry's payload is its
+// target as a band-local index (u * band + v - lo; u = n_u past the last
+// row) times 8 plus a code for the predecessor, which is always the target
+// itself (a start entry) or one of five neighbours; the settled pixels keep
+// the code (one byte) instead of the predecessor's coordinates. Needs
+// (n_u + 1) * band < 2^29; false (output untouched) otherwise.
+enum : uint32_t {  // predecessor of target (u, v)
+  kFromUpNext = 0,   // (u - 1, v + 1)
+  kFromNext = 1,     // (u, v + 1)
+  kFromUp = 2,       // (u - 1, v)
+  kFromUpPrev = 3,   // (u - 1, v - 1)
+  kFromPrev = 4,     // (u, v - 1)
+  kFromStart = 5,    // (u, v) itself
+};
+
+template <bool kVertical>
+bool DivideExactPacked(const float* image, float* output, size_t width, size_t height,
+                       size_t lo, size_t hi, std::atomic<int>* race) {
+  const size_t n_u = kVertical ? height : width;
+  const size_t band = hi - lo;
+  if (band == 0 || (n_u + 1) * band >= (size_t(1) << 29)) return false;
+  auto pixel = [&](size_t u, size_t v) -> size_t {
+    return kVertical ? u * width + v : v * width + u;
+  };
+  std::vector<float> weight(band * n_u);
+  std::vector<float> dist(band * n_u, std::numeric_limits<float>::max());
+  for (size_t u = 0; u != n_u; ++u)
+    for (size_t v = lo; v != hi; ++v) weight[u * band + (v - lo)] = std::fabs(image[pixel(u, v)]);
+  std::unique_ptr<uint8_t[]> back(new uint8_t[band * n_u]);  // written when settled
+  PackedOpenList open(8 * band);
+  for (size_t v = 0; v != band; ++v) open.Push(uint64_t(v) << 3 | kFromStart);
+  const size_t n_settle = n_u * band;
+  // the last entry popped: its predecessor starts the trace (the entry past
+  // the last row, or, when none gets there, the last one the queue held)
+  size_t end_at = 0;
+  uint32_t end_code = kFromStart;
+  for (uint32_t poll = 0; !open.Empty();) {
+    if (race && ++poll == 0x1000u) {  // cancelled by a key-order result
+      poll = 0;
+      if (race->load(std::memory_order_relaxed) == 1) return true;
+    }
+    const uint64_t top = open.Top();
+    open.Pop();
+    const size_t at = size_t(uint32_t(top) >> 3);
+    const uint32_t code = uint32_t(top) & 7u;
+    end_at = at;
+    end_code = code;
+    if (at >= n_settle) break;  // an entry past the last row ends the search
+    const float cost = KeyFloat(uint32_t(top >> 32)) + weight[at];
+    if (!(cost < dist[at])) continue;
+    dist[at] = cost;
+    back[at] = uint8_t(code);
+    const uint64_t key = uint64_t(KeyBits(cost)) << 32;
+    const size_t v = at % band;
+    const uint64_t down = uint64_t(at + band) << 3;
+    if (v > 0) {
+      open.Push(key | (down - 8) | kFromUpNext);
+      open.Push(key | (uint64_t(at - 1) << 3) | kFromNext);
+    }
+    open.Push(key | down | kFromUp);
+    if (v + 1 < band) {
+      open.Push(key | (down + 8) | kFromUpPrev);
+      open.Push(key | (uint64_t(at + 1) << 3) | kFromPrev);
+    }
+  }
+  int running = 0;
+  if (race && !race->compare_exchange_strong(running, 2)) return true;
+  for (size_t u = 0; u != n_u; ++u)
+    for (size_t v = lo; v != hi; ++v) output[pixel(u, v)] = 0.0f;
+  auto pred = [band](size_t at, uint32_t code) -> size_t {
+    switch (code) {
+      case kFromUpNext: return at - band + 1;
+      case kFromNext: return at + 1;
+      case kFromUp: return at - band;
+      case kFromUpPrev: return at - band - 1;
+      case kFromPrev: return at - 1;
+      default: return at;
+    }
+  };
+  size_t p = pred(end_at, end_code);
+  for (; p >= band; p = pred(p, back[p])) output[pixel(p / band, p % band + lo)] = 1.0f;
+  output[pixel(0, p + lo)] = 1.0f;
+  return true;
+}
+
 }  // namespace
 
 DivideStats DijkstraSplitter::Stats() {
@@ -326,6 +477,8 @@ void DijkstraSplitter::Divide(const float* image, float* output, size_t lo,
 template <bool kVertical>
 void DijkstraSplitter::DivideExact(const float* image, float* output, size_t lo,
                                    size_t hi, std::atomic<int>* race) const {
+  if (DivideExactPacked<kVertical>(image, output, width_, height_, lo, hi, race)) return;
+  // (bands of 2^29 pixels or more) the same search on OpenList
   const size_t n_u = kVertical ? height_ : width_;  // path length axis
   const size_t band = hi - lo;
   auto pixel = [&](size_t u, size_t v) -> size_t {

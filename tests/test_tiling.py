@@ -50,7 +50,7 @@ def _divide_counts():
     return np.array(rd.tiling.divide_stats(), np.int64)
 
 
-@pytest.mark.parametrize("kind", ["noise", "quantized", "zeros", "nan"])
+@pytest.mark.parametrize("kind", ["noise", "quantized", "zeros", "nan", "blocked"])
 def test_splitter_key_order_search_matches_oracle(kind):
     """The dividers come from the key-order search (radix heap) when no tie
     decides the path, else from the reference's heap order; either way the
@@ -67,6 +67,10 @@ def test_splitter_key_order_search_matches_oracle(kind):
     elif kind == "nan":
         img = img.copy()
         img[rng.integers(0, 640, 50), rng.integers(0, 768, 50)] = np.nan
+    elif kind == "blocked":  # no divider can cross: every search drains its queue
+        img = img.copy()
+        img[200, :] = np.nan
+        img[:, 500] = np.inf
     before = _divide_counts()
     boxes, labels = rd.tiling.make_subimages(img, 4, 3)
     used = _divide_counts() - before
