@@ -336,8 +336,11 @@ def with_amdahl(rd, once):
     if total <= 0.0:
         return out, None
     f = max(0.0, total - passes) / total
+    serial = {k: round(prof[k][1], 4) for k in ("par.split", "split.divide", "split.masks",
+                                                "perform.load", "perform.load_psfs",
+                                                "perform.store") if k in prof}
     return out, {"perform_s": round(total, 4), "subimage_passes_s": round(passes, 4),
-                 "serial_fraction": round(f, 4),
+                 "serial_fraction": round(f, 4), "serial_sections_s": serial,
                  "speedup_bound": {str(n): round(1.0 / (f + (1.0 - f) / n), 2)
                                    for n in (2, 4, 8)},
                  "note": "passes: find-peak + cleaning over the subimages (split over "
