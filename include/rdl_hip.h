@@ -584,6 +584,22 @@ int rdl_conv_columns_window(rdl_conv* c, const void* d_in, void* d_out,
 /* kernel_f32 (float64 convolution-column plans only): d_kernel holds the
  * kernel spectrum as float complex (rdl_complex_narrow of the float64 one),
  * widened to double where it is multiplied. */
+/* The padded convolve-and-subtract of CorrectResidualDirty
+ * (subminor_loop.cc:199-216: Untrim, Convolve, Trim, residual -= result) as
+ * one call: d_residual (img_w x img_h) -= the window (ox, oy) of
+ * image (x) kernel, with d_image the window's content of a zero plane and
+ * d_row_mask (optional) marking the plane rows that may be non-zero. Equal to
+ * rdl_conv_rows_forward(_masked) + rdl_conv_columns_window + rdl_conv_rows_
+ * inverse(subtract); the float64 convolution-column plans keep the
+ * intermediate spectrum in the tiled layout (RDL_CONV_FAST_TILED's element
+ * order, in double) so every pass moves whole cache lines. d_work holds
+ * rdl_conv_convolve_subtract_bytes(c) bytes. */
+size_t rdl_conv_convolve_subtract_bytes(const rdl_conv* c);
+int rdl_conv_convolve_subtract(rdl_conv* c, const float* d_image, uint32_t img_w,
+                               uint32_t img_h, uint32_t ox, uint32_t oy,
+                               const void* d_kernel, int kernel_layout, int kernel_f32,
+                               double scale, const uint8_t* d_row_mask, void* d_work,
+                               float* d_residual);
 /* d_dst[i] = (float complex) d_src[i], i < n_complex (double complex in). */
 int rdl_complex_narrow(rdl_session* s, void* d_dst, const void* d_src, size_t n_complex);
 /* As rdl_conv_columns_ex with the input layout too (in_layout

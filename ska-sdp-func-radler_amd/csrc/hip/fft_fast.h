@@ -128,7 +128,8 @@ int FastRowsInverseLaunch(rdl_session* s, const FastRows* p, const void* spec, f
 int FastRowsForwardLaunch(rdl_session* s, const FastRows* p, const float* in, void* spec,
                           const void* tw, const void* ptw, uint32_t height, uint32_t img_w, uint32_t img_h,
                           uint32_t ox, uint32_t oy, const uint32_t* rows,
-                          const uint32_t* n_rows, int tiled = 0, const void* twd = nullptr);
+                          const uint32_t* n_rows, int tiled = 0, const void* twd = nullptr,
+                          int all_rows = -1);
 /* the two-level double twiddle base of length `base` (ff::TwdLds layout) */
 int MakeTwiddleBase(uint32_t base, void** out);
 /* float64 convolution columns (mode 1: forward, x K x s, inverse; row-major
@@ -140,7 +141,8 @@ int ConvColumnsDLaunch(rdl_session* s, const FastColumns* p, const void* in, voi
                        const void* kern, const void* tw, uint32_t n_cols, int kern_cm,
                        int out_cm, const uint32_t* rows, const uint32_t* n_rows, uint32_t row0,
                        uint32_t row_n, double scale, uint32_t out_row0 = 0,
-                       uint32_t out_row_n = 0xffffffffu, bool kernel_f32 = false);
+                       uint32_t out_row_n = 0xffffffffu, bool kernel_f32 = false,
+                       bool tiled = false);
 /* ascending list of the rows whose mask byte is non-zero, and its length */
 int FastCompactRows(rdl_session* s, const uint8_t* mask, uint32_t n, uint32_t* rows,
                     uint32_t* count);

@@ -306,6 +306,9 @@ struct ColArgs {
   // ColumnsConvD: output rows outside [out_row0, out_row0 + out_row_n) are
   // not written (the inverse row pass reads the output window's rows only)
   uint32_t out_row0, out_row_n;
+  // ColumnsConvD: input and output in the tiled layout (TileIndex, column
+  // length N) instead of row-major
+  uint32_t tiled;
 };
 
 // PF: the kernel column is loaded into registers before the forward
@@ -407,6 +410,14 @@ __global__ __launch_bounds__(TH) void Columns(ColArgs a, const Cx<T>* __restrict
     }
     LdsSync();
   }
+}
+
+// Tiled spectrum layout of the four-step column passes: 16 adjacent columns
+// (128 B of float complex, 256 B of double complex) of every row side by side, tile after tile, so
+// both the row passes and the column passes move whole cache lines.
+constexpr uint32_t kTile = 16;
+__device__ __forceinline__ size_t TileIndex(uint32_t y, uint32_t k, uint32_t height) {
+  return (size_t(k / kTile) * height + y) * kTile + (k % kTile);
 }
 
 // ----------------------------------- float64 correction columns (mode 1)
@@ -547,7 +558,10 @@ __global__ __launch_bounds__(TH) void ColumnsConvD(ColArgs a, const Cx<double>* 
     const uint32_t c = round * G + (b & 7u) * a.per_xcd + (b >> 3);
     const bool active = c < a.n_cols;
     const uint32_t cc = active ? c : 0u;
-    const Cx<double>* in_c = in + cc;
+    // column c: row-major (stride ld) or tiled (stride kTile in its tile)
+    const size_t in_stride = a.tiled ? kTile : a.ld;
+    const Cx<double>* in_c =
+        in + (a.tiled ? size_t(cc / kTile) * N * kTile + cc % kTile : size_t(cc));
     const uint32_t k_stride = a.kern_cm ? 1u : a.ld;
     const KT* kern_c = a.kern_cm ? kern + size_t(cc) * N : kern + cc;
     auto kload = [&](uint32_t y) {
@@ -573,7 +587,7 @@ __global__ __launch_bounds__(TH) void ColumnsConvD(ColArgs a, const Cx<double>* 
     }
     // forward pass 1: straight from global memory through the row bitmap
     auto load = [&](uint32_t y) {
-      return ((bits[y >> 5] >> (y & 31u)) & 1u) && active ? in_c[size_t(y) * a.ld]
+      return ((bits[y >> 5] >> (y & 31u)) & 1u) && active ? in_c[size_t(y) * in_stride]
                                                            : Cx<double>{0.0, 0.0};
     };
     CPass<TH, N, R1, 1, 1, 0>(buf, t1, t2, tid, load,
@@ -590,7 +604,8 @@ __global__ __launch_bounds__(TH) void ColumnsConvD(ColArgs a, const Cx<double>* 
     // inverse = conj(forward(conj(X K s))); the last pass stores row-major
     auto store = [&](uint32_t, uint32_t, uint32_t y, Cx<double> v) {
       if (active && y - a.out_row0 < a.out_row_n)
-        out[a.out_cm ? size_t(c) * N + y : size_t(y) * a.ld + c] = Conj(v);
+        out[a.tiled ? TileIndex(y, c, N) : a.out_cm ? size_t(c) * N + y : size_t(y) * a.ld + c] =
+            Conj(v);
     };
     // (its LDS reads end in a barrier, before the next round's first stores)
     CInv<TH, N, 1, decltype(store), R1, Rs...>(buf, t1, t2, tid, store);
@@ -614,13 +629,6 @@ struct RowArgs {
   RowPeak peak;         // inverse: fused peak search when peak.partials
 };
 
-// Tiled spectrum layout of the four-step column passes: 16 adjacent columns
-// (128 B of float complex) of every row side by side, tile after tile, so
-// both the row passes and the column passes move whole cache lines.
-constexpr uint32_t kTile = 16;
-__device__ __forceinline__ size_t TileIndex(uint32_t y, uint32_t k, uint32_t height) {
-  return (size_t(k / kTile) * height + y) * kTile + (k % kTile);
-}
 
 // spectrum rows (X[0..H]) -> real rows written into / subtracted from the
 // window. Z[k] = (X[k] + conj X[H-k]) + i W^-k (X[k] - conj X[H-k]) gives
@@ -1962,7 +1970,7 @@ int ConvColumnsDLaunch(rdl_session* s, const FastColumns* p, const void* in, voi
                        const void* kern, const void* tw, uint32_t n_cols, int kern_cm,
                        int out_cm, const uint32_t* rows, const uint32_t* n_rows, uint32_t row0,
                        uint32_t row_n, double scale, uint32_t out_row0, uint32_t out_row_n,
-                       bool kernel_f32) {
+                       bool kernel_f32, bool tiled) {
   const size_t lds = ConvColumnsDLdsBytes(p->n);
   const void* fn = kernel_f32 ? p->kernel_kf : p->kernel;
   if (!fn) {
@@ -1987,6 +1995,7 @@ int ConvColumnsDLaunch(rdl_session* s, const FastColumns* p, const void* in, voi
   a.scale = scale;
   a.out_row0 = out_row0;
   a.out_row_n = out_row_n;
+  a.tiled = tiled ? 1u : 0u;
   const uint32_t want = std::min<uint32_t>(n_cols, uint32_t(s->n_cus) * uint32_t(slots));
   a.per_xcd = std::max<uint32_t>(1, (want + 7) / 8);
   const uint32_t grid = 8 * a.per_xcd;
@@ -2079,7 +2088,7 @@ int FastRowsInverseLaunch(rdl_session* s, const FastRows* p, const void* spec, f
 int FastRowsForwardLaunch(rdl_session* s, const FastRows* p, const float* in, void* spec,
                           const void* tw, const void* ptw, uint32_t height, uint32_t img_w, uint32_t img_h,
                           uint32_t ox, uint32_t oy, const uint32_t* rows,
-                          const uint32_t* n_rows, int tiled, const void* twd) {
+                          const uint32_t* n_rows, int tiled, const void* twd, int all_rows) {
   // the LDS-DMA kernel: a whole float plane into a tiled spectrum
   // (RDL_ROWS_DMA=0: the persistent row kernel)
   static const bool dma_on = [] {
@@ -2125,8 +2134,9 @@ int FastRowsForwardLaunch(rdl_session* s, const FastRows* p, const float* in, vo
   a.rows = rows;
   a.n_rows = n_rows;
   a.tiled = tiled;
-  a.all_rows = tiled;
-  const uint32_t max_rows = (rows || tiled) ? height : img_h;
+  // (all_rows < 0: every plane row for a tiled spectrum, the window rows otherwise)
+  a.all_rows = all_rows < 0 ? tiled : all_rows;
+  const uint32_t max_rows = (rows || a.all_rows) ? height : img_h;
   if (max_rows == 0) return RDL_OK;
   const uint32_t grid =
       std::min<uint32_t>(max_rows, uint32_t(s->n_cus) * uint32_t(slots) * 2);

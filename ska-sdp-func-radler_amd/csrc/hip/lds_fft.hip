@@ -1065,6 +1065,79 @@ int rdl_conv_columns_window(rdl_conv* c, const void* d_in, void* d_out,
                                  kernel_f32 != 0);
 }
 
+namespace {
+// the float64 convolution-column plans keep the correction's spectrum in the
+// tiled layout (RDL_CONV64_TILED=0: row-major, for comparison)
+bool Tiled64(const rdl_conv* c) {
+  static const bool on = [] {
+    const char* e = std::getenv("RDL_CONV64_TILED");
+    return !(e && e[0] == '0');
+  }();
+  return on && c->f64 && c->conv_cols && c->fast_rows && !c->split && !c->tiled;
+}
+}  // namespace
+
+size_t rdl_conv_convolve_subtract_bytes(const rdl_conv* c) {
+  if (!c) return 0;
+  return Tiled64(c) ? rdl::TiledComplexCount(c->width, c->height) * 16
+                    : size_t(SpectrumBytes(c));
+}
+
+int rdl_conv_convolve_subtract(rdl_conv* c, const float* d_image, uint32_t img_w,
+                               uint32_t img_h, uint32_t ox, uint32_t oy,
+                               const void* d_kernel, int kernel_layout, int kernel_f32,
+                               double scale, const uint8_t* d_row_mask, void* d_work,
+                               float* d_residual) {
+  RDL_ARG_CHECK(c && d_image && d_kernel && d_work && d_residual, "NULL argument");
+  RDL_ARG_CHECK(uint64_t(ox) + img_w <= c->width && uint64_t(oy) + img_h <= c->height,
+                "image window outside the plane");
+  if (!Tiled64(c)) {
+    RDL_TRY(d_row_mask
+                ? rdl_conv_rows_forward_masked(c, d_image, img_w, img_h, ox, oy, d_work,
+                                               d_row_mask)
+                : rdl_conv_rows_forward(c, d_image, img_w, img_h, ox, oy, d_work));
+    RDL_TRY(rdl_conv_columns_window(c, d_work, d_work, d_kernel, scale, d_row_mask,
+                                    kernel_layout, oy, img_h, kernel_f32));
+    return rdl_conv_rows_inverse(c, d_work, d_residual, img_w, img_h, ox, oy, 1);
+  }
+  RDL_ARG_CHECK(kernel_layout == RDL_CONV_ROW_MAJOR || kernel_layout == RDL_CONV_COL_MAJOR,
+                "bad kernel layout");
+  // the same three passes on the tiled layout: the row passes move whole
+  // 256-byte tile rows, the column pass reads and writes column c at a
+  // 256-byte stride inside its tile (not a full row stride)
+  const double sb = SpectrumBytes(c);
+  const double win = sb * double(img_h) / double(c->height);
+  const uint32_t* rows = nullptr;
+  const uint32_t* n_rows = nullptr;
+  {
+    rdl::ScopedTiming t(c->s, d_row_mask ? "conv64_rows_sparse" : "conv64_rows",
+                        d_row_mask ? 0.0 : double(img_w) * img_h * 4.0 + win);
+    if (d_row_mask) {
+      RDL_TRY(CompactRowsFor(c, d_row_mask, false));
+      rows = c->rows_list;
+      n_rows = c->rows_list + c->height;
+    }
+    RDL_TRY(rdl::FastRowsForwardLaunch(c->s, c->fast_rows, d_image, d_work, c->tw_row,
+                                       c->ptw_row, c->height, img_w, img_h, ox, oy, rows,
+                                       n_rows, 1, c->twd_row, 0));
+  }
+  {
+    const double kb = kernel_f32 ? 0.5 * sb : sb;
+    rdl::ScopedTiming t(c->s, d_row_mask ? "conv64_cols_sparse" : "conv64_cols",
+                        d_row_mask ? kb + win : kb + 2.0 * win);
+    // unmasked: the rows outside the window are zero (never written)
+    RDL_TRY(rdl::ConvColumnsDLaunch(c->s, c->conv_cols, d_work, d_work, d_kernel, c->tw_col,
+                                    c->width / 2 + 1, kernel_layout == RDL_CONV_COL_MAJOR, 0,
+                                    rows, n_rows, oy, img_h, scale, oy, img_h,
+                                    kernel_f32 != 0, true));
+    c->rows_list_mask = nullptr;  // the mask's contents may change next time
+  }
+  rdl::ScopedTiming t(c->s, "conv64_rows", win + double(img_w) * img_h * 8.0);
+  return rdl::FastRowsInverseLaunch(c->s, c->fast_rows, d_work, d_residual, c->tw_row,
+                                    c->ptw_row, c->height, img_w, img_h, ox, oy, 1, 1, nullptr,
+                                    c->twd_row);
+}
+
 int rdl_conv_columns_layout(rdl_conv* c, const void* d_in, void* d_out,
                             const void* d_kernel, int mode, double scale,
                             const uint8_t* d_row_mask, int in_layout,

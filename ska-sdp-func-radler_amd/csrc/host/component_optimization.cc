@@ -15,7 +15,7 @@ void PaddedConvolveSubtract(gpu::Session& s, const float* d_src, float* d_dst,
   gpu::Fft& fft = s.GetFft(padded_width, padded_height, true);
   const size_t ox = (padded_width - width) / 2, oy = (padded_height - height) / 2;
   if (fft.UsesLds()) {
-    gpu::Buffer work(s, fft.SpectrumBytes());
+    gpu::Buffer work(s, fft.ConvolveSubtractBytes());
     fft.ConvolveSubtract(d_src, width, height, ox, oy, d_psf_spectrum, work.Ptr(), d_dst,
                          nullptr, !fft.SplitColumns());
     return;

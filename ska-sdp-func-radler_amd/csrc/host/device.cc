@@ -258,24 +258,16 @@ void Fft::ConvolveSubtract(const float* d_image, size_t img_w, size_t img_h,
                            bool kernel_f32) {
   if (!conv_) throw std::logic_error("Fft::ConvolveSubtract needs the LDS engine");
   const double norm = 1.0 / (double(width_) * double(height_));
-  if (d_row_mask)
-    Check(rdl_conv_rows_forward_masked(conv_, d_image, uint32_t(img_w),
-                                       uint32_t(img_h), uint32_t(ox), uint32_t(oy),
-                                       d_work, d_row_mask),
-          "rdl_conv_rows_forward_masked");
-  else
-    Check(rdl_conv_rows_forward(conv_, d_image, uint32_t(img_w), uint32_t(img_h),
-                                uint32_t(ox), uint32_t(oy), d_work),
-          "rdl_conv_rows_forward");
-  // only the window's rows of the column output are read back
-  Check(rdl_conv_columns_window(conv_, d_work, d_work, d_kernel_spectrum,
-                                f64_ ? norm : double(float(norm)), d_row_mask,
-                                kernel_col_major ? RDL_CONV_COL_MAJOR : RDL_CONV_ROW_MAJOR,
-                                uint32_t(oy), uint32_t(img_h), kernel_f32 ? 1 : 0),
-        "rdl_conv_columns_window");
-  Check(rdl_conv_rows_inverse(conv_, d_work, d_residual, uint32_t(img_w),
-                              uint32_t(img_h), uint32_t(ox), uint32_t(oy), 1),
-        "rdl_conv_rows_inverse");
+  Check(rdl_conv_convolve_subtract(
+            conv_, d_image, uint32_t(img_w), uint32_t(img_h), uint32_t(ox), uint32_t(oy),
+            d_kernel_spectrum, kernel_col_major ? RDL_CONV_COL_MAJOR : RDL_CONV_ROW_MAJOR,
+            kernel_f32 ? 1 : 0, f64_ ? norm : double(float(norm)), d_row_mask, d_work,
+            d_residual),
+        "rdl_conv_convolve_subtract");
+}
+
+size_t Fft::ConvolveSubtractBytes() const {
+  return conv_ ? rdl_conv_convolve_subtract_bytes(conv_) : spectrum_bytes_;
 }
 
 void Fft::Forward64(const double* d_in, void* d_spectrum) {

@@ -90,11 +90,14 @@ class Fft {
   /// the image (img_w x img_h) placed at (ox, oy) in the plane.
   /// d_row_mask (plane rows, 0 = the image row is all zero) skips the empty
   /// rows; kernel_col_major reads a spectrum made by ForwardColumnMajor.
+  /// d_work holds ConvolveSubtractBytes() (the float64 convolution-column
+  /// plans keep its spectrum in the tiled layout: rdl_conv_convolve_subtract).
   void ConvolveSubtract(const float* d_image, size_t img_w, size_t img_h,
                         size_t ox, size_t oy, const void* d_kernel_spectrum,
                         void* d_work, float* d_residual,
                         const uint8_t* d_row_mask = nullptr,
                         bool kernel_col_major = false, bool kernel_f32 = false);
+  size_t ConvolveSubtractBytes() const;
   /// LDS engine only: forward spectrum stored column by column (column k at
   /// k * height), the layout the column pass reads contiguously.
   void ForwardColumnMajor(const float* d_in, void* d_spectrum);

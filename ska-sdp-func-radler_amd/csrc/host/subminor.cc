@@ -135,7 +135,8 @@ void SubMinorLoop::CorrectResidualDirtyWithSpectrum(size_t image_index,
     // the subtraction run inside the three transform passes
     gpu::Buffer& model = s_.Scratch(gpu::Session::kCorrectionModel,
                                     width_ * height_ * sizeof(float));
-    gpu::Buffer& work = s_.Scratch(gpu::Session::kCorrectionSpectrum, fft.SpectrumBytes());
+    gpu::Buffer& work =
+        s_.Scratch(gpu::Session::kCorrectionSpectrum, fft.ConvolveSubtractBytes());
     gpu::Buffer& rows = s_.Scratch(gpu::Session::kCorrectionRows, padded_height_);
     // the model holds a few hundred components per outer iteration: the
     // transform skips its empty rows (exactly zero, so nothing changes), and
