@@ -309,9 +309,6 @@ struct ColArgs {
   // ColumnsConvD: input and output in the tiled layout (TileIndex, column
   // length N) instead of row-major
   uint32_t tiled;
-  // ColumnsConvD, column-major kernel: the next round's kernel column is
-  // fetched into the cache hierarchy while this round's inverse runs
-  uint32_t prefetch_k;
 };
 
 // PF: the kernel column is loaded into registers before the forward
@@ -413,21 +410,6 @@ __global__ __launch_bounds__(TH) void Columns(ColArgs a, const Cx<T>* __restrict
     }
     LdsSync();
   }
-}
-
-// One 16-byte-per-lane LDS-DMA load (global_load_lds_dwordx4): lane i's 16 B
-// land at LDS byte `lds` + 16 i (lds wave-uniform, through m0). In inline asm
-// so the compiler does not treat it as an LDS write of unknown extent (see
-// RowsInverseDma); the caller retires it with its own s_waitcnt vmcnt and a
-// barrier before any wave reads those bytes.
-__device__ __forceinline__ void DmaLoad16(const void* g, uint32_t lds) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(g), "s"(lds)
-      : "memory");
 }
 
 // Tiled spectrum layout of the four-step column passes: 16 adjacent columns
@@ -553,11 +535,6 @@ __global__ __launch_bounds__(TH) void ColumnsConvD(ColArgs a, const Cx<double>* 
   Cx<double>* t1 = buf + N;
   Cx<double>* t2 = t1 + NT1;
   uint32_t* bits = reinterpret_cast<uint32_t*>(t2 + kTwLo);
-  // 1 KiB that the kernel prefetch's LDS-DMA lands in (never read)
-  typedef __attribute__((address_space(3))) void* LdsPtr;
-  const uint32_t junk = __builtin_amdgcn_readfirstlane(
-      uint32_t(uintptr_t((LdsPtr)lds_raw)) +
-      uint32_t((size_t(N + NT1 + kTwLo) * 16 + NWORDS * 4 + 15) & ~size_t(15)));
   const uint32_t b = blockIdx.x, G = gridDim.x;
   const double s = a.scale;
   {
@@ -624,14 +601,6 @@ __global__ __launch_bounds__(TH) void ColumnsConvD(ColArgs a, const Cx<double>* 
       buf[y] = Conj(Scale(Mul(v, k), s));
     };
     CFwdTail<TH, N, R1, decltype(mulk), Rs...>(buf, t1, t2, tid, mulk);
-    // the next round's kernel column (contiguous) through LDS-DMA into the
-    // junk bytes: its lines are in L2 / the Infinity Cache when that round's
-    // last forward pass reads them (no registers held, nothing waits here)
-    if (a.prefetch_k && a.kern_cm && c + G < a.n_cols) {
-      const char* nk = reinterpret_cast<const char*>(kern + size_t(c + G) * N);
-      constexpr uint32_t NB16 = uint32_t(N * sizeof(KT) / 16);
-      for (uint32_t q = tid; q < NB16; q += TH) DmaLoad16(nk + size_t(q) * 16, junk);
-    }
     // inverse = conj(forward(conj(X K s))); the last pass stores row-major
     auto store = [&](uint32_t, uint32_t, uint32_t y, Cx<double> v) {
       if (active && y - a.out_row0 < a.out_row_n)
@@ -641,7 +610,6 @@ __global__ __launch_bounds__(TH) void ColumnsConvD(ColArgs a, const Cx<double>* 
     // (its LDS reads end in a barrier, before the next round's first stores)
     CInv<TH, N, 1, decltype(store), R1, Rs...>(buf, t1, t2, tid, store);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA in flight at exit
 }
 
 // ----------------------------------------------------------------- rows
@@ -835,6 +803,21 @@ __global__ __launch_bounds__(TH) void RowsInverse(RowArgs a, const Cx<T>* __rest
   finish_peak();
   if constexpr (LT) LdsSync();
   }
+}
+
+// One 16-byte-per-lane LDS-DMA load (global_load_lds_dwordx4): lane i's 16 B
+// land at LDS byte `lds` + 16 i (lds wave-uniform, through m0). In inline asm
+// so the compiler does not treat it as an LDS write of unknown extent (see
+// RowsInverseDma); the caller retires it with its own s_waitcnt vmcnt and a
+// barrier before any wave reads those bytes.
+__device__ __forceinline__ void DmaLoad16(const void* g, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(g), "s"(lds)
+      : "memory");
 }
 
 // RowsInverse (float, tiled spectrum, write mode, even window) with the next
@@ -1882,9 +1865,8 @@ const FastColumns* FindConvColumnsD(uint32_t n) {
 #undef RDL_CONV_D
 
 size_t ConvColumnsDLdsBytes(uint32_t n) {
-  const size_t tables = size_t(n) * 16 + size_t((n + ff::kTwLo - 1) / ff::kTwLo + ff::kTwLo) * 16 +
-                        size_t((n + 31) / 32) * 4;
-  return ((tables + 15) & ~size_t(15)) + 1024;  // + the prefetch's junk bytes
+  return size_t(n) * 16 + size_t((n + ff::kTwLo - 1) / ff::kTwLo + ff::kTwLo) * 16 +
+         size_t((n + 31) / 32) * 4;
 }
 
 #define RDL_FAST_STEPS(N1, N2, GA, GB, RA, RB)                                     \
@@ -2014,11 +1996,6 @@ int ConvColumnsDLaunch(rdl_session* s, const FastColumns* p, const void* in, voi
   a.out_row0 = out_row0;
   a.out_row_n = out_row_n;
   a.tiled = tiled ? 1u : 0u;
-  static const bool prefetch = [] {
-    const char* e = std::getenv("RDL_CONVD_PREFETCH");
-    return e && e[0] == '1';
-  }();
-  a.prefetch_k = prefetch ? 1u : 0u;
   const uint32_t want = std::min<uint32_t>(n_cols, uint32_t(s->n_cus) * uint32_t(slots));
   a.per_xcd = std::max<uint32_t>(1, (want + 7) / 8);
   const uint32_t grid = 8 * a.per_xcd;
