@@ -40,7 +40,7 @@ FAMILY_KERNELS = {
     "add": r"^rdl::AddKernel\(",
     # the LDS FFT engine: float32 scale convolutions (four-step columns)
     "conv_cols": r"rdl::ff::(ColStepA|ColStepB|ColStepBScales|ColStepAInv|Columns<float)",
-    "conv_rows": r"rdl::ff::Rows(Inverse|Forward)<float",
+    "conv_rows": r"rdl::ff::Rows(Inverse|Forward)(<float|Dma<)",
 }
 # families whose kernels are shared with a sibling family: measured together,
 # over the summed launches and algorithmic bytes of both (the *_sparse
