@@ -105,6 +105,11 @@ class Timing:
                                                 C.POINTER(C.c_uint64), C.POINTER(C.c_double)]
 
     def enable(self, on):
+        # RDL_BENCH_EVENTS=0: no HIP event pairs at all (a profiler run of the
+        # pooled legs, whose interception of thousands of event records from
+        # 16 worker threads faults inside the profiler); no roofline then
+        if os.environ.get("RDL_BENCH_EVENTS") == "0":
+            return
         self.lib.rdl_timing_enable_all(int(on))
 
     def only(self, family):
