@@ -201,7 +201,45 @@ inline float KeyFloat(uint32_t u) {
   return f;
 }
 
-std::atomic<uint64_t> g_fast_divides{0}, g_exact_divides{0};
+std::atomic<uint64_t> g_fast_divides{0}, g_exact_divides{0}, g_hybrid_divides{0};
+
+enum : uint32_t {  // predecessor of target (u, v)
+  kFromUpNext = 0,   // (u - 1, v + 1)
+  kFromNext = 1,     // (u, v + 1)
+  kFromUp = 2,       // (u - 1, v)
+  kFromUpPrev = 3,   // (u - 1, v - 1)
+  kFromPrev = 4,     // (u, v - 1)
+  kFromStart = 5,    // (u, v) itself
+};
+
+// band-local index of the predecessor a code names
+inline size_t PredOf(size_t at, uint32_t code, size_t band) {
+  switch (code) {
+    case kFromUpNext: return at - band + 1;
+    case kFromNext: return at + 1;
+    case kFromUp: return at - band;
+    case kFromUpPrev: return at - band - 1;
+    case kFromPrev: return at - 1;
+    default: return at;
+  }
+}
+
+// A prefix of the exact search that a key-order search can use (the race
+// in DijkstraSplitter::Divide): when the key-order divider is decided by ties
+// only at pixels settled at keys <= k (see DivideByKeyOrder), the exact
+// search is stopped once every entry of key <= k has popped (stop_key = the
+// bits of k), and its predecessor codes for those pixels complete the
+// divider: above k the key-order search's predecessors are the unique ones.
+}  // namespace
+
+struct DivideReplay {
+  std::atomic<uint32_t> stop_key{UINT32_MAX};
+  std::atomic<int> stopped{0};  // the exact search stopped at stop_key (back is valid there)
+  std::atomic<int> done{0};     // the exact search has returned (any way)
+  std::unique_ptr<uint8_t[]> back;
+};
+
+namespace {
 
 // The reference's search visits pixels in key order (the key of an entry is
 // its predecessor's path cost) and keeps, per pixel, the predecessor of the
@@ -213,10 +251,15 @@ std::atomic<uint64_t> g_fast_divides{0}, g_exact_divides{0};
 // the trace reads is marked, none was settled at the final key, and no other
 // last-row pixel ends at the final cost: then every predecessor on the path
 // and the end pixel are the unique minimum, whatever the pop order among
-// equal keys. Returns false (output untouched) otherwise.
+// equal keys. With `replay` (the exact search running alongside), a path
+// whose first marked pixel from the end was settled at key k < the final key
+// is completed from the exact search stopped after key k: keys never rise
+// along the path towards its start, so every predecessor the trace reads
+// from there on is final in that prefix. Returns false (output untouched)
+// when neither applies, or when the exact search finished first.
 template <bool kVertical>
 bool DivideByKeyOrder(const float* image, float* output, size_t width, size_t height,
-                      size_t lo, size_t hi, std::atomic<int>* race) {
+                      size_t lo, size_t hi, std::atomic<int>* race, DivideReplay* replay = nullptr) {
   const size_t n_u = kVertical ? height : width;
   const size_t band = hi - lo;
   auto pixel = [&](size_t u, size_t v) -> size_t {
@@ -290,26 +333,43 @@ bool DivideByKeyOrder(const float* image, float* output, size_t width, size_t he
   const size_t last = (n_u - 1) * band;
   for (size_t v = 0; v != band; ++v)
     if (v + lo != end_pv && KeyBits(dist[last + v]) == end_key) return false;
+  // the first marked pixel from the end (keys only fall towards the start)
+  uint32_t split_key = UINT32_MAX;
   for (uint32_t pu = end_pu, pv = end_pv; pu > 0;) {
     const size_t at = size_t(pu) * band + (pv - lo);
-    if (tied[at] || KeyBits(key_of[at]) >= end_key) return false;
+    if (KeyBits(key_of[at]) >= end_key) return false;
+    if (tied[at]) {
+      if (!replay) return false;
+      split_key = KeyBits(key_of[at]);
+      break;
+    }
     pu = back[at] >> 16;
     pv = back[at] & 0xffffu;
+  }
+  if (split_key != UINT32_MAX) {
+    // the exact search's prefix up to split_key decides the rest
+    replay->stop_key.store(split_key, std::memory_order_release);
+    while (!replay->done.load(std::memory_order_acquire)) std::this_thread::yield();
+    if (!replay->stopped.load(std::memory_order_acquire)) return false;  // it finished first
   }
   // racing the exact search: the first to claim the band writes it (the
   // two dividers are then identical)
   int running = 0;
-  if (race && !race->compare_exchange_strong(running, 1)) return true;
+  if (race && !race->compare_exchange_strong(running, split_key == UINT32_MAX ? 1 : 3))
+    return split_key == UINT32_MAX;
   for (size_t u = 0; u != n_u; ++u)
     for (size_t v = lo; v != hi; ++v) output[pixel(u, v)] = 0.0f;
-  uint32_t pu = end_pu, pv = end_pv;
-  for (; pu > 0;) {
-    output[pixel(pu, pv)] = 1.0f;
-    const uint32_t p = back[size_t(pu) * band + (pv - lo)];
-    pu = p >> 16;
-    pv = p & 0xffffu;
+  size_t at = size_t(end_pu) * band + (end_pv - lo);
+  while (at >= band) {  // u > 0
+    output[pixel(at / band, at % band + lo)] = 1.0f;
+    if (KeyBits(key_of[at]) > split_key || split_key == UINT32_MAX) {
+      const uint32_t p = back[at];
+      at = size_t(p >> 16) * band + ((p & 0xffffu) - lo);
+    } else {
+      at = PredOf(at, replay->back[at], band);
+    }
   }
-  output[pixel(0, pv)] = 1.0f;
+  output[pixel(0, at + lo)] = 1.0f;
   return true;
 }
 
@@ -320,18 +380,9 @@ bool DivideByKeyOrder(const float* image, float* output, size_t width, size_t he
 // itself (a start entry) or one of five neighbours; the settled pixels keep
 // the code (one byte) instead of the predecessor's coordinates. Needs
 // (n_u + 1) * band < 2^29; false (output untouched) otherwise.
-enum : uint32_t {  // predecessor of target (u, v)
-  kFromUpNext = 0,   // (u - 1, v + 1)
-  kFromNext = 1,     // (u, v + 1)
-  kFromUp = 2,       // (u - 1, v)
-  kFromUpPrev = 3,   // (u - 1, v - 1)
-  kFromPrev = 4,     // (u, v - 1)
-  kFromStart = 5,    // (u, v) itself
-};
-
 template <bool kVertical>
 bool DivideExactPacked(const float* image, float* output, size_t width, size_t height,
-                       size_t lo, size_t hi, std::atomic<int>* race) {
+                       size_t lo, size_t hi, std::atomic<int>* race, DivideReplay* replay) {
   const size_t n_u = kVertical ? height : width;
   const size_t band = hi - lo;
   if (band == 0 || (n_u + 1) * band >= (size_t(1) << 29)) return false;
@@ -342,7 +393,11 @@ bool DivideExactPacked(const float* image, float* output, size_t width, size_t h
   std::vector<float> dist(band * n_u, std::numeric_limits<float>::max());
   for (size_t u = 0; u != n_u; ++u)
     for (size_t v = lo; v != hi; ++v) weight[u * band + (v - lo)] = std::fabs(image[pixel(u, v)]);
-  std::unique_ptr<uint8_t[]> back(new uint8_t[band * n_u]);  // written when settled
+  // predecessor codes, written when a pixel settles (the replay's own
+  // array when a key-order search may read a prefix of them)
+  std::unique_ptr<uint8_t[]> own;
+  if (!replay) own.reset(new uint8_t[band * n_u]);
+  uint8_t* const back = replay ? replay->back.get() : own.get();
   PackedOpenList open(8 * band);
   for (size_t v = 0; v != band; ++v) open.Push(uint64_t(v) << 3 | kFromStart);
   const size_t n_settle = n_u * band;
@@ -354,6 +409,11 @@ bool DivideExactPacked(const float* image, float* output, size_t width, size_t h
     if (race && ++poll == 0x1000u) {  // cancelled by a key-order result
       poll = 0;
       if (race->load(std::memory_order_relaxed) == 1) return true;
+      // or stopped after the prefix a key-order divider needs
+      if (replay && uint32_t(open.Top() >> 32) > replay->stop_key.load(std::memory_order_acquire)) {
+        replay->stopped.store(1, std::memory_order_release);
+        return true;
+      }
     }
     const uint64_t top = open.Top();
     open.Pop();
@@ -383,18 +443,8 @@ bool DivideExactPacked(const float* image, float* output, size_t width, size_t h
   if (race && !race->compare_exchange_strong(running, 2)) return true;
   for (size_t u = 0; u != n_u; ++u)
     for (size_t v = lo; v != hi; ++v) output[pixel(u, v)] = 0.0f;
-  auto pred = [band](size_t at, uint32_t code) -> size_t {
-    switch (code) {
-      case kFromUpNext: return at - band + 1;
-      case kFromNext: return at + 1;
-      case kFromUp: return at - band;
-      case kFromUpPrev: return at - band - 1;
-      case kFromPrev: return at - 1;
-      default: return at;
-    }
-  };
-  size_t p = pred(end_at, end_code);
-  for (; p >= band; p = pred(p, back[p])) output[pixel(p / band, p % band + lo)] = 1.0f;
+  size_t p = PredOf(end_at, end_code, band);
+  for (; p >= band; p = PredOf(p, back[p], band)) output[pixel(p / band, p % band + lo)] = 1.0f;
   output[pixel(0, p + lo)] = 1.0f;
   return true;
 }
@@ -402,7 +452,7 @@ bool DivideExactPacked(const float* image, float* output, size_t width, size_t h
 }  // namespace
 
 DivideStats DijkstraSplitter::Stats() {
-  return {g_fast_divides.load(), g_exact_divides.load()};
+  return {g_fast_divides.load(), g_exact_divides.load(), g_hybrid_divides.load()};
 }
 
 template <bool kVertical>
@@ -436,16 +486,21 @@ void DijkstraSplitter::Divide(const float* image, float* output, size_t lo,
   // key-order result (about a fifth of its time) cancels it, else it
   // finishes. The divider costs max(key order, exact) at worst instead of
   // their sum.
-  std::atomic<int> race{0};  // 0 running, 1 key order wrote, 2 exact wrote
+  // 0 running, 1 key order wrote, 2 exact wrote, 3 key order wrote with the
+  // exact search's prefix (DivideReplay)
+  std::atomic<int> race{0};
+  DivideReplay replay;
+  replay.back.reset(new uint8_t[(hi - lo) * (kVertical ? height_ : width_)]);
   std::exception_ptr exact_error;
   std::thread exact;
   try {
     exact = std::thread([&] {
       try {
-        DivideExact<kVertical>(image, output, lo, hi, &race);
+        DivideExact<kVertical>(image, output, lo, hi, &race, &replay);
       } catch (...) {
         exact_error = std::current_exception();
       }
+      replay.done.store(1, std::memory_order_release);
     });
   } catch (const std::system_error&) {
     // no thread to be had: the two searches in turn
@@ -459,7 +514,7 @@ void DijkstraSplitter::Divide(const float* image, float* output, size_t lo,
   }
   bool fast = false;
   try {
-    fast = DivideByKeyOrder<kVertical>(image, output, width_, height_, lo, hi, &race);
+    fast = DivideByKeyOrder<kVertical>(image, output, width_, height_, lo, hi, &race, &replay);
   } catch (...) {
     fast = false;  // the exact search still decides
   }
@@ -470,14 +525,15 @@ void DijkstraSplitter::Divide(const float* image, float* output, size_t lo,
   if (writer != 1 && exact_error) std::rethrow_exception(exact_error);
   if (writer == 0)
     throw std::logic_error("DijkstraSplitter: neither divider search wrote the band");
-  ++(writer == 1 ? g_fast_divides : g_exact_divides);
+  ++(writer == 1 ? g_fast_divides : writer == 3 ? g_hybrid_divides : g_exact_divides);
   (void)fast;
 }
 
 template <bool kVertical>
 void DijkstraSplitter::DivideExact(const float* image, float* output, size_t lo,
-                                   size_t hi, std::atomic<int>* race) const {
-  if (DivideExactPacked<kVertical>(image, output, width_, height_, lo, hi, race)) return;
+                                   size_t hi, std::atomic<int>* race,
+                                   DivideReplay* replay) const {
+  if (DivideExactPacked<kVertical>(image, output, width_, height_, lo, hi, race, replay)) return;
   // (bands of 2^29 pixels or more) the same search on OpenList
   const size_t n_u = kVertical ? height_ : width_;  // path length axis
   const size_t band = hi - lo;

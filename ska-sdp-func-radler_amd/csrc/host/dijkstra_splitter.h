@@ -11,10 +11,14 @@
 namespace radler::math {
 
 /// Divider searches so far (process-wide): settled by the key-order search
-/// with a unique minimum path, or run through the reference's heap order.
+/// with a unique minimum path, run through the reference's heap order, or
+/// the key-order path completed from a prefix of that heap order (ties only
+/// below some key; DivideReplay).
 struct DivideStats {
-  unsigned long long key_order, exact;
+  unsigned long long key_order, exact, hybrid;
 };
+
+struct DivideReplay;  // a prefix of the exact search shared with the key-order search
 
 class DijkstraSplitter {
  public:
@@ -62,9 +66,11 @@ class DijkstraSplitter {
   /// The reference's search with its binary heap's exact pop order. With
   /// `race`, it returns without writing once a key-order result claimed the
   /// band (race == 1), and claims it (race = 2) before writing.
+  /// With `replay`, it also stops (without writing) once every entry of key
+  /// <= replay's stop key has popped, leaving its predecessors there.
   template <bool kVertical>
   void DivideExact(const float* image, float* output, size_t lo, size_t hi,
-                   std::atomic<int>* race) const;
+                   std::atomic<int>* race, DivideReplay* replay = nullptr) const;
 
   size_t width_, height_;
 };

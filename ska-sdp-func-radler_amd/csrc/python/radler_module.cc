@@ -475,8 +475,9 @@ void InitTiling(py::module& m) {
   };
   t.def("divide_stats", [] {
     const radler::math::DivideStats st = radler::math::DijkstraSplitter::Stats();
-    return py::make_tuple(st.key_order, st.exact);
-  }, "(key-order searches, exact heap-order searches) run by this process");
+    return py::make_tuple(st.key_order, st.exact, st.hybrid);
+  }, "(key-order searches, exact heap-order searches, key-order paths completed from an "
+     "exact prefix) run by this process");
   t.def("divide_vertically", [splitter](const F32& image, F32& output, size_t x1,
                                         size_t x2) {
     splitter(image).DivideVertically(image.data(), output.mutable_data(), x1, x2);

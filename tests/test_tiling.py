@@ -50,12 +50,15 @@ def _divide_counts():
     return np.array(rd.tiling.divide_stats(), np.int64)
 
 
-@pytest.mark.parametrize("kind", ["noise", "quantized", "zeros", "nan", "blocked"])
+@pytest.mark.parametrize("kind", ["noise", "quantized", "fine_quantized", "zeros", "nan",
+                                  "blocked"])
 def test_splitter_key_order_search_matches_oracle(kind):
     """The dividers come from the key-order search (radix heap) when no tie
-    decides the path, else from the reference's heap order; either way the
-    geometry is the oracle's (whose search is the reference's heap). Noisy
-    images take the key-order search; tie-heavy ones fall back."""
+    decides the path, from the key-order path completed by a prefix of the
+    reference's heap order when ties decide it only below some key, else from
+    the reference's heap order; either way the geometry is the oracle's (whose
+    search is the reference's heap). Noisy images take the key-order search;
+    tie-heavy ones fall back."""
     rng = np.random.default_rng(11)
     _, img = problem(768, 640, 60, 6, seed=12)
     if kind == "quantized":  # few distinct values: equal path costs everywhere
@@ -67,6 +70,10 @@ def test_splitter_key_order_search_matches_oracle(kind):
     elif kind == "nan":
         img = img.copy()
         img[rng.integers(0, 640, 50), rng.integers(0, 768, 50)] = np.nan
+    elif kind == "fine_quantized":  # a few equal path costs inside the bands
+        img = img + rng.normal(0, np.abs(img).max() * 0.01, img.shape).astype(np.float32)
+        step = np.abs(img).max() * 1e-4
+        img = (np.round(img / step) * step).astype(np.float32)
     elif kind == "blocked":  # no divider can cross: every search drains its queue
         img = img.copy()
         img[200, :] = np.nan
@@ -82,6 +89,8 @@ def test_splitter_key_order_search_matches_oracle(kind):
         assert used[0] == used.sum()  # no tie on any divider
     if kind == "quantized":
         assert used[1] > 0
+    if kind == "fine_quantized":  # key-order paths completed from an exact prefix
+        assert used[2] > 0
 
 
 def _settings(kind, w, thr, max_iter, mgain, gw, gh, threads):
