@@ -2,6 +2,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstring>
 #include <cmath>
 #include <cstdint>
@@ -349,7 +350,10 @@ bool DivideByKeyOrder(const float* image, float* output, size_t width, size_t he
   if (split_key != UINT32_MAX) {
     // the exact search's prefix up to split_key decides the rest
     replay->stop_key.store(split_key, std::memory_order_release);
-    while (!replay->done.load(std::memory_order_acquire)) std::this_thread::yield();
+    // (sleeping, not spinning: the exact searches of other bands may need
+    // this core)
+    while (!replay->done.load(std::memory_order_acquire))
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
     if (!replay->stopped.load(std::memory_order_acquire)) return false;  // it finished first
   }
   // racing the exact search: the first to claim the band writes it (the
