@@ -3068,9 +3068,14 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   rdl::LoopResult res{};
   uint32_t err = 0;
   {
-    const rdl::SmallRead r[2] = {{&res, la.result, sizeof(res)},
-                                 {&err, la.result + 8, sizeof(err)}};
-    RDL_TRY(rdl::ReadSmall(s, r, 2));
+    // the result (words 0-5) and the exchange's timeout flag (word 8) in ONE
+    // read: each read-back is a blit launch plus host latency per component run
+    static_assert(sizeof(rdl::LoopResult) <= 8 * sizeof(uint32_t), "result before word 8");
+    uint32_t raw[9];
+    const rdl::SmallRead r{raw, la.result, sizeof(raw)};
+    RDL_TRY(rdl::ReadSmall(s, &r, 1));
+    std::memcpy(&res, raw, sizeof(res));
+    err = raw[8];
   }
   if (err) {
     rdl::SetError("sub-minor loop: grid exchange timed out");

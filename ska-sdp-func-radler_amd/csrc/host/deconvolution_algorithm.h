@@ -98,6 +98,11 @@ class DeconvolutionAlgorithm {
   const std::shared_ptr<const std::vector<float>>& RmsFactorImage() const {
     return rms_factor_;
   }
+  /// Keep the component trace of each call (LastTrace(): the parity tests
+  /// and DeviceRun); off in Radler::Perform, where nothing reads it and its
+  /// per-sub-minor-loop read-back would cost a device round trip.
+  void SetRecordTrace(bool on) { record_trace_ = on; }
+  bool RecordTrace() const { return record_trace_; }
 
  protected:
   DeconvolutionAlgorithm() = default;
@@ -109,7 +114,8 @@ class DeconvolutionAlgorithm {
         n_polarizations_(o.n_polarizations_),
         logpoly_(o.logpoly_),
         has_logpoly_(o.has_logpoly_),
-        rms_factor_(o.rms_factor_) {}
+        rms_factor_(o.rms_factor_),
+        record_trace_(o.record_trace_) {}
 
   /// Device copy (uint8) of CleanMask() for the current call, or nullptr.
   const uint8_t* DeviceCleanMask(gpu::Session& s, size_t width, size_t height);
@@ -162,6 +168,7 @@ class DeconvolutionAlgorithm {
   gpu::Session* spectral_map_session_ = nullptr;
   bool spectral_map_identity_ = false;
   std::shared_ptr<const std::vector<float>> rms_factor_;
+  bool record_trace_ = false;
   std::shared_ptr<gpu::Buffer> rms_device_;
   gpu::Session* rms_device_session_ = nullptr;
 };

@@ -72,6 +72,7 @@ DeviceRun::DeviceRun(const Settings& settings, const float* psf,
     algorithm = std::make_unique<algorithms::IuwtDeconvolution>();
   else
     throw std::runtime_error("DeviceRun: unsupported algorithm");
+  algorithm->SetRecordTrace(true);  // Trace(): the parity tests' component traces
   algorithm->SetMaxIterations(settings.minor_iteration_count);
   algorithm->SetThreshold(settings.absolute_threshold);
   algorithm->SetMinorLoopGain(settings.minor_loop_gain);

@@ -147,7 +147,7 @@ DeconvolutionResult GenericClean::ExecuteMajorIteration(
     sub.SetRmsFactor(DeviceRmsFactor(s, width, height));  // :126-128
     sub.SetCleanBorders(size_t(std::round(width * CleanBorderRatio())),
                         size_t(std::round(height * CleanBorderRatio())));
-    sub.SetTrace(&trace_);
+    if (RecordTrace()) sub.SetTrace(&trace_);
     const SubMinorLoop::RunResult r = sub.Run(dirty_set, psfs);
     diverging = r.diverging;
     max_value.found = r.has_peak;

@@ -662,7 +662,7 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
       sub.SetLogPolyFit(LogPolyFit());
       sub.SetRmsFactor(DeviceRmsFactor(session, width, height));  // :401-402
       std::vector<uint32_t> xy;
-      sub.SetTrace(&xy);
+      if (RecordTrace()) sub.SetTrace(&xy);
       SubMinorLoop::RunResult r;
       {
         prof::Section prof_run("ms.subminor_run");
