@@ -344,15 +344,6 @@ int rdl_session_create(int device, rdl_session** out) {
     ~Restore() { (void)hipSetDevice(d); }
   } restore{prev};
   RDL_HIP_CHECK(hipSetDevice(device));
-  {
-    // RDL_SYNC_SPIN=1: host waits on the device spin instead of blocking
-    // (each read-back of the outer loop wakes the host thread); the flags
-    // can only be set before the device is in use, so a refusal is ignored
-    const char* spin = std::getenv("RDL_SYNC_SPIN");
-    if (spin && spin[0] == '1') {
-      if (hipSetDeviceFlags(hipDeviceScheduleSpin) != hipSuccess) (void)hipGetLastError();
-    }
-  }
   auto s = std::make_unique<rdl_session>();
   s->device = device;
   RDL_HIP_CHECK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));

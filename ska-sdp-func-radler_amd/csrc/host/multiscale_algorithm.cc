@@ -242,10 +242,18 @@ void MultiScaleAlgorithm::FindActiveScaleConvolvedMaxima(
   else
     image_set.GetLinearIntegrated(d_integrated);
   bool need_fft = false;
+  const bool fused_search = !report_rms && !RmsFactorImage();
+  // the scale-0 search: queued with the other scales' (one read-back for
+  // all) when the convolved scales' searches are queued too
+  int direct = -1;
   for (size_t si = 0; si != scale_infos_.size(); ++si) {
     ScaleInfo& e = scale_infos_[si];
     if (!e.is_active) continue;
     if (e.scale == 0.0f) {
+      if (fused_search) {
+        direct = int(si);
+        continue;
+      }
       FindPeakDirect(d_source, si);
       if (report_rms)
         gpu::Check(rdl_rms(s, d_source, w * h, &e.rms), "rdl_rms");
@@ -253,16 +261,27 @@ void MultiScaleAlgorithm::FindActiveScaleConvolvedMaxima(
       need_fft = true;
     }
   }
-  if (!need_fft) return;
-  if (scale_infos_.size() > RDL_PEAK_SLOTS)
+  if (!need_fft) {
+    if (direct >= 0) FindPeakDirect(d_source, size_t(direct));
+    return;
+  }
+  if (scale_infos_.size() + 1 > RDL_PEAK_SLOTS)
     throw std::runtime_error("MultiScaleAlgorithm: too many scales");
-  const bool fused_search = !report_rms && !RmsFactorImage();
+  std::vector<size_t> pending;  // scale of each queued peak search (slot = index)
+  if (direct >= 0) {  // FindPeakDirect's search (:700-748), collected below
+    const uint32_t hb = uint32_t(std::round(w * CleanBorderRatio()));
+    const uint32_t vb = uint32_t(std::round(h * CleanBorderRatio()));
+    gpu::Check(rdl_find_peak_enqueue(s, d_source, uint32_t(w), uint32_t(h), 0, uint32_t(h), hb,
+                                     vb, AllowNegativeComponents(), MaskFor(size_t(direct)), 1,
+                                     0),
+               "rdl_find_peak_enqueue");
+    pending.push_back(size_t(direct));
+  }
   if (fused_search && FusedScalesOn() && transforms_->Fused()) {
-    FindMaximaFused(d_source, identity);
+    FindMaximaFused(d_source, identity, pending);
     return;
   }
   transforms_->Forward(d_source, spectrum_->Ptr());
-  std::vector<size_t> pending;  // scale of each queued peak search
   // The scales' inverse transforms + fused peak searches are independent
   // (the reference runs them on threads, threaded_deconvolution_tools.cc):
   // with a kept image per scale they alternate over two session lanes, so
@@ -361,7 +380,8 @@ void MultiScaleAlgorithm::FindActiveScaleConvolvedMaxima(
   }
 }
 
-void MultiScaleAlgorithm::FindMaximaFused(const float* d_source, bool identity) {
+void MultiScaleAlgorithm::FindMaximaFused(const float* d_source, bool identity,
+                                          std::vector<size_t> pending) {
   // The same searches as below, with the scales' convolutions made from ONE
   // forward half by one launch (rdl_conv_scales: the forward spectrum never
   // reaches HBM, the scale kernels are real), then per scale the outer
@@ -413,18 +433,19 @@ void MultiScaleAlgorithm::FindMaximaFused(const float* d_source, bool identity) 
     if (forked) gpu::Check(rdl_session_lane(s, lane), "rdl_session_lane");
     void* work = lane ? spectrum_work2_->Ptr() : spectrum_work_->Ptr();
     transforms_->FinishPeak(outs[k], e.scale, work, conv[k], xb, yb, AllowNegativeComponents(),
-                            MaskFor(idx[k]), uint32_t(k));
+                            MaskFor(idx[k]), uint32_t(pending.size()));
+    pending.push_back(idx[k]);
     if (forked) lane ^= 1;
   }
   if (forked) {
     forked = false;
     gpu::Check(rdl_session_join(s), "rdl_session_join");
   }
-  std::vector<rdl_peak> peaks(idx.size());
-  gpu::Check(rdl_find_peak_collect(s, uint32_t(idx.size()), peaks.data()),
+  std::vector<rdl_peak> peaks(pending.size());
+  gpu::Check(rdl_find_peak_collect(s, uint32_t(pending.size()), peaks.data()),
              "rdl_find_peak_collect");
-  for (size_t k = 0; k != idx.size(); ++k) {
-    ScaleInfo& e = scale_infos_[idx[k]];
+  for (size_t k = 0; k != pending.size(); ++k) {
+    ScaleInfo& e = scale_infos_[pending[k]];
     const rdl_peak& p = peaks[k];
     e.max_normalized_image_value = p.found ? Normalized(p.value, p.x, p.y, w) : 0.0f;
     e.max_unnormalized_image_value = p.found ? p.value : 0.0f;

@@ -112,7 +112,7 @@ class MultiScaleAlgorithm final : public DeconvolutionAlgorithm {
   std::shared_ptr<gpu::Buffer> rms_scratch_;  // W x H: image x RMS factor
   /// d_image, or d_image x the RMS factor (multiscale_algorithm.cc:707-713)
   /// FindActiveScaleConvolvedMaxima through the fused multi-scale launch
-  void FindMaximaFused(const float* d_source, bool identity);
+  void FindMaximaFused(const float* d_source, bool identity, std::vector<size_t> pending);
   const float* PeakSearchInput(const float* d_image, size_t w, size_t h);
   /// unnormalized / factor at the peak (:736-743), the value itself without
   float Normalized(float value, size_t x, size_t y, size_t w) const;
