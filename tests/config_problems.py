@@ -81,7 +81,7 @@ CONFIGS = {
     "c4": dict(kind="iuwt", size=4096, points=1000, blobs=100, threshold=5 * NOISE,
                cap=24),
     "c5": dict(kind="tiled", size=16384, points=2000, blobs=200, threshold=5 * NOISE,
-               max_scales=6, grid=8, cap=200),
+               max_scales=6, grid=8, cap=2000),
     # bench.py's headline (BASELINE metric) workload, capped: the trace up to
     # and past the first near-tie, the image checkpoint AT the first near-tie
     # (make_config_golden.py: image_cap "near_tie")
