@@ -422,7 +422,8 @@ __device__ __forceinline__ size_t TileIndex(uint32_t y, uint32_t k, uint32_t hei
 
 // ----------------------------------- float64 correction columns (mode 1)
 // ColumnsConvD: the column pass of CorrectResidualDirty's padded convolution
-// (forward, x K x s, inverse; sparse input rows, output row-major), with the
+// (forward, x K x s, inverse; sparse input rows; input and output row-major
+// or, ColArgs::tiled, in the tiled layout), with the
 // per-round latency chain of Columns cut down:
 //   * pass twiddles from two small LDS tables (W^e = T1[e >> 7] T2[e & 127],
 //     both exact entries of the plan's length-N table) instead of a global
@@ -601,7 +602,7 @@ __global__ __launch_bounds__(TH) void ColumnsConvD(ColArgs a, const Cx<double>* 
       buf[y] = Conj(Scale(Mul(v, k), s));
     };
     CFwdTail<TH, N, R1, decltype(mulk), Rs...>(buf, t1, t2, tid, mulk);
-    // inverse = conj(forward(conj(X K s))); the last pass stores row-major
+    // inverse = conj(forward(conj(X K s))); the last pass stores the window rows
     auto store = [&](uint32_t, uint32_t, uint32_t y, Cx<double> v) {
       if (active && y - a.out_row0 < a.out_row_n)
         out[a.tiled ? TileIndex(y, c, N) : a.out_cm ? size_t(c) * N + y : size_t(y) * a.ld + c] =
