@@ -147,7 +147,7 @@ DeconvolutionResult GenericClean::ExecuteMajorIteration(
     sub.SetRmsFactor(DeviceRmsFactor(s, width, height));  // :126-128
     sub.SetCleanBorders(size_t(std::round(width * CleanBorderRatio())),
                         size_t(std::round(height * CleanBorderRatio())));
-    if (RecordTrace()) sub.SetTrace(&trace_);
+    sub.SetTrace(&trace_);  // (kept for GenericClean: not on the headline path)
     const SubMinorLoop::RunResult r = sub.Run(dirty_set, psfs);
     diverging = r.diverging;
     max_value.found = r.has_peak;
