@@ -253,8 +253,11 @@ static int Execute(rdl_fft* f, bool forward, void* in, void* out) {
                       real_bytes + double(rdl_fft_spectrum_bytes(f)));
   void* ins[1] = {in};
   void* outs[1] = {out};
-  RDL_FFT_CHECK(rocfft_execute(forward ? f->fwd : f->inv, ins, outs,
-                               forward ? f->info_fwd : f->info_inv));
+  // the session's current lane: a plan made while lane 1 was current must not
+  // keep running on that lane's stream
+  rocfft_execution_info info = forward ? f->info_fwd : f->info_inv;
+  RDL_FFT_CHECK(rocfft_execution_info_set_stream(info, f->s->stream));
+  RDL_FFT_CHECK(rocfft_execute(forward ? f->fwd : f->inv, ins, outs, info));
   return RDL_OK;
 }
 

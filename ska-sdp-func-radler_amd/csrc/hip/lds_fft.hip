@@ -174,11 +174,16 @@ __global__ __launch_bounds__(kFftThreads) void RowsForward(RowArgs a,
     const uint32_t y0 = 2 * (pair0 + t), y1 = y0 + 1;
     T va = T(0), vb = T(0);
     const int64_t ix = int64_t(x) - a.ox;
+    // A masked row is zero whatever the plane holds there: the two rows of a
+    // pair share one complex transform, so a stale row would leak into its
+    // partner's spectrum through rounding (the partial-zeroing correction
+    // model plane keeps old data in its unmarked rows).
+    const bool use0 = !a.row_mask || a.row_mask[y0] != 0;
+    const bool use1 = y1 < a.height && (!a.row_mask || a.row_mask[y1] != 0);
     if (ix >= 0 && ix < a.img_w) {
       const int64_t iy0 = int64_t(y0) - a.oy, iy1 = int64_t(y1) - a.oy;
-      if (iy0 >= 0 && iy0 < a.img_h) va = T(in[size_t(iy0) * a.img_w + ix]);
-      if (y1 < a.height && iy1 >= 0 && iy1 < a.img_h)
-        vb = T(in[size_t(iy1) * a.img_w + ix]);
+      if (use0 && iy0 >= 0 && iy0 < a.img_h) va = T(in[size_t(iy0) * a.img_w + ix]);
+      if (use1 && iy1 >= 0 && iy1 < a.img_h) vb = T(in[size_t(iy1) * a.img_w + ix]);
     }
     buf[idx] = {va, vb};
   }
@@ -792,6 +797,7 @@ int EnsureSplitScratch(rdl_conv* c, size_t bytes) {
     c->scratch_bytes[l] = 0;
   }
   RDL_HIP_CHECK(rdl::DevMalloc(&c->scratch, bytes));
+  if (rdl::PoisonOn()) RDL_HIP_CHECK(hipMemsetAsync(c->scratch, 0xff, bytes, c->s->stream));
   c->scratch_lane[l] = c->scratch;
   c->scratch_bytes[l] = bytes;
   return RDL_OK;

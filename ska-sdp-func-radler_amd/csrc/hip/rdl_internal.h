@@ -5,6 +5,7 @@
 
 #include <atomic>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -72,6 +73,15 @@ hipError_t DevMalloc(T** p, size_t bytes) {
 inline hipError_t DevFree(void* p) {
   UntrackBlock(p);
   return hipFree(p);
+}
+// RDL_POISON=1 (debug): fresh device buffers are filled with 0xff bytes
+// (NaN floats) so reads of memory nothing wrote show up in results
+inline bool PoisonOn() {
+  static const bool on = [] {
+    const char* e = std::getenv("RDL_POISON");
+    return e && e[0] == '1';
+  }();
+  return on;
 }
 template <typename T>
 hipError_t HostMalloc(T** p, size_t bytes) {

@@ -1716,8 +1716,11 @@ constexpr uint32_t kTabParticipantStride = 8;  // blocks per participant (LoopAr
 // all participants on one XCC). A target whose L1 could hold such stores
 // needs the agent-scope form, which RDL_SUBMINOR_EXCHANGE=agent selects (and
 // tests/test_gpu_kernels.py compares with the fast one).
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
-#error "subminor.hip: the workgroup-scope exchange relies on gfx950's write-through vector L1"
+// Other targets always take the agent-scope form (kFastExchange false).
+#if defined(__gfx950__) || !defined(__HIP_DEVICE_COMPILE__)
+constexpr bool kFastExchange = true;
+#else
+constexpr bool kFastExchange = false;
 #endif
 
 __device__ __forceinline__ uint32_t XccId() {
@@ -1771,7 +1774,7 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTab(LoopArgs a) {
       failed = spins > (uint64_t(1) << 24);
     }
     const uint32_t x0 = uint32_t(__builtin_amdgcn_readlane(int(xcc), 0));
-    fast = __all(lane >= G || xcc == x0) && !a.agent_exchange;
+    fast = kFastExchange && __all(lane >= G || xcc == x0) && !a.agent_exchange;
   }
   const float* table = a.table;
   float c = 0.0f, m = 0.0f, start_abs = 0.0f, flux = 0.0f;
@@ -2121,7 +2124,7 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTabN(LoopArgs a) {
       failed = spins > (uint64_t(1) << 24);
     }
     const uint32_t x0 = uint32_t(__builtin_amdgcn_readlane(int(xcc), 0));
-    fast = __all(lane >= G || xcc == x0) && !a.agent_exchange;
+    fast = kFastExchange && __all(lane >= G || xcc == x0) && !a.agent_exchange;
   }
   const size_t sq = size_t(n) * n;
   float c[NI];
@@ -2528,6 +2531,8 @@ int Grow(void** p, size_t* have, size_t need, hipStream_t stream) {
   }
   RDL_HIP_CHECK(rdl::DevMalloc(p, need));
   *have = need;
+  // RDL_POISON=1: NaN bytes in every fresh buffer (uninitialised reads show)
+  if (PoisonOn()) RDL_HIP_CHECK(hipMemsetAsync(*p, 0xff, need, stream));
   return RDL_OK;
 }
 

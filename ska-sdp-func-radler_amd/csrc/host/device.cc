@@ -1,5 +1,6 @@
 #include "device.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <mutex>
 
@@ -225,9 +226,18 @@ void Fft::ForwardHalf(const float* d_in, void* d_half) {
 void Fft::Scales(const void* d_half, const std::vector<const void*>& d_kernels,
                  const std::vector<void*>& d_outs) {
   const double norm = 1.0 / (double(width_) * double(height_));
-  Check(rdl_conv_scales(conv_, d_half, uint32_t(d_kernels.size()), d_kernels.data(),
-                        d_outs.data(), double(float(norm))),
-        "rdl_conv_scales");
+  // rdl_conv_scales takes at most 8 scales per launch (rdl_hip.h); a longer
+  // ladder (a 1-pixel beam at 2048^2, a scale_list of 10) runs in chunks of
+  // the same forward half, which the launches only read
+  constexpr size_t kPerLaunch = 8;
+  if (d_kernels.size() != d_outs.size())
+    throw std::logic_error("Fft::Scales: one output per kernel");
+  for (size_t i = 0; i < d_kernels.size(); i += kPerLaunch) {
+    const size_t n = std::min(kPerLaunch, d_kernels.size() - i);
+    Check(rdl_conv_scales(conv_, d_half, uint32_t(n), d_kernels.data() + i,
+                          d_outs.data() + i, double(float(norm))),
+          "rdl_conv_scales");
+  }
 }
 
 void Fft::ScaleFinishWindowPeak(const void* d_u, void* d_work, float* d_out, size_t out_w,

@@ -493,14 +493,19 @@ void DijkstraSplitter::Divide(const float* image, float* output, size_t lo,
   // 0 running, 1 key order wrote, 2 exact wrote, 3 key order wrote with the
   // exact search's prefix (DivideReplay)
   std::atomic<int> race{0};
+  // the replay prefix only exists for bands the packed exact search holds
+  // (the OpenList fallback never honours stop_key)
+  const size_t n_u = kVertical ? height_ : width_;
+  const bool packed = hi > lo && (n_u + 1) * (hi - lo) < (size_t(1) << 29);
   DivideReplay replay;
-  replay.back.reset(new uint8_t[(hi - lo) * (kVertical ? height_ : width_)]);
+  if (packed) replay.back.reset(new uint8_t[(hi - lo) * n_u]);
+  DivideReplay* const with_replay = packed ? &replay : nullptr;
   std::exception_ptr exact_error;
   std::thread exact;
   try {
     exact = std::thread([&] {
       try {
-        DivideExact<kVertical>(image, output, lo, hi, &race, &replay);
+        DivideExact<kVertical>(image, output, lo, hi, &race, with_replay);
       } catch (...) {
         exact_error = std::current_exception();
       }
@@ -516,11 +521,11 @@ void DijkstraSplitter::Divide(const float* image, float* output, size_t lo,
     DivideExact<kVertical>(image, output, lo, hi, nullptr);
     return;
   }
-  bool fast = false;
   try {
-    fast = DivideByKeyOrder<kVertical>(image, output, width_, height_, lo, hi, &race, &replay);
+    (void)DivideByKeyOrder<kVertical>(image, output, width_, height_, lo, hi, &race,
+                                      with_replay);
   } catch (...) {
-    fast = false;  // the exact search still decides
+    // the exact search still decides
   }
   exact.join();
   // the search that claimed the band wrote it (DivideByKeyOrder also returns
@@ -530,7 +535,6 @@ void DijkstraSplitter::Divide(const float* image, float* output, size_t lo,
   if (writer == 0)
     throw std::logic_error("DijkstraSplitter: neither divider search wrote the band");
   ++(writer == 1 ? g_fast_divides : writer == 3 ? g_hybrid_divides : g_exact_divides);
-  (void)fast;
 }
 
 template <bool kVertical>

@@ -156,3 +156,32 @@ def test_multiscale_joined_channels_parity(w, n_ch, weights, max_scales, fast):
     tol = 2e-5 * np.abs(dirties).max()
     np.testing.assert_allclose(run.residual().reshape(n_ch, h, w), res_o, atol=tol)  # NaN == NaN
     np.testing.assert_allclose(run.model().reshape(n_ch, h, w), mod_o, atol=tol)
+
+
+def test_multiscale_more_than_eight_scales_on_tiled_plan():
+    """A ladder of 10 non-zero scales on a four-step (tiled) plan: 1280^2 with
+    a 0.25-pixel beam gives scales 0, 1, 2, 4, ..., 512
+    (multiscale_algorithm.cc:97-113). The fused scale convolutions take at most
+    8 scales per launch (rdl_conv_scales), so the ladder runs in two chunks of
+    one forward half; the trace must equal the oracle's."""
+    w = h = 1280
+    beam_px, thr, max_iter = 0.25, 2e-2, 60
+    psf, dirty = problem(w, h, 30, 6, seed=1280)
+    orc = get_oracle()
+    orc.set_threads(8)
+    res_o, mod_o = dirty[None].copy(), np.zeros((1, h, w), np.float32)
+    alg = OracleAlgorithm(orc, 1, threshold=thr, max_iterations=max_iter, border_ratio=0.0,
+                          max_scales=0, beam_size_in_pixels=beam_px)
+    r_o, trace_o = alg.execute(res_o, mod_o, psf[None])
+    s = gpu_settings(w, h, thr, max_iter, 0)
+    run = rd.gpu.DeviceRun(s, psf, dirty, [], beam_px * PIXEL_SCALE)
+    r_g = run.execute()
+    trace_g = run.trace()
+    # (every scale is active in the first search: 10 convolutions in one call)
+    assert r_g["iterations"] == r_o.iteration_number
+    if not np.array_equal(trace_g, trace_o):
+        first = int(np.argmax(np.any(trace_g != trace_o, axis=1)))
+        pytest.fail(f"component trace differs first at {first}: gpu {trace_g[first]} "
+                    f"oracle {trace_o[first]}")
+    tol = 2e-5 * np.abs(dirty).max()
+    np.testing.assert_allclose(run.residual().reshape(h, w), res_o[0], atol=tol)
