@@ -589,6 +589,16 @@ def main():
                               "split into grid x grid subimages (the partitioning N > 1 "
                               "shares over ranks, DESIGN.md §6), a different problem from "
                               "the unsplit C3 run in `unsplit`"}
+        # the split run's best case on N ranks (its Amdahl bound) against the
+        # unsplit C3 run on one GPU: what the subimage split can reach
+        bound = {n: round(j_el / f, 4) for n, f in j_amdahl.get("speedup_bound", {}).items()}
+        joined_ref["vs_unsplit"] = {
+            "unsplit_s": round(u_el, 4), "split_bound_s": bound,
+            "note": ("best-case wall clock of the split problem on N ranks (perform_s / "
+                     "speedup_bound) beside the unsplit run on one GPU; the channel-sharded "
+                     "alternative (north_star's ordered slab reduction + integrated-peak "
+                     "allreduce) would add one RCCL round trip (~10 us) to every ~7 us "
+                     "joined component, DESIGN.md §6")}
         del j_psf, j_dirty
 
     # C2 (4096^2) to the threshold on this GPU: the same problem as the

@@ -117,13 +117,16 @@ struct RowPeak {
   uint32_t xs, xe, ys, ye;
   int allow_negative;
 };
-/* spectrum rows oy .. oy+img_h-1 -> the img_w x img_h window at (ox, oy) */
+/* spectrum rows oy .. oy+img_h-1 -> the img_w x img_h window at (ox, oy);
+ * with `peak`, *n_partials = the peak partials written (one per row, or one
+ * per workgroup for the LDS-DMA kernel) */
 /* twd: MakeTwiddleBase(n) for the float plans' LDS-twiddle kernels (NULL:
  * the global pass tables) */
 int FastRowsInverseLaunch(rdl_session* s, const FastRows* p, const void* spec, float* out,
                           const void* tw, const void* ptw, uint32_t height, uint32_t img_w, uint32_t img_h,
                           uint32_t ox, uint32_t oy, int subtract, int tiled = 0,
-                          const RowPeak* peak = nullptr, const void* twd = nullptr);
+                          const RowPeak* peak = nullptr, const void* twd = nullptr,
+                          uint32_t* n_partials = nullptr);
 /* the window's rows (or the listed plane rows) -> spectrum rows */
 int FastRowsForwardLaunch(rdl_session* s, const FastRows* p, const float* in, void* spec,
                           const void* tw, const void* ptw, uint32_t height, uint32_t img_w, uint32_t img_h,

@@ -874,6 +874,24 @@ __global__ __launch_bounds__(TH) void RowsInverseDma(RowArgs a, const Cx<float>*
   InitTwiddles<TH, H, 2, 1, Rs...>(td, ctab, 0, clast, threadIdx.x);
   constexpr uint32_t NP = H / 2 + 1;
   constexpr uint32_t EP = (NP + TH - 1) / TH;
+  // the split's twiddles W^-k, W^-(H-k): a thread takes the same bins k in
+  // every row, so they are made once (the per-row double products were a
+  // tenth of the kernel's VALU)
+  Cx<float> wk[EP], wm[EP];
+#pragma unroll
+  for (uint32_t i = 0; i < EP; ++i) {
+    const uint32_t k = threadIdx.x + i * TH;
+    if (NP % TH != 0 && k >= NP) continue;
+    wk[i] = ToF(TwD(td, k));
+    wm[i] = ToF(TwD(td, H - k));
+  }
+  // fused peak search: this thread's best key over all its rows (value
+  // word, then the lowest index), one block reduction at the end: the
+  // partials are per workgroup (FastRowsInverseLaunch's n_partials)
+  const bool peak = a.peak.partials != nullptr;
+  const uint32_t pxs = a.peak.xs, pxn = a.peak.xe - a.peak.xs;
+  const uint32_t sign_mask = a.peak.allow_negative != 0 ? 0x7fffffffu : 0xffffffffu;
+  uint64_t run_best = 0ull;
   bool first = true;
   for (uint32_t iy = blockIdx.x; iy < a.img_h; iy += gridDim.x) {
     uint32_t tid = threadIdx.x;
@@ -888,11 +906,10 @@ __global__ __launch_bounds__(TH) void RowsInverseDma(RowArgs a, const Cx<float>*
       asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     first = false;
     LdsSync();
-    auto zc = [&](Cx<float> xk, Cx<float> xm, uint32_t k) {
+    auto zc = [&](Cx<float> xk, Cx<float> xm, Cx<float> w) {
       const Cx<float> sum = {xk.x + xm.x, xk.y - xm.y};
       const Cx<float> dif = {xk.x - xm.x, xk.y + xm.y};
-      const Cx<float> wk = ToF(TwD(td, k));
-      const Cx<float> t = Mul(Conj(wk), dif);
+      const Cx<float> t = Mul(Conj(w), dif);
       return Cx<float>{sum.x - t.y, -(sum.y + t.x)};
     };
 #pragma unroll
@@ -905,29 +922,20 @@ __global__ __launch_bounds__(TH) void RowsInverseDma(RowArgs a, const Cx<float>*
         xk.y = 0.0f;
         xm.y = 0.0f;
       }
-      buf[Lx<float>(k)] = zc(xk, xm, k);
-      if (k != 0 && m != k) buf[Lx<float>(m)] = zc(xm, xk, m);
+      buf[Lx<float>(k)] = zc(xk, xm, wk[i]);
+      if (k != 0 && m != k) buf[Lx<float>(m)] = zc(xm, xk, wm[i]);
     }
     LdsSync();  // raw is read: the next row's DMA may overwrite it
     if (iy + gridDim.x < a.img_h) issue(iy + gridDim.x);
     FftC<TH, H, 1, Rs...>(buf, ctab, 0, clast, tid);
     float* o = out + size_t(iy) * a.img_w;
-    const bool peak = a.peak.partials != nullptr;
     const bool peak_row = peak && iy >= a.peak.ys && iy < a.peak.ye;
-    const uint32_t pxs = a.peak.xs, pxn = a.peak.xe - a.peak.xs;
     const uint8_t* mrow = a.peak.mask ? a.peak.mask + size_t(iy) * a.img_w : nullptr;
-    const uint32_t sign_mask = a.peak.allow_negative != 0 ? 0x7fffffffu : 0xffffffffu;
-    uint32_t best_u = 0u, best_x = 0u;
-    auto consider = [&](uint32_t x, float v) {
-      if (!peak_row) return;
-      const uint32_t u = __float_as_uint(v) & sign_mask;
-      const bool q = u > 0x00800000u && u <= 0x7f800000u && x - pxs < pxn &&
-                     (!mrow || mrow[x]);
-      const uint32_t uq = q ? u : 0u;
-      const bool better = uq > best_u;
-      best_u = better ? uq : best_u;
-      best_x = better ? x : best_x;
-    };
+    // per value the PeakKey value word (|v| or v as bits; 0 when it cannot
+    // be a peak: NaN, a negative value without allow_negative, outside the
+    // box or the mask); values <= FLT_MIN are excluded by the row's maximum
+    uint32_t uq[EH][2];
+    uint32_t tb = 0u;
     // the whole plane row is the window (the launcher's condition): every
     // thread stores EH float2, in ascending x
 #pragma unroll
@@ -936,23 +944,40 @@ __global__ __launch_bounds__(TH) void RowsInverseDma(RowArgs a, const Cx<float>*
       const Cx<float> z = buf[Lx<float>(n)];
       const float2 v = {z.x, -z.y};
       reinterpret_cast<float2*>(o)[n] = v;
-      consider(2 * n, v.x);
-      consider(2 * n + 1, v.y);
-    }
-    if (peak) {
-      uint64_t best = best_u ? ((uint64_t(best_u) << 32) |
-                                uint64_t(0xffffffffu - (iy * a.img_w + best_x)))
-                             : 0ull;
-      best = WaveMaxU64(best);
-      if (lane == 0) red[wave] = best;
-      LdsSync();
-      if (tid < 64) {
-        uint64_t w = lane < WAVES ? red[lane] : 0ull;
-        w = WaveMaxU64(w);
-        if (tid == 0) a.peak.partials[iy] = w;
+      if (peak_row) {
+#pragma unroll
+        for (uint32_t h = 0; h < 2; ++h) {
+          const uint32_t x = 2 * n + h;
+          const uint32_t u = __float_as_uint(h ? v.y : v.x) & sign_mask;
+          const bool q = u <= 0x7f800000u && x - pxs < pxn && (!mrow || mrow[x]);
+          uq[i][h] = q ? u : 0u;
+          tb = uq[i][h] > tb ? uq[i][h] : tb;
+        }
       }
     }
-    LdsSync();  // the row's LDS reads (buf, red) before the next row's writes
+    if (peak_row && tb > 0x00800000u) {
+      // the first x holding the row's maximum (x ascends with i, h)
+      uint32_t bx = 0u;
+#pragma unroll
+      for (int i = int(EH) - 1; i >= 0; --i)
+#pragma unroll
+        for (int h = 1; h >= 0; --h)
+          bx = uq[i][h] == tb ? 2 * (tid + uint32_t(i) * TH) + uint32_t(h) : bx;
+      const uint64_t key =
+          (uint64_t(tb) << 32) | uint64_t(0xffffffffu - (iy * a.img_w + bx));
+      run_best = key > run_best ? key : run_best;
+    }
+    LdsSync();  // the row's LDS reads (buf) before the next row's writes
+  }
+  if (peak) {
+    const uint64_t best = WaveMaxU64(run_best);
+    if (lane == 0) red[wave] = best;
+    LdsSync();
+    if (threadIdx.x < 64) {
+      uint64_t w = lane < WAVES ? red[lane] : 0ull;
+      w = WaveMaxU64(w);
+      if (threadIdx.x == 0) a.peak.partials[blockIdx.x] = w;
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -1110,6 +1135,16 @@ __global__ __launch_bounds__(TH) void RowsForwardDma(RowArgs a, const float* __r
   if (blockIdx.x < a.height) issue(blockIdx.x);
   LdsSync();
   InitTwiddles<TH, H, 2, 1, Rs...>(td, ctab, 0, clast, threadIdx.x);
+  // the split's twiddles W^k, W^(H-k): the same bins in every row of this
+  // thread, made once (as RowsInverseDma)
+  Cx<float> wk[EP], wm[EP];
+#pragma unroll
+  for (uint32_t i = 0; i < EP; ++i) {
+    const uint32_t k = threadIdx.x + i * TH;
+    if (NP % TH != 0 && k >= NP) continue;
+    wk[i] = ToF(TwD(td, k));
+    wm[i] = ToF(TwD(td, H - k));
+  }
   bool first = true;
   for (uint32_t y = blockIdx.x; y < a.height; y += gridDim.x) {
     uint32_t tid = threadIdx.x;
@@ -1132,11 +1167,10 @@ __global__ __launch_bounds__(TH) void RowsForwardDma(RowArgs a, const float* __r
     if (y + gridDim.x < a.height) issue(y + gridDim.x);
     FftC<TH, H, 1, Rs...>(buf, ctab, 0, clast, tid);
     const float h = 0.5f;
-    auto put = [&](uint32_t k, Cx<float> zk, Cx<float> zc) {
+    auto put = [&](uint32_t k, Cx<float> zk, Cx<float> zc, Cx<float> w) {
       const Cx<float> ev = {h * (zk.x + zc.x), h * (zk.y + zc.y)};
       const Cx<float> od = {h * (zk.y - zc.y), -h * (zk.x - zc.x)};  // (zk - zc) / 2i
-      const Cx<float> wk = ToF(TwD(td, k));
-      spec[TileIndex(y, k, a.height)] = Add(ev, Mul(wk, od));
+      spec[TileIndex(y, k, a.height)] = Add(ev, Mul(w, od));
     };
 #pragma unroll
     for (uint32_t i = 0; i < EP; ++i) {
@@ -1144,8 +1178,8 @@ __global__ __launch_bounds__(TH) void RowsForwardDma(RowArgs a, const float* __r
       if (NP % TH != 0 && k >= NP) continue;
       const Cx<float> zlo = buf[Lx<float>(k)];
       const Cx<float> zhi = k == 0 ? zlo : buf[Lx<float>(H - k)];
-      put(k, zlo, Conj(zhi));
-      if (H - k != k) put(H - k, zhi, Conj(zlo));
+      put(k, zlo, Conj(zhi), wk[i]);
+      if (H - k != k) put(H - k, zhi, Conj(zlo), wm[i]);
     }
     LdsSync();
   }
@@ -2019,9 +2053,10 @@ bool RowTwiddlesInLds() {
 int FastRowsInverseLaunch(rdl_session* s, const FastRows* p, const void* spec, float* out,
                           const void* tw, const void* ptw, uint32_t height, uint32_t img_w, uint32_t img_h,
                           uint32_t ox, uint32_t oy, int subtract, int tiled, const RowPeak* peak,
-                          const void* twd) {
+                          const void* twd, uint32_t* n_partials) {
   // the LDS-DMA kernel: a tiled float spectrum written whole into the
   // window (RDL_ROWS_DMA=0: the persistent row kernel)
+  if (n_partials) *n_partials = img_h;  // per-row partials (the persistent row kernel)
   static const bool dma_on = [] {
     const char* e = std::getenv("RDL_ROWS_DMA");
     return !(e && e[0] == '0');
@@ -2048,6 +2083,7 @@ int FastRowsInverseLaunch(rdl_session* s, const FastRows* p, const void* spec, f
     void* args[] = {&a, (void*)&spec, (void*)&out, (void*)&twd};
     RDL_HIP_CHECK(hipLaunchKernel(p->inverse_dma, dim3(grid), dim3(p->threads), args, lds,
                                   s->stream));
+    if (n_partials) *n_partials = grid;  // one partial per workgroup
     return RDL_OK;
   }
   const size_t lds = FastLdsBytes(p->n / 2, p->f64);

@@ -1231,6 +1231,7 @@ int rdl_conv_rows_inverse_peak(rdl_conv* c, const void* d_spec, float* d_out,
   const size_t rows = std::max<size_t>(out_h, 1);
   RDL_TRY(s->EnsureScratch(s->partials, RDL_PEAK_SLOTS * rows * sizeof(uint64_t)));
   pk.partials = static_cast<uint64_t*>(s->partials.ptr) + slot * rows;
+  uint32_t n_partials = 1;
   {
     rdl::ScopedTiming t(s, "conv_rows",
                         SpectrumBytes(c) + double(out_w) * out_h * 4.0);
@@ -1239,9 +1240,9 @@ int rdl_conv_rows_inverse_peak(rdl_conv* c, const void* d_spec, float* d_out,
     else
       RDL_TRY(rdl::FastRowsInverseLaunch(s, c->fast_rows, d_spec, d_out, c->tw_row,
                                          c->ptw_row, c->height, out_w, out_h, ox, oy, 0,
-                                         c->tiled ? 1 : 0, &pk, c->twd_row));
+                                         c->tiled ? 1 : 0, &pk, c->twd_row, &n_partials));
   }
-  return rdl::LaunchPeakFinal(s, pk.partials, std::max<uint32_t>(out_h, 1), d_out, out_w,
+  return rdl::LaunchPeakFinal(s, pk.partials, std::max<uint32_t>(n_partials, 1), d_out, out_w,
                               out_h, 1, d_mask != nullptr, rdl::PeakSlot(s, slot));
 }
 

@@ -87,6 +87,19 @@ CONFIGS = {
     # (make_config_golden.py: image_cap "near_tie")
     "h8k": dict(kind="multiscale", size=8192, points=2000, blobs=200, threshold=5 * NOISE,
                 max_scales=6, cap=16000, image_cap="near_tie", image_cap2=2400),
+    # C2 run to the 5-sigma threshold (no component cap): the end state of a
+    # to-threshold run (component count, stop, final peak, residual RMS,
+    # model flux, image samples) against the oracle's
+    # (multiscale_algorithm.cc:323-543, countdown :249, :363-373)
+    "c2t": dict(kind="multiscale", size=4096, points=1000, blobs=100, threshold=5 * NOISE,
+                max_scales=6, cap=10 ** 9),
+    # the bench's tiled_n1 workload (the h8k image split 8 x 8) on the
+    # concurrent pool (settings.parallel.max_threads 16): every subimage trims
+    # from the residual as it was when the pass started, the schedule the
+    # pool computes (parallel_deconvolution.cc:583-617 with all threads
+    # trimming before the first copy-back); `cap` components per subimage
+    "p8k": dict(kind="tiled", size=8192, points=2000, blobs=200, threshold=5 * NOISE,
+                max_scales=6, grid=8, cap=300, snapshot=True, pool=16),
     # bench.py's live CPU-vs-GPU wall-clock-to-threshold leg: C2's sky density
     # on 2048^2, small enough for the CPU oracle to reach the threshold inside
     # the default bench run (no fixture: both sides run it in the same job)

@@ -36,7 +36,8 @@ def image_summary(prefix, planes):
     return {f"{prefix}_sha256": cp.sha256(planes),
             f"{prefix}_sample": flat[:, idx],
             f"{prefix}_absmax": np.abs(flat).max(axis=1),
-            f"{prefix}_rms": np.sqrt(np.mean(flat.astype(np.float64) ** 2, axis=1))}
+            f"{prefix}_rms": np.sqrt(np.mean(flat.astype(np.float64) ** 2, axis=1)),
+            f"{prefix}_sum": flat.astype(np.float64).sum(axis=1)}
 
 
 def settings(c):
@@ -65,7 +66,7 @@ def make(name):
     t0 = time.time()
     if c["kind"] == "tiled":
         par = OracleParallel(orc, 1, c["grid"], c["grid"], **settings(c))
-        par.set_snapshot(False)
+        par.set_snapshot(bool(c.get("snapshot", False)))
         r, boxes, labels, trace = par.execute(res, mod, psfs, 1.0)
         m, v = par.margins()
         out.update(boxes=boxes, labels_sha256=cp.sha256(labels), trace=trace,

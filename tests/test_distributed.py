@@ -26,6 +26,9 @@ import pytest
 from oracle_lib import OracleParallel, get_oracle
 from synthetic import problem
 
+# the residual/model agreement of tests/test_configs_gpu.py (x max|dirty|)
+IMG_TOL = 1e-6
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
@@ -119,7 +122,7 @@ def test_distributed_tiled_matches_oracle_snapshot(tmp_path, world, kind, w, gw,
     par.set_snapshot(True)
     res_o, mod_o = dirty.copy(), np.zeros((channels, h, w), np.float32)
     prev = 0
-    tol = 2e-5 * np.abs(dirty).max()
+    tol = IMG_TOL * np.abs(dirty).max()
     for major in range(majors):
         r_o, _, _, trace_o = par.execute(res_o, mod_o, psf, mgain)
         # every rank holds the same merged images and counters
@@ -139,8 +142,10 @@ def test_distributed_tiled_matches_oracle_snapshot(tmp_path, world, kind, w, gw,
         assert int(outs[0][f"iterations{major}"]) == r_o.total_iterations - prev
         prev = r_o.total_iterations
         assert bool(outs[0][f"another{major}"]) == bool(r_o.another_iteration_required)
-        assert np.abs(outs[0][f"residual{major}"].reshape(res_o.shape) - res_o).max() <= tol
-        assert np.abs(outs[0][f"model{major}"].reshape(mod_o.shape) - mod_o).max() <= tol
+        dr = np.abs(outs[0][f"residual{major}"].reshape(res_o.shape) - res_o).max()
+        dm = np.abs(outs[0][f"model{major}"].reshape(mod_o.shape) - mod_o).max()
+        print(f"major {major}: residual {dr:.3g}, model {dm:.3g} (tolerance {tol:.3g})")
+        assert dr <= tol and dm <= tol, (dr, dm, tol)
 
 
 @pytest.mark.gpu
@@ -168,7 +173,7 @@ def test_rccl_communicator_single_rank():
     assert r["iterations"] == r_o.total_iterations
     for i in range(gw * gh):
         assert np.array_equal(run.trace(i), trace_o[trace_o[:, 0] == i][:, 1:])
-    tol = 2e-5 * np.abs(dirty).max()
+    tol = IMG_TOL * np.abs(dirty).max()
     assert np.abs(run.residual().reshape(w, w) - res_o[0]).max() <= tol
     assert np.abs(run.model().reshape(w, w) - mod_o[0]).max() <= tol
     del run
