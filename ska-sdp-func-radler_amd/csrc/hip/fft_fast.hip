@@ -574,7 +574,8 @@ __global__ __launch_bounds__(TH) void ColumnsConvD(ColArgs a, const Cx<double>* 
     // multiplied (1024 threads: the registers go to the second set of waves)
     // (register K before the forward transform costs more than it hides:
     // the first pass's input loads then wait for it in order, vmcnt; with a
-    // float K at 1 024 threads: 623 -> 668 us per 9072^2 pass)
+    // float K at 1 024 threads: 623 -> 668 us per 9072^2 pass; the first two
+    // rounds' K issued after the first pass instead: 630 -> 758 us, r05)
     constexpr bool KREG = TH <= 512;
     KT K[KREG ? BL : 1][KREG ? RL : 1];
     if constexpr (KREG) {
@@ -628,6 +629,7 @@ struct RowArgs {
   int tiled;            // spectrum in column tiles (see TileIndex), else row-major
   int all_rows;         // forward: every plane row (zero outside the window)
   RowPeak peak;         // inverse: fused peak search when peak.partials
+  int prefetch;         // inverse, subtract: load the residual row before the transform
 };
 
 
@@ -724,12 +726,27 @@ __global__ __launch_bounds__(TH) void RowsInverse(RowArgs a, const Cx<T>* __rest
   }
   if constexpr (LT && PF)
     if (iy + gridDim.x < a.img_h) prefetch(iy + gridDim.x, tid);
+  float* o = out + size_t(iy) * a.img_w;
+  // subtract (the residual correction): the row's residual values loaded
+  // now, issued after the spectrum loads, so they arrive during the
+  // transform instead of after it (LdsSync waits for LDS only)
+  const bool even_win = ((a.ox | a.img_w) & 1u) == 0;
+  float2 rpre[EH];
+  if (a.subtract && a.prefetch && even_win) {
+#pragma unroll
+    for (uint32_t i = 0; i < EH; ++i) {
+      const uint32_t n = tid + i * TH;
+      if (H % TH != 0 && n >= H) continue;
+      const uint32_t x0 = 2 * n;
+      if (x0 < a.ox || x0 >= a.ox + a.img_w) continue;
+      rpre[i] = *reinterpret_cast<const float2*>(o + (x0 - a.ox));
+    }
+  }
   LdsSync();
   if constexpr (LT)
     FftC<TH, H, 1, Rs...>(buf, ctab, 0, clast, tid);
   else
     Fft<T, TH, H, 0, 1, Rs...>(buf, ptw, tid);
-  float* o = out + size_t(iy) * a.img_w;
   // fused peak search over the values as written (window coordinates): per
   // thread the largest PeakKey value word (0: none qualifies) and its first
   // x, in 32-bit compares (a thread visits its x in ascending order, so the
@@ -759,7 +776,7 @@ __global__ __launch_bounds__(TH) void RowsInverse(RowArgs a, const Cx<T>* __rest
     best = BlockMaxU64(best, red);
     if (tid == 0) a.peak.partials[iy] = best;
   };
-  if (((a.ox | a.img_w) & 1u) == 0) {
+  if (even_win) {
     // even window: (x[2n], x[2n+1]) both in or both out, one 8-B access
 #pragma unroll
     for (uint32_t i = 0; i < EH; ++i) {
@@ -771,7 +788,7 @@ __global__ __launch_bounds__(TH) void RowsInverse(RowArgs a, const Cx<T>* __rest
       float2* p = reinterpret_cast<float2*>(o + (x0 - a.ox));
       float2 v = {float(z.x), float(-z.y)};
       if (a.subtract) {
-        const float2 r = *p;
+        const float2 r = a.prefetch ? rpre[i] : *p;
         v = {r.x - v.x, r.y - v.y};
       }
       *p = v;
@@ -2040,6 +2057,7 @@ int ConvColumnsDLaunch(rdl_session* s, const FastColumns* p, const void* in, voi
   a.out_row0 = out_row0;
   a.out_row_n = out_row_n;
   a.tiled = tiled ? 1u : 0u;
+
   const uint32_t want = std::min<uint32_t>(n_cols, uint32_t(s->n_cus) * uint32_t(slots));
   a.per_xcd = std::max<uint32_t>(1, (want + 7) / 8);
   const uint32_t grid = 8 * a.per_xcd;
@@ -2114,6 +2132,12 @@ int FastRowsInverseLaunch(rdl_session* s, const FastRows* p, const void* spec, f
   a.subtract = subtract;
   a.tiled = tiled;
   if (peak) a.peak = *peak;
+  // RDL_ROWS_RPRE=0: the residual read where it is subtracted (comparison)
+  static const int rpre = [] {
+    const char* e = std::getenv("RDL_ROWS_RPRE");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  a.prefetch = rpre;
   // LT kernels are persistent (rows grid-strided): one table load per workgroup.
   // A session with a second lane keeps one slot per CU free for the other
   // lane's column passes (8192^2 bench: 762.8 -> 757.3 ms per step; 770.9
