@@ -69,7 +69,7 @@ int rdl_comm_allreduce_max(rdl_session* s, float* value) {
 
 int rdl_comm_allreduce_max_n(rdl_session* s, float* values, size_t n) {
   RDL_ARG_CHECK(s && values && s->comm, "communicator not initialised");
-  RDL_ARG_CHECK(n * sizeof(float) <= (1u << 16), "too many values");
+  RDL_ARG_CHECK(n * sizeof(float) <= rdl::kPeakTickets, "too many values");
   if (n == 0) return RDL_OK;
   float* d = static_cast<float*>(s->d_small);
   RDL_HIP_CHECK(hipMemcpyAsync(d, values, n * sizeof(float), hipMemcpyHostToDevice,

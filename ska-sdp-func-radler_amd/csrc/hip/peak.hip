@@ -24,7 +24,7 @@ struct BoxArgs {
 
 template <bool kVec>
 __global__ __launch_bounds__(256) void FindPeakPartial(BoxArgs a,
-                                                       uint64_t* partials) {
+                                                       uint64_t* partials, PeakFinish f) {
   __shared__ uint64_t lds[16];
   uint64_t best = 0;
   const uint32_t y0 = a.ys + blockIdx.x * a.rows_per_block;
@@ -58,15 +58,14 @@ __global__ __launch_bounds__(256) void FindPeakPartial(BoxArgs a,
     }
   }
   best = BlockMaxU64(best, lds);
-  if (threadIdx.x == 0) partials[blockIdx.x] = best;
+  if (!f.ticket) {
+    if (threadIdx.x == 0) partials[blockIdx.x] = best;
+    return;
+  }
+  if (threadIdx.x == 0)
+    __hip_atomic_store(partials + blockIdx.x, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  PeakArrive(f, lds);
 }
-
-struct PeakOut {
-  uint64_t key;
-  float value;
-  uint32_t x, y;
-  int32_t found;
-};
 
 __global__ __launch_bounds__(1024) void FindPeakFinal(
     const uint64_t* partials, uint32_t n, const float* image, uint32_t width,
@@ -76,29 +75,7 @@ __global__ __launch_bounds__(1024) void FindPeakFinal(
   for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
     best = partials[i] > best ? partials[i] : best;
   best = BlockMaxU64(best, lds);
-  if (threadIdx.x == 0) {
-    PeakOut o;
-    o.key = best;
-    if (best != 0) {
-      const uint32_t idx = 0xffffffffu - uint32_t(best & 0xffffffffu);
-      o.x = idx % width;
-      o.y = idx / width;
-      o.value = image[idx];
-      o.found = 1;
-    } else if (avx_semantics && !has_mask) {
-      // peak_finder.cc:202,250-252: peakIndex starts at 0
-      o.x = 0;
-      o.y = 0;
-      o.value = image[0];
-      o.found = 1;
-    } else {
-      o.x = width;
-      o.y = height;
-      o.value = 0.0f;
-      o.found = 0;
-    }
-    *out = o;
-  }
+  if (threadIdx.x == 0) PeakOutOfKey(best, image, width, height, avx_semantics, has_mask, out);
 }
 
 __global__ __launch_bounds__(256) void SumSquaresPartial(const float* v,
@@ -141,13 +118,17 @@ int LaunchPeakFinal(rdl_session* s, const uint64_t* partials, uint32_t n,
 }
 
 void* PeakSlot(rdl_session* s, uint32_t slot) {
-  return static_cast<char*>(s->d_small) + 32 * 1024 + size_t(slot) * sizeof(PeakOut);
+  return MappedResult(s, kMappedPeakSlots + size_t(slot) * sizeof(PeakOut));
+}
+
+uint32_t* PeakTicket(rdl_session* s, uint32_t slot) {
+  return reinterpret_cast<uint32_t*>(static_cast<char*>(s->d_small) + kPeakTickets) + slot;
 }
 
 int LaunchFindPeak(rdl_session* s, const float* d_image, uint32_t width,
                    uint32_t height, uint32_t start_y, uint32_t end_y,
                    uint32_t h_border, uint32_t v_border, int allow_negative,
-                   const uint8_t* d_mask, int avx_semantics, void* d_out) {
+                   const uint8_t* d_mask, int avx_semantics, void* d_out, uint32_t ticket) {
   BoxArgs a;
   a.image = d_image;
   a.mask = d_mask;
@@ -176,16 +157,30 @@ int LaunchFindPeak(rdl_session* s, const float* d_image, uint32_t width,
   const double bytes = double(rows) * (a.xe - a.xs) * (d_mask ? 5.0 : 4.0);
   {
     ScopedTiming t(s, "find_peak", bytes);
+    // the last workgroup finishes the search (PeakArrive); an empty box
+    // keeps the two launches
+    PeakFinish f;
+    if (rows != 0) {
+      f.ticket = PeakTicket(s, ticket);
+      f.out = static_cast<PeakOut*>(d_out);
+      f.partials = partials;
+      f.n_partials = blocks;
+      f.image = d_image;
+      f.width = width;
+      f.height = height;
+      f.avx_semantics = avx_semantics;
+      f.has_mask = d_mask != nullptr;
+    }
     if (rows == 0) {
       RDL_HIP_CHECK(hipMemsetAsync(partials, 0, sizeof(uint64_t), s->stream));
+      FindPeakFinal<<<1, 1024, 0, s->stream>>>(
+          partials, blocks, d_image, width, height, avx_semantics,
+          d_mask != nullptr, static_cast<PeakOut*>(d_out));
     } else if (vec) {
-      FindPeakPartial<true><<<blocks, 256, 0, s->stream>>>(a, partials);
+      FindPeakPartial<true><<<blocks, 256, 0, s->stream>>>(a, partials, f);
     } else {
-      FindPeakPartial<false><<<blocks, 256, 0, s->stream>>>(a, partials);
+      FindPeakPartial<false><<<blocks, 256, 0, s->stream>>>(a, partials, f);
     }
-    FindPeakFinal<<<1, 1024, 0, s->stream>>>(
-        partials, blocks, d_image, width, height, avx_semantics,
-        d_mask != nullptr, static_cast<PeakOut*>(d_out));
   }
   RDL_HIP_CHECK(hipGetLastError());
   return RDL_OK;
@@ -203,11 +198,12 @@ int rdl_find_peak(rdl_session* s, const float* d_image, uint32_t width,
   RDL_ARG_CHECK(width > 0 && height > 0, "empty image");
   RDL_ARG_CHECK(uint64_t(width) * height < 0xffffffffull,
                 "image too large for 32-bit pixel index");
+  void* d_out = rdl::MappedResult(s, rdl::kMappedPeak);
   RDL_TRY(rdl::LaunchFindPeak(s, d_image, width, height, start_y, end_y,
                               h_border, v_border, allow_negative, d_mask,
-                              avx_semantics, s->d_small));
+                              avx_semantics, d_out, RDL_PEAK_SLOTS));
   rdl::PeakOut o;
-  const rdl::SmallRead r{&o, s->d_small, sizeof(o)};
+  const rdl::SmallRead r{&o, d_out, sizeof(o)};
   RDL_TRY(rdl::ReadSmall(s, &r, 1));
   out->value = o.value;
   out->x = o.x;
@@ -238,7 +234,7 @@ int rdl_find_peak_enqueue(rdl_session* s, const float* d_image, uint32_t width,
                 "image too large for 32-bit pixel index");
   RDL_ARG_CHECK(slot < RDL_PEAK_SLOTS, "peak slot out of range");
   return rdl::LaunchFindPeak(s, d_image, width, height, start_y, end_y, h_border, v_border,
-                             allow_negative, d_mask, avx_semantics, PeakSlots(s) + slot);
+                             allow_negative, d_mask, avx_semantics, PeakSlots(s) + slot, slot);
 }
 
 int rdl_find_peak_collect(rdl_session* s, uint32_t n, rdl_peak* out) {
@@ -263,7 +259,7 @@ int rdl_rms(rdl_session* s, const float* d_image, size_t n, float* out) {
   const uint32_t blocks = std::min<size_t>(1024, rdl::DivUp(n, 256));
   RDL_TRY(s->EnsureScratch(s->partials, blocks * sizeof(double)));
   double* partials = static_cast<double*>(s->partials.ptr);
-  float* d_out = static_cast<float*>(s->d_small);
+  float* d_out = static_cast<float*>(rdl::MappedResult(s, rdl::kMappedRms));
   {
     rdl::ScopedTiming t(s, "rms", double(n) * 4.0);
     rdl::SumSquaresPartial<<<blocks, 256, 0, s->stream>>>(d_image, n,

@@ -93,6 +93,22 @@ inline hipError_t HostFree(void* p) {
   UntrackBlock(p);
   return hipHostFree(p);
 }
+// Coherent pinned host memory the device writes directly (zero-copy): the
+// results a host waits for (peaks, selection counts, loop results) are
+// stored there by the kernel that makes them, so reading one back costs a
+// stream sync and no copy launch. *d is the device's address of it.
+inline hipError_t MappedMalloc(void** h, void** d, size_t bytes) {
+  hipError_t e = hipHostMalloc(h, bytes, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e != hipSuccess) return e;
+  TrackBlock(*h, bytes, 'h');
+  e = hipHostGetDevicePointer(d, *h, 0);
+  if (e != hipSuccess) {
+    UntrackBlock(*h);
+    (void)hipHostFree(*h);
+    *h = nullptr;
+  }
+  return e;
+}
 
 }  // namespace rdl
 
@@ -116,6 +132,11 @@ struct rdl_session {
   // small device/host scratch used by reductions
   void* d_small = nullptr;       // 64 KiB device
   void* h_small = nullptr;       // 64 KiB pinned host
+  // 64 KiB coherent host memory written by kernels (MappedMalloc): [0, 4K)
+  // single results (rdl_find_peak, rdl_rms, the selection count), [4K, 8K)
+  // the sub-minor loop result, [32K, 64K) the deferred peak slots
+  void* m_small = nullptr;       // host address
+  void* m_small_dev = nullptr;   // device address of the same bytes
   rdl::Scratch partials;         // per-block partial keys
   rdl::Scratch radix;            // radix-select histograms
   bool poison = false;                 // RDL_POISON=1: NaN-fill fresh allocations
@@ -284,6 +305,8 @@ int LaunchPeakFinal(rdl_session* s, const uint64_t* partials, uint32_t n,
                     const float* image, uint32_t width, uint32_t height, int avx_semantics,
                     int has_mask, void* d_out);
 void* PeakSlot(rdl_session* s, uint32_t slot);
+// the arrival ticket of peak slot `slot` (RDL_PEAK_SLOTS: rdl_find_peak's)
+uint32_t* PeakTicket(rdl_session* s, uint32_t slot);
 
 // Block-wide max of a uint64 (blockDim multiple of 64, <= 1024).
 __device__ __forceinline__ uint64_t BlockMaxU64(uint64_t v, uint64_t* lds) {
@@ -301,6 +324,83 @@ __device__ __forceinline__ uint64_t BlockMaxU64(uint64_t v, uint64_t* lds) {
   __syncthreads();
   const uint64_t r = lds[0];
   return r;
+}
+
+// A peak search's result (rdl_find_peak / _collect read it from the
+// session's mapped buffer).
+struct PeakOut {
+  uint64_t key;
+  float value;
+  uint32_t x, y;
+  int32_t found;
+};
+
+// The result of the best key (peak_finder.cc:202,250-252: with the AVX
+// semantics and no mask an empty box reports pixel 0).
+__device__ __forceinline__ void PeakOutOfKey(uint64_t best, const float* image, uint32_t width,
+                                             uint32_t height, int avx_semantics, int has_mask,
+                                             PeakOut* out) {
+  PeakOut o;
+  o.key = best;
+  if (best != 0) {
+    const uint32_t idx = 0xffffffffu - uint32_t(best & 0xffffffffu);
+    o.x = idx % width;
+    o.y = idx / width;
+    o.value = image[idx];
+    o.found = 1;
+  } else if (avx_semantics && !has_mask) {
+    o.x = 0;
+    o.y = 0;
+    o.value = image[0];
+    o.found = 1;
+  } else {
+    o.x = width;
+    o.y = height;
+    o.value = 0.0f;
+    o.found = 0;
+  }
+  *out = o;
+}
+
+// In-kernel second stage of a peak search over an image an earlier launch
+// wrote: every workgroup arrives once, after thread 0 stored its partial key
+// with an agent-scope (write-through) store; the last to arrive reduces the
+// n_partials keys and writes the PeakOut (no FindPeakFinal launch). No
+// fences: the partials travel by write-through stores and agent-scope loads
+// (a release fence here writes back the whole L2). The ticket is 0 between
+// launches (the last workgroup resets it); one per concurrently pending
+// search (PeakTicket).
+struct PeakFinish {
+  uint32_t* ticket = nullptr;  // nullptr: the caller launches FindPeakFinal
+  PeakOut* out = nullptr;
+  const uint64_t* partials = nullptr;
+  uint32_t n_partials = 0;
+  const float* image = nullptr;
+  uint32_t width = 0, height = 0;
+  int avx_semantics = 0, has_mask = 0;
+};
+
+// Every thread of every workgroup calls this once (it holds barriers).
+// lds: >= 16 uint64 of the caller's shared memory.
+__device__ __forceinline__ void PeakArrive(const PeakFinish& f, uint64_t* lds) {
+  __shared__ uint32_t last;
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the partial has landed
+    last = atomicAdd(f.ticket, 1u) == gridDim.x - 1u ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!last) return;
+  uint64_t best = 0;
+  for (uint32_t i = threadIdx.x; i < f.n_partials; i += blockDim.x) {
+    const uint64_t v = __hip_atomic_load(f.partials + i, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    best = v > best ? v : best;
+  }
+  best = BlockMaxU64(best, lds);
+  if (threadIdx.x == 0) {
+    PeakOutOfKey(best, f.image, f.width, f.height, f.avx_semantics, f.has_mask, f.out);
+    __hip_atomic_store(f.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 inline unsigned DivUp(size_t a, size_t b) { return unsigned((a + b - 1) / b); }
@@ -334,9 +434,18 @@ struct SmallRead {
   const void* d_src;
   size_t bytes;
 };
+// A region inside the session's mapped buffer (m_small) is read in place
+// after the sync: no copy.
+inline const char* MappedHost(const rdl_session* s, const void* d_src, size_t bytes) {
+  const char* d = static_cast<const char*>(d_src);
+  const char* m = static_cast<const char*>(s->m_small_dev);
+  if (!m || d < m || d + bytes > m + (size_t(1) << 16)) return nullptr;
+  return static_cast<const char*>(s->m_small) + (d - m);
+}
 inline int ReadSmall(rdl_session* s, const SmallRead* reads, int n) {
   size_t off = 0;
   for (int i = 0; i < n; ++i) {
+    if (MappedHost(s, reads[i].d_src, reads[i].bytes)) continue;
     const size_t b = (reads[i].bytes + 15) / 16 * 16;
     if (off + b > (size_t(1) << 16)) {
       SetError("ReadSmall: more than 64 KiB");
@@ -349,10 +458,34 @@ inline int ReadSmall(rdl_session* s, const SmallRead* reads, int n) {
   RDL_HIP_CHECK(hipStreamSynchronize(s->stream));
   off = 0;
   for (int i = 0; i < n; ++i) {
+    if (const char* m = MappedHost(s, reads[i].d_src, reads[i].bytes)) {
+      std::memcpy(reads[i].h_dst, m, reads[i].bytes);
+      continue;
+    }
     std::memcpy(reads[i].h_dst, static_cast<const char*>(s->h_small) + off,
                 reads[i].bytes);
     off += (reads[i].bytes + 15) / 16 * 16;
   }
   return RDL_OK;
 }
+// the mapped buffer's regions (device addresses); RDL_ZERO_COPY=0 keeps
+// the results in device memory and reads them back by copies (comparison)
+inline bool ZeroCopyOn() {
+  static const bool on = [] {
+    const char* e = std::getenv("RDL_ZERO_COPY");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+inline void* MappedResult(rdl_session* s, size_t offset) {
+  return static_cast<char*>(ZeroCopyOn() ? s->m_small_dev : s->d_small) + offset;
+}
+constexpr size_t kMappedSelTotal = 0;      // uint64_t selection count
+constexpr size_t kMappedPeak = 64;         // PeakOut of rdl_find_peak
+constexpr size_t kMappedRms = 128;         // float of rdl_rms
+constexpr size_t kMappedLoop = 4096;       // sub-minor LoopResult (+ phase probes)
+constexpr size_t kMappedPeakSlots = 32 * 1024;
+// the device small buffer's last 1 KiB: peak search tickets (PeakTicket),
+// zeroed at session creation
+constexpr size_t kPeakTickets = 63 * 1024;
 }  // namespace rdl

@@ -361,7 +361,10 @@ int rdl_session_create(int device, rdl_session** out) {
   s->cache_on = !(cache && cache[0] == '0');
   s->trace_subminor_phases = trace && trace[0] == '1';  // 2: timing only
   RDL_HIP_CHECK(rdl::DevMalloc(&s->d_small, 1 << 16));
+  RDL_HIP_CHECK(hipMemset(s->d_small, 0, 1 << 16));  // the peak tickets start at 0
   RDL_HIP_CHECK(rdl::HostMalloc(&s->h_small, 1 << 16));
+  RDL_HIP_CHECK(rdl::MappedMalloc(&s->m_small, &s->m_small_dev, 1 << 16));
+  std::memset(s->m_small, 0, 1 << 16);
   {
     const std::lock_guard<std::mutex> lock(rdl::g_registry_mutex);
     rdl::g_sessions.push_back(s.get());
@@ -412,6 +415,7 @@ int rdl_session_destroy(rdl_session* s) {
   if (s->iuwt.ptr) (void)rdl::DevFree(s->iuwt.ptr);
   if (s->d_small) (void)rdl::DevFree(s->d_small);
   if (s->h_small) (void)rdl::HostFree(s->h_small);
+  if (s->m_small) (void)rdl::HostFree(s->m_small);
   if (s->comm) rdl_comm_destroy(s);
   if (s->aux) (void)hipStreamDestroy(s->aux);
   if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);

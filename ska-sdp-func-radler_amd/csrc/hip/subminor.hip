@@ -161,7 +161,7 @@ __global__ __launch_bounds__(kSelThreads) void SelCount(SelArgs a,
 // Thread t owns the contiguous segment [t seg, (t + 1) seg): sums it, one
 // block scan of the 1024 sums, then rewrites its segment as offsets.
 __global__ __launch_bounds__(1024) void SelScan(uint32_t* counts, uint32_t n,
-                                                uint64_t* total) {
+                                                uint64_t* total, uint64_t* total_host) {
   __shared__ uint64_t lds[1024];
   const uint32_t t = threadIdx.x;
   const uint32_t seg = (n + 1023) / 1024;
@@ -182,7 +182,10 @@ __global__ __launch_bounds__(1024) void SelScan(uint32_t* counts, uint32_t n,
     counts[i] = uint32_t(run);
     run += c;
   }
-  if (t == 1023) *total = lds[1023];
+  if (t == 1023) {
+    *total = lds[1023];
+    *total_host = lds[1023];  // the host's copy (mapped memory, no read-back copy)
+  }
 }
 
 __global__ __launch_bounds__(kSelThreads) void SelScatter(
@@ -1063,7 +1066,13 @@ __global__ __launch_bounds__(256) void BuildPairTable(const uint32_t* __restrict
                                                       const float* __restrict__ psfs,
                                                       uint32_t n_sel, uint32_t n_psf,
                                                       uint32_t width, uint32_t height,
-                                                      float* __restrict__ table) {
+                                                      float* __restrict__ table,
+                                                      uint64_t* __restrict__ zero,
+                                                      uint32_t zero_words) {
+  // the loop's per-launch exchange area, zeroed here (no memset launch: the
+  // loop runs after this kernel on the same stream)
+  if (blockIdx.x == 0 && blockIdx.y == 0)
+    for (uint32_t w = threadIdx.x; w < zero_words; w += 256) zero[w] = 0ull;
   const uint32_t j = blockIdx.x * 256 + threadIdx.x;
   const uint32_t p = blockIdx.y;
   if (j >= n_sel) return;
@@ -2669,6 +2678,8 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
                                                                  : rdl::kSpChunk));
   const uint32_t chunk_slots = quad ? rdl::kQuadChunk : rdl::kSpChunk;
   uint64_t* d_total = reinterpret_cast<uint64_t*>(s->d_small);
+  // the count the host reads: SelScan also stores it in the mapped buffer
+  uint64_t* m_total = static_cast<uint64_t*>(rdl::MappedResult(s, rdl::kMappedSelTotal));
   const double sel_bytes = double(sa.box_pixels) * 4.0 * p->n_images;
   // positions of up to the whole box (single pass) or the counts (three
   // kernels: RDL_SUBMINOR_SELECT=3, for comparison)
@@ -2690,7 +2701,7 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
     else
       rdl::SelLocal<<<n_chunks, rdl::kSpThreads, 0, st>>>(
           sa, counts, static_cast<uint32_t*>(h->local_buf));
-    rdl::SelScan<<<1, 1024, 0, st>>>(counts, n_chunks, d_total);
+    rdl::SelScan<<<1, 1024, 0, st>>>(counts, n_chunks, d_total, m_total);
     rdl::SelPlace<<<n_chunks, 256, 0, st>>>(counts, n_chunks, d_total,
                                             static_cast<const uint32_t*>(h->local_buf),
                                             chunk_slots, static_cast<uint32_t*>(h->pos_buf));
@@ -2713,13 +2724,14 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
     counts = static_cast<uint32_t*>(h->counts);
     rdl::ScopedTiming t(s, "subminor_select", 2.0 * sel_bytes);
     rdl::SelCount<<<n_chunks, rdl::kSelThreads, 0, st>>>(sa, counts);
-    rdl::SelScan<<<1, 1024, 0, st>>>(counts, n_chunks, d_total);
+    rdl::SelScan<<<1, 1024, 0, st>>>(counts, n_chunks, d_total, m_total);
   }
   RDL_HIP_CHECK(hipGetLastError());
   uint64_t n_sel = 0;
   uint32_t failed = 0;
   {
-    const rdl::SmallRead r[2] = {{&n_sel, d_total, sizeof(n_sel)},
+    const rdl::SmallRead r[2] = {{&n_sel, h->select_passes == 1 ? d_total : m_total,
+                                  sizeof(n_sel)},
                                  {&failed, sel_failed, sizeof(failed)}};
     RDL_TRY(rdl::ReadSmall(s, r, sel_failed ? 2 : 1));
   }
@@ -2980,22 +2992,33 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   RDL_TRY(rdl::Grow(&h->sync, &h->sync_bytes, sync_need, st));
   char* sb = static_cast<char*>(h->sync);
   la.counter = reinterpret_cast<uint32_t*>(sb);
-  la.result = reinterpret_cast<uint32_t*>(sb + 256);
+  // the result (and the timeout flag, word 8) goes straight to the mapped
+  // buffer: no read-back copy; the previous run's words are cleared here (the
+  // stream is idle: every run ends in ReadSmall's sync)
+  la.result = static_cast<uint32_t*>(rdl::MappedResult(s, rdl::kMappedLoop));
+  if (rdl::ZeroCopyOn())
+    std::memset(static_cast<char*>(s->m_small) + rdl::kMappedLoop, 0, 256);
+  else
+    RDL_HIP_CHECK(hipMemsetAsync(la.result, 0, 256, st));
   la.records = reinterpret_cast<uint32_t*>(sb + 512);
   la.trace = n_trace ? reinterpret_cast<uint32_t*>(sb + 512 + rec_bytes) : nullptr;
   la.trace_cap = n_trace;
-  // zero counter, result and (register kernel) the epoch-tagged granules
-  RDL_HIP_CHECK(hipMemsetAsync(sb, 0, (use_reg || use_tab || use_tabn) ? 512 + rec_bytes : 512, st));
+  // zero counter, result and (register kernel) the epoch-tagged granules:
+  // with a pairwise table, by BuildPairTable
+  const size_t zero_bytes = (use_reg || use_tab || use_tabn) ? 512 + rec_bytes : 512;
+  const bool table_zeroes = (use_reg || use_tab || use_tabn) && want_table;
+  if (!table_zeroes) RDL_HIP_CHECK(hipMemsetAsync(sb, 0, zero_bytes, st));
   la.table = nullptr;
   const uint32_t n_psf = ni / p->n_pol;
-  if ((use_reg || use_tab || use_tabn) && want_table) {
+  if (table_zeroes) {
     // (+ 32 KiB: the table loop reads whole workgroup-sized slices of a row)
     const size_t table_bytes = size_t(n_psf) * n_sel * n_sel * sizeof(float) + (32 << 10);
     RDL_TRY(rdl::Grow(&h->table, &h->table_bytes, table_bytes, st));
     rdl::ScopedTiming t(s, "subminor_table", 8.0 * double(n_psf) * n_sel * n_sel);
     rdl::BuildPairTable<<<dim3(rdl::DivUp(n_sel, 256), uint32_t(n_sel)), 256, 0, st>>>(
         h->d_pos, d_psfs, uint32_t(n_sel), n_psf, p->width, p->height,
-        static_cast<float*>(h->table));
+        static_cast<float*>(h->table), reinterpret_cast<uint64_t*>(sb),
+        uint32_t((zero_bytes + 7) / 8));
     RDL_HIP_CHECK(hipGetLastError());
     la.table = static_cast<const float*>(h->table);
   }

@@ -641,6 +641,30 @@ void ParallelDeconvolution::RunSubImagesConcurrently(
   std::vector<size_t> todo;  // the subimages this call runs, in index order
   for (size_t i = 0; i != n_sub; ++i)
     if (!run || (*run)[i]) todo.push_back(i);
+  // RADLER_POOL_QUEUE=1: workers on the main device take subimages from one
+  // queue, the costliest first (the longest-processing-time rule: the
+  // cleaning pass's estimate from the start peaks, as the ranks' LptOwners;
+  // the find-peak pass by area). Off by default: the passes are bound by the
+  // GPU's throughput over the 16 streams, not by the workers' balance, and
+  // the queue measured slower on the box (8192^2 8 x 8 tiled cleaning pass
+  // 3.20-3.25 s round-robin vs 3.33-3.40 s queued, r05). Workers on other
+  // GPUs always keep the fixed assignment (their planes are staged on the
+  // main device before the pass).
+  const char* queue_env = std::getenv("RADLER_POOL_QUEUE");
+  bool all_local = !force_staging && queue_env && queue_env[0] == '1';
+  for (size_t w = 0; w != W; ++w) all_local = all_local && workers_[w]->Device() == main_device;
+  std::vector<size_t> order = todo;
+  if (all_local) {
+    const double thr = std::max<double>(algorithms_.front()->Threshold(), 1e-30);
+    std::vector<double> cost(n_sub, 0.0);
+    for (const size_t i : todo) {
+      const SubImage& sub = subimages_[i];
+      const double above = find_peak_only ? 1.0 : std::max(std::fabs(sub.peak), thr) / thr;
+      cost[i] = double(sub.width * sub.height) * (1.0 + std::log2(above));
+    }
+    std::stable_sort(order.begin(), order.end(),
+                     [&](size_t a, size_t b) { return cost[a] > cost[b]; });
+  }
   for (size_t k = 0; k != todo.size(); ++k) {
     const size_t i = todo[k];
     Slot& slot = slots[i];
@@ -663,13 +687,17 @@ void ParallelDeconvolution::RunSubImagesConcurrently(
   s.Sync();
 
   std::vector<std::exception_ptr> errors(W);
+  std::atomic<size_t> next{0};
+  std::atomic<bool> failed{false};
   auto work = [&](size_t w) {
     try {
       gpu::Session& ws = *workers_[w];
       ws.Bind();
-      for (size_t k = w; k < todo.size(); k += W) {
-        const size_t i = todo[k];
+      for (size_t k = all_local ? next.fetch_add(1) : w; k < todo.size() && !failed;
+           k = all_local ? next.fetch_add(1) : k + W) {
+        const size_t i = all_local ? order[k] : todo[k];
         Slot& slot = slots[i];
+        slot.ws = &ws;
         SubImage& sub = subimages_[i];
         const size_t sw = sub.width, sh = sub.height, n = sw * sh;
         const gpu::Planes& psfs = psf_images[psf_indices[i]];
@@ -720,6 +748,7 @@ void ParallelDeconvolution::RunSubImagesConcurrently(
       ws.Sync();
     } catch (...) {
       errors[w] = std::current_exception();
+      failed = true;
     }
   };
   std::vector<std::thread> threads;

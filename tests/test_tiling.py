@@ -172,6 +172,16 @@ def test_concurrent_pool_staging_path(monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kind,w,gw,gh,threads", [(1, 320, 3, 3, 4), (0, 192, 2, 2, 3)])
+def test_concurrent_pool_queue(kind, w, gw, gh, threads, monkeypatch):
+    """RADLER_POOL_QUEUE=1: workers take subimages from a cost-ordered queue
+    instead of the round-robin assignment; the snapshot schedule makes the
+    result independent of which worker runs which subimage."""
+    monkeypatch.setenv("RADLER_POOL_QUEUE", "1")
+    _check_tiled(kind, w, gw, gh, threads=threads, majors=2)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("threads", [1, 4])
 def test_tiled_two_major_iterations(threads):
     """The worker pool and per-subimage algorithms persist across major
