@@ -60,6 +60,8 @@ def natural(sess, c, flat, w, h):
 # plan of `height`
 CASES = [(4536, 4608, True), (4800, 5000, True), (4704, 4536, True), (9072, 9216, True),
          (9450, 9408, True), (8192, 4096, False), (4096, 8192, False),
+         # 9072-point float64 columns: the 8192^2 correction's (ColumnsConvPair)
+         (9216, 9072, True),
          # the subimage planes of tiled runs (CanonicalFftSize ladder)
          (2560, 3072, False), (3584, 1280, False), (1536, 2048, False), (2048, 1792, False),
          # the float64 corrections of gridded runs' subimages
@@ -139,7 +141,7 @@ def test_fast_convolutions_match_numpy(sess, w, h, f64):
 
 
 @pytest.mark.parametrize("pw,ph,w,h", [(4536, 4536, 4096, 4096), (9216, 9216, 8192, 8192),
-                                       (4800, 4800, 4096, 4096)])
+                                       (4800, 4800, 4096, 4096), (9072, 9072, 8192, 8192)])
 def test_fast_masked_correction(sess, pw, ph, w, h):
     """CorrectResidualDirty's sequence: sparse model rows (row mask) placed at
     the centred offset, x column-major PSF spectrum, trimmed subtraction from
