@@ -683,7 +683,7 @@ def main():
     resident = None
     if args.device_resident and not split:
         run = rd.gpu.DeviceRun(s, psf, dirty, [1.0] * args.channels if joined else [],
-                               BEAM_PX * PIXEL_SCALE)
+                               BEAM_PX * PIXEL_SCALE, trace=False)
         run.restore()
         run.execute()  # warm-up
         run.sync()

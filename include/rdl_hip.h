@@ -426,6 +426,18 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
                      rdl_subminor_result* out, uint32_t* h_trace,
                      uint64_t trace_cap);
 
+/* rdl_subminor_run in two halves, so the host can queue the work that does
+ * not depend on the loop's result (the residual correction, the model update,
+ * the next peak searches: multiscale_algorithm.cc:436-462, 521-524) before it
+ * waits for that result. _launch selects (reads the selection count) and
+ * launches the loop; out->n_selected and out->has_peak are final, the other
+ * fields are filled by _collect, which waits for the loop. The handle's
+ * selection (positions, model values) may be used by other calls on the
+ * session's stream in between. A second _launch before _collect fails. */
+int rdl_subminor_launch(rdl_subminor* h, const float* d_residuals, const float* d_psfs,
+                        const rdl_subminor_params* p, rdl_subminor_result* out);
+int rdl_subminor_collect(rdl_subminor* h, rdl_subminor_result* out);
+
 /* Kernel choice for rdl_subminor_run (results are identical): mode 0 picks
  * automatically, 1 forces the LDS-resident loop, 2 the register-resident
  * loop, 3 the single-wave loop, 4 one 1024-thread workgroup, 5 a grid of

@@ -65,6 +65,16 @@ struct rdl_subminor {
   uint32_t tab_threads = 0;           // 0: 512 up to 2048 pixels per participant, else 1024
   uint32_t tab_target = 1024;         // pixels per participant (RDL_SUBMINOR_TAB_TARGET)
   uint32_t tab_single = 8192;         // one workgroup up to this (RDL_SUBMINOR_TAB_SINGLE)
+  // a launched loop whose result has not been read (rdl_subminor_launch ->
+  // rdl_subminor_collect)
+  bool pending = false;
+  uint64_t pending_start = 0;       // iteration_start of the launch
+  double pending_bytes_per_it = 0;  // algorithmic bytes per iteration
+  const uint32_t* pending_result = nullptr;
+  hipEvent_t pending_ev0 = nullptr, pending_ev1 = nullptr;  // RDL_TRACE_SUBMINOR
+  uint64_t pending_n_sel = 0;
+  uint32_t pending_g = 0;
+  int pending_kind = 0, pending_threads = 0, pending_table = 0;
 };
 
 namespace rdl {
@@ -2620,10 +2630,45 @@ int rdl_subminor_destroy(rdl_subminor* h) {
   return RDL_OK;
 }
 
+namespace {
+int SubminorLaunch(rdl_subminor* h, const float* d_residuals, const float* d_psfs,
+                   const rdl_subminor_params* p, rdl_subminor_result* out, uint64_t trace_cap,
+                   uint32_t** trace_dev);
+int SubminorCollect(rdl_subminor* h, rdl_subminor_result* out, uint32_t* h_trace,
+                    uint64_t trace_cap, const uint32_t* trace_dev);
+}  // namespace
+
 int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
                      const float* d_psfs, const rdl_subminor_params* p,
                      rdl_subminor_result* out, uint32_t* h_trace,
                      uint64_t trace_cap) {
+  RDL_ARG_CHECK(h && d_residuals && d_psfs && p && out, "NULL argument");
+  uint32_t* trace_dev = nullptr;
+  const uint64_t cap = h_trace ? trace_cap : 0;
+  RDL_TRY(SubminorLaunch(h, d_residuals, d_psfs, p, out, cap, &trace_dev));
+  if (!h->pending) return RDL_OK;  // nothing selected: no loop
+  return SubminorCollect(h, out, h_trace, cap, trace_dev);
+}
+
+int rdl_subminor_launch(rdl_subminor* h, const float* d_residuals, const float* d_psfs,
+                        const rdl_subminor_params* p, rdl_subminor_result* out) {
+  RDL_ARG_CHECK(h && d_residuals && d_psfs && p && out, "NULL argument");
+  RDL_ARG_CHECK(!h->pending, "rdl_subminor_launch: the previous loop was not collected");
+  uint32_t* trace_dev = nullptr;
+  return SubminorLaunch(h, d_residuals, d_psfs, p, out, 0, &trace_dev);
+}
+
+int rdl_subminor_collect(rdl_subminor* h, rdl_subminor_result* out) {
+  RDL_ARG_CHECK(h && out, "NULL argument");
+  if (!h->pending) return RDL_OK;  // nothing was launched (no selection)
+  return SubminorCollect(h, out, nullptr, 0, nullptr);
+}
+
+namespace {
+int SubminorLaunch(rdl_subminor* h, const float* d_residuals, const float* d_psfs,
+                   const rdl_subminor_params* p, rdl_subminor_result* out, uint64_t trace_cap,
+                   uint32_t** trace_dev) {
+  uint32_t* h_trace = nullptr;  // (the trace is read by SubminorCollect)
   RDL_ARG_CHECK(h && d_residuals && d_psfs && p && out, "NULL argument");
   RDL_ARG_CHECK(p->n_images >= 1 && p->n_images <= RDL_MAX_IMAGES,
                 "n_images out of range");
@@ -2982,7 +3027,8 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
     const char* e = std::getenv("RDL_SUBMINOR_EXCHANGE");  // read per run (tests toggle it)
     la.agent_exchange = e && std::strcmp(e, "agent") == 0 ? 1 : 0;
   }
-  const uint64_t n_trace = (h_trace && trace_cap) ? trace_cap : 0;
+  const uint64_t n_trace = trace_cap;
+  (void)h_trace;
   const size_t rec_bytes =
       use_tab    ? (size_t(7) * g * sizeof(uint64_t) + 15) / 16 * 16
       : use_tabn ? ((size_t(1) + 2 * (3 + ni)) * g * sizeof(uint64_t) + 15) / 16 * 16
@@ -3093,6 +3139,29 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
     }
   }
   if (s->trace_subminor) RDL_HIP_CHECK(hipEventRecord(ev1, st));
+  out->has_peak = 1;  // a selection: the loop's first component exists
+  h->pending = true;
+  h->pending_start = p->iteration_start;
+  h->pending_bytes_per_it = 12.0 * double(ni) * double(n_sel);
+  h->pending_result = la.result;
+  h->pending_ev0 = ev0;
+  h->pending_ev1 = ev1;
+  h->pending_n_sel = n_sel;
+  h->pending_g = g;
+  h->pending_kind = use_tab ? 30 + int(tab_items) : use_tabn ? 50 + int(tabn_items)
+                    : use_reg ? 10 + int(items) : int(use_lds);
+  h->pending_threads = use_tab ? int(tab_threads) : use_tabn ? 256
+                       : use_wave ? 64 : use_big ? 1024 : use_reg ? int(rdl::kRegThreads) : 512;
+  h->pending_table = la.table ? 1 : 0;
+  *trace_dev = la.trace;
+  return RDL_OK;
+}
+
+int SubminorCollect(rdl_subminor* h, rdl_subminor_result* out, uint32_t* h_trace,
+                    uint64_t trace_cap, const uint32_t* trace_dev) {
+  rdl_session* s = h->s;
+  hipStream_t st = s->stream;
+  h->pending = false;
   rdl::LoopResult res{};
   uint32_t err = 0;
   {
@@ -3100,7 +3169,7 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
     // read: each read-back is a blit launch plus host latency per component run
     static_assert(sizeof(rdl::LoopResult) <= 8 * sizeof(uint32_t), "result before word 8");
     uint32_t raw[9];
-    const rdl::SmallRead r{raw, la.result, sizeof(raw)};
+    const rdl::SmallRead r{raw, h->pending_result, sizeof(raw)};
     RDL_TRY(rdl::ReadSmall(s, &r, 1));
     std::memcpy(&res, raw, sizeof(res));
     err = raw[8];
@@ -3111,9 +3180,9 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
   }
   // algorithmic bytes: 12 B x N_img x N_sel per iteration
   rdl::AddTimingBytes(s, "subminor_loop",
-                      12.0 * double(ni) * double(n_sel) *
-                          double(res.iteration - p->iteration_start));
+                      h->pending_bytes_per_it * double(res.iteration - h->pending_start));
   if (s->trace_subminor) {
+    const hipEvent_t ev0 = h->pending_ev0, ev1 = h->pending_ev1;
     float ms = 0.0f;
     RDL_HIP_CHECK(hipEventElapsedTime(&ms, ev0, ev1));
     {
@@ -3122,35 +3191,33 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
       s->event_pool.push_back(ev1);
     }
     uint64_t ph[6] = {};
-    const rdl::SmallRead r{ph, la.result + 16, sizeof(ph)};
+    const rdl::SmallRead r{ph, h->pending_result + 16, sizeof(ph)};
     RDL_TRY(rdl::ReadSmall(s, &r, 1));
     std::fprintf(stderr,
                  "[subminor] n_sel=%llu g=%u kind=%d threads=%d table=%d iters=%llu us=%.1f "
                  "gather=%llu integ=%llu wred=%llu bar=%llu xchg=%llu dec=%llu\n",
-                 (unsigned long long)n_sel, g,
-                 use_tab ? 30 + int(tab_items) : use_tabn ? 50 + int(tabn_items)
-                 : use_reg ? 10 + int(items) : int(use_lds),
-                 use_tab ? int(tab_threads) : use_tabn ? 256
-                 : use_wave ? 64 : use_big ? 1024 : use_reg ? int(rdl::kRegThreads) : 512,
-                 la.table ? 1 : 0,
-                 (unsigned long long)(res.iteration - p->iteration_start),
+                 (unsigned long long)h->pending_n_sel, h->pending_g, h->pending_kind,
+                 h->pending_threads, h->pending_table,
+                 (unsigned long long)(res.iteration - h->pending_start),
                  double(ms) * 1e3, (unsigned long long)ph[0], (unsigned long long)ph[1],
                  (unsigned long long)ph[2], (unsigned long long)ph[3],
                  (unsigned long long)ph[4], (unsigned long long)ph[5]);
   }
+  out->n_selected = h->pending_n_sel;
   out->iteration = res.iteration;
   out->has_peak = 1;
   out->peak = res.peak;
   out->diverging = res.diverging;
   out->flux_cleaned = res.flux;
-  if (n_trace) {
-    const uint64_t n = std::min<uint64_t>(res.iteration - p->iteration_start, n_trace);
-    RDL_HIP_CHECK(hipMemcpyAsync(h_trace, la.trace, n * 8,
+  if (h_trace && trace_cap && trace_dev) {
+    const uint64_t n = std::min<uint64_t>(res.iteration - h->pending_start, trace_cap);
+    RDL_HIP_CHECK(hipMemcpyAsync(h_trace, trace_dev, n * 8,
                                  hipMemcpyDeviceToHost, st));
     RDL_HIP_CHECK(hipStreamSynchronize(st));
   }
   return RDL_OK;
 }
+}  // namespace
 
 int rdl_subminor_set_tuning(rdl_subminor* h, int mode,
                             uint32_t target_per_block) {

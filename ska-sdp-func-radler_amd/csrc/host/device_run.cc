@@ -27,7 +27,8 @@ class VectorAccessor final : public aocommon::ImageAccessor {
 
 DeviceRun::DeviceRun(const Settings& settings, const float* psf,
                      const float* residual, size_t n_channels,
-                     const std::vector<double>& weights, double beam_size)
+                     const std::vector<double>& weights, double beam_size,
+                     bool record_trace)
     : settings_(settings) {
   const size_t w = settings.trimmed_image_width, h = settings.trimmed_image_height;
   const size_t n = w * h;
@@ -72,7 +73,7 @@ DeviceRun::DeviceRun(const Settings& settings, const float* psf,
     algorithm = std::make_unique<algorithms::IuwtDeconvolution>();
   else
     throw std::runtime_error("DeviceRun: unsupported algorithm");
-  algorithm->SetRecordTrace(true);  // Trace(): the parity tests' component traces
+  algorithm->SetRecordTrace(record_trace);  // Trace(): the parity tests' component traces
   algorithm->SetMaxIterations(settings.minor_iteration_count);
   algorithm->SetThreshold(settings.absolute_threshold);
   algorithm->SetMinorLoopGain(settings.minor_loop_gain);

@@ -21,9 +21,11 @@ class DeviceRun {
   /// psf, residual: n_images planes (one per deconvolution channel x pol,
   /// all polarizations Stokes I when n_images > 1 means channels) of
   /// width x height floats in host memory; weights per channel (may be empty).
+  /// record_trace: keep every algorithm's component trace (Trace(); the
+  /// parity tests); off, the run is Perform()'s, which records none.
   DeviceRun(const Settings& settings, const float* psf, const float* residual,
             size_t n_channels, const std::vector<double>& weights,
-            double beam_size);
+            double beam_size, bool record_trace = true);
   ~DeviceRun();
 
   /// Restore the residual to its initial state and zero the model (device

@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <map>
+#include <optional>
 #include <set>
 #include <stdexcept>
 
@@ -31,6 +32,16 @@ int ScaleLanes() {
 // RDL_FUSED_SCALES=0: the scales' convolutions through the forward spectrum
 // and one two-pass column inverse each instead of the fused multi-scale
 // launch (read per call, for comparisons)
+// RDL_SUBMINOR_DEFER=0: read each sub-minor loop's result before queuing the
+// correction (comparison)
+bool DeferLoopResult() {
+  static const bool on = [] {
+    const char* e = std::getenv("RDL_SUBMINOR_DEFER");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 bool FusedScalesOn() {
   const char* e = std::getenv("RDL_FUSED_SCALES");
   return !(e && e[0] == '0');
@@ -614,6 +625,7 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
           scale_infos_[scale_with_peak].max_unnormalized_image_value >= 0.0) &&
          threshold_countdown > 0 && !diverging) {  // :323-543
     ScaleInfo& info = scale_infos_[scale_with_peak];
+    bool searched = false;  // the next peak searches already ran (deferred result)
     // twice-convolved PSFs for this scale (:331-350), cached per major iteration
     auto tw = twice_cache.find(scale_with_peak);
     if (tw == twice_cache.end()) {
@@ -684,29 +696,41 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
       sub.SetRmsFactor(DeviceRmsFactor(session, width, height));  // :401-402
       std::vector<uint32_t> xy;
       if (RecordTrace()) sub.SetTrace(&xy);
+      // Without a trace or a component list, the loop's result (its
+      // component count, last peak, divergence) is read only after the work
+      // that does not depend on it is queued: the correction, the model
+      // update and the next peak searches (:436-462, :521-524) run behind the
+      // loop on the stream instead of after a host round trip.
+      const bool defer = !RecordTrace() && !track_components_ && DeferLoopResult();
       SubMinorLoop::RunResult r;
       {
         prof::Section prof_run("ms.subminor_run");
-        r = sub.Run(alias_residual ? data_image : individual, twice);
+        if (defer)
+          r = {false, sub.Launch(alias_residual ? data_image : individual, twice), 0.0f};
+        else
+          r = sub.Run(alias_residual ? data_image : individual, twice);
       }
       for (size_t c = 0; c + 1 < xy.size(); c += 2) {
         trace_.push_back(xy[c]);
         trace_.push_back(xy[c + 1]);
         trace_.push_back(uint32_t(scale_with_peak));
       }
-      diverging = r.diverging;
-      if (DivergenceLimit() != 0.0f && r.has_peak)
-        diverging = diverging ||
-                    std::fabs(r.peak) > initial_peak_value * DivergenceLimit();
       if (!r.has_peak) {
         log::Warn() << "Could not continue multi-scale clean, because the "
                        "sub-minor loop failed to find components.\n";
         break;
       }
-      SetIterationNumber(sub.CurrentIteration());
-      info.n_components_cleaned += IterationNumber() - sub_start;
-      info.total_flux_cleaned += sub.FluxCleaned();
-      prof::Section prof_correct("ms.correct_and_model");
+      auto account = [&](const SubMinorLoop::RunResult& rr) {
+        diverging = rr.diverging;
+        if (DivergenceLimit() != 0.0f)
+          diverging = diverging ||
+                      std::fabs(rr.peak) > initial_peak_value * DivergenceLimit();
+        SetIterationNumber(sub.CurrentIteration());
+        info.n_components_cleaned += IterationNumber() - sub_start;
+        info.total_flux_cleaned += sub.FluxCleaned();
+      };
+      if (!defer) account(r);
+      std::optional<prof::Section> prof_correct(std::in_place, "ms.correct_and_model");
       for (size_t i = 0; i != data_image.Size(); ++i) {
         const size_t psf_index = data_image.PsfIndex(i);
         auto key = std::make_pair(psf_index, scale_with_peak);
@@ -741,6 +765,13 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
       }
       if (track_components_)  // :447-448
         sub.UpdateComponentList(*component_list_, scale_with_peak);
+      prof_correct.reset();
+      if (defer) {
+        ActivateScales(scale_with_peak);
+        FindActiveScaleConvolvedMaxima(data_image, integrated.F(), false);
+        searched = true;
+        account(sub.Collect());
+      }
     } else {  // :463-519
       size_t n_kernel = 0;
       std::vector<float> shape_kernel;
@@ -803,8 +834,10 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
       }
     }
 
-    ActivateScales(scale_with_peak);
-    FindActiveScaleConvolvedMaxima(data_image, integrated.F(), false);
+    if (!searched) {
+      ActivateScales(scale_with_peak);
+      FindActiveScaleConvolvedMaxima(data_image, integrated.F(), false);
+    }
     if (log::Verbosity() >= 3) {
       char buf[256];
       std::string line = "[ms] it=" + std::to_string(IterationNumber());

@@ -17,7 +17,62 @@ SubMinorLoop::SubMinorLoop(gpu::Session& s, size_t width, size_t height,
   h_ = s.SharedSubminor();
 }
 
-SubMinorLoop::~SubMinorLoop() = default;
+SubMinorLoop::~SubMinorLoop() {
+  // a launched loop whose result was never read (an exception between
+  // Launch and Collect): read it, so the session's shared handle is free
+  if (launched_has_peak_) {
+    rdl_subminor_result r{};
+    (void)rdl_subminor_collect(h_, &r);
+  }
+}
+
+namespace {
+rdl_subminor_params MakeParams(const ImageSet& residual) {
+  rdl_subminor_params p{};
+  p.width = uint32_t(residual.Width());
+  p.height = uint32_t(residual.Height());
+  p.n_images = uint32_t(residual.Size());
+  p.n_pol = uint32_t(residual.NPolarizations());
+  p.integ = residual.Integration(false);  // GetLinearIntegrated
+  return p;
+}
+}  // namespace
+
+bool SubMinorLoop::Launch(ImageSet& residual, const gpu::Planes& psfs) {
+  rdl_subminor_params p = MakeParams(residual);
+  p.width = uint32_t(width_);
+  p.height = uint32_t(height_);
+  p.h_border = uint32_t(horizontal_border_);
+  p.v_border = uint32_t(vertical_border_);
+  p.allow_negative = allow_negative_;
+  p.stop_on_negative = stop_on_negative_;
+  p.threshold = threshold_;
+  p.gain = gain_;
+  p.divergence_limit = divergence_limit_;
+  p.iteration_start = current_iteration_;
+  p.max_iterations = max_iterations_;
+  p.d_mask = d_mask_;
+  p.d_spectral = d_spectral_;
+  p.logpoly = logpoly_;
+  p.d_rms = d_rms_;
+  n_images_ = residual.Size();
+  rdl_subminor_result r{};
+  gpu::Check(rdl_subminor_launch(h_, residual.Base(), psfs.Base(), &p, &r),
+             "rdl_subminor_launch");
+  n_selected_ = r.n_selected;
+  launched_has_peak_ = r.has_peak != 0;
+  return launched_has_peak_;
+}
+
+SubMinorLoop::RunResult SubMinorLoop::Collect() {
+  if (!launched_has_peak_) return {false, false, 0.0f};
+  launched_has_peak_ = false;
+  rdl_subminor_result r{};
+  gpu::Check(rdl_subminor_collect(h_, &r), "rdl_subminor_collect");
+  current_iteration_ = r.iteration;
+  flux_cleaned_ += r.flux_cleaned;
+  return {r.diverging != 0, true, r.peak};
+}
 
 SubMinorLoop::RunResult SubMinorLoop::Run(ImageSet& residual,
                                           const gpu::Planes& psfs) {

@@ -56,6 +56,13 @@ class SubMinorLoop {
   };
   RunResult Run(ImageSet& convolved_residual,
                 const gpu::Planes& twice_convolved_psfs);
+  /// Run() in two halves (rdl_subminor_launch / _collect): Launch selects and
+  /// starts the loop and returns whether it found a component (NSelected()
+  /// is final); the selection's model may be used (corrections, model
+  /// updates) before Collect, which waits for the loop and returns Run()'s
+  /// result. No trace.
+  bool Launch(ImageSet& convolved_residual, const gpu::Planes& twice_convolved_psfs);
+  RunResult Collect();
 
   /// subminor_loop.cc:195-218. `psf_key` identifies the PSF so its padded
   /// spectrum is computed once per loop object.
@@ -112,6 +119,7 @@ class SubMinorLoop {
   const float* d_rms_ = nullptr;
   float flux_cleaned_ = 0.0f;
   size_t n_selected_ = 0, n_images_ = 0;
+  bool launched_has_peak_ = false;  // Launch found a component (Collect pending)
   std::vector<uint32_t>* trace_ = nullptr;
   std::map<size_t, std::shared_ptr<gpu::Buffer>> psf_spectra_;
 };

@@ -895,13 +895,14 @@ void InitGpu(py::module& m) {
   py::class_<radler::DeviceRun>(g, "DeviceRun")
       .def(py::init([](const radler::Settings& settings, FloatArray psf,
                        FloatArray residual, std::vector<double> weights,
-                       double beam_size) {
+                       double beam_size, bool trace) {
              const size_t n = psf.ndim() == 2 ? 1 : psf.shape(0);
              return std::make_unique<radler::DeviceRun>(
-                 settings, psf.data(), residual.data(), n, weights, beam_size);
+                 settings, psf.data(), residual.data(), n, weights, beam_size, trace);
            }),
            py::arg("settings"), py::arg("psf"), py::arg("residual"),
-           py::arg("weights") = std::vector<double>(), py::arg("beam_size") = 0.0)
+           py::arg("weights") = std::vector<double>(), py::arg("beam_size") = 0.0,
+           py::arg("trace") = true)
       .def("restore", &radler::DeviceRun::Restore)
       .def("set_communicator", &radler::DeviceRun::SetCommunicator,
            py::arg("communicator"))
