@@ -972,16 +972,53 @@ __device__ __forceinline__ void TileSpan(int32_t lo, int32_t hi, uint32_t size,
   b[k++] = uint32_t(hi) / kStampTile;
 }
 
+// Per chunk of kStampThreads components (StampShapeModel's walk), the box
+// its stamps cover, unwrapped: {x lo, x hi, y lo, y hi}; x lo > x hi when no
+// component of the chunk is non-zero. One workgroup per chunk.
 __global__ __launch_bounds__(256) void MarkStampTiles(const uint32_t* __restrict__ pos,
                                                       const float* __restrict__ m,
                                                       uint64_t n_sel, uint32_t n,
                                                       uint32_t width, uint32_t height,
                                                       uint32_t tiles_x,
-                                                      uint8_t* __restrict__ mark) {
+                                                      uint8_t* __restrict__ mark,
+                                                      int4* __restrict__ bounds) {
   const int32_t h = int32_t(n / 2);
-  for (uint64_t c = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; c < n_sel;
-       c += uint64_t(gridDim.x) * blockDim.x) {
-    if (m[c] == 0.0f) continue;
+  __shared__ int32_t red[4][256 / 64];
+  int32_t bx0 = INT32_MAX, bx1 = INT32_MIN, by0 = INT32_MAX, by1 = INT32_MIN;
+  const uint64_t c = blockIdx.x * uint64_t(256) + threadIdx.x;
+  if (c < n_sel && m[c] != 0.0f) {
+    const int32_t xc = int32_t(pos[c] & 0xffffu), yc = int32_t(pos[c] >> 16);
+    bx0 = xc - h;
+    bx1 = xc + h;
+    by0 = yc - h;
+    by1 = yc + h;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    bx0 = min(bx0, __shfl_xor(bx0, off, 64));
+    bx1 = max(bx1, __shfl_xor(bx1, off, 64));
+    by0 = min(by0, __shfl_xor(by0, off, 64));
+    by1 = max(by1, __shfl_xor(by1, off, 64));
+  }
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[0][wave] = bx0;
+    red[1][wave] = bx1;
+    red[2][wave] = by0;
+    red[3][wave] = by1;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (uint32_t w = 1; w < 256 / 64; ++w) {
+      red[0][0] = min(red[0][0], red[0][w]);
+      red[1][0] = max(red[1][0], red[1][w]);
+      red[2][0] = min(red[2][0], red[2][w]);
+      red[3][0] = max(red[3][0], red[3][w]);
+    }
+    bounds[blockIdx.x] = make_int4(red[0][0], red[1][0], red[2][0], red[3][0]);
+  }
+  {
+    if (c >= n_sel || m[c] == 0.0f) return;
     const int32_t xc = int32_t(pos[c] & 0xffffu), yc = int32_t(pos[c] >> 16);
     uint32_t xa[2], xb[2], ya[2], yb[2];
     int nx, ny;
@@ -994,10 +1031,19 @@ __global__ __launch_bounds__(256) void MarkStampTiles(const uint32_t* __restrict
   }
 }
 
+// a chunk's stamps miss the tile [t0, t0 + l) on one axis (a box that wraps
+// around the plane never misses)
+__device__ __forceinline__ bool StampMisses(int32_t lo, int32_t hi, uint32_t t0, uint32_t l,
+                                            uint32_t size) {
+  if (lo < 0 || hi >= int32_t(size)) return false;
+  return hi < int32_t(t0) || lo >= int32_t(t0 + l);
+}
+
 __global__ __launch_bounds__(kStampThreads) void StampShapeModel(
     const uint32_t* __restrict__ pos, const float* __restrict__ m, uint64_t n_sel,
     const float* __restrict__ kern, uint32_t n, float* __restrict__ model,
-    uint32_t width, uint32_t height, uint32_t tiles_x, const uint8_t* __restrict__ mark) {
+    uint32_t width, uint32_t height, uint32_t tiles_x, const uint8_t* __restrict__ mark,
+    const int4* __restrict__ bounds) {
   if (!mark[blockIdx.x]) return;
   __shared__ uint32_t list[kStampThreads];
   __shared__ uint32_t wave_count[kStampThreads / 64];
@@ -1014,6 +1060,12 @@ __global__ __launch_bounds__(kStampThreads) void StampShapeModel(
   for (uint32_t r = 0; r < kStampRows; ++r) acc[r] = 0.0f;
   bool any = false;
   for (uint64_t base = 0; base < n_sel; base += kStampThreads) {
+    // chunks whose stamps cannot reach this tile (components come in raster
+    // order, so a chunk covers a few rows): skipped whole, uniformly
+    const int4 bb = bounds[base / kStampThreads];
+    if (bb.x > bb.y || StampMisses(bb.x, bb.y, tx0, lx, width) ||
+        StampMisses(bb.z, bb.w, ty0, ly, height))
+      continue;
     const uint64_t c = base + tid;
     bool hit = false;
     if (c < n_sel && m[c] != 0.0f) {
@@ -3291,15 +3343,20 @@ int rdl_subminor_add_shape_model(rdl_subminor* h, uint32_t image_index,
     // model read-modify-write of the whole plane
     rdl::ScopedTiming t(s, "stamp_model", 8.0 * double(width) * height);
     const size_t n_tiles = size_t(tiles_x) * tiles_y;
-    RDL_TRY(rdl::Grow(&h->stamp_mark, &h->stamp_mark_bytes, n_tiles, s->stream));
+    const size_t n_chunks = rdl::DivUp(h->n_selected, rdl::kStampThreads);
+    const size_t mark_bytes = (n_tiles + 15) / 16 * 16;
+    RDL_TRY(rdl::Grow(&h->stamp_mark, &h->stamp_mark_bytes,
+                      mark_bytes + n_chunks * sizeof(int4), s->stream));
     uint8_t* mark = static_cast<uint8_t*>(h->stamp_mark);
+    int4* bounds = reinterpret_cast<int4*>(mark + mark_bytes);
     RDL_HIP_CHECK(hipMemsetAsync(mark, 0, n_tiles, s->stream));
     const float* mi = h->d_m + size_t(image_index) * h->n_selected;
-    rdl::MarkStampTiles<<<unsigned(std::min<uint64_t>(1024, rdl::DivUp(h->n_selected, 256))),
-                          256, 0, s->stream>>>(h->d_pos, mi, h->n_selected, n, width, height,
-                                               tiles_x, mark);
+    static_assert(rdl::kStampThreads == 256, "one MarkStampTiles workgroup per chunk");
+    rdl::MarkStampTiles<<<unsigned(n_chunks), 256, 0, s->stream>>>(
+        h->d_pos, mi, h->n_selected, n, width, height, tiles_x, mark, bounds);
     rdl::StampShapeModel<<<tiles_x * tiles_y, rdl::kStampThreads, 0, s->stream>>>(
-        h->d_pos, mi, h->n_selected, d_kernel, n, d_model, width, height, tiles_x, mark);
+        h->d_pos, mi, h->n_selected, d_kernel, n, d_model, width, height, tiles_x, mark,
+        bounds);
   }
   RDL_HIP_CHECK(hipGetLastError());
   return RDL_OK;

@@ -690,12 +690,16 @@ def test_ms_transform_any_size(orc, w, h, shape):
         assert err <= 2e-6 * np.abs(img).max() * np.sqrt(np.log2(pw * ph)), (sc, err)
 
 
-@pytest.mark.parametrize("w,h,n", [(300, 200, 33), (256, 256, 129), (1000, 130, 65), (130, 97, 97)])
-def test_subminor_shape_model_stamp(sess, w, h, n):
+@pytest.mark.parametrize("w,h,n,k", [(300, 200, 33, 400), (256, 256, 129, 400),
+                                     (1000, 130, 65, 400), (130, 97, 97, 400),
+                                     (2048, 1024, 9, 4000), (1536, 1536, 31, 6000)])
+def test_subminor_shape_model_stamp(sess, w, h, n, k):
     """rdl_subminor_add_shape_model (the scale > 0 model update): every
     selected component's n x n stamp added circularly, each pixel summing the
     components in selection order — against the same sums in numpy float32
-    (partial edge tiles, stamps wrapping both edges, tiles no stamp reaches)."""
+    (partial edge tiles, stamps wrapping both edges, tiles no stamp reaches;
+    k selected pixels: many 256-component chunks, most of which a tile skips
+    by their stamps' bounding box)."""
     rng = np.random.default_rng(w + n)
     psf, dirty = synthetic(w, h, 40, 3)
     dirty = dirty.astype(np.float32)
@@ -706,7 +710,7 @@ def test_subminor_shape_model_stamp(sess, w, h, n):
     p.width, p.height, p.n_images, p.n_pol = w, h, 1, 1
     p.integ = integration(1, 1, mode=0)
     p.allow_negative, p.stop_on_negative = 1, 0
-    p.threshold = float(np.sort(np.abs(dirty).ravel())[-400])
+    p.threshold = float(np.sort(np.abs(dirty).ravel())[-k])
     p.gain, p.divergence_limit = 0.1, 0.0
     p.iteration_start, p.max_iterations = 0, 300
     out = SubminorResult()
