@@ -731,8 +731,12 @@ __global__ __launch_bounds__(TH) void RowsInverse(RowArgs a, const Cx<T>* __rest
   // now, issued after the spectrum loads, so they arrive during the
   // transform instead of after it (LdsSync waits for LDS only)
   const bool even_win = ((a.ox | a.img_w) & 1u) == 0;
-  float2 rpre[EH];
-  if (a.subtract && a.prefetch && even_win) {
+  // only the 512-thread float64 plans (the 8192^2 / 4096^2 corrections'):
+  // the registers cost the smaller plans a wave per SIMD (the gridded runs'
+  // subimage corrections: 7 -> 5 waves at 128 threads, measured slower)
+  constexpr bool kRpre = std::is_same_v<T, double> && TH >= 512;
+  float2 rpre[kRpre ? EH : 1];
+  if (kRpre && a.subtract && a.prefetch && even_win) {
 #pragma unroll
     for (uint32_t i = 0; i < EH; ++i) {
       const uint32_t n = tid + i * TH;
@@ -788,7 +792,7 @@ __global__ __launch_bounds__(TH) void RowsInverse(RowArgs a, const Cx<T>* __rest
       float2* p = reinterpret_cast<float2*>(o + (x0 - a.ox));
       float2 v = {float(z.x), float(-z.y)};
       if (a.subtract) {
-        const float2 r = a.prefetch ? rpre[i] : *p;
+        const float2 r = (kRpre && a.prefetch) ? rpre[kRpre ? i : 0] : *p;
         v = {r.x - v.x, r.y - v.y};
       }
       *p = v;
