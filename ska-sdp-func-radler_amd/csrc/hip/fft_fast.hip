@@ -1222,10 +1222,19 @@ __global__ __launch_bounds__(TH) void RowsForwardDma(RowArgs a, const float* __r
 // 16, so the first passes' radix-8/16 stores (lanes R elements apart) fall
 // on distinct banks (PMC: 49-57 % of these kernels' LDS cycles were bank
 // conflicts with the plain stride)
-__device__ __forceinline__ constexpr uint32_t Pd(uint32_t e) { return e + (e >> 4); }
-// column stride of a padded length-N transform (odd: adjacent columns on
+// Only the 4096- and 8192-point plans (the headline's and C2's columns,
+// where it was measured); the smaller plans of the gridded runs' subimages
+// keep the plain stride: the padded indexing raised ColStepBScales' registers
+// (1792-3584 plans: occupancy 4 -> 3 waves per SIMD).
+constexpr bool PadOn(uint32_t n) { return n >= 4096; }
+template <bool PAD>
+__device__ __forceinline__ constexpr uint32_t PdIf(uint32_t e) {
+  return PAD ? e + (e >> 4) : e;
+}
+// column stride of a (padded) length-n transform (odd: adjacent columns on
 // other banks)
-constexpr uint32_t PaddedStride(uint32_t n) { return n + (n >> 4) + 1; }
+template <bool PAD>
+constexpr uint32_t StrideIf(uint32_t n) { return PAD ? n + (n >> 4) + 1 : n + 1; }
 
 // `COUNT` transforms of length N at stride S in LDS (batched Pass); the
 // pass tables as for Pass, read once per workgroup into LDS (`wt`, shared by
@@ -1233,6 +1242,7 @@ constexpr uint32_t PaddedStride(uint32_t n) { return n + (n >> 4) + 1; }
 template <typename T, uint32_t TH, uint32_t N, uint32_t R, uint32_t NS, uint32_t OFF,
           uint32_t COUNT, uint32_t S>
 __device__ __forceinline__ void BPass(Cx<T>* buf, const Cx<T>* wt, uint32_t tid) {
+  constexpr bool PAD = S != N + 1;  // the padded layout (StrideIf<true>)
   constexpr uint32_t NB = N / R;
   constexpr uint32_t TOT = COUNT * NB;
   constexpr uint32_t BPT = (TOT + TH - 1) / TH;
@@ -1249,7 +1259,7 @@ __device__ __forceinline__ void BPass(Cx<T>* buf, const Cx<T>* wt, uint32_t tid)
         for (uint32_t q = 0; q + 1 < R; ++q) w[i][q] = wt[OFF + q * NS + k];
       }
 #pragma unroll
-      for (uint32_t r = 0; r < R; ++r) v[i][r] = buf[t * S + Pd(j + r * NB)];
+      for (uint32_t r = 0; r < R; ++r) v[i][r] = buf[t * S + PdIf<PAD>(j + r * NB)];
     }
   }
   LdsSync();
@@ -1266,7 +1276,7 @@ __device__ __forceinline__ void BPass(Cx<T>* buf, const Cx<T>* wt, uint32_t tid)
       Dft<T, int(R)>::Run(v[i]);
       const uint32_t d = (j / NS) * NS * R + k;
 #pragma unroll
-      for (uint32_t r = 0; r < R; ++r) buf[t * S + Pd(d + r * NS)] = v[i][r];
+      for (uint32_t r = 0; r < R; ++r) buf[t * S + PdIf<PAD>(d + r * NS)] = v[i][r];
     }
   }
   LdsSync();
@@ -1306,7 +1316,8 @@ __global__ __launch_bounds__(TH) void ColStepA(StepArgs a, const Cx<float>* __re
                                                const Cx<float>* __restrict__ tw,
                                                const Cx<float>* __restrict__ ptw) {
   constexpr uint32_t N = N1 * N2;
-  constexpr uint32_t S = PaddedStride(N1);  // columns of one row on distinct banks
+  constexpr bool PAD = PadOn(N1 * N2);
+  constexpr uint32_t S = StrideIf<PAD>(N1);  // columns of one row on distinct banks
   constexpr uint32_t COUNT = kTile * GA;
   constexpr uint32_t EL = COUNT * N1;
   constexpr uint32_t E = (EL + TH - 1) / TH;
@@ -1332,7 +1343,7 @@ __global__ __launch_bounds__(TH) void ColStepA(StepArgs a, const Cx<float>* __re
     const size_t off = base + size_t(n2_0 + g + N2 * n1) * kTile + col;
     Cx<float> v = in[off];
     if (a.inverse) v = Conj(Scale(Mul(v, kern[off]), a.scale));
-    buf[(g * kTile + col) * S + Pd(n1)] = v;
+    buf[(g * kTile + col) * S + PdIf<PAD>(n1)] = v;
   }
   LdsSync();
   BFft<float, TH, N1, COUNT, S, 0, 1, R1...>(buf, wt, tid);
@@ -1343,7 +1354,7 @@ __global__ __launch_bounds__(TH) void ColStepA(StepArgs a, const Cx<float>* __re
     const uint32_t col = idx % kTile, q = idx / kTile;
     const uint32_t g = q % GA, k1 = q / GA;
     const uint32_t n2 = n2_0 + g;
-    const Cx<float> v = Mul(buf[(g * kTile + col) * S + Pd(k1)], wa[g * N1 + k1]);
+    const Cx<float> v = Mul(buf[(g * kTile + col) * S + PdIf<PAD>(k1)], wa[g * N1 + k1]);
     out[base + size_t(k1 * N2 + n2) * kTile + col] = v;
   }
 }
@@ -1353,7 +1364,8 @@ template <uint32_t TH, uint32_t N1, uint32_t N2, uint32_t GB, uint32_t... R2>
 __global__ __launch_bounds__(TH) void ColStepB(StepArgs a, const Cx<float>* __restrict__ in,
                                                Cx<float>* __restrict__ out,
                                                const Cx<float>* __restrict__ ptw) {
-  constexpr uint32_t S = PaddedStride(N2);
+  constexpr bool PAD = PadOn(N1 * N2);
+  constexpr uint32_t S = StrideIf<PAD>(N2);
   constexpr uint32_t N = N1 * N2;
   constexpr uint32_t COUNT = kTile * GB;
   constexpr uint32_t EL = COUNT * N2;
@@ -1372,7 +1384,7 @@ __global__ __launch_bounds__(TH) void ColStepB(StepArgs a, const Cx<float>* __re
     if (EL % TH != 0 && idx >= EL) continue;
     const uint32_t col = idx % kTile, q = idx / kTile;
     const uint32_t n2 = q % N2, g = q / N2;  // rows k1 N2 .. k1 N2 + N2 - 1: contiguous
-    buf[(g * kTile + col) * S + Pd(n2)] = in[base + size_t((k1_0 + g) * N2 + n2) * kTile + col];
+    buf[(g * kTile + col) * S + PdIf<PAD>(n2)] = in[base + size_t((k1_0 + g) * N2 + n2) * kTile + col];
   }
   LdsSync();
   BFft<float, TH, N2, COUNT, S, 0, 1, R2...>(buf, wt, tid);
@@ -1382,7 +1394,7 @@ __global__ __launch_bounds__(TH) void ColStepB(StepArgs a, const Cx<float>* __re
     if (EL % TH != 0 && idx >= EL) continue;
     const uint32_t col = idx % kTile, q = idx / kTile;
     const uint32_t g = q % GB, k2 = q / GB;  // rows k1 + N1 k2: GB adjacent rows per k2
-    Cx<float> v = buf[(g * kTile + col) * S + Pd(k2)];
+    Cx<float> v = buf[(g * kTile + col) * S + PdIf<PAD>(k2)];
     if (a.inverse) v = Conj(v);
     out[base + size_t(k1_0 + g + N1 * k2) * kTile + col] = v;
   }
@@ -1419,7 +1431,8 @@ __global__ __launch_bounds__(TH) void ColStepBScales(ScalesArgs a,
                                                      const Cx<float>* __restrict__ in,
                                                      const Cx<float>* __restrict__ tw,
                                                      const Cx<float>* __restrict__ ptw) {
-  constexpr uint32_t S = PaddedStride(N2);
+  constexpr bool PAD = PadOn(N1 * N2);
+  constexpr uint32_t S = StrideIf<PAD>(N2);
   constexpr uint32_t N = N1 * N2;
   constexpr uint32_t COUNT = kTile * GB;
   constexpr uint32_t EL = COUNT * N2;
@@ -1443,7 +1456,7 @@ __global__ __launch_bounds__(TH) void ColStepBScales(ScalesArgs a,
     if (EL % TH != 0 && idx >= EL) continue;
     const uint32_t col = idx % kTile, q = idx / kTile;
     const uint32_t n2 = q % N2, g = q / N2;  // rows k1 N2 .. k1 N2 + N2 - 1: contiguous
-    buf[(g * kTile + col) * S + Pd(n2)] = in[base + size_t((k1_0 + g) * N2 + n2) * kTile + col];
+    buf[(g * kTile + col) * S + PdIf<PAD>(n2)] = in[base + size_t((k1_0 + g) * N2 + n2) * kTile + col];
   }
   LdsSync();
   BFft<float, TH, N2, COUNT, S, 0, 1, R2...>(buf, wt, tid);
@@ -1455,7 +1468,7 @@ __global__ __launch_bounds__(TH) void ColStepBScales(ScalesArgs a,
     if (EL % TH != 0 && idx >= EL) continue;
     const uint32_t col = idx % kTile, q = idx / kTile;
     const uint32_t g = q % GB, k2 = q / GB;
-    X[i] = buf[(g * kTile + col) * S + Pd(k2)];
+    X[i] = buf[(g * kTile + col) * S + PdIf<PAD>(k2)];
   }
   for (uint32_t sc = 0; sc < a.n_scales; ++sc) {
     // opaque per scale (see Columns): the per-element addresses are
@@ -1473,7 +1486,7 @@ __global__ __launch_bounds__(TH) void ColStepBScales(ScalesArgs a,
       const float k = kern[(size_t(tile) * N + k1_0 + g + N1 * k2) * kTile + col];
       // conj(X K s), K real: the complex product's terms with Im K = 0
       const Cx<float> v = {(X[i].x * k) * a.scale, -((X[i].y * k) * a.scale)};
-      buf[(g * kTile + col) * S + Pd(k2)] = v;
+      buf[(g * kTile + col) * S + PdIf<PAD>(k2)] = v;
     }
     LdsSync();
     BFft<float, TH, N2, COUNT, S, 0, 1, R2...>(buf, wt, tid);
@@ -1485,7 +1498,7 @@ __global__ __launch_bounds__(TH) void ColStepBScales(ScalesArgs a,
       const uint32_t col = idx % kTile, q = idx / kTile;
       const uint32_t m2 = q % N2, g = q / N2;  // rows k1 N2 + m2: contiguous
       out[base + size_t((k1_0 + g) * N2 + m2) * kTile + col] =
-          Mul(buf[(g * kTile + col) * S + Pd(m2)], wb[g * N2 + m2]);
+          Mul(buf[(g * kTile + col) * S + PdIf<PAD>(m2)], wb[g * N2 + m2]);
     }
   }
 }
@@ -1497,7 +1510,8 @@ __global__ __launch_bounds__(TH) void ColStepAInv(StepArgs a, const Cx<float>* _
                                                   Cx<float>* __restrict__ out,
                                                   const Cx<float>* __restrict__ ptw) {
   constexpr uint32_t N = N1 * N2;
-  constexpr uint32_t S = PaddedStride(N1);
+  constexpr bool PAD = PadOn(N1 * N2);
+  constexpr uint32_t S = StrideIf<PAD>(N1);
   constexpr uint32_t COUNT = kTile * GA;
   constexpr uint32_t EL = COUNT * N1;
   constexpr uint32_t E = (EL + TH - 1) / TH;
@@ -1515,7 +1529,7 @@ __global__ __launch_bounds__(TH) void ColStepAInv(StepArgs a, const Cx<float>* _
     if (EL % TH != 0 && idx >= EL) continue;
     const uint32_t col = idx % kTile, q = idx / kTile;
     const uint32_t g = q % GA, k1 = q / GA;  // rows k1 N2 + m2_0 ..: GA contiguous
-    buf[(g * kTile + col) * S + Pd(k1)] = in[base + size_t(k1 * N2 + m2_0 + g) * kTile + col];
+    buf[(g * kTile + col) * S + PdIf<PAD>(k1)] = in[base + size_t(k1 * N2 + m2_0 + g) * kTile + col];
   }
   LdsSync();
   BFft<float, TH, N1, COUNT, S, 0, 1, R1...>(buf, wt, tid);
@@ -1526,7 +1540,7 @@ __global__ __launch_bounds__(TH) void ColStepAInv(StepArgs a, const Cx<float>* _
     const uint32_t col = idx % kTile, q = idx / kTile;
     const uint32_t g = q % GA, m1 = q / GA;  // rows m2 + N2 m1: GA adjacent per m1
     out[base + size_t(m2_0 + g + N2 * m1) * kTile + col] =
-        Conj(buf[(g * kTile + col) * S + Pd(m1)]);
+        Conj(buf[(g * kTile + col) * S + PdIf<PAD>(m1)]);
   }
   (void)a;
 }

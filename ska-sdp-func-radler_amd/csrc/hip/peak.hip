@@ -8,6 +8,7 @@
 // reproduces the reference's "strict '>' from FLT_MIN, first index wins".
 // A single-workgroup second stage reduces the per-block keys.
 #include <cfloat>
+#include <cstdlib>
 
 #include "rdl_internal.h"
 
@@ -160,7 +161,12 @@ int LaunchFindPeak(rdl_session* s, const float* d_image, uint32_t width,
     // the last workgroup finishes the search (PeakArrive); an empty box
     // keeps the two launches
     PeakFinish f;
-    if (rows != 0) {
+    // RDL_PEAK_FINISH=0: the separate FindPeakFinal launch (comparison)
+    static const bool finish_on = [] {
+      const char* e = std::getenv("RDL_PEAK_FINISH");
+      return !(e && e[0] == '0');
+    }();
+    if (rows != 0 && finish_on) {
       f.ticket = PeakTicket(s, ticket);
       f.out = static_cast<PeakOut*>(d_out);
       f.partials = partials;
@@ -173,14 +179,15 @@ int LaunchFindPeak(rdl_session* s, const float* d_image, uint32_t width,
     }
     if (rows == 0) {
       RDL_HIP_CHECK(hipMemsetAsync(partials, 0, sizeof(uint64_t), s->stream));
-      FindPeakFinal<<<1, 1024, 0, s->stream>>>(
-          partials, blocks, d_image, width, height, avx_semantics,
-          d_mask != nullptr, static_cast<PeakOut*>(d_out));
     } else if (vec) {
       FindPeakPartial<true><<<blocks, 256, 0, s->stream>>>(a, partials, f);
     } else {
       FindPeakPartial<false><<<blocks, 256, 0, s->stream>>>(a, partials, f);
     }
+    if (!f.ticket)
+      FindPeakFinal<<<1, 1024, 0, s->stream>>>(
+          partials, blocks, d_image, width, height, avx_semantics,
+          d_mask != nullptr, static_cast<PeakOut*>(d_out));
   }
   RDL_HIP_CHECK(hipGetLastError());
   return RDL_OK;

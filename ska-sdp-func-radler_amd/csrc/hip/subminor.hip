@@ -1062,10 +1062,12 @@ __global__ __launch_bounds__(kStampThreads) void StampShapeModel(
   for (uint64_t base = 0; base < n_sel; base += kStampThreads) {
     // chunks whose stamps cannot reach this tile (components come in raster
     // order, so a chunk covers a few rows): skipped whole, uniformly
-    const int4 bb = bounds[base / kStampThreads];
-    if (bb.x > bb.y || StampMisses(bb.x, bb.y, tx0, lx, width) ||
-        StampMisses(bb.z, bb.w, ty0, ly, height))
-      continue;
+    if (bounds) {
+      const int4 bb = bounds[base / kStampThreads];
+      if (bb.x > bb.y || StampMisses(bb.x, bb.y, tx0, lx, width) ||
+          StampMisses(bb.z, bb.w, ty0, ly, height))
+        continue;
+    }
     const uint64_t c = base + tid;
     bool hit = false;
     if (c < n_sel && m[c] != 0.0f) {
@@ -3354,9 +3356,14 @@ int rdl_subminor_add_shape_model(rdl_subminor* h, uint32_t image_index,
     static_assert(rdl::kStampThreads == 256, "one MarkStampTiles workgroup per chunk");
     rdl::MarkStampTiles<<<unsigned(n_chunks), 256, 0, s->stream>>>(
         h->d_pos, mi, h->n_selected, n, width, height, tiles_x, mark, bounds);
+    // RDL_STAMP_BOUNDS=0: every tile walks every chunk (comparison)
+    static const bool bounds_on = [] {
+      const char* e = std::getenv("RDL_STAMP_BOUNDS");
+      return !(e && e[0] == '0');
+    }();
     rdl::StampShapeModel<<<tiles_x * tiles_y, rdl::kStampThreads, 0, s->stream>>>(
         h->d_pos, mi, h->n_selected, d_kernel, n, d_model, width, height, tiles_x, mark,
-        bounds);
+        bounds_on ? bounds : nullptr);
   }
   RDL_HIP_CHECK(hipGetLastError());
   return RDL_OK;
