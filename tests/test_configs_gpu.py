@@ -306,6 +306,13 @@ def test_c4_iuwt_4096_steps():
                   run.model().reshape(dirty.shape), tol)
 
 
+# C5's deepest divergence on MI355X: subimage 34, component 1 350, at an
+# oracle decision margin of 5.9e-6 x max|dirty| (0.013 x that subimage's
+# |peak| of 4.5e-4 there); the bound for a divergence past a subimage's first
+# near-tie, in units of max|dirty|
+TILED_DIV_ATOL = 2e-5
+
+
 def _tiled(name):
     """A tiled configuration (C5, p8k) against its fixture: the subimage
     geometry bit-exact, every subimage's trace tie-aware (identical at least
@@ -334,7 +341,7 @@ def _tiled(name):
     # the rule test_c2 / test_h8k apply to their prefixes.
     from trace_compare import compare
     identical = np.zeros(n_sub, bool)
-    n_near, matched = 0, 0
+    n_near, matched, worst = 0, 0, 0.0
     for i in range(n_sub):
         sel = trace[:, 0] == i
         m = np.append(margins[:len(trace)][sel], end_margins[i])
@@ -346,11 +353,20 @@ def _tiled(name):
         n_near += int(len(near) > 0)
         c = compare(run.trace(i), trace[sel][:, 1:], m, v)
         assert c.identical or c.first_divergence >= first_near, (i, first_near, c)
+        if not c.identical:
+            # past its first near-tie a subimage may separate where the float32
+            # corrections' accumulated rounding (which scales with max|dirty|,
+            # not with the shrinking peak) reaches the oracle's margin, but
+            # not at a larger one
+            m_abs = float(m[min(c.first_divergence, len(m) - 1)])
+            worst = max(worst, m_abs / float(fx["dirty_absmax"]))
+            assert m_abs <= TILED_DIV_ATOL * float(fx["dirty_absmax"]), (i, m_abs, c)
         identical[i] = c.identical
         matched += c.matched
     print(f"{name}: {int(identical.sum())}/{n_sub} subimage traces identical "
           f"({n_near} reach an oracle near-tie); {matched} of {len(trace)} components "
-          f"matched, every subimage at least to its first near-tie")
+          f"matched, every subimage at least to its first near-tie; largest oracle "
+          f"margin at a divergence {worst:.3g} x max|dirty| (bound {TILED_DIV_ATOL:g})")
     print(f"{name}: {r['iterations']} iterations reported, oracle "
           f"{int(fx['total_iterations'])}")
     # the images of the identical subimages (the boundary masks give every
