@@ -363,8 +363,10 @@ int rdl_session_create(int device, rdl_session** out) {
   RDL_HIP_CHECK(rdl::DevMalloc(&s->d_small, 1 << 16));
   RDL_HIP_CHECK(hipMemset(s->d_small, 0, 1 << 16));  // the peak tickets start at 0
   RDL_HIP_CHECK(rdl::HostMalloc(&s->h_small, 1 << 16));
-  RDL_HIP_CHECK(rdl::MappedMalloc(&s->m_small, &s->m_small_dev, 1 << 16));
-  std::memset(s->m_small, 0, 1 << 16);
+  if (rdl::ZeroCopyOn()) {  // RDL_ZERO_COPY=0: no mapped host memory at all
+    RDL_HIP_CHECK(rdl::MappedMalloc(&s->m_small, &s->m_small_dev, 1 << 16));
+    std::memset(s->m_small, 0, 1 << 16);
+  }
   {
     const std::lock_guard<std::mutex> lock(rdl::g_registry_mutex);
     rdl::g_sessions.push_back(s.get());
