@@ -44,6 +44,17 @@ const char* rdl_version(void);
 int rdl_device_count(int* count);
 int rdl_session_create(int device, rdl_session** out);
 int rdl_session_destroy(rdl_session* s);
+/* Releases everything this library holds, process-wide: drains and destroys
+ * every session's streams and events, its RCCL communicator, the rocFFT
+ * plans, and frees every device, pinned and mapped host block (block caches,
+ * scratch, plan work buffers, buffers of host objects still alive). Afterwards
+ * every destroy/free entry point is a no-op and rdl_session_create fails.
+ * Runs automatically at process exit (an atexit handler registered by the
+ * first rdl_session_create, so it precedes the HIP runtime's own exit
+ * handlers; RDL_EXIT_SHUTDOWN=0 disables it). The reference has no device
+ * state to release (its images are host memory freed by their destructors,
+ * cpp/radler.cc); this is the device-side counterpart of process teardown. */
+int rdl_shutdown(void);
 int rdl_session_sync(rdl_session* s);
 /* hipStream_t of the session, for callers that record events on it. */
 void* rdl_session_stream(rdl_session* s);
@@ -433,7 +444,10 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
  * launches the loop; out->n_selected and out->has_peak are final, the other
  * fields are filled by _collect, which waits for the loop. The handle's
  * selection (positions, model values) may be used by other calls on the
- * session's stream in between. A second _launch before _collect fails. */
+ * session's stream in between. A second _launch before _collect fails, and
+ * so does a _launch or _run of ANOTHER handle of the same session while this
+ * one is uncollected (the session keeps one loop-result slot in mapped host
+ * memory): collect first. */
 int rdl_subminor_launch(rdl_subminor* h, const float* d_residuals, const float* d_psfs,
                         const rdl_subminor_params* p, rdl_subminor_result* out);
 int rdl_subminor_collect(rdl_subminor* h, rdl_subminor_result* out);

@@ -21,6 +21,13 @@
     }                                                                       \
   } while (0)
 
+void rdl::CommRelease(rdl_session* s) {
+  if (s->comm) {
+    ncclCommDestroy(static_cast<ncclComm_t>(s->comm));
+    s->comm = nullptr;
+  }
+}
+
 extern "C" {
 
 int rdl_comm_id_size(void) { return int(sizeof(ncclUniqueId)); }
@@ -47,10 +54,8 @@ int rdl_comm_init(rdl_session* s, int n_ranks, int rank, const void* h_id) {
 
 int rdl_comm_destroy(rdl_session* s) {
   RDL_ARG_CHECK(s, "NULL argument");
-  if (s->comm) {
-    ncclCommDestroy(static_cast<ncclComm_t>(s->comm));
-    s->comm = nullptr;
-  }
+  if (rdl::ShutDown()) return RDL_OK;  // released by rdl_shutdown
+  rdl::CommRelease(s);
   return RDL_OK;
 }
 

@@ -11,10 +11,13 @@
 // transform, one multiply pass and one inverse transform.
 #include <rocfft/rocfft.h>
 
+#include <set>
+
 #include "rdl_internal.h"
 
 namespace {
 std::once_flag g_rocfft_once;
+std::atomic<bool> g_rocfft_used{false};
 }
 
 struct rdl_fft {
@@ -204,11 +207,33 @@ inline unsigned Grid(size_t n) {
 
 }  // namespace rdl
 
+// every live rdl_fft (rdl_shutdown destroys their rocFFT plans)
+static std::mutex g_fft_registry_mutex;
+static std::set<rdl_fft*> g_fft_registry;
+
+void rdl::ReleaseFftPlans() {
+  const std::lock_guard<std::mutex> lock(g_fft_registry_mutex);
+  for (rdl_fft* f : g_fft_registry) {
+    if (f->fwd) rocfft_plan_destroy(f->fwd);
+    if (f->inv) rocfft_plan_destroy(f->inv);
+    if (f->info_fwd) rocfft_execution_info_destroy(f->info_fwd);
+    if (f->info_inv) rocfft_execution_info_destroy(f->info_inv);
+    f->fwd = f->inv = nullptr;
+    f->info_fwd = f->info_inv = nullptr;
+    f->work = nullptr;  // a tracked block: rdl_shutdown frees it
+  }
+  g_fft_registry.clear();
+  if (g_rocfft_used.load()) rocfft_cleanup();
+}
+
 static int CreateFft(rdl_session* s, uint32_t width, uint32_t height, bool f64,
                      rdl_fft** out) {
   RDL_ARG_CHECK(s && out, "NULL argument");
   RDL_ARG_CHECK(width >= 2 && height >= 1, "bad FFT size");
-  std::call_once(g_rocfft_once, [] { rocfft_setup(); });
+  std::call_once(g_rocfft_once, [] {
+    rocfft_setup();
+    g_rocfft_used.store(true);
+  });
   // plans are created from the subimage workers' threads; keep rocFFT's
   // plan cache single-threaded
   static std::mutex plan_mutex;
@@ -243,6 +268,10 @@ static int CreateFft(rdl_session* s, uint32_t width, uint32_t height, bool f64,
     RDL_FFT_CHECK(
         rocfft_execution_info_set_work_buffer(f->info_inv, f->work, f->work_bytes));
   }
+  {
+    const std::lock_guard<std::mutex> rlock(g_fft_registry_mutex);
+    g_fft_registry.insert(f.get());
+  }
   *out = f.release();
   return RDL_OK;
 }
@@ -275,6 +304,11 @@ int rdl_fft_create_f64(rdl_session* s, uint32_t width, uint32_t height,
 
 int rdl_fft_destroy(rdl_fft* f) {
   if (!f) return RDL_OK;
+  if (rdl::ShutDown()) return RDL_OK;  // rdl_shutdown released the plans
+  {
+    const std::lock_guard<std::mutex> lock(g_fft_registry_mutex);
+    g_fft_registry.erase(f);
+  }
   (void)hipStreamSynchronize(f->s->stream);
   if (f->fwd) rocfft_plan_destroy(f->fwd);
   if (f->inv) rocfft_plan_destroy(f->inv);

@@ -947,6 +947,7 @@ int rdl_conv_create_ex(rdl_session* s, uint32_t width, uint32_t height, int f64,
 
 int rdl_conv_destroy(rdl_conv* c) {
   if (!c) return RDL_OK;
+  if (rdl::ShutDown()) return RDL_OK;  // its blocks were released by rdl_shutdown
   (void)hipStreamSynchronize(c->s->stream);
   if (c->tw_row) (void)rdl::DevFree(c->tw_row);
   if (c->tw_col) (void)rdl::DevFree(c->tw_col);

@@ -146,6 +146,10 @@ struct rdl_session {
   rdl::Scratch loop_state;       // Högbom loop state / partials / trace
   rdl::Scratch iuwt;             // IUWT i0 / recompose accumulator plane
   void* comm = nullptr;          // ncclComm_t when initialised
+  // the rdl_subminor handle whose launched loop has not been collected: its
+  // result lives in the session's one mapped loop slot (kMappedLoop), so no
+  // other handle of this session may launch until it is collected
+  const void* loop_owner = nullptr;
   // rdl_malloc / rdl_free block cache: a freed block is kept for reuse by a
   // later allocation of this session (stream-ordered on `stream`), so the
   // per-Perform buffers cost no hipFree (which idles the device) and no
@@ -168,6 +172,14 @@ struct rdl_session {
 namespace rdl {
 // hands every cached block of every session on `device` back (out of memory)
 int FlushDeviceCaches(int device);
+// rdl_shutdown has run: every block, stream and plan of this library is
+// released, and the destroy/free entry points are no-ops from then on
+extern std::atomic<bool> g_shutdown;
+inline bool ShutDown() { return g_shutdown.load(std::memory_order_acquire); }
+// rocFFT plans of the live rdl_fft objects (fftconv.hip), for rdl_shutdown
+void ReleaseFftPlans();
+// destroys a session's RCCL communicator (comm.hip)
+void CommRelease(rdl_session* s);
 // rdl_timing_enable_all: time every session of the process
 extern std::atomic<bool> g_timing_all;
 inline bool TimingOn(const rdl_session* s) {

@@ -193,6 +193,21 @@ void InstallSegvReport() {
 }
 std::once_flag g_segv_once;
 
+// rdl_shutdown at process exit (RDL_EXIT_SHUTDOWN=0: leave everything to the
+// runtime's own teardown, as before r06). Registered by the first
+// rdl_session_create, after HIP has initialised, so it runs BEFORE the HIP
+// runtime's exit handlers (atexit order is the reverse of registration): the
+// process-lifetime sessions (one per GPU, the subimage pool's workers), their
+// block caches, plans, mapped host buffers and streams are released while the
+// runtime is still whole.
+std::once_flag g_exit_once;
+void ExitShutdown() { (void)rdl_shutdown(); }
+void RegisterExitShutdown() {
+  const char* e = std::getenv("RDL_EXIT_SHUTDOWN");
+  if (e && e[0] == '0') return;
+  std::atexit(ExitShutdown);
+}
+
 void Fold(std::map<std::string, TimingEntry>& into,
           const std::map<std::string, TimingEntry>& from) {
   for (const auto& [name, t] : from) {
@@ -204,6 +219,7 @@ void Fold(std::map<std::string, TimingEntry>& into,
 }
 }  // namespace
 std::atomic<bool> g_timing_all{false};
+std::atomic<bool> g_shutdown{false};
 char g_timing_family[64] = {0};
 void SetError(const std::string& msg) { g_last_error = msg; }
 
@@ -331,9 +347,11 @@ int rdl_device_count(int* count) {
 
 int rdl_session_create(int device, rdl_session** out) {
   RDL_ARG_CHECK(out, "out is NULL");
+  RDL_ARG_CHECK(!rdl::ShutDown(), "rdl_shutdown has run");
   std::call_once(rdl::g_segv_once, rdl::InstallSegvReport);
   int n = 0;
   RDL_HIP_CHECK(hipGetDeviceCount(&n));
+  std::call_once(rdl::g_exit_once, rdl::RegisterExitShutdown);
   RDL_ARG_CHECK(device >= 0 && device < n, "invalid device index");
   // leave the caller's current device as it was (a pool creates sessions
   // for other GPUs from the main thread)
@@ -391,6 +409,7 @@ int rdl_session::FlushCache() {
 
 int rdl_session_destroy(rdl_session* s) {
   if (!s) return RDL_OK;
+  if (rdl::ShutDown()) return RDL_OK;  // released by rdl_shutdown
   (void)hipSetDevice(s->device);
   if (s->aux) (void)hipStreamSynchronize(s->aux);
   s->stream = s->home;
@@ -424,6 +443,72 @@ int rdl_session_destroy(rdl_session* s) {
   if (s->ev_join) (void)hipEventDestroy(s->ev_join);
   (void)hipStreamDestroy(s->home);
   delete s;
+  return RDL_OK;
+}
+
+int rdl_shutdown(void) {
+  bool expected = false;
+  if (!rdl::g_shutdown.compare_exchange_strong(expected, true)) return RDL_OK;
+  std::vector<rdl_session*> sessions;
+  {
+    const std::lock_guard<std::mutex> lock(rdl::g_registry_mutex);
+    sessions.swap(rdl::g_sessions);
+  }
+  // drain every stream before anything is released
+  for (rdl_session* s : sessions) {
+    (void)hipSetDevice(s->device);
+    if (s->aux) (void)hipStreamSynchronize(s->aux);
+    (void)hipStreamSynchronize(s->home);
+  }
+  for (rdl_session* s : sessions) {
+    (void)hipSetDevice(s->device);
+    rdl::CommRelease(s);
+    {
+      const std::lock_guard<std::recursive_mutex> tlock(s->timing_mutex);
+      for (auto& [name, t] : s->timings) {
+        for (auto& [a, b] : t.pending) {
+          (void)hipEventDestroy(a);
+          (void)hipEventDestroy(b);
+        }
+        t.pending.clear();
+      }
+      for (hipEvent_t e : s->event_pool) (void)hipEventDestroy(e);
+      s->event_pool.clear();
+    }
+    if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);
+    if (s->ev_join) (void)hipEventDestroy(s->ev_join);
+    if (s->aux) (void)hipStreamDestroy(s->aux);
+    (void)hipStreamDestroy(s->home);
+    s->ev_fork = s->ev_join = nullptr;
+    s->aux = s->home = s->stream = nullptr;
+    const std::lock_guard<std::mutex> clock(s->cache_mutex);
+    s->cache_free.clear();
+    s->cache_live.clear();
+    s->cache_bytes = 0;
+    // the session structs stay allocated (the host wrappers may still hold
+    // them; every destroy/free entry point is a no-op from here on)
+  }
+  rdl::ReleaseFftPlans();
+  // every device block, pinned and mapped host block this library holds:
+  // the sessions' caches and scratch, plans' work buffers, sub-minor handles,
+  // and the buffers of host objects that outlive the process's last call
+  size_t n = 0;
+  for (rdl::BlockSlot& b : rdl::g_blocks) {
+    const uintptr_t p = b.base.load(std::memory_order_relaxed);
+    if (!p) continue;
+    const char kind = b.kind.load(std::memory_order_relaxed);
+    b.base.store(0, std::memory_order_relaxed);
+    b.bytes.store(0, std::memory_order_relaxed);
+    b.kind.store(0, std::memory_order_relaxed);
+    if (kind == 'h')
+      (void)hipHostFree(reinterpret_cast<void*>(p));
+    else
+      (void)hipFree(reinterpret_cast<void*>(p));
+    ++n;
+  }
+  if (const char* e = std::getenv("RDL_SHUTDOWN_LOG"); e && e[0] == '1')
+    std::fprintf(stderr, "[rdl] shutdown: %zu sessions, %zu blocks released\n",
+                 sessions.size(), n);
   return RDL_OK;
 }
 
@@ -527,7 +612,7 @@ int rdl_malloc(rdl_session* s, size_t bytes, void** d_out) {
 // everything beyond the cache cap, is freed after the stream drains.
 int rdl_free(rdl_session* s, void* d_ptr) {
   RDL_ARG_CHECK(s, "NULL session");
-  if (!d_ptr) return RDL_OK;
+  if (!d_ptr || rdl::ShutDown()) return RDL_OK;
   if (s->cache_on) {
     const std::lock_guard<std::mutex> lock(s->cache_mutex);
     auto it = s->cache_live.find(d_ptr);
@@ -574,6 +659,7 @@ int rdl_host_alloc(size_t bytes, void** h_out) {
 }
 
 int rdl_host_free(void* h_ptr) {
+  if (rdl::ShutDown()) return RDL_OK;
   if (h_ptr) RDL_HIP_CHECK(rdl::HostFree(h_ptr));
   return RDL_OK;
 }

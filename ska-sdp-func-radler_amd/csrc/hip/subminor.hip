@@ -2672,6 +2672,8 @@ int rdl_subminor_create(rdl_session* s, rdl_subminor** out) {
 
 int rdl_subminor_destroy(rdl_subminor* h) {
   if (!h) return RDL_OK;
+  if (rdl::ShutDown()) return RDL_OK;  // rdl_shutdown released everything
+  if (h->s->loop_owner == h) h->s->loop_owner = nullptr;
   (void)hipStreamSynchronize(h->s->stream);
   if (h->counts) (void)rdl::DevFree(h->counts);
   if (h->sel) (void)rdl::DevFree(h->sel);
@@ -2697,6 +2699,7 @@ int rdl_subminor_run(rdl_subminor* h, const float* d_residuals,
                      rdl_subminor_result* out, uint32_t* h_trace,
                      uint64_t trace_cap) {
   RDL_ARG_CHECK(h && d_residuals && d_psfs && p && out, "NULL argument");
+  RDL_ARG_CHECK(!h->pending, "rdl_subminor_run: the previous loop was not collected");
   uint32_t* trace_dev = nullptr;
   const uint64_t cap = h_trace ? trace_cap : 0;
   RDL_TRY(SubminorLaunch(h, d_residuals, d_psfs, p, out, cap, &trace_dev));
@@ -2736,6 +2739,11 @@ int SubminorLaunch(rdl_subminor* h, const float* d_residuals, const float* d_psf
                     p->height <= 65535,
                 "image size out of range (1..65535)");
   rdl_session* s = h->s;
+  // one mapped result slot per session (kMappedLoop): a second handle's
+  // launch would overwrite a result that is still to be collected
+  RDL_ARG_CHECK(!s->loop_owner || s->loop_owner == h,
+                "another rdl_subminor handle of this session has a launched loop that was "
+                "not collected (rdl_subminor_collect it first)");
   hipStream_t st = s->stream;
   h->width = p->width;
   h->height = p->height;
@@ -3195,6 +3203,7 @@ int SubminorLaunch(rdl_subminor* h, const float* d_residuals, const float* d_psf
   if (s->trace_subminor) RDL_HIP_CHECK(hipEventRecord(ev1, st));
   out->has_peak = 1;  // a selection: the loop's first component exists
   h->pending = true;
+  s->loop_owner = h;
   h->pending_start = p->iteration_start;
   h->pending_bytes_per_it = 12.0 * double(ni) * double(n_sel);
   h->pending_result = la.result;
@@ -3216,6 +3225,7 @@ int SubminorCollect(rdl_subminor* h, rdl_subminor_result* out, uint32_t* h_trace
   rdl_session* s = h->s;
   hipStream_t st = s->stream;
   h->pending = false;
+  if (s->loop_owner == h) s->loop_owner = nullptr;
   rdl::LoopResult res{};
   uint32_t err = 0;
   {

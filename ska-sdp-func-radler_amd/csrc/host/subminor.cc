@@ -122,9 +122,9 @@ SubMinorLoop::RunResult SubMinorLoop::Run(ImageSet& residual,
 
 std::shared_ptr<gpu::Buffer> SubMinorLoop::MakePaddedPsfSpectrum(
     gpu::Session& s, const float* d_psf, size_t width, size_t height,
-    size_t pw, size_t ph) {
-  // float64 transforms: see rdl_fft_create_f64 / DESIGN.md
-  gpu::Fft& fft = s.GetFft(pw, ph, true);
+    size_t pw, size_t ph, bool f64) {
+  // float64 transforms by default: see rdl_fft_create_f64 / DESIGN.md
+  gpu::Fft& fft = s.GetFft(pw, ph, f64);
   auto spectrum = std::make_shared<gpu::Buffer>(s, fft.SpectrumBytes());
   if (fft.UsesLds()) {
     // Image::Untrim + PrepareConvolutionKernel (subminor_loop.cc:199-202)
@@ -143,10 +143,28 @@ std::shared_ptr<gpu::Buffer> SubMinorLoop::MakePaddedPsfSpectrum(
                                           uint32_t(ph), d_psf, uint32_t(width),
                                           uint32_t(height)),
                "rdl_prepare_psf_kernel_f64");
-    fft.Forward64(kernel.D(), spectrum->Ptr());
+    if (f64) {
+      fft.Forward64(kernel.D(), spectrum->Ptr());
+    } else {
+      gpu::Check(rdl_prepare_psf_kernel(s.Handle(), kernel.F(), uint32_t(pw), uint32_t(ph),
+                                        d_psf, uint32_t(width), uint32_t(height)),
+                 "rdl_prepare_psf_kernel");
+      fft.Forward(kernel.F(), spectrum->Ptr());
+    }
   }
   s.Sync();
   return spectrum;
+}
+
+bool SubMinorLoop::CorrectionF64() {
+  // RDL_CORR_F32=1: CorrectResidualDirty's padded convolution in float32, the
+  // reference's precision (FFTW float, subminor_loop.cc:210) -- a comparison
+  // switch (DESIGN.md §4 "Residual correction precision")
+  static const bool f64 = [] {
+    const char* e = std::getenv("RDL_CORR_F32");
+    return !(e && e[0] == '1');
+  }();
+  return f64;
 }
 
 bool SubMinorLoop::CorrectionKernelF32() {
@@ -156,8 +174,8 @@ bool SubMinorLoop::CorrectionKernelF32() {
 
 std::shared_ptr<gpu::Buffer> SubMinorLoop::MakeCorrectionPsfSpectrum(
     gpu::Session& s, const float* d_psf, size_t width, size_t height, size_t pw, size_t ph) {
-  auto spectrum = MakePaddedPsfSpectrum(s, d_psf, width, height, pw, ph);
-  gpu::Fft& fft = s.GetFft(pw, ph, true);
+  auto spectrum = MakePaddedPsfSpectrum(s, d_psf, width, height, pw, ph, CorrectionF64());
+  gpu::Fft& fft = s.GetFft(pw, ph, CorrectionF64());
   if (!CorrectionKernelF32() || !fft.ConvColumnsD()) return spectrum;
   const size_t n = fft.SpectrumBytes() / 16;
   auto narrow = std::make_shared<gpu::Buffer>(s, n * 8);
@@ -182,7 +200,7 @@ void SubMinorLoop::CorrectResidualDirty(size_t image_index, float* d_residual,
 void SubMinorLoop::CorrectResidualDirtyWithSpectrum(size_t image_index,
                                                     float* d_residual,
                                                     const void* d_spectrum) {
-  gpu::Fft& fft = s_.GetFft(padded_width_, padded_height_, true);
+  gpu::Fft& fft = s_.GetFft(padded_width_, padded_height_, CorrectionF64());
   const uint32_t ox = uint32_t((padded_width_ - width_) / 2);
   const uint32_t oy = uint32_t((padded_height_ - height_) / 2);
   if (fft.UsesLds()) {
@@ -207,6 +225,19 @@ void SubMinorLoop::CorrectResidualDirtyWithSpectrum(size_t image_index,
     fft.ConvolveSubtract(model.F(), width_, height_, ox, oy, d_spectrum, work.Ptr(),
                          d_residual, static_cast<const uint8_t*>(rows.Ptr()),
                          !fft.SplitColumns(), CorrectionKernelF32() && fft.ConvColumnsD());
+    return;
+  }
+  if (!fft.IsF64()) {  // rocFFT float (RDL_CORR_F32=1 at a size the LDS engine lacks)
+    gpu::Buffer& padded = s_.Scratch(gpu::Session::kCorrectionSpectrum,
+                                     padded_width_ * padded_height_ * sizeof(float));
+    gpu::Check(rdl_subminor_model(h_, uint32_t(image_index), padded.F(),
+                                  uint32_t(padded_width_), uint32_t(padded_height_), ox, oy, 0),
+               "rdl_subminor_model");
+    fft.Convolve(padded.F(), d_spectrum);
+    gpu::Check(rdl_trim_subtract(s_.Handle(), d_residual, uint32_t(width_), uint32_t(height_),
+                                 padded.F(), uint32_t(padded_width_),
+                                 uint32_t(padded_height_)),
+               "rdl_trim_subtract");
     return;
   }
   gpu::Buffer& padded_ = s_.Scratch(gpu::Session::kCorrectionSpectrum,

@@ -74,7 +74,9 @@ class SubMinorLoop {
                                         const void* d_psf_spectrum);
   static std::shared_ptr<gpu::Buffer> MakePaddedPsfSpectrum(
       gpu::Session& s, const float* d_psf, size_t width, size_t height,
-      size_t padded_width, size_t padded_height);
+      size_t padded_width, size_t padded_height, bool f64 = true);
+  /// CorrectResidualDirty's transforms are float64 unless RDL_CORR_F32=1.
+  static bool CorrectionF64();
   /// The padded PSF spectrum as CorrectResidualDirty(WithSpectrum) reads it:
   /// MakePaddedPsfSpectrum's float64 spectrum, or its float narrowing when
   /// CorrectionKernelF32() (RDL_CORR_KERNEL=f32) and the LDS engine runs the

@@ -587,6 +587,18 @@ void InitGpu(py::module& m) {
         py::arg("original_size"), py::arg("padding"));
   py::module g = m.def_submodule("gpu", "MI355X device helpers (bench/tests)");
   g.def("set_verbosity", &radler::log::SetVerbosity);
+  // rdl_shutdown (rdl_hip.h): every device block, plan, stream and mapped
+  // host buffer of the process released. Registered with Python's atexit,
+  // which runs at interpreter finalization, before any C-level exit handler
+  // (the HIP runtime's, a profiler's finalization); the C-level handler
+  // librdl_hip registers itself stays as the fallback for C++ callers.
+  // RDL_EXIT_SHUTDOWN=0 leaves teardown to the runtime.
+  g.def("shutdown", []() { radler::gpu::Check(rdl_shutdown(), "rdl_shutdown"); });
+  {
+    const char* e = std::getenv("RDL_EXIT_SHUTDOWN");
+    if (!(e && e[0] == '0'))
+      py::module_::import("atexit").attr("register")(g.attr("shutdown"));
+  }
   // RADLER_HOST_PROFILE=1 sections: {name: (count, total seconds)}
   g.def("host_profile", []() {
     py::dict out;

@@ -93,6 +93,12 @@ CONFIGS = {
     # (multiscale_algorithm.cc:323-543, countdown :249, :363-373)
     "c2t": dict(kind="multiscale", size=4096, points=1000, blobs=100, threshold=5 * NOISE,
                 max_scales=6, cap=10 ** 9),
+    # the bench's headline workload (h8k) run to the 5-sigma threshold, the
+    # exact problem bench.py times: the end state of the timed run (component
+    # count, stop, final peak, residual / model statistics and samples)
+    # against the oracle's (multiscale_algorithm.cc:249, 323-543)
+    "h8kt": dict(kind="multiscale", size=8192, points=2000, blobs=200, threshold=5 * NOISE,
+                 max_scales=6, cap=10 ** 9),
     # the bench's tiled_n1 workload (the h8k image split 8 x 8) on the
     # concurrent pool (settings.parallel.max_threads 16): every subimage trims
     # from the residual as it was when the pass started, the schedule the

@@ -22,6 +22,7 @@ import config_problems as cp  # noqa: E402
 from oracle_lib import OracleAlgorithm, OracleParallel, get_oracle  # noqa: E402
 
 SAMPLE = 65536
+THREADS = int(os.environ.get("ORACLE_THREADS", os.cpu_count() or 8))
 
 
 def sample_index(n_pixels, seed=1):
@@ -61,7 +62,7 @@ def make(name):
            "dirty_absmax": np.float32(np.abs(dirty).max())}
     print(f"{name}: inputs {dirty.shape} in {time.time() - t0:.1f} s", flush=True)
     orc = get_oracle()
-    orc.set_threads(os.cpu_count() or 8)
+    orc.set_threads(THREADS)
     res, mod = dirty.copy(), np.zeros_like(dirty)
     t0 = time.time()
     if c["kind"] == "tiled":
@@ -129,7 +130,7 @@ def checkpoint(name, key="image_cap", prefix="ck_"):
     psfs, dirty = cp.problem(name)
     assert cp.sha256(dirty) == str(out["dirty_sha256"])
     orc = get_oracle()
-    orc.set_threads(os.cpu_count() or 8)
+    orc.set_threads(THREADS)
     res, mod = dirty.copy(), np.zeros_like(dirty)
     st = settings(c)
     cap = c[key]

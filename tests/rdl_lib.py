@@ -3,6 +3,7 @@
 GPU parity tests call through this boundary; the CPU suite only checks that
 the library loads and exports every declared symbol.
 """
+import atexit
 import ctypes as C
 import os
 import re
@@ -133,6 +134,10 @@ class Rdl:
         self.lib.rdl_fft_spectrum_bytes.argtypes = [C.c_void_p]
         self.lib.rdl_conv_spectrum_bytes.restype = C.c_size_t
         self.lib.rdl_conv_spectrum_bytes.argtypes = [C.c_void_p]
+        # release the library's device state at interpreter exit, before the
+        # runtime's C-level exit handlers (as the radler module does)
+        if os.environ.get("RDL_EXIT_SHUTDOWN") != "0":
+            atexit.register(self.lib.rdl_shutdown)
 
     def __getattr__(self, name):
         fn = getattr(self.lib, name)
