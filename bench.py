@@ -22,8 +22,11 @@ Workloads (--workload):
           SURVEY.md C5) shared by the ranks: find-peak pass, one RCCL
           allreduce(max) of the start peak, owner broadcasts of the subimage
           results (strong scaling; N > 1 default, 8192^2 8 x 8)
-  joined  the C3 image set (8 channels x 4096^2); at N > 1 split into
-          subimages shared by the ranks like `tiled`
+  joined  the C3 image set (8 channels x 4096^2); at N > 1 one image set
+          whose per-channel work (residual corrections, model updates) the
+          ranks share by channel, the integrated-image work on every rank
+          (--joined-split channels, the default), or the set split into
+          subimages shared by the ranks like `tiled` (--joined-split subimages)
 
 At N = 1 the line also carries: tiled_n1 / joined_n1 (the split workloads
 and the unsplit C3 run on this GPU), c2_to_threshold, and cpu_baseline with a
@@ -357,6 +360,104 @@ def with_amdahl(rd, once):
                          "merges all of them), so f is a lower bound"}
 
 
+def iuwt_leg(rd, reps=10):
+    """SURVEY.md C4 (IUWT, 4096^2) on this GPU: (1) the component the config
+    names, IuwtDecomposition(6 scales).Decompose + Recompose on one 4096^2
+    plane (rdl_iuwt_decompose / _recompose, include_largest), HIP-event device
+    time per call against the algorithmic bytes of SURVEY.md 8(d) (12 B/px
+    per decomposition scale, 8 B/px per recomposition scale); (2) the IUWT
+    deconvolution algorithm on the C4 problem (tests/config_problems.py: 1000
+    points + 100 blobs, 5 sigma, the fixture's 24 steps) to its stop, with
+    every kernel family's device time."""
+    import config_problems as cp
+    from rdl_lib import Session
+    size, n_scales = 4096, 6
+    sess = Session(0)
+    lib = sess.rdl.lib
+    lib.rdl_timing_get.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.c_double),
+                                   C.POINTER(C.c_uint64), C.POINTER(C.c_double)]
+    img = np.random.default_rng(1).standard_normal((size, size)).astype(np.float32)
+    d_in, d_scratch = sess.array(img), sess.array(shape=(size, size))
+    d_coeffs = sess.array(shape=(n_scales + 1, size, size))
+    d_out = sess.array(shape=(size, size))
+    px = size * size
+    calls = {"decompose": (lambda: sess.rdl.rdl_iuwt_decompose(
+                 sess.h, d_in.vp, d_scratch.vp, size, size, n_scales, d_coeffs.vp, 1),
+                 12.0 * px * n_scales),
+             "recompose": (lambda: sess.rdl.rdl_iuwt_recompose(
+                 sess.h, d_coeffs.vp, size, size, n_scales, 1, d_out.vp),
+                 8.0 * px * n_scales)}
+    comp = {}
+    for name, (fn, alg_bytes) in calls.items():
+        fn()
+        sess.sync()
+        lib.rdl_timing_reset(sess.h)
+        lib.rdl_timing_enable(sess.h, 1)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        sess.sync()
+        wall = (time.perf_counter() - t0) / reps
+        lib.rdl_timing_enable(sess.h, 0)
+        ms, n, b = C.c_double(), C.c_uint64(), C.c_double()
+        lib.rdl_timing_get(sess.h, b"iuwt", C.byref(ms), C.byref(n), C.byref(b))
+        dev_s = ms.value / reps * 1e-3
+        comp[name] = {"device_ms": round(dev_s * 1e3, 4), "wall_ms": round(wall * 1e3, 4),
+                      "launches_per_call": n.value // reps,
+                      "algorithmic_bytes": alg_bytes,
+                      "achieved": round(alg_bytes / dev_s / 1e9, 1), "unit": "GB/s",
+                      "frac": round(alg_bytes / dev_s / 1e9 / HBM_PEAK_GBS, 4)}
+    for x in (d_in, d_scratch, d_coeffs, d_out):
+        x.free()
+    sess.close()
+    # the algorithm on C4
+    psfs, dirty = cp.problem("c4")
+    c = cp.CONFIGS["c4"]
+    st = rd.Settings()
+    st.algorithm_type = rd.AlgorithmType.iuwt
+    st.trimmed_image_width = st.trimmed_image_height = size
+    st.pixel_scale.x = st.pixel_scale.y = cp.PIXEL_SCALE
+    st.absolute_threshold = c["threshold"]
+    st.minor_loop_gain = 0.1
+    st.major_loop_gain = 1.0
+    st.allow_negative_components = True
+    st.border_ratio = 0.0
+    st.minor_iteration_count = c["cap"]
+    run = rd.gpu.DeviceRun(st, psfs[0], dirty[0], [], 0.0)
+    run.execute()  # warm-up (plans for the box sizes met)
+    timing = Timing()
+    run.restore()
+    run.sync()
+    timing.reset()
+    timing.only(None)
+    timing.enable(True)
+    t0 = time.perf_counter()
+    r = run.execute()
+    run.sync()
+    el = time.perf_counter() - t0
+    timing.enable(False)
+    fams = timing.get()
+    timing.reset()
+    steps = run.iuwt_steps()
+    del run
+    dev = sum(v["ms"] for v in fams.values())
+    top = []
+    for k, v in sorted(fams.items(), key=lambda kv: -kv[1]["ms"])[:6]:
+        gbs = v["bytes"] / (v["ms"] * 1e-3) / 1e9 if v["ms"] else 0.0
+        top.append({"kernel": k, "share_of_device_time": round(v["ms"] / dev, 3) if dev else None,
+                    "avg_launch_us": round(1e3 * v["ms"] / v["launches"], 2),
+                    "achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)})
+    return {"workload": "c4: IUWT 4096x4096 (SURVEY.md C4, tests/config_problems.py)",
+            "decomposition_6_scales": comp,
+            "algorithm": {"seconds": round(el, 4), "iterations": int(r["iterations"]),
+                          "steps": len(steps),
+                          "successful_steps": int(sum(1 for x in steps if x[0])),
+                          "another_iteration_required": bool(r["another_iteration_required"]),
+                          "device_ms": round(dev, 2), "families": top,
+                          "note": "one DeviceRun.execute to the algorithm's stop (the "
+                                  "fixture's 24-step cap), HIP events on every family"}}
+
+
 def committed_cpu_to_threshold():
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_cpu_c2_to_threshold.json")))
@@ -394,6 +495,10 @@ def main():
     ap.add_argument("--size", type=int, default=None,
                     help="image side (default 8192; joined: 4096, SURVEY.md C3)")
     ap.add_argument("--channels", type=int, default=8, help="joined: channels")
+    ap.add_argument("--joined-split", choices=["channels", "subimages"], default="channels",
+                    help="joined at N > 1: share the per-channel work of ONE image set "
+                         "(channels; the C3 computation itself) or split the set into "
+                         "subimages (subimages; a different problem)")
     ap.add_argument("--grid", type=int, default=8, help="tiled: subimages per axis")
     ap.add_argument("--pool", type=int, default=16,
                     help="tiled: subimages in flight per GPU (settings.parallel.max_threads)")
@@ -419,6 +524,9 @@ def main():
                     help="outer iterations of the CPU baseline on one thread after the "
                          "all-threads ones (0 = skip; one 8192^2 outer iteration on one "
                          "thread takes one to two minutes)")
+    ap.add_argument("--iuwt-reference", type=int, default=1,
+                    help="N = 1 fields: also time SURVEY.md C4 (IUWT 4096^2: the 6-scale "
+                         "decomposition component and the algorithm to its stop)")
     ap.add_argument("--c2-reference", type=int, default=1,
                     help="N = 1 fields: also time Radler.perform to the threshold on the C2 "
                          "configuration (4096^2), the workload of the committed CPU "
@@ -456,7 +564,11 @@ def main():
         args.size = 4096 if joined else 8192
     # joined over N > 1 ranks: the image set (all channels) split into
     # grid x grid subimages owned by the ranks, as tiled
-    split = tiled or (joined and world > 1)
+    split = tiled or (joined and world > 1 and args.joined_split == "subimages")
+    # joined over N > 1 ranks by channel: every rank the whole computation's
+    # integrated work, its own channels' corrections (MultiScaleAlgorithm::
+    # SetChannelShard); every rank reports the same components
+    chan_shard = joined and world > 1 and args.joined_split == "channels"
     dist = None
     if world > 1:
         import torch
@@ -486,7 +598,7 @@ def main():
     s = settings_for(rd, args.size, args.max_iter, args.scales, threshold,
                      args.grid if split else 1, args.pool if split else 1)
     comm = None
-    if split and dist is not None:
+    if (split or chan_shard) and dist is not None:
         # RCCL communicator of the product (rdl_comm_*), id from rank 0
         import torch
         idl = torch.zeros(rd.distributed.rccl_id_size(), dtype=torch.uint8, device="cuda")
@@ -571,6 +683,47 @@ def main():
               flush=True)
         joined_once(su)
         u_comps, u_el = joined_once(su)
+        # the channel-sharded form of the same run (`--workload joined --gpus
+        # N`, MultiScaleAlgorithm::SetChannelShard): its per-image work (the
+        # float64 residual corrections and the model stamping) is what N ranks
+        # share; one more unsplit run with every family timed prices it
+        timing.reset()
+        timing.only(None)
+        timing.enable(True)
+        joined_once(su)
+        timing.enable(False)
+        jf = timing.get()
+        timing.reset()
+        dev_ms = sum(v["ms"] for v in jf.values())
+        shard_ms = sum(v["ms"] for k, v in jf.items()
+                       if k.startswith("conv64") or k == "stamp_model")
+        outer = jf.get("subminor_loop", {}).get("launches", 0)
+        f_shard = shard_ms / dev_ms if dev_ms else 0.0
+        plane_bytes = jsize * jsize * 4
+        link_gbs = 153.0  # one xGMI link (MI355X_MICROARCH.md: 7 per GPU)
+        chan_bound = {}
+        for n in (2, 4, 8):
+            # every rank receives the other ranks' corrected planes each outer
+            # iteration: (n - 1) / n of the channels' planes
+            xbytes = outer * (n - 1) / n * jch * plane_bytes
+            chan_bound[str(n)] = {
+                "compute_bound_s": round(u_el * ((1.0 - f_shard) + f_shard / n), 4),
+                "exchange_gb": round(xbytes / 1e9, 2),
+                "exchange_s_ring_one_link": round(xbytes / (link_gbs * 1e9), 4),
+                "exchange_s_all_links": round(xbytes / (min(n - 1, 7) * link_gbs * 1e9), 4)}
+        channel_shard = {
+            "shardable_device_fraction": round(f_shard, 4),
+            "device_ms": round(dev_ms, 1), "shardable_ms": round(shard_ms, 1),
+            "outer_iterations": outer, "bound": chan_bound,
+            "note": "`--workload joined --gpus N` (default --joined-split channels): ONE "
+                    "image set, image i's residual correction + model update on rank i % N, "
+                    "the integrated-image work (integration, scale convolutions, peak "
+                    "searches, selection, sub-minor loop) on every rank, corrected planes "
+                    "broadcast from their owners each outer iteration. compute_bound_s = "
+                    "the unsplit run with the shardable device time divided by N; the "
+                    "exchange adds exchange_s (one link: a ring; all links: a full mesh) "
+                    "unless overlapped. Bit-identical to the unsplit run "
+                    "(tests/test_distributed.py::test_channel_sharded_joined_equals_one_process)"}
         print("[bench] joined reference, split (warm-up + 1 step) ...", file=sys.stderr,
               flush=True)
         joined_once()
@@ -586,6 +739,7 @@ def main():
                                   "value": round(u_comps / u_el, 2),
                                   "wall_clock_to_threshold_s": round(u_el, 4),
                                   "components_per_step": u_comps,
+                                  "channel_shard": channel_shard,
                                   "note": "SURVEY.md C3 as one image set on one GPU: the "
                                           "joined N = 1 point of the C3 computation"},
                       "note": "`--workload joined --gpus N` at N = 1: the channels' image set "
@@ -599,10 +753,15 @@ def main():
             "unsplit_s": round(u_el, 4), "split_bound_s": bound,
             "note": ("best-case wall clock of the split problem on N ranks (perform_s / "
                      "speedup_bound) beside the unsplit run on one GPU; the channel-sharded "
-                     "alternative (north_star's ordered slab reduction + integrated-peak "
-                     "allreduce) would add one RCCL round trip (~10 us) to every ~7 us "
-                     "joined component, DESIGN.md §6")}
+                     "form of the unsplit run is unsplit.channel_shard")}
         del j_psf, j_dirty
+
+    # C4: the IUWT decomposition component and algorithm on this GPU
+    iuwt_ref = None
+    if args.iuwt_reference and world == 1 and workload == "fields":
+        print("[bench] C4 IUWT 4096^2 (decomposition + algorithm) ...", file=sys.stderr,
+              flush=True)
+        iuwt_ref = iuwt_leg(rd)
 
     # C2 (4096^2) to the threshold on this GPU: the same problem as the
     # committed CPU to-threshold run (wall clock against wall clock)
@@ -694,6 +853,8 @@ def main():
     if has_resident:
         run = rd.gpu.DeviceRun(s, psf, dirty, [1.0] * args.channels if joined else [],
                                BEAM_PX * PIXEL_SCALE, trace=False)
+        if comm is not None:
+            run.set_communicator(comm)
         run.restore()
         run.execute()  # warm-up
         run.sync()
@@ -724,7 +885,7 @@ def main():
         t = torch.tensor([vals[0], vals[2]], dtype=torch.float64, device="cuda")
         c = torch.tensor([vals[1], vals[3]], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        if not split:  # split: every rank reports the whole job's components
+        if not (split or chan_shard):  # split / by channel: every rank reports the job's
             dist.all_reduce(c, op=dist.ReduceOp.SUM)
         max_elapsed, total_comps = float(t[0].item()), int(c[0].item())
         if resident:
@@ -832,7 +993,8 @@ def main():
     # resident leg: their line is the Radler.perform rate (config.step says so).
     host = {"ms_per_step": round(ms_per_step, 2),
             "value": round(total_comps / max_elapsed, 2),
-            "components_per_step": total_comps // (args.steps * (1 if split else world)),
+            "components_per_step": total_comps // (args.steps * (1 if split or chan_shard
+                                                                 else world)),
             "step": "Radler.perform (accessor load over PCIe + major iteration + store)"}
     if resident:
         v_value, v_ms = resident["value"], resident["ms_per_step"]
@@ -860,7 +1022,7 @@ def main():
                              if resident else
                              "v1: Radler.perform over host buffers (accessor load + major "
                              "iteration + store)"),
-        "scaling": "strong" if split else "weak",
+        "scaling": "strong" if split or chan_shard else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (seeded sky: points + Gaussian blobs, analytic PSF, noise)",
@@ -871,9 +1033,11 @@ def main():
                    "points": args.points, "blobs": args.blobs, "noise": NOISE,
                    "threshold": threshold, "minor_loop_gain": 0.1, "major_loop_gain": 1.0,
                    "channels": args.channels if joined else 1,
-                   "fields_per_gpu": 0 if split else 1,
+                   "fields_per_gpu": 0 if split or chan_shard else 1,
                    "parallelism": (f"subimages{args.grid * args.grid}/ranks{world}"
-                                   f"/pool{args.pool}" if split else f"fields{world}"),
+                                   f"/pool{args.pool}" if split else
+                                   f"channels{args.channels}/ranks{world}" if chan_shard
+                                   else f"fields{world}"),
                    **({"problem": ("the joined image set split into grid x grid subimages "
                                    "shared by the ranks (ParallelDeconvolution over the "
                                    "channels' set): at N > 1 this solves the tiled problem, "
@@ -884,6 +1048,7 @@ def main():
         "tiled_n1": tiled_ref,
         "joined_n1": joined_ref,
         "c2_to_threshold": c2_ref,
+        "iuwt_c4": iuwt_ref,
         "roofline": roofline,
         "cpu_baseline": cpu,
     }

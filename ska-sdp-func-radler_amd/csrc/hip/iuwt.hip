@@ -146,6 +146,99 @@ __global__ __launch_bounds__(256) void IuwtAccumulateVAdd(float* out,
   }
 }
 
+// ---- fused row kernels (r06). Each block owns image rows; a row of the
+// intermediate lives in LDS between the vertical and horizontal filters, so
+// the intermediates of the four passes per scale do not all reach HBM. Every
+// value is computed by the same per-pixel operations as the kernels above
+// (VerticalValue / HorizontalValue / the Recompose accumulations), so the
+// outputs are bit-identical.
+//
+// DecomposeRows (one scale, spacing d; DecomposeMt's i1 = V(H(a)) and the
+// scratch = H(i1) of iuwt_decomposition.cc:9-54): row y of i1 = V_d(s1) from
+// rows y + k d of s1 = H_d(a), kept in LDS, then s2 = H_d(i1) for this
+// scale's difference pass and, when d_next > 0, s1' = H_d_next(i1), the
+// next scale's first pass (a_{s+1} = i1).
+__global__ __launch_bounds__(256) void IuwtDecomposeRows(float* i1, float* s2, float* s1_next,
+                                                         const float* s1, uint32_t w,
+                                                         uint32_t h, int d, int d_next) {
+  extern __shared__ float row[];
+  const int64_t y = blockIdx.x;
+  for (uint32_t x = threadIdx.x; x < w; x += blockDim.x) {
+    float t[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const int64_t yy = y + int64_t(d) * (k - 2);
+      t[k] = (yy >= 0 && yy < int64_t(h)) ? s1[size_t(yy) * w + x] : 0.0f;
+    }
+    const float v = VerticalValue(t, y, int64_t(h), d);
+    row[x] = v;
+    i1[size_t(y) * w + x] = v;
+  }
+  __syncthreads();
+  for (uint32_t x = threadIdx.x; x < w; x += blockDim.x) {
+    float t[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const int64_t xx = int64_t(x) + int64_t(d) * (k - 2);
+      t[k] = (xx >= 0 && xx < int64_t(w)) ? row[xx] : 0.0f;
+    }
+    s2[size_t(y) * w + x] = HorizontalValue(t, x, int64_t(w), d);
+    if (d_next > 0) {
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const int64_t xx = int64_t(x) + int64_t(d_next) * (k - 2);
+        t[k] = (xx >= 0 && xx < int64_t(w)) ? row[xx] : 0.0f;
+      }
+      s1_next[size_t(y) * w + x] = HorizontalValue(t, x, int64_t(w), d_next);
+    }
+  }
+}
+
+// RecomposeRows (one scale of Recompose, iuwt_decomposition.h:121-146 with
+// IuwtDecomposition::convolve, .h:243-261): out_new row y = V_acc(H_acc(out))
+// + coefficients, the H-accumulated rows y + k d made in LDS from out.
+__global__ __launch_bounds__(256) void IuwtRecomposeRows(float* out_new, const float* out,
+                                                         const float* add, uint32_t w,
+                                                         uint32_t h, int d) {
+  extern __shared__ float rows[];  // [5][w] H-accumulated rows (0 outside)
+  const int64_t y = blockIdx.x;
+  for (int k = 0; k < 5; ++k) {
+    const int64_t yy = y + int64_t(d) * (k - 2);
+    if (yy < 0 || yy >= int64_t(h)) continue;
+    const float* src = out + size_t(yy) * w;
+    for (uint32_t x = threadIdx.x; x < w; x += blockDim.x) {
+      float acc = 0.0f;
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        const int64_t xx = int64_t(x) + int64_t(d) * (j - 2);
+        if (xx >= 0 && xx < int64_t(w)) acc = __builtin_fmaf(src[xx], IuwtTap(j), acc);
+      }
+      rows[size_t(k) * w + x] = acc;
+    }
+  }
+  __syncthreads();
+  for (uint32_t x = threadIdx.x; x < w; x += blockDim.x) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const int64_t yy = y + int64_t(d) * (k - 2);
+      if (yy >= 0 && yy < int64_t(h))
+        acc = __builtin_fmaf(rows[size_t(k) * w + x], IuwtTap(k), acc);
+    }
+    out_new[size_t(y) * w + x] = acc + add[size_t(y) * w + x];
+  }
+}
+
+// RDL_IUWT_FUSED=0: the four-pass kernels for every call (comparison)
+inline bool IuwtFusedOn() {
+  const char* e = std::getenv("RDL_IUWT_FUSED");
+  return !(e && e[0] == '0');
+}
+// rows of at most this many floats go through LDS (one row per decompose
+// block: 64 KiB at most; five rows per recompose block: 120 KiB at most)
+constexpr uint32_t kIuwtFusedMaxWidth = 16384;
+constexpr uint32_t kIuwtFusedMaxWidthRecompose = 6144;
+
 inline unsigned IuwtGrid(size_t n) {
   return unsigned(std::min<size_t>(16384, std::max<size_t>(1, (n + 255) / 256)));
 }
@@ -184,6 +277,36 @@ int rdl_iuwt_decompose(rdl_session* s, float* d_input, float* d_scratch,
   RDL_ARG_CHECK(width >= 1 && height >= 1, "bad size");
   // DecomposeMt (iuwt_decomposition.cc:9-54)
   const size_t n = size_t(width) * height;
+  if (d_input != d_scratch && width <= rdl::kIuwtFusedMaxWidth && rdl::IuwtFusedOn()) {
+    // fused: per scale one row kernel (i1, s2 = H(i1), next scale's H(i1))
+    // and the difference pass; the approximation planes alternate between
+    // the largest-scale plane and a scratch plane (no copy), arranged so the
+    // last one lands in the largest-scale plane as the four-pass form leaves
+    // it. The caller's scratch is not written (not aliased: nothing reads it).
+    RDL_TRY(s->EnsureScratch(s->iuwt, 4 * n * sizeof(float)));
+    float* big = d_coeffs + size_t(n_scales) * n;
+    float* spare = static_cast<float*>(s->iuwt.ptr);
+    float* s1[2] = {spare + n, spare + 2 * n};
+    float* s2 = spare + 3 * n;
+    RDL_TRY(rdl::Horizontal(s, s1[0], d_input, width, height, 1));
+    const float* a = d_input;
+    for (uint32_t sc = 0; sc < n_scales; ++sc) {
+      const int d = (1 << (sc + 1)) - 1;
+      const int d_next = sc + 1 < n_scales ? (1 << (sc + 2)) - 1 : 0;
+      float* i1 = ((n_scales - 1 - sc) % 2 == 0) ? big : spare;
+      {
+        rdl::ScopedTiming t(s, "iuwt", double(n) * (d_next ? 16.0 : 12.0));
+        rdl::IuwtDecomposeRows<<<height, 256, width * sizeof(float), s->stream>>>(
+            i1, s2, s1[(sc + 1) & 1u], s1[sc & 1u], width, height, d, d_next);
+        RDL_HIP_CHECK(hipGetLastError());
+      }
+      RDL_TRY(rdl::Vertical(s, d_coeffs + size_t(sc) * n, s2, a, width, height, d));
+      a = i1;
+    }
+    if (!include_largest)
+      RDL_HIP_CHECK(hipMemsetAsync(big, 0, n * sizeof(float), s->stream));
+    return RDL_OK;
+  }
   RDL_TRY(s->EnsureScratch(s->iuwt, n * sizeof(float)));
   float* i0 = static_cast<float*>(s->iuwt.ptr);
   float* i1 = d_coeffs + size_t(n_scales) * n;  // the largest scale aliases i1
@@ -220,6 +343,36 @@ int rdl_iuwt_recompose(rdl_session* s, const float* d_coeffs, uint32_t width,
   RDL_TRY(s->EnsureScratch(s->iuwt, n * sizeof(float)));
   float* tmp = static_cast<float*>(s->iuwt.ptr);
   int sc = int(n_scales) - 1;
+  if (width <= rdl::kIuwtFusedMaxWidthRecompose && rdl::IuwtFusedOn()) {
+    // fused: one row kernel per scale (out_new = V(H(out)) + coefficients),
+    // alternating between d_out and the scratch plane so the last scale
+    // writes d_out
+    const float* first = d_coeffs + size_t(include_largest ? n_scales : uint32_t(sc)) * n;
+    if (!include_largest) --sc;
+    const int n_pass = sc + 1;
+    // pass k (k = 0 .. n_pass-1, scale sc - k) writes d_out when
+    // n_pass - 1 - k is even; the starting plane goes to the other buffer
+    float* start = (n_pass % 2 == 0) ? d_out : tmp;
+    RDL_HIP_CHECK(hipMemcpyAsync(start, first, n * sizeof(float), hipMemcpyDeviceToDevice,
+                                 s->stream));
+    const float* cur = start;
+    for (int k = 0; sc >= 0; --sc, ++k) {
+      const int d = (1 << (sc + 1)) - 1;
+      float* dst = ((n_pass - 1 - k) % 2 == 0) ? d_out : tmp;
+      static std::once_flag lds_once;
+      std::call_once(lds_once, [] {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&rdl::IuwtRecomposeRows),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  int(5 * rdl::kIuwtFusedMaxWidthRecompose * sizeof(float)));
+      });
+      rdl::ScopedTiming t(s, "iuwt", double(n) * 12.0);
+      rdl::IuwtRecomposeRows<<<height, 256, 5 * width * sizeof(float), s->stream>>>(
+          dst, cur, d_coeffs + size_t(sc) * n, width, height, d);
+      RDL_HIP_CHECK(hipGetLastError());
+      cur = dst;
+    }
+    return RDL_OK;
+  }
   if (include_largest) {
     RDL_HIP_CHECK(hipMemcpyAsync(d_out, d_coeffs + size_t(n_scales) * n,
                                  n * sizeof(float), hipMemcpyDeviceToDevice,

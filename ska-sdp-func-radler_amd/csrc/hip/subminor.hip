@@ -2837,7 +2837,12 @@ int SubminorLaunch(rdl_subminor* h, const float* d_residuals, const float* d_psf
   uint64_t n_sel = 0;
   uint32_t failed = 0;
   {
-    const rdl::SmallRead r[2] = {{&n_sel, h->select_passes == 1 ? d_total : m_total,
+    // RDL_SEL_COUNT_COPY=1: read the count back by a copy (r04 form; bisect)
+    static const bool count_copy = [] {
+      const char* e = std::getenv("RDL_SEL_COUNT_COPY");
+      return e && e[0] == '1';
+    }();
+    const rdl::SmallRead r[2] = {{&n_sel, h->select_passes == 1 || count_copy ? d_total : m_total,
                                   sizeof(n_sel)},
                                  {&failed, sel_failed, sizeof(failed)}};
     RDL_TRY(rdl::ReadSmall(s, r, sel_failed ? 2 : 1));
@@ -3114,11 +3119,17 @@ int SubminorLaunch(rdl_subminor* h, const float* d_residuals, const float* d_psf
   // zero counter, result and (register kernel) the epoch-tagged granules:
   // with a pairwise table, by BuildPairTable
   const size_t zero_bytes = (use_reg || use_tab || use_tabn) ? 512 + rec_bytes : 512;
-  const bool table_zeroes = (use_reg || use_tab || use_tabn) && want_table;
+  // RDL_TABLE_ZERO=0: a separate memset of the exchange area (r04 form; bisect)
+  static const bool table_zero_on = [] {
+    const char* e = std::getenv("RDL_TABLE_ZERO");
+    return !(e && e[0] == '0');
+  }();
+  const bool build_table = (use_reg || use_tab || use_tabn) && want_table;
+  const bool table_zeroes = build_table && table_zero_on;
   if (!table_zeroes) RDL_HIP_CHECK(hipMemsetAsync(sb, 0, zero_bytes, st));
   la.table = nullptr;
   const uint32_t n_psf = ni / p->n_pol;
-  if (table_zeroes) {
+  if (build_table) {
     // (+ 32 KiB: the table loop reads whole workgroup-sized slices of a row)
     const size_t table_bytes = size_t(n_psf) * n_sel * n_sel * sizeof(float) + (32 << 10);
     RDL_TRY(rdl::Grow(&h->table, &h->table_bytes, table_bytes, st));
@@ -3126,7 +3137,7 @@ int SubminorLaunch(rdl_subminor* h, const float* d_residuals, const float* d_psf
     rdl::BuildPairTable<<<dim3(rdl::DivUp(n_sel, 256), uint32_t(n_sel)), 256, 0, st>>>(
         h->d_pos, d_psfs, uint32_t(n_sel), n_psf, p->width, p->height,
         static_cast<float*>(h->table), reinterpret_cast<uint64_t*>(sb),
-        uint32_t((zero_bytes + 7) / 8));
+        table_zeroes ? uint32_t((zero_bytes + 7) / 8) : 0u);
     RDL_HIP_CHECK(hipGetLastError());
     la.table = static_cast<const float*>(h->table);
   }

@@ -14,6 +14,10 @@
 #include "settings.h"
 #include "spectral_fitter.h"
 
+namespace radler {
+class Communicator;
+}
+
 namespace radler::algorithms {
 
 struct DeconvolutionResult {
@@ -32,6 +36,10 @@ class DeconvolutionAlgorithm {
       ImageSet& data_image, ImageSet& model_image,
       const gpu::Planes& psf_images) = 0;
   virtual std::unique_ptr<DeconvolutionAlgorithm> Clone() const = 0;
+  /// Process-per-GPU joined channels: the ranks of
+  /// `comm` share the per-channel work of ONE image set (MultiScale only;
+  /// the others ignore it). nullptr: everything on this rank.
+  virtual void SetChannelShard(Communicator* comm) { (void)comm; }
 
   void SetMaxIterations(size_t v) { settings_.max_iterations = v; }
   void SetThreshold(float v) { settings_.threshold = v; }

@@ -11,6 +11,7 @@
 #include <set>
 #include <stdexcept>
 
+#include "communicator.h"
 #include "component_optimization.h"
 #include "fft_sizes.h"
 #include "host_profile.h"
@@ -521,6 +522,20 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
 
   bool has_hit_threshold_in_sub_loop = false;
   size_t threshold_countdown = std::max(size_t{8}, scale_infos_.size() * 3 / 2);
+  // joined channels over the ranks of shard_ (SetChannelShard): image i's
+  // residual correction and model update run on rank i % size only
+  const int n_ranks = shard_ ? shard_->Size() : 1;
+  const int my_rank = shard_ ? shard_->Rank() : 0;
+  const bool sharded = n_ranks > 1 && data_image.Size() > 1;
+  auto owner = [&](size_t i) { return sharded ? int(i % size_t(n_ranks)) : my_rank; };
+  // the owners' planes to every rank (stream-ordered on the session; the
+  // ranks issue the same broadcasts in the same order)
+  auto share_planes = [&](ImageSet& set) {
+    if (!sharded) return;
+    prof::Section prof_share("ms.shard_broadcast");
+    for (size_t i = 0; i != set.Size(); ++i)
+      shard_->Broadcast(session, set.Data(i), npx * sizeof(float), owner(i));
+  };
 
   // rebuilt when another worker session runs this subimage (the ranks'
   // ownership, parallel_deconvolution.cc, changes between major iterations)
@@ -731,7 +746,10 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
       };
       if (!defer) account(r);
       std::optional<prof::Section> prof_correct(std::in_place, "ms.correct_and_model");
+      if (track_masks_ && scale_with_peak < dev_masks_.size())  // :444-445
+        sub.UpdateAutoMask(static_cast<uint8_t*>(dev_masks_[scale_with_peak].Ptr()));
       for (size_t i = 0; i != data_image.Size(); ++i) {
+        if (owner(i) != my_rank) continue;  // another rank's image
         const size_t psf_index = data_image.PsfIndex(i);
         auto key = std::make_pair(psf_index, scale_with_peak);
         auto pc = padded_cache.find(key);
@@ -743,8 +761,6 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
                    .first;
         sub.CorrectResidualDirtyWithSpectrum(i, data_image.Data(i),
                                              pc->second->Ptr());
-        if (i == 0 && track_masks_ && scale_with_peak < dev_masks_.size())  // :444-445
-          sub.UpdateAutoMask(static_cast<uint8_t*>(dev_masks_[scale_with_peak].Ptr()));
         if (info.scale != 0.0f) {
           // the sub-minor model is a few hundred components: stamping the
           // shape kernel costs n_sel * n^2 multiply-adds against two
@@ -766,6 +782,7 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
       if (track_components_)  // :447-448
         sub.UpdateComponentList(*component_list_, scale_with_peak);
       prof_correct.reset();
+      share_planes(data_image);  // the corrected residuals, from their owners
       if (defer) {
         ActivateScales(scale_with_peak);
         FindActiveScaleConvolvedMaxima(data_image, integrated.F(), false);
@@ -854,6 +871,7 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
       log::Warn() << "No peak found in main loop of multi-scale cleaning! "
                      "Aborting deconvolution.\n";
       result.another_iteration_required = false;
+      share_planes(model_image);
       return result;
     }
     scale_with_peak = *optional_scale;
@@ -877,6 +895,7 @@ DeconvolutionResult MultiScaleAlgorithm::ExecuteMajorIteration(
   result.final_peak_value =
       scale_infos_[scale_with_peak].max_unnormalized_image_value *
       scale_infos_[scale_with_peak].bias_factor;
+  share_planes(model_image);  // the owners' model updates
   session.Sync();
   return result;
 }

@@ -33,6 +33,15 @@ class MultiScaleAlgorithm final : public DeconvolutionAlgorithm {
   DeconvolutionResult ExecuteMajorIteration(ImageSet& data_image,
                                             ImageSet& model_image,
                                             const gpu::Planes& psf_images) final;
+  /// Joined channels over the ranks of `comm` (one process per GPU): every
+  /// rank runs the integrated-image work (integration, the scales' peak
+  /// searches, the selection and the sub-minor loop: identical inputs give
+  /// identical results) and the per-image residual correction and model
+  /// update of the images it owns (image i: rank i % size); the corrected
+  /// residual planes are then broadcast from their owners, the model planes
+  /// at the end of the major iteration. Same operations on the same data as
+  /// one process: bit-identical residuals, models and traces.
+  void SetChannelShard(Communicator* comm) final { shard_ = comm; }
 
   struct ScaleInfo {
     float scale = 0.0;
@@ -106,6 +115,7 @@ class MultiScaleAlgorithm final : public DeconvolutionAlgorithm {
 
   // per-major-iteration device state
   gpu::Session* session_ = nullptr;
+  Communicator* shard_ = nullptr;  // SetChannelShard (not copied by Clone)
   std::unique_ptr<multiscale::MultiScaleTransforms> transforms_;
   const uint8_t* d_mask_ = nullptr;
   std::shared_ptr<gpu::Buffer> scratch_;  // W x H

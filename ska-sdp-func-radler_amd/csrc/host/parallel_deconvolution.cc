@@ -164,6 +164,9 @@ ParallelDeconvolutionResult ParallelDeconvolution::ExecuteSingleThreadedRun(
     const std::vector<PsfOffset>& psf_offsets, double major_loop_gain) {
   // :510-553
   DeconvolutionAlgorithm& algorithm = *algorithms_.front();
+  // one image set over the ranks: joined channels are shared by channel
+  // (MultiScaleAlgorithm::SetChannelShard)
+  algorithm.SetChannelShard(comm_ && comm_->Size() > 1 ? comm_.get() : nullptr);
   const size_t psf_index = NearestPsfIndex(
       psf_offsets, model_image.Width() / 2, model_image.Height() / 2);
   const gpu::Planes& psfs = psf_images[psf_index];

@@ -95,6 +95,25 @@ def main():
         out["max"] = np.float32(comm.allreduce_max(float(args.rank) * 1.5 - 7.0))
         out["owners"] = np.array([rd.distributed.subimage_owner(i, args.world)
                                   for i in range(10)])
+    elif args.case == "channels":
+        # ONE joined image set (grid 1 x 1) whose per-channel work the ranks
+        # share (MultiScaleAlgorithm::SetChannelShard)
+        w = args.size
+        psf, dirty = tiled_problem(w, 1, args.channels)
+        thr, max_iter = 4e-3, 1500
+        mgain = 0.9 if args.majors == 1 else 0.5
+        s = tiled_settings(rd, 1, w, thr, max_iter, mgain, 1, 1)
+        run = rd.gpu.DeviceRun(s, psf, dirty, [1.0] * args.channels, 2.0 * PIXEL_SCALE)
+        run.set_communicator(comm)
+        for major in range(args.majors):
+            r = run.execute()
+            out[f"residual{major}"] = run.residual()
+            out[f"model{major}"] = run.model()
+            out[f"iterations{major}"] = np.int64(r["iterations"])
+            out[f"another{major}"] = np.int64(r["another_iteration_required"])
+            out[f"trace{major}"] = run.trace(0)
+        run.sync()
+        del run
     else:
         w = args.size
         gw, gh = args.grid

@@ -395,50 +395,99 @@ def test_p8k_tiled_8192_8x8_concurrent_pool():
     _tiled("p8k")
 
 
-@pytest.mark.gpu
-def test_c2_to_threshold_end_state():
-    """C2 run to the 5-sigma threshold (no component cap, one major
-    iteration): the end state against the oracle's to-threshold run. The
-    float32 trajectory separates from the float64 oracle's after its first
-    near-ties (test_c2), so the end state is compared by quantities that do
-    not depend on the exact component order, with tolerances from the
-    measured float32-vs-float64 spread:
-    component count, stop (another_iteration_required), final peak, residual
-    RMS and max, model total flux and max."""
+def end_state_tolerances(name):
+    """Tolerances of a to-threshold end state (relative to the oracle's value)
+    from the GPU's own rounding sensitivity: tools/end_state_spread.py runs the
+    problem as given, with a random half of the dirty pixels moved by one
+    float ulp (6 seeds) and with the two-pass scale convolutions, and records
+    the largest relative deviation of each quantity from the unperturbed run
+    and the largest pairwise RMS distance of the residual / model samples
+    (profiles/r06_end_state_spread_<name>.json). A trajectory that separates
+    at its first near-ties can end anywhere in that cloud; the float64
+    oracle is one more member of it, so each quantity is allowed
+    END_STATE_FACTOR x the cloud's measured extent (7 members: the largest
+    of a handful of draws understates the tail)."""
+    import json
+    path = os.path.join(os.path.dirname(GOLDEN), "..", "profiles",
+                        f"r06_end_state_spread_{name}.json")
+    path = os.path.normpath(path)
+    if not os.path.exists(path):
+        pytest.skip(f"{path} not measured")
+    d = json.load(open(path))
+    tol = {k: END_STATE_FACTOR * v["max_rel"] for k, v in d["spread"].items()
+           if k != "final_peak"}
+    tol.update({f"{k}_samples": END_STATE_FACTOR * v["max"]
+                for k, v in d["sample_rms_distance"].items()})
+    return tol, d
+
+
+END_STATE_FACTOR = 2.0
+
+
+def _to_threshold_end_state(name):
+    """A configuration run to its 5-sigma threshold (no component cap, one
+    major iteration; the end state of multiscale_algorithm.cc:323-543,
+    countdown :249, :363-373) against the oracle's to-threshold run: the
+    trace tie-aware up to its first near-tie, then the end state by
+    quantities that do not depend on the exact component order -- component
+    count, stop (another_iteration_required), |final peak|, residual RMS and
+    max, model total flux and max -- and the residual / model at the
+    fixture's 65 536 sampled pixels (RMS of the difference over the
+    oracle's sample RMS), each within end_state_tolerances(name)."""
     from radler_import import radler as rd
-    fx = fixture("c2t")
-    psfs, dirty = inputs("c2t", fx)
-    run = _device_run(rd, "c2t", psfs, dirty)
+    fx = fixture(name)
+    tol, spread = end_state_tolerances(name)
+    psfs, dirty = inputs(name, fx)
+    run = _device_run(rd, name, psfs, dirty)
     r = run.execute()
     k = min_prefix(fx)
     c = assert_tie_aware(run.trace(), fx["trace"], fx["margins"], fx["values"], RTOL,
                          min_prefix=k)
-    res = run.residual().astype(np.float64)
-    mod = run.model().astype(np.float64)
+    res = run.residual().astype(np.float64).reshape(-1)
+    mod = run.model().astype(np.float64).reshape(-1)
+    idx = sample_index(res.size)
     n_g, n_o = int(r["iterations"]), int(fx["iteration_number"])
-    got = {"components": n_g, "final_peak": float(r["end_peak"]),
+    got = {"components": n_g, "abs_final_peak": abs(float(r["end_peak"])),
            "residual_rms": float(np.sqrt(np.mean(res ** 2))),
            "residual_absmax": float(np.abs(res).max()),
            "model_sum": float(mod.sum()), "model_absmax": float(np.abs(mod).max())}
-    ref = {"components": n_o, "final_peak": float(fx["final_peak"]),
+    ref = {"components": n_o, "abs_final_peak": abs(float(fx["final_peak"])),
            "residual_rms": float(fx["residual_rms"][0]),
            "residual_absmax": float(fx["residual_absmax"][0]),
            "model_sum": float(fx["model_sum"][0]), "model_absmax": float(fx["model_absmax"][0])}
     rel = {key: abs(got[key] - ref[key]) / max(abs(ref[key]), 1e-30) for key in got}
-    print(f"c2t: {c}")
-    for key in got:
-        print(f"c2t {key}: gpu {got[key]:.6g} oracle {ref[key]:.6g} rel {rel[key]:.3g} "
-              f"(tolerance {C2T_RTOL[key]:g})")
+    rs, ms = fx["residual_sample"][0].astype(np.float64), fx["model_sample"][0].astype(np.float64)
+    rel["residual_samples"] = float(np.sqrt(np.mean((res[idx] - rs) ** 2)) /
+                                    np.sqrt(np.mean(rs ** 2)))
+    rel["model_samples"] = float(np.sqrt(np.mean((mod[idx] - ms) ** 2)) /
+                                 np.sqrt(np.mean(ms ** 2)))
+    print(f"{name}: {c}")
+    for key in rel:
+        g = got.get(key, float("nan"))
+        o = ref.get(key, float("nan"))
+        print(f"{name} {key}: gpu {g:.6g} oracle {o:.6g} rel {rel[key]:.3g} "
+              f"(tolerance {tol[key]:.3g}; GPU ensemble extent "
+              f"{tol[key] / END_STATE_FACTOR:.3g})")
     assert bool(r["another_iteration_required"]) == bool(fx["another_iteration_required"])
-    thr = cp.CONFIGS["c2t"]["threshold"]
-    assert abs(got["final_peak"]) <= 2 * thr and abs(ref["final_peak"]) <= 2 * thr
-    for key, t in C2T_RTOL.items():
-        assert rel[key] <= t, (key, got[key], ref[key], rel[key])
+    thr = cp.CONFIGS[name]["threshold"]
+    # the loop ends on its threshold countdown: both last peaks near the threshold
+    assert got["abs_final_peak"] <= 2 * thr and ref["abs_final_peak"] <= 2 * thr
+    for key, v in rel.items():
+        assert v <= tol[key], (key, got.get(key), ref.get(key), v, tol[key])
+    return rel, tol
 
 
-# end-state tolerances of test_c2_to_threshold_end_state (relative to the
-# oracle's value), 3-10x the spread measured on MI355X (r05: components
-# 1.55e-3, final peak 3.8e-2, residual RMS 7.9e-4, residual max 5.9e-2, model
-# flux 6.1e-5, model max 6.0e-8; DESIGN.md §7)
-C2T_RTOL = {"components": 5e-3, "final_peak": 0.2, "residual_rms": 5e-3,
-            "residual_absmax": 0.2, "model_sum": 5e-4, "model_absmax": 1e-5}
+@pytest.mark.gpu
+def test_c2_to_threshold_end_state():
+    """C2 (4096^2) run to the 5-sigma threshold: end state against the oracle's
+    (see _to_threshold_end_state)."""
+    _to_threshold_end_state("c2t")
+
+
+@pytest.mark.gpu
+def test_h8k_to_threshold_end_state():
+    """The headline bench run itself (h8k: 8192^2, 2 000 points + 200 blobs,
+    6 scales, run to the 5-sigma threshold as bench.py times it): its end
+    state against the oracle's to-threshold run of the same inputs
+    (tests/golden/config_h8kt.npz)."""
+    _to_threshold_end_state("h8kt")

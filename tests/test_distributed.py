@@ -23,7 +23,7 @@ import sys
 import numpy as np
 import pytest
 
-from oracle_lib import OracleParallel, get_oracle
+from oracle_lib import OracleAlgorithm, OracleParallel, get_oracle
 from synthetic import problem
 
 # the residual/model agreement of tests/test_configs_gpu.py (x max|dirty|)
@@ -145,6 +145,45 @@ def test_distributed_tiled_matches_oracle_snapshot(tmp_path, world, kind, w, gw,
         dr = np.abs(outs[0][f"residual{major}"].reshape(res_o.shape) - res_o).max()
         dm = np.abs(outs[0][f"model{major}"].reshape(mod_o.shape) - mod_o).max()
         print(f"major {major}: residual {dr:.3g}, model {dm:.3g} (tolerance {tol:.3g})")
+        assert dr <= tol and dm <= tol, (dr, dm, tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,channels", [(2, 8), (3, 8), (2, 4)])
+def test_channel_sharded_joined_equals_one_process(tmp_path, world, channels):
+    """SURVEY.md 8(e) C3 as the reference computes it: ONE joined image set
+    (grid 1 x 1), its per-channel residual corrections and model updates
+    shared by the ranks (image i on rank i % world), the integrated-image
+    work on every rank, corrected planes broadcast from their owners. Every
+    rank ends with the same images, bit-identical to the one-process run, and
+    the component traces are the oracle's unsplit joined run's
+    (image_set.cc:423-462 integration, multiscale_algorithm.cc:323-543)."""
+    majors = 2
+    extra = ["--size", "256", "--majors", str(majors), "--channels", str(channels)]
+    (tmp_path / "one").mkdir()
+    (tmp_path / "many").mkdir()
+    one = _launch(tmp_path / "one", 1, "channels", extra)[0]
+    outs = _launch(tmp_path / "many", world, "channels", extra)
+    from dist_worker import tiled_problem
+    psf, dirty = tiled_problem(256, 1, channels)
+    orc = get_oracle()
+    orc.set_threads(8)
+    alg = OracleAlgorithm(orc, 1, threshold=4e-3, max_iterations=1500, border_ratio=0.0,
+                          major_loop_gain=0.5, max_scales=4, beam_size_in_pixels=2.0)
+    res_o, mod_o = dirty.copy(), np.zeros_like(dirty)
+    tol = IMG_TOL * np.abs(dirty).max()
+    for major in range(majors):
+        r_o, trace_o = alg.execute(res_o, mod_o, psf)
+        for o in outs:
+            for key in ("residual", "model", "trace", "iterations", "another"):
+                assert np.array_equal(o[f"{key}{major}"], one[f"{key}{major}"]), (major, key)
+        assert np.array_equal(one[f"trace{major}"], trace_o), major
+        assert bool(one[f"another{major}"]) == bool(r_o.another_iteration_required)
+        dr = np.abs(one[f"residual{major}"].reshape(res_o.shape) - res_o).max()
+        dm = np.abs(one[f"model{major}"].reshape(mod_o.shape) - mod_o).max()
+        print(f"world {world}, {channels} channels, major {major}: "
+              f"{len(trace_o)} components identical to the oracle; residual {dr:.3g}, "
+              f"model {dm:.3g} (tolerance {tol:.3g})")
         assert dr <= tol and dm <= tol, (dr, dm, tol)
 
 

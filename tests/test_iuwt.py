@@ -8,6 +8,7 @@ GPU: rdl_iuwt_decompose / rdl_iuwt_recompose are bit-exact with the oracle
 (tap order per boundary region and FMA contraction of the reference build),
 aliased and not, with and without the approximation plane.
 """
+import os
 import ctypes as C
 
 import numpy as np
@@ -73,3 +74,37 @@ def test_gpu_iuwt_bit_exact(w, h, n, aliased, include_largest):
     for x in {id(a): a for a in (d_in, d_scratch, d_coeffs, d_out)}.values():
         x.free()
     s.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,h", [(4096, 4096), (1000, 37), (8192, 64)])
+@pytest.mark.parametrize("include_largest", [True, False])
+def test_gpu_iuwt_fused_rows_equal_four_pass(w, h, include_largest):
+    """The fused row kernels (r06: IuwtDecomposeRows / IuwtRecomposeRows, the
+    intermediate row in LDS, approximation planes alternating instead of
+    copied) against the four-pass kernels (RDL_IUWT_FUSED=0), bit for bit, at
+    the C4 size and at widths / heights below the larger spacings."""
+    from rdl_lib import Session
+    n = 6
+    img = image(w, h, 77)
+    s = Session(0)
+    outs = []
+    for fused in ("1", "0"):
+        os.environ["RDL_IUWT_FUSED"] = fused
+        try:
+            d_in, d_scratch = s.array(img), s.array(shape=(h, w))
+            d_coeffs = s.array(shape=(n + 1, h, w))
+            d_out = s.array(shape=(h, w))
+            s.rdl.rdl_iuwt_decompose(s.h, d_in.vp, d_scratch.vp, w, h, n, d_coeffs.vp,
+                                     int(include_largest))
+            s.rdl.rdl_iuwt_recompose(s.h, d_coeffs.vp, w, h, n, int(include_largest),
+                                     d_out.vp)
+            outs.append((d_coeffs.get(), d_out.get(), d_in.get()))
+            for x in (d_in, d_scratch, d_coeffs, d_out):
+                x.free()
+        finally:
+            del os.environ["RDL_IUWT_FUSED"]
+    s.close()
+    assert np.array_equal(bits(outs[0][0]), bits(outs[1][0]))
+    assert np.array_equal(bits(outs[0][1]), bits(outs[1][1]))
+    assert np.array_equal(bits(outs[0][2]), bits(img))  # the input is not written

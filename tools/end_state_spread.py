@@ -101,10 +101,15 @@ def main():
         del os.environ["RDL_FUSED_SCALES"]
     base = members["base"]
     spread = {}
-    for key in SCALARS:
-        devs = [abs(m[key] - base[key]) / max(abs(base[key]), 1e-30)
-                for n, m in members.items() if n != "base"]
-        spread[key] = {"max_rel": max(devs), "mean_rel": float(np.mean(devs))}
+    for key in SCALARS + ["abs_final_peak"]:
+        if key == "abs_final_peak":  # the last selected scale's signed peak: its size
+            devs = [abs(abs(m["final_peak"]) - abs(base["final_peak"])) /
+                    max(abs(base["final_peak"]), 1e-30) for n, m in members.items() if n != "base"]
+        else:
+            devs = [abs(m[key] - base[key]) / max(abs(base[key]), 1e-30)
+                    for n, m in members.items() if n != "base"]
+        spread[key] = {"max_rel": max(devs, default=0.0),
+                       "mean_rel": float(np.mean(devs)) if devs else 0.0}
     names = list(samples)
     pair = {"residual": [], "model": []}
     ref_rms = {"residual": float(np.sqrt(np.mean(samples["base"][0] ** 2))),
@@ -115,7 +120,8 @@ def main():
                 a, b = samples[names[i]][k], samples[names[j]][k]
                 pair[key].append(float(np.sqrt(np.mean((a - b) ** 2))) / ref_rms[key])
     out = {"config": args.name, "members": members, "spread": spread,
-           "sample_rms_distance": {k: {"max": max(v), "mean": float(np.mean(v))}
+           "sample_rms_distance": {k: {"max": max(v, default=0.0),
+                                       "mean": float(np.mean(v)) if v else 0.0}
                                    for k, v in pair.items()},
            "sample_rms": ref_rms,
            "note": "spread = max over members of |member - base| / |base|; sample "
