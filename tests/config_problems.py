@@ -106,6 +106,12 @@ CONFIGS = {
     # trimming before the first copy-back); `cap` components per subimage
     "p8k": dict(kind="tiled", size=8192, points=2000, blobs=200, threshold=5 * NOISE,
                 max_scales=6, grid=8, cap=300, snapshot=True, pool=16),
+    # t2k split 8 x 8 on the concurrent pool (snapshot schedule), run to the
+    # threshold: the component count of a gridded run to threshold against the
+    # unsplit run's (the 7x of bench.py's tiled_n1 leg) at a
+    # size the oracle finishes in minutes
+    "t2k8": dict(kind="tiled", size=2048, points=250, blobs=25, threshold=5 * NOISE,
+                 max_scales=6, grid=8, cap=10 ** 9, snapshot=True, pool=16),
     # bench.py's live CPU-vs-GPU wall-clock-to-threshold leg: C2's sky density
     # on 2048^2, small enough for the CPU oracle to reach the threshold inside
     # the default bench run (no fixture: both sides run it in the same job)

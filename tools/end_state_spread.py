@@ -46,10 +46,14 @@ def sample_index(n_pixels, seed=1):
     return np.sort(np.random.default_rng(seed).choice(n_pixels, 65536, replace=False))
 
 
+LABELS = {}  # tiled configurations: subimage label (+1) of every sampled pixel
+
+
 def end_state(rd, name, psfs, dirty):
     from test_configs_gpu import settings
+    tiled = cp.CONFIGS[name]["kind"] == "tiled"
     run = rd.gpu.DeviceRun(settings(rd, name), psfs[0], dirty[0], [],
-                           cp.BEAM_PX * cp.PIXEL_SCALE, trace=False)
+                           cp.BEAM_PX * cp.PIXEL_SCALE, trace=tiled)
     t = time.perf_counter()
     r = run.execute()
     run.sync()
@@ -65,6 +69,9 @@ def end_state(rd, name, psfs, dirty):
            "model_sum": float(mod.astype(np.float64).sum()),
            "model_absmax": float(np.abs(mod).max()), "seconds": round(el, 3)}
     samples = (res[idx].astype(np.float64), mod[idx].astype(np.float64))
+    if tiled and name not in LABELS:
+        size = dirty.shape[-1]
+        LABELS[name] = run.subimages(size, size)[1].reshape(-1)[idx].astype(np.int64) - 1
     del run
     return out, samples
 
@@ -119,7 +126,26 @@ def main():
             for k, key in enumerate(("residual", "model")):
                 a, b = samples[names[i]][k], samples[names[j]][k]
                 pair[key].append(float(np.sqrt(np.mean((a - b) ** 2))) / ref_rms[key])
+    per_sub = None
+    if args.name in LABELS:
+        # tiled: the same distances per subimage (its own samples, over its
+        # own base RMS); tests/test_configs_gpu.py compares the samples of the
+        # subimages whose traces separate from the oracle's with the largest
+        lab = LABELS[args.name]
+        per_sub = {"residual": [], "model": []}
+        for sub in range(int(lab.max()) + 1):
+            sel = lab == sub
+            for k, key in enumerate(("residual", "model")):
+                base_rms = float(np.sqrt(np.mean(samples["base"][k][sel] ** 2)))
+                worst = 0.0
+                for i in range(len(names)):
+                    for j in range(i + 1, len(names)):
+                        a, b = samples[names[i]][k][sel], samples[names[j]][k][sel]
+                        worst = max(worst, float(np.sqrt(np.mean((a - b) ** 2))) /
+                                    max(base_rms, 1e-30))
+                per_sub[key].append(worst)
     out = {"config": args.name, "members": members, "spread": spread,
+           "subimage_sample_rms_distance": per_sub,
            "sample_rms_distance": {k: {"max": max(v, default=0.0),
                                        "mean": float(np.mean(v)) if v else 0.0}
                                    for k, v in pair.items()},
