@@ -163,16 +163,37 @@ __global__ __launch_bounds__(256) void IuwtDecomposeRows(float* i1, float* s2, f
                                                          uint32_t h, int d, int d_next) {
   extern __shared__ float row[];
   const int64_t y = blockIdx.x;
-  for (uint32_t x = threadIdx.x; x < w; x += blockDim.x) {
-    float t[5];
+  // the vertical filter four pixels (one float4 per tap row) at a time, all
+  // five tap rows' loads issued before the sums (w % 4 == 0: the launcher)
+  const float4* s1v = reinterpret_cast<const float4*>(s1);
+  float4* i1v = reinterpret_cast<float4*>(i1);
+  const uint32_t w4 = w / 4;
+  for (uint32_t x4 = threadIdx.x; x4 < w4; x4 += blockDim.x) {
+    float4 t4[5];
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
       const int64_t yy = y + int64_t(d) * (k - 2);
-      t[k] = (yy >= 0 && yy < int64_t(h)) ? s1[size_t(yy) * w + x] : 0.0f;
+      t4[k] = (yy >= 0 && yy < int64_t(h)) ? s1v[size_t(yy) * w4 + x4]
+                                            : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
-    const float v = VerticalValue(t, y, int64_t(h), d);
-    row[x] = v;
-    i1[size_t(y) * w + x] = v;
+    float4 v;
+    {
+      float t[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) t[k] = t4[k].x;
+      v.x = VerticalValue(t, y, int64_t(h), d);
+#pragma unroll
+      for (int k = 0; k < 5; ++k) t[k] = t4[k].y;
+      v.y = VerticalValue(t, y, int64_t(h), d);
+#pragma unroll
+      for (int k = 0; k < 5; ++k) t[k] = t4[k].z;
+      v.z = VerticalValue(t, y, int64_t(h), d);
+#pragma unroll
+      for (int k = 0; k < 5; ++k) t[k] = t4[k].w;
+      v.w = VerticalValue(t, y, int64_t(h), d);
+    }
+    reinterpret_cast<float4*>(row)[x4] = v;
+    i1v[size_t(y) * w4 + x4] = v;
   }
   __syncthreads();
   for (uint32_t x = threadIdx.x; x < w; x += blockDim.x) {
@@ -194,38 +215,41 @@ __global__ __launch_bounds__(256) void IuwtDecomposeRows(float* i1, float* s2, f
   }
 }
 
-// RecomposeRows (one scale of Recompose, iuwt_decomposition.h:121-146 with
-// IuwtDecomposition::convolve, .h:243-261): out_new row y = V_acc(H_acc(out))
-// + coefficients, the H-accumulated rows y + k d made in LDS from out.
-__global__ __launch_bounds__(256) void IuwtRecomposeRows(float* out_new, const float* out,
-                                                         const float* add, uint32_t w,
+// out = lhs - V_d(in), four pixels per thread (w % 4 == 0): the difference
+// pass of the fused decomposition, one float4 per tap row in flight
+__global__ __launch_bounds__(256) void IuwtVerticalDiff4(float* out, const float* in,
+                                                         const float* lhs, uint32_t w,
                                                          uint32_t h, int d) {
-  extern __shared__ float rows[];  // [5][w] H-accumulated rows (0 outside)
-  const int64_t y = blockIdx.x;
-  for (int k = 0; k < 5; ++k) {
-    const int64_t yy = y + int64_t(d) * (k - 2);
-    if (yy < 0 || yy >= int64_t(h)) continue;
-    const float* src = out + size_t(yy) * w;
-    for (uint32_t x = threadIdx.x; x < w; x += blockDim.x) {
-      float acc = 0.0f;
-#pragma unroll
-      for (int j = 0; j < 5; ++j) {
-        const int64_t xx = int64_t(x) + int64_t(d) * (j - 2);
-        if (xx >= 0 && xx < int64_t(w)) acc = __builtin_fmaf(src[xx], IuwtTap(j), acc);
-      }
-      rows[size_t(k) * w + x] = acc;
-    }
-  }
-  __syncthreads();
-  for (uint32_t x = threadIdx.x; x < w; x += blockDim.x) {
-    float acc = 0.0f;
+  const uint32_t w4 = w / 4;
+  const size_t n4 = size_t(w4) * h;
+  const float4* inv = reinterpret_cast<const float4*>(in);
+  for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n4;
+       i += size_t(gridDim.x) * blockDim.x) {
+    const int64_t y = int64_t(i / w4);
+    const size_t x4 = i % w4;
+    float4 t4[5];
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
       const int64_t yy = y + int64_t(d) * (k - 2);
-      if (yy >= 0 && yy < int64_t(h))
-        acc = __builtin_fmaf(rows[size_t(k) * w + x], IuwtTap(k), acc);
+      t4[k] = (yy >= 0 && yy < int64_t(h)) ? inv[size_t(yy) * w4 + x4]
+                                            : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
-    out_new[size_t(y) * w + x] = acc + add[size_t(y) * w + x];
+    const float4 l = reinterpret_cast<const float4*>(lhs)[i];
+    float t[5];
+    float4 o;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) t[k] = t4[k].x;
+    o.x = l.x - VerticalValue(t, y, int64_t(h), d);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) t[k] = t4[k].y;
+    o.y = l.y - VerticalValue(t, y, int64_t(h), d);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) t[k] = t4[k].z;
+    o.z = l.z - VerticalValue(t, y, int64_t(h), d);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) t[k] = t4[k].w;
+    o.w = l.w - VerticalValue(t, y, int64_t(h), d);
+    reinterpret_cast<float4*>(out)[i] = o;
   }
 }
 
@@ -234,10 +258,9 @@ inline bool IuwtFusedOn() {
   const char* e = std::getenv("RDL_IUWT_FUSED");
   return !(e && e[0] == '0');
 }
-// rows of at most this many floats go through LDS (one row per decompose
-// block: 64 KiB at most; five rows per recompose block: 120 KiB at most)
+// rows of at most this many floats go through LDS (one row per block: 64 KiB
+// at most)
 constexpr uint32_t kIuwtFusedMaxWidth = 16384;
-constexpr uint32_t kIuwtFusedMaxWidthRecompose = 6144;
 
 inline unsigned IuwtGrid(size_t n) {
   return unsigned(std::min<size_t>(16384, std::max<size_t>(1, (n + 255) / 256)));
@@ -277,7 +300,9 @@ int rdl_iuwt_decompose(rdl_session* s, float* d_input, float* d_scratch,
   RDL_ARG_CHECK(width >= 1 && height >= 1, "bad size");
   // DecomposeMt (iuwt_decomposition.cc:9-54)
   const size_t n = size_t(width) * height;
-  if (d_input != d_scratch && width <= rdl::kIuwtFusedMaxWidth && rdl::IuwtFusedOn()) {
+  if (d_input != d_scratch && width <= rdl::kIuwtFusedMaxWidth && width % 4 == 0 &&
+      (reinterpret_cast<uintptr_t>(d_input) | reinterpret_cast<uintptr_t>(d_coeffs)) % 16 == 0 &&
+      rdl::IuwtFusedOn()) {
     // fused: per scale one row kernel (i1, s2 = H(i1), next scale's H(i1))
     // and the difference pass; the approximation planes alternate between
     // the largest-scale plane and a scratch plane (no copy), arranged so the
@@ -300,7 +325,12 @@ int rdl_iuwt_decompose(rdl_session* s, float* d_input, float* d_scratch,
             i1, s2, s1[(sc + 1) & 1u], s1[sc & 1u], width, height, d, d_next);
         RDL_HIP_CHECK(hipGetLastError());
       }
-      RDL_TRY(rdl::Vertical(s, d_coeffs + size_t(sc) * n, s2, a, width, height, d));
+      {
+        rdl::ScopedTiming t(s, "iuwt", double(n) * 12.0);
+        rdl::IuwtVerticalDiff4<<<rdl::IuwtGrid(n / 4), 256, 0, s->stream>>>(
+            d_coeffs + size_t(sc) * n, s2, a, width, height, d);
+        RDL_HIP_CHECK(hipGetLastError());
+      }
       a = i1;
     }
     if (!include_largest)
@@ -343,36 +373,6 @@ int rdl_iuwt_recompose(rdl_session* s, const float* d_coeffs, uint32_t width,
   RDL_TRY(s->EnsureScratch(s->iuwt, n * sizeof(float)));
   float* tmp = static_cast<float*>(s->iuwt.ptr);
   int sc = int(n_scales) - 1;
-  if (width <= rdl::kIuwtFusedMaxWidthRecompose && rdl::IuwtFusedOn()) {
-    // fused: one row kernel per scale (out_new = V(H(out)) + coefficients),
-    // alternating between d_out and the scratch plane so the last scale
-    // writes d_out
-    const float* first = d_coeffs + size_t(include_largest ? n_scales : uint32_t(sc)) * n;
-    if (!include_largest) --sc;
-    const int n_pass = sc + 1;
-    // pass k (k = 0 .. n_pass-1, scale sc - k) writes d_out when
-    // n_pass - 1 - k is even; the starting plane goes to the other buffer
-    float* start = (n_pass % 2 == 0) ? d_out : tmp;
-    RDL_HIP_CHECK(hipMemcpyAsync(start, first, n * sizeof(float), hipMemcpyDeviceToDevice,
-                                 s->stream));
-    const float* cur = start;
-    for (int k = 0; sc >= 0; --sc, ++k) {
-      const int d = (1 << (sc + 1)) - 1;
-      float* dst = ((n_pass - 1 - k) % 2 == 0) ? d_out : tmp;
-      static std::once_flag lds_once;
-      std::call_once(lds_once, [] {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&rdl::IuwtRecomposeRows),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  int(5 * rdl::kIuwtFusedMaxWidthRecompose * sizeof(float)));
-      });
-      rdl::ScopedTiming t(s, "iuwt", double(n) * 12.0);
-      rdl::IuwtRecomposeRows<<<height, 256, 5 * width * sizeof(float), s->stream>>>(
-          dst, cur, d_coeffs + size_t(sc) * n, width, height, d);
-      RDL_HIP_CHECK(hipGetLastError());
-      cur = dst;
-    }
-    return RDL_OK;
-  }
   if (include_largest) {
     RDL_HIP_CHECK(hipMemcpyAsync(d_out, d_coeffs + size_t(n_scales) * n,
                                  n * sizeof(float), hipMemcpyDeviceToDevice,

@@ -569,6 +569,9 @@ struct LoopArgs {
   // stores even when every participant is on one XCD (RDL_SUBMINOR_EXCHANGE=agent)
   uint32_t part_stride;
   int32_t agent_exchange;
+  // SubminorLoopTab with one workgroup: the block argmax as ONE 64-bit LDS
+  // atomic max per 16-lane row (RDL_SUBMINOR_ATOMIC=0: the wave slots)
+  int32_t atomic_reduce;
 };
 
 struct LoopResult {
@@ -1807,6 +1810,12 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTab(LoopArgs a) {
   constexpr int SLANES = WAVES <= 8 ? 8 : 16;
   // {key hi, key lo, value bits, -}, parity double-buffered
   __shared__ uint4 slots[2][WAVES];
+  // the atomic form (G == 1): per iteration one 64-bit key cell and the
+  // bits of selection index 0's value, triple-buffered (a cell is cleared
+  // two iterations before its next use, after a barrier every reader of
+  // its last use has passed)
+  __shared__ unsigned long long cells[3];
+  __shared__ uint32_t first_bits[3];
   const uint32_t G = a.n_blocks;
   if (G > 1 && blockIdx.x % a.part_stride != 0u) return;
   const uint32_t rank = G > 1 ? blockIdx.x / a.part_stride : 0u;
@@ -1859,6 +1868,12 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTab(LoopArgs a) {
   bool have = false, diverging = false;
   uint64_t iteration = a.iteration_start;
   const bool tracer = rank == 0 && tid == 0 && a.trace;
+  const bool atomic = G == 1 && a.atomic_reduce != 0;
+  uint32_t cell = 0;  // iteration % 3
+  if (atomic) {
+    if (tid < 3u) cells[tid] = 0ull;
+    LdsBarrier();
+  }
   // the loop's comparisons as integer tests on float bits (see decisions)
   const uint32_t thr_bits = __float_as_uint(a.threshold) & 0x7fffffffu;
   const uint32_t thr_mode = a.threshold != a.threshold        ? 0u
@@ -1933,6 +1948,48 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTab(LoopArgs a) {
       }
     }
     RDL_TPHASE(1)
+    uint32_t gh, gl, gv;
+    if (atomic) {
+      // ---- block winner: the 64-bit key (value word, then the lowest
+      // selection index, then the value's sign bit to rebuild it) as one LDS
+      // atomic max per 16-lane row after a DPP max within the row; the same
+      // total order as the two-level (hi, ~j) reduction below. A key-0 lane
+      // (every item NaN / beyond the slice) holds 0; selection index 0's
+      // value bits stand for the all-zero (and the NaN-at-0) outcome.
+      uint64_t key = 0ull;
+      if (bh != 0u)
+        key = (uint64_t(bh) << 32) | (uint64_t((0x7fffffffu - bj) << 1) | (bv >> 31));
+      uint64_t t;
+      t = DppU64<0xb1>(key);
+      key = t > key ? t : key;
+      t = DppU64<0x4e>(key);
+      key = t > key ? t : key;
+      t = DppU64<0x141>(key);
+      key = t > key ? t : key;
+      t = DppU64<0x140>(key);
+      key = t > key ? t : key;
+      if ((lane & 15u) == 0u && key != 0ull) atomicMax(&cells[cell], (unsigned long long)key);
+      if (tid == 0) first_bits[cell] = __float_as_uint(R[0]);
+      RDL_TPHASE(2)
+      LdsBarrier();
+      RDL_TPHASE(3)
+      const uint64_t k = cells[cell];
+      const uint32_t fb = first_bits[cell];
+      if (tid == 0) cells[cell == 0u ? 2u : cell - 1u] = 0ull;  // used two iterations on
+      cell = cell == 2u ? 0u : cell + 1u;
+      gh = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(k >> 32))));
+      const uint32_t lo = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(k))));
+      const uint32_t fbs = uint32_t(__builtin_amdgcn_readfirstlane(int(fb)));
+      const uint32_t j = 0x7fffffffu - (lo >> 1);
+      gl = gh == 0u ? 0u : ~j;
+      if (gh == 0u || gh == 0xffffffffu) {
+        gv = fbs;  // selection index 0's value (all keys 0, or NaN at index 0)
+      } else if (NEG || neg) {
+        gv = (gh & 0x7fffffffu) | (lo << 31);  // |R| bits, R's sign
+      } else {
+        gv = (gh & 0x80000000u) ? (gh & 0x7fffffffu) : ~gh;  // the key transform inverted
+      }
+    } else {
     // ---- wave winner: DPP max of the keys; the lowest index on exact ties
     const uint32_t mh = MaxU32<64>(bh);
     const uint64_t tie = __ballot(bh == mh);
@@ -1954,7 +2011,7 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTab(LoopArgs a) {
     // ---- block winner over the wave slots
     const uint4 s4 = lane < uint32_t(WAVES) ? slots[par][lane] : make_uint4(0u, 0u, 0u, 0u);
     par ^= 1u;
-    uint32_t gh = MaxU32<SLANES>(s4.x);
+    gh = MaxU32<SLANES>(s4.x);
     {
       const bool mine = lane < uint32_t(WAVES) && s4.x == gh;
       const uint64_t t2 = __ballot(mine);
@@ -1967,8 +2024,8 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTab(LoopArgs a) {
       }
       owner = win;
     }
-    uint32_t gl = uint32_t(__builtin_amdgcn_readlane(int(s4.y), owner));
-    uint32_t gv = uint32_t(__builtin_amdgcn_readlane(int(s4.z), owner));
+    gl = uint32_t(__builtin_amdgcn_readlane(int(s4.y), owner));
+    gv = uint32_t(__builtin_amdgcn_readlane(int(s4.z), owner));
     if (G > 1) {
       // ---- exchange of the participants' winners
       ++epoch;  // 1, 2, ... (granules are zeroed per launch)
@@ -2018,6 +2075,7 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTab(LoopArgs a) {
       gl = uint32_t(__builtin_amdgcn_readlane(int(xl), win));
       gv = uint32_t(__builtin_amdgcn_readlane(int(xv), win));
     }
+    }  // the wave-slot reduction
     RDL_TPHASE(4)
     // ---- identical decisions everywhere (subminor_loop.cc:56-89), on the
     // bit patterns in scalar registers (exact: |x| > t for t >= 0 is the
@@ -3093,6 +3151,8 @@ int SubminorLaunch(rdl_subminor* h, const float* d_residuals, const float* d_psf
   {
     const char* e = std::getenv("RDL_SUBMINOR_EXCHANGE");  // read per run (tests toggle it)
     la.agent_exchange = e && std::strcmp(e, "agent") == 0 ? 1 : 0;
+    const char* at = std::getenv("RDL_SUBMINOR_ATOMIC");  // read per run (A/B in one job)
+    la.atomic_reduce = at && at[0] == '0' ? 0 : 1;
   }
   const uint64_t n_trace = trace_cap;
   (void)h_trace;

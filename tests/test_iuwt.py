@@ -80,10 +80,11 @@ def test_gpu_iuwt_bit_exact(w, h, n, aliased, include_largest):
 @pytest.mark.parametrize("w,h", [(4096, 4096), (1000, 37), (8192, 64)])
 @pytest.mark.parametrize("include_largest", [True, False])
 def test_gpu_iuwt_fused_rows_equal_four_pass(w, h, include_largest):
-    """The fused row kernels (r06: IuwtDecomposeRows / IuwtRecomposeRows, the
-    intermediate row in LDS, approximation planes alternating instead of
-    copied) against the four-pass kernels (RDL_IUWT_FUSED=0), bit for bit, at
-    the C4 size and at widths / heights below the larger spacings."""
+    """The fused decomposition (r06: IuwtDecomposeRows, the intermediate row
+    in LDS, approximation planes alternating instead of copied, float4 tap
+    rows) against the four-pass kernels (RDL_IUWT_FUSED=0), bit for bit, at
+    the C4 size and at widths / heights below the larger spacings; the
+    recomposition is the same kernels either way."""
     from rdl_lib import Session
     n = 6
     img = image(w, h, 77)

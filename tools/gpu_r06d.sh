@@ -34,3 +34,4 @@ echo "rocprof control A (rdl_lib peak) exit $?"
 timeout -k 10 200 rocprofv3 --kernel-trace -d $OUT/prof_ctl_b -o run -- \
   python3 -c "import sys; sys.path.insert(0, '$R'); import __graft_entry__ as g; g.smoke()" > $OUT/prof_ctl_b.out 2>&1
 echo "rocprof control B (smoke) exit $?"
+cd $R && timeout -k 10 300 python -u tools/end_state_spread.py t2k8 --ulp 4 --twopass 0 > $OUT/spread_t2k8.json 2> $OUT/spread_t2k8.err || exit $?
