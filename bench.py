@@ -458,9 +458,9 @@ def iuwt_leg(rd, reps=10):
                                   "fixture's 24-step cap), HIP events on every family"}}
 
 
-def committed_cpu_to_threshold():
+def committed_cpu_to_threshold(pattern="r*_cpu_c2_to_threshold.json"):
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_cpu_c2_to_threshold.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
     if not files:
         return None
     try:
@@ -538,6 +538,9 @@ def main():
     ap.add_argument("--cpu-to-threshold", metavar="OUT_JSON",
                     help="host only: run the CPU oracle to the threshold on C2 (setup "
                          "included), write the JSON and exit")
+    ap.add_argument("--cpu-to-threshold-config", default="c2",
+                    help="the tests/config_problems.py problem of --cpu-to-threshold (c2, "
+                         "h8kt: the headline 8192^2 problem)")
     ap.add_argument("--breakdown", action="store_true", help="per-kernel times to stderr")
     ap.add_argument("--timing-all", action="store_true",
                     help="count every launch of the process (PMC passes, tools/pmc_traffic.py)")
@@ -545,7 +548,7 @@ def main():
     args = ap.parse_args()
 
     if args.cpu_to_threshold:
-        out = cpu_to_threshold("c2", args.cpu_threads or cpu_share())
+        out = cpu_to_threshold(args.cpu_to_threshold_config, args.cpu_threads or cpu_share())
         with open(args.cpu_to_threshold, "w") as f:
             json.dump(out, f, indent=1)
         print(json.dumps(out), flush=True)
@@ -677,6 +680,15 @@ def main():
             r.perform(0)
             return rd.gpu.total_iteration_number(r), time.perf_counter() - t
 
+        # split first: its 16 subimage worker sessions are then made before
+        # the 8-channel unsplit runs' allocations. Made after them (with
+        # --tiled-reference 0, the tiled leg's workers are absent), every
+        # kernel family of this leg ran 1.3x longer on the device (r06:
+        # 23.5 vs 17.9 s of kernel time, 9.0 vs 5.6 s a Perform)
+        print("[bench] joined reference, split (warm-up + 1 step) ...", file=sys.stderr,
+              flush=True)
+        joined_once()
+        (j_comps, j_el), j_amdahl = with_amdahl(rd, joined_once)
         # unsplit: the C3 computation itself (one image set, one GPU)
         su = settings_for(rd, jsize, args.max_iter, args.scales, threshold, 1, 1)
         print("[bench] joined reference, unsplit (warm-up + 1 step) ...", file=sys.stderr,
@@ -724,10 +736,6 @@ def main():
                     "exchange adds exchange_s (one link: a ring; all links: a full mesh) "
                     "unless overlapped. Bit-identical to the unsplit run "
                     "(tests/test_distributed.py::test_channel_sharded_joined_equals_one_process)"}
-        print("[bench] joined reference, split (warm-up + 1 step) ...", file=sys.stderr,
-              flush=True)
-        joined_once()
-        (j_comps, j_el), j_amdahl = with_amdahl(rd, joined_once)
         joined_ref = {"workload": (f"joined{jch}ch-multiscale-{jsize}x{jsize}-{args.scales}"
                                    f"scales-tiled{args.grid}x{args.grid}"),
                       "value": round(j_comps / j_el, 2), "ms_per_step": round(1e3 * j_el, 2),
@@ -982,6 +990,18 @@ def main():
                     ref["wall_clock_to_threshold_s"] / c2_ref["wall_clock_to_threshold_s"], 1)
             ref["measured"] = "committed file (not this job)"
             cpu["to_threshold_c2_committed"] = ref
+        h8k = committed_cpu_to_threshold("r*_cpu_h8k_to_threshold*.json")
+        if h8k is not None:
+            # the headline problem itself to the threshold on the CPU (the
+            # oracle run behind tests/golden/config_h8kt.npz); the GPU side is
+            # this job's DeviceRun leg (`value`)
+            if resident is not None:
+                h8k["gpu_wall_clock_to_threshold_s"] = round(resident["ms_per_step"] / 1e3, 4)
+                h8k["gpu_components"] = resident["components_per_step"]
+                h8k["speedup_wall_clock"] = round(
+                    h8k["wall_clock_to_threshold_s"] / (resident["ms_per_step"] / 1e3), 1)
+            h8k["measured"] = "committed file (not this job)"
+            cpu["to_threshold_h8k_committed"] = h8k
 
     grid = f"-tiled{args.grid}x{args.grid}" if split else ""
     chans = f"joined{args.channels}ch-" if joined else ""

@@ -158,11 +158,22 @@ __global__ __launch_bounds__(256) void IuwtAccumulateVAdd(float* out,
 // rows y + k d of s1 = H_d(a), kept in LDS, then s2 = H_d(i1) for this
 // scale's difference pass and, when d_next > 0, s1' = H_d_next(i1), the
 // next scale's first pass (a_{s+1} = i1).
+// The dispatcher deals workgroups round-robin over the 8 XCDs; a workgroup's
+// row comes from its XCD's contiguous band of rows, so the vertical taps
+// (rows y +- d, y +- 2d) another workgroup of the same XCD read moments
+// earlier are still in that XCD's L2.
+__device__ __forceinline__ int64_t XcdBandRow(uint32_t block, uint32_t h) {
+  const uint32_t band = (h + 7u) / 8u;
+  return int64_t((block % 8u) * band + block / 8u);
+}
+inline unsigned XcdBandBlocks(uint32_t h) { return 8u * ((h + 7u) / 8u); }
+
 __global__ __launch_bounds__(256) void IuwtDecomposeRows(float* i1, float* s2, float* s1_next,
                                                          const float* s1, uint32_t w,
                                                          uint32_t h, int d, int d_next) {
   extern __shared__ float row[];
-  const int64_t y = blockIdx.x;
+  const int64_t y = XcdBandRow(blockIdx.x, h);
+  if (y >= int64_t(h)) return;
   // the vertical filter four pixels (one float4 per tap row) at a time, all
   // five tap rows' loads issued before the sums (w % 4 == 0: the launcher)
   const float4* s1v = reinterpret_cast<const float4*>(s1);
@@ -220,13 +231,13 @@ __global__ __launch_bounds__(256) void IuwtDecomposeRows(float* i1, float* s2, f
 __global__ __launch_bounds__(256) void IuwtVerticalDiff4(float* out, const float* in,
                                                          const float* lhs, uint32_t w,
                                                          uint32_t h, int d) {
+  // one row per workgroup, rows in XCD bands (XcdBandRow)
   const uint32_t w4 = w / 4;
-  const size_t n4 = size_t(w4) * h;
+  const int64_t y = XcdBandRow(blockIdx.x, h);
+  if (y >= int64_t(h)) return;
   const float4* inv = reinterpret_cast<const float4*>(in);
-  for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n4;
-       i += size_t(gridDim.x) * blockDim.x) {
-    const int64_t y = int64_t(i / w4);
-    const size_t x4 = i % w4;
+  for (uint32_t x4 = threadIdx.x; x4 < w4; x4 += blockDim.x) {
+    const size_t i = size_t(y) * w4 + x4;
     float4 t4[5];
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
@@ -321,13 +332,14 @@ int rdl_iuwt_decompose(rdl_session* s, float* d_input, float* d_scratch,
       float* i1 = ((n_scales - 1 - sc) % 2 == 0) ? big : spare;
       {
         rdl::ScopedTiming t(s, "iuwt", double(n) * (d_next ? 16.0 : 12.0));
-        rdl::IuwtDecomposeRows<<<height, 256, width * sizeof(float), s->stream>>>(
+        rdl::IuwtDecomposeRows<<<rdl::XcdBandBlocks(height), 256, width * sizeof(float),
+                                 s->stream>>>(
             i1, s2, s1[(sc + 1) & 1u], s1[sc & 1u], width, height, d, d_next);
         RDL_HIP_CHECK(hipGetLastError());
       }
       {
         rdl::ScopedTiming t(s, "iuwt", double(n) * 12.0);
-        rdl::IuwtVerticalDiff4<<<rdl::IuwtGrid(n / 4), 256, 0, s->stream>>>(
+        rdl::IuwtVerticalDiff4<<<rdl::XcdBandBlocks(height), 256, 0, s->stream>>>(
             d_coeffs + size_t(sc) * n, s2, a, width, height, d);
         RDL_HIP_CHECK(hipGetLastError());
       }

@@ -397,8 +397,20 @@ struct PeakFinish {
 __device__ __forceinline__ void PeakArrive(const PeakFinish& f, uint64_t* lds) {
   __shared__ uint32_t last;
   if (threadIdx.x == 0) {
+#if defined(__gfx950__) || !defined(__HIP_DEVICE_COMPILE__)
+    // gfx950: the vector L1 is write-through, so once vmcnt(0) has retired
+    // the partial's agent-scope store it is in the L2 every workgroup reads
+    // (the loads below bypass L1); the ticket needs no release/acquire
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the partial has landed
     last = atomicAdd(f.ticket, 1u) == gridDim.x - 1u ? 1u : 0u;
+#else
+    // other targets: the C++ memory model's ordering (release of the
+    // partial, acquire of the others' before the last workgroup reads them)
+    last = __hip_atomic_fetch_add(f.ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+                   gridDim.x - 1u
+               ? 1u
+               : 0u;
+#endif
   }
   __syncthreads();
   if (!last) return;

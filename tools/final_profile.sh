@@ -24,7 +24,7 @@ case $PASS in
     mkdir -p $OUT/$PASS
     cd /tmp && export TMPDIR=/tmp
     timeout -k 10 400 rocprofv3 --pmc $COUNTER --kernel-trace -d $OUT/$PASS -o run -- \
-      python3 $R/bench.py --warmup 0 --steps 1 --cpu-outer 0 --tiled-reference 0 --c2-reference 0 --joined-reference 0 --device-resident 0 --timing-all \
+      python3 $R/bench.py --warmup 0 --steps 1 --cpu-outer 0 --tiled-reference 0 --c2-reference 0 --joined-reference 0 --iuwt-reference 0 --device-resident 0 --timing-all \
       --dump-families $OUT/$PASS/fams.json > $OUT/$PASS/bench.json 2> $OUT/$PASS/bench.err ;;
   bench)
     cd $R
