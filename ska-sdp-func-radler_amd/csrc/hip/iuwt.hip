@@ -47,6 +47,16 @@ __device__ __forceinline__ float VerticalValue(const float* t, int64_t y,
   return TapSum<3>(t, {0, 1, 2});
 }
 
+// The dispatcher deals workgroups round-robin over the 8 XCDs; a workgroup's
+// row comes from its XCD's contiguous band of rows, so the vertical taps
+// (rows y +- d, y +- 2d) another workgroup of the same XCD read moments
+// earlier are still in that XCD's L2.
+__device__ __forceinline__ int64_t XcdBandRow(uint32_t block, uint32_t h) {
+  const uint32_t band = (h + 7u) / 8u;
+  return int64_t((block % 8u) * band + block / 8u);
+}
+inline unsigned XcdBandBlocks(uint32_t h) { return 8u * ((h + 7u) / 8u); }
+
 __global__ __launch_bounds__(256) void IuwtHorizontalKernel(float* out,
                                                             const float* in,
                                                             uint32_t w, uint32_t h,
@@ -90,10 +100,11 @@ __global__ __launch_bounds__(256) void IuwtVerticalKernel(float* out,
                                                           const float* lhs,
                                                           uint32_t w, uint32_t h,
                                                           int d) {
-  const size_t n = size_t(w) * h;
-  for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n;
-       i += size_t(gridDim.x) * blockDim.x) {
-    const int64_t y = int64_t(i / w), x = int64_t(i % w);
+  // one row per workgroup, rows in XCD bands (XcdBandRow)
+  const int64_t y = XcdBandRow(blockIdx.x, h);
+  if (y >= int64_t(h)) return;
+  for (uint32_t x = threadIdx.x; x < w; x += blockDim.x) {
+    const size_t i = size_t(y) * w + x;
     float t[5];
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
@@ -131,10 +142,11 @@ __global__ __launch_bounds__(256) void IuwtAccumulateVAdd(float* out,
                                                           const float* add,
                                                           uint32_t w, uint32_t h,
                                                           int d) {
-  const size_t n = size_t(w) * h;
-  for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n;
-       i += size_t(gridDim.x) * blockDim.x) {
-    const int64_t y = int64_t(i / w), x = int64_t(i % w);
+  // one row per workgroup, rows in XCD bands (XcdBandRow)
+  const int64_t y = XcdBandRow(blockIdx.x, h);
+  if (y >= int64_t(h)) return;
+  for (uint32_t x = threadIdx.x; x < w; x += blockDim.x) {
+    const size_t i = size_t(y) * w + x;
     float acc = 0.0f;
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
@@ -158,16 +170,6 @@ __global__ __launch_bounds__(256) void IuwtAccumulateVAdd(float* out,
 // rows y + k d of s1 = H_d(a), kept in LDS, then s2 = H_d(i1) for this
 // scale's difference pass and, when d_next > 0, s1' = H_d_next(i1), the
 // next scale's first pass (a_{s+1} = i1).
-// The dispatcher deals workgroups round-robin over the 8 XCDs; a workgroup's
-// row comes from its XCD's contiguous band of rows, so the vertical taps
-// (rows y +- d, y +- 2d) another workgroup of the same XCD read moments
-// earlier are still in that XCD's L2.
-__device__ __forceinline__ int64_t XcdBandRow(uint32_t block, uint32_t h) {
-  const uint32_t band = (h + 7u) / 8u;
-  return int64_t((block % 8u) * band + block / 8u);
-}
-inline unsigned XcdBandBlocks(uint32_t h) { return 8u * ((h + 7u) / 8u); }
-
 __global__ __launch_bounds__(256) void IuwtDecomposeRows(float* i1, float* s2, float* s1_next,
                                                          const float* s1, uint32_t w,
                                                          uint32_t h, int d, int d_next) {
@@ -293,8 +295,7 @@ int Horizontal(rdl_session* s, float* out, const float* in, uint32_t w, uint32_t
 int Vertical(rdl_session* s, float* out, const float* in, const float* lhs,
              uint32_t w, uint32_t h, int d) {
   ScopedTiming t(s, "iuwt", double(w) * h * (lhs ? 12.0 : 8.0));
-  IuwtVerticalKernel<<<IuwtGrid(size_t(w) * h), 256, 0, s->stream>>>(out, in, lhs, w,
-                                                                      h, d);
+  IuwtVerticalKernel<<<XcdBandBlocks(h), 256, 0, s->stream>>>(out, in, lhs, w, h, d);
   RDL_HIP_CHECK(hipGetLastError());
   return RDL_OK;
 }
@@ -400,7 +401,7 @@ int rdl_iuwt_recompose(rdl_session* s, const float* d_coeffs, uint32_t width,
       rdl::ScopedTiming t(s, "iuwt", double(n) * 20.0);
       rdl::IuwtAccumulateH<<<rdl::IuwtGrid(n), 256, 0, s->stream>>>(tmp, d_out, width,
                                                                   height, d);
-      rdl::IuwtAccumulateVAdd<<<rdl::IuwtGrid(n), 256, 0, s->stream>>>(
+      rdl::IuwtAccumulateVAdd<<<rdl::XcdBandBlocks(height), 256, 0, s->stream>>>(
           d_out, tmp, d_coeffs + size_t(sc) * n, width, height, d);
     }
     RDL_HIP_CHECK(hipGetLastError());

@@ -23,7 +23,10 @@ struct BoxArgs {
   int allow_negative;
 };
 
-template <bool kVec>
+// kFinish: the last workgroup finishes the search (PeakArrive); without it
+// the kernel carries none of that code (the two-launch form's register and
+// LDS footprint)
+template <bool kVec, bool kFinish>
 __global__ __launch_bounds__(256) void FindPeakPartial(BoxArgs a,
                                                        uint64_t* partials, PeakFinish f) {
   __shared__ uint64_t lds[16];
@@ -59,13 +62,14 @@ __global__ __launch_bounds__(256) void FindPeakPartial(BoxArgs a,
     }
   }
   best = BlockMaxU64(best, lds);
-  if (!f.ticket) {
+  if constexpr (!kFinish) {
     if (threadIdx.x == 0) partials[blockIdx.x] = best;
-    return;
+  } else {
+    if (threadIdx.x == 0)
+      __hip_atomic_store(partials + blockIdx.x, best, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    PeakArrive(f, lds);
   }
-  if (threadIdx.x == 0)
-    __hip_atomic_store(partials + blockIdx.x, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  PeakArrive(f, lds);
 }
 
 __global__ __launch_bounds__(1024) void FindPeakFinal(
@@ -180,9 +184,15 @@ int LaunchFindPeak(rdl_session* s, const float* d_image, uint32_t width,
     if (rows == 0) {
       RDL_HIP_CHECK(hipMemsetAsync(partials, 0, sizeof(uint64_t), s->stream));
     } else if (vec) {
-      FindPeakPartial<true><<<blocks, 256, 0, s->stream>>>(a, partials, f);
+      if (f.ticket)
+        FindPeakPartial<true, true><<<blocks, 256, 0, s->stream>>>(a, partials, f);
+      else
+        FindPeakPartial<true, false><<<blocks, 256, 0, s->stream>>>(a, partials, f);
     } else {
-      FindPeakPartial<false><<<blocks, 256, 0, s->stream>>>(a, partials, f);
+      if (f.ticket)
+        FindPeakPartial<false, true><<<blocks, 256, 0, s->stream>>>(a, partials, f);
+      else
+        FindPeakPartial<false, false><<<blocks, 256, 0, s->stream>>>(a, partials, f);
     }
     if (!f.ticket)
       FindPeakFinal<<<1, 1024, 0, s->stream>>>(

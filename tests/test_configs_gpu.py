@@ -396,7 +396,8 @@ def _diverged_subimage_samples(name, fx, residual, model, sample_labels, identic
     path = os.path.normpath(os.path.join(os.path.dirname(GOLDEN), "..", "profiles",
                                          f"r06_end_state_spread_{name}.json"))
     if not os.path.exists(path):
-        pytest.skip(f"{path} not measured")
+        print(f"{name}: {path} not measured: the separated subimages' samples are not compared")
+        return
     per_sub = json.load(open(path))["subimage_sample_rms_distance"]
     idx = sample_index(residual.shape[-1] * residual.shape[-2])
     lab = sample_labels.astype(np.int64) - 1

@@ -10,7 +10,8 @@ OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 T="--timeout 900 --timeout-method thread -p no:cacheprovider"
 timeout -k 10 900 python -u -m pytest tests/test_gpu_kernels.py tests/test_multiscale_gpu.py \
-  tests/test_deferred_result.py -m gpu -q -x $T > $OUT/tests_kernels.log 2>&1
+  tests/test_deferred_result.py tests/test_iuwt.py tests/test_iuwt_algorithm.py -m gpu -q -x $T \
+  > $OUT/tests_kernels.log 2>&1
 rc=$?; tail -3 $OUT/tests_kernels.log; [ $rc -le 1 ] || exit $rc
 timeout -k 10 900 python -u -m pytest tests/test_configs_gpu.py -k "c2_multi or h8k_headline or c3 or p8k" -m gpu -v -s $T \
   > $OUT/tests_configs.log 2>&1
@@ -23,11 +24,6 @@ python tools/subminor_stats.py $OUT/trace1.err --last-iterations 129505 > $OUT/s
 RDL_ZERO_COPY=0 RDL_PEAK_FINISH=0 RDL_TABLE_ZERO=0 RDL_SEL_COUNT_COPY=1 timeout -k 10 300 \
   python -u tools/bench_legs.py joined_split --reps 2 > $OUT/legs_alltog.jsonl 2> $OUT/legs_alltog.err || exit $?
 timeout -k 10 300 python -u tools/bench_legs.py joined_split --reps 2 > $OUT/legs_default.jsonl 2> $OUT/legs_default.err || exit $?
-if [ ! -f profiles/r06_end_state_spread_c5.json ]; then
-  timeout -k 10 900 python -u tools/end_state_spread.py c5 --ulp 3 --twopass 0 \
-    > $OUT/spread_c5.json 2> $OUT/spread_c5.err || exit $?
-  cp $OUT/spread_c5.json profiles/r06_end_state_spread_c5.json
-fi
-timeout -k 10 1200 python -u -m pytest tests/test_configs_gpu.py -k "c5 or t2k8 or c2_to_threshold" -m gpu -v -s $T \
-  > $OUT/tests_tiled.log 2>&1
-rc=$?; tail -3 $OUT/tests_tiled.log; [ $rc -le 1 ] || exit $rc
+RDL_PEAK_FINISH=0 timeout -k 10 300 python -u tools/bench_legs.py joined_split --reps 2 > $OUT/legs_nofinish.jsonl 2> $OUT/legs_nofinish.err || exit $?
+timeout -k 10 300 python -u bench.py --steps 1 --warmup 1 --cpu-outer 0 --tiled-reference 0 \
+  --joined-reference 0 --c2-reference 0 --device-resident 0 > $OUT/bench_c4.json 2> $OUT/bench_c4.err || exit $?
