@@ -1810,11 +1810,10 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTab(LoopArgs a) {
   constexpr int SLANES = WAVES <= 8 ? 8 : 16;
   // {key hi, key lo, value bits, -}, parity double-buffered
   __shared__ uint4 slots[2][WAVES];
-  // the atomic form: per iteration one 64-bit key cell (the block winner;
-  // with G > 1 participants the exchange follows) and the bits of the
-  // block's first selected value, triple-buffered (a cell is cleared two
-  // iterations before its next use, after a barrier every reader of its
-  // last use has passed)
+  // the atomic form (G == 1): per iteration one 64-bit key cell and the
+  // bits of selection index 0's value, triple-buffered (a cell is cleared
+  // two iterations before its next use, after a barrier every reader of
+  // its last use has passed)
   __shared__ unsigned long long cells[3];
   __shared__ uint32_t first_bits[3];
   const uint32_t G = a.n_blocks;
@@ -1869,7 +1868,7 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTab(LoopArgs a) {
   bool have = false, diverging = false;
   uint64_t iteration = a.iteration_start;
   const bool tracer = rank == 0 && tid == 0 && a.trace;
-  const bool atomic = a.atomic_reduce != 0;
+  const bool atomic = G == 1 && a.atomic_reduce != 0;
   uint32_t cell = 0;  // iteration % 3
   if (atomic) {
     if (tid < 3u) cells[tid] = 0ull;
@@ -1955,9 +1954,8 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTab(LoopArgs a) {
       // selection index, then the value's sign bit to rebuild it) as one LDS
       // atomic max per 16-lane row after a DPP max within the row; the same
       // total order as the two-level (hi, ~j) reduction below. A key-0 lane
-      // (every item NaN / beyond the slice) holds 0; the block's first
-      // selected value (thread 0's item 0) stands for the all-zero outcome,
-      // as the wave-slot form's lane-0 value does (and for NaN at index 0).
+      // (every item NaN / beyond the slice) holds 0; selection index 0's
+      // value bits stand for the all-zero (and the NaN-at-0) outcome.
       uint64_t key = 0ull;
       if (bh != 0u)
         key = (uint64_t(bh) << 32) | (uint64_t((0x7fffffffu - bj) << 1) | (bv >> 31));
@@ -2028,7 +2026,6 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTab(LoopArgs a) {
     }
     gl = uint32_t(__builtin_amdgcn_readlane(int(s4.y), owner));
     gv = uint32_t(__builtin_amdgcn_readlane(int(s4.z), owner));
-    }  // the wave-slot reduction
     if (G > 1) {
       // ---- exchange of the participants' winners
       ++epoch;  // 1, 2, ... (granules are zeroed per launch)
@@ -2078,6 +2075,7 @@ __global__ __launch_bounds__(THREADS) void SubminorLoopTab(LoopArgs a) {
       gl = uint32_t(__builtin_amdgcn_readlane(int(xl), win));
       gv = uint32_t(__builtin_amdgcn_readlane(int(xv), win));
     }
+    }  // the wave-slot reduction
     RDL_TPHASE(4)
     // ---- identical decisions everywhere (subminor_loop.cc:56-89), on the
     // bit patterns in scalar registers (exact: |x| > t for t >= 0 is the
