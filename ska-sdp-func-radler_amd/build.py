@@ -69,6 +69,14 @@ def compile_all(jobs, items):
         raise RuntimeError("\n".join(errors))
 
 
+def link(cmd_prefix, out, rest):
+    """Link to a temporary name, then rename over `out` (atomic): a copy of the
+    tree taken while a build runs never holds a half-written library."""
+    tmp = out + ".tmp"
+    run([*cmd_prefix, "-o", tmp, *rest])
+    os.replace(tmp, out)
+
+
 def build(jobs=8, verbose=False):
     os.makedirs(BUILD, exist_ok=True)
     os.makedirs(LIB, exist_ok=True)
@@ -85,8 +93,8 @@ def build(jobs=8, verbose=False):
     compile_all(jobs, items)
     hip_so = os.path.join(LIB, "librdl_hip.so")
     if items or not os.path.exists(hip_so):
-        run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", hip_so, *hip_objs,
-             f"-L{ROCM}/lib", "-lrocfft", "-lrccl", f"-Wl,-rpath,{ROCM}/lib"])
+        link([HIPCC, "-shared", f"--offload-arch={ARCH}"], hip_so,
+             [*hip_objs, f"-L{ROCM}/lib", "-lrocfft", "-lrccl", f"-Wl,-rpath,{ROCM}/lib"])
 
     # ---- libradler_amd.so (host C++ mirror of the radler API)
     host_srcs = sorted(glob.glob(os.path.join(CSRC, "host", "*.cc")))
@@ -99,8 +107,8 @@ def build(jobs=8, verbose=False):
     compile_all(jobs, items)
     host_so = os.path.join(LIB, "libradler_amd.so")
     if host_objs and (items or stale(host_so, [hip_so], 0.0)):
-        run([CXX, "-shared", "-pthread", "-o", host_so, *host_objs, f"-L{LIB}",
-             "-lrdl_hip", "-Wl,-rpath,$ORIGIN"])
+        link([CXX, "-shared", "-pthread"], host_so,
+             [*host_objs, f"-L{LIB}", "-lrdl_hip", "-Wl,-rpath,$ORIGIN"])
 
     # ---- radler pybind11 module
     py_srcs = sorted(glob.glob(os.path.join(CSRC, "python", "*.cc")))
@@ -118,8 +126,8 @@ def build(jobs=8, verbose=False):
                 items.append((obj, [CXX, *py_flags, "-c", src, "-o", obj]))
         compile_all(jobs, items)
         if items or stale(mod, [host_so], 0.0):
-            run([CXX, "-shared", "-pthread", "-o", mod, *py_objs, f"-L{LIB}",
-                 "-lradler_amd", "-lrdl_hip", "-Wl,-rpath,$ORIGIN/lib"])
+            link([CXX, "-shared", "-pthread"], mod,
+                 [*py_objs, f"-L{LIB}", "-lradler_amd", "-lrdl_hip", "-Wl,-rpath,$ORIGIN/lib"])
     return hip_so
 
 

@@ -170,9 +170,12 @@ __global__ __launch_bounds__(256) void IuwtAccumulateVAdd(float* out,
 // rows y + k d of s1 = H_d(a), kept in LDS, then s2 = H_d(i1) for this
 // scale's difference pass and, when d_next > 0, s1' = H_d_next(i1), the
 // next scale's first pass (a_{s+1} = i1).
-__global__ __launch_bounds__(256) void IuwtDecomposeRows(float* i1, float* s2, float* s1_next,
-                                                         const float* s1, uint32_t w,
-                                                         uint32_t h, int d, int d_next) {
+__global__ __launch_bounds__(256) void IuwtDecomposeRows(float* __restrict__ i1,
+                                                         float* __restrict__ s2,
+                                                         float* __restrict__ s1_next,
+                                                         const float* __restrict__ s1,
+                                                         uint32_t w, uint32_t h, int d,
+                                                         int d_next) {
   extern __shared__ float row[];
   const int64_t y = XcdBandRow(blockIdx.x, h);
   if (y >= int64_t(h)) return;
@@ -181,6 +184,9 @@ __global__ __launch_bounds__(256) void IuwtDecomposeRows(float* i1, float* s2, f
   const float4* s1v = reinterpret_cast<const float4*>(s1);
   float4* i1v = reinterpret_cast<float4*>(i1);
   const uint32_t w4 = w / 4;
+  // (restrict pointers and unrolling: every tap row's load of the next
+  // float4s issues before this one's sums and stores)
+#pragma unroll 4
   for (uint32_t x4 = threadIdx.x; x4 < w4; x4 += blockDim.x) {
     float4 t4[5];
 #pragma unroll
@@ -230,14 +236,16 @@ __global__ __launch_bounds__(256) void IuwtDecomposeRows(float* i1, float* s2, f
 
 // out = lhs - V_d(in), four pixels per thread (w % 4 == 0): the difference
 // pass of the fused decomposition, one float4 per tap row in flight
-__global__ __launch_bounds__(256) void IuwtVerticalDiff4(float* out, const float* in,
-                                                         const float* lhs, uint32_t w,
-                                                         uint32_t h, int d) {
+__global__ __launch_bounds__(256) void IuwtVerticalDiff4(float* __restrict__ out,
+                                                         const float* __restrict__ in,
+                                                         const float* __restrict__ lhs,
+                                                         uint32_t w, uint32_t h, int d) {
   // one row per workgroup, rows in XCD bands (XcdBandRow)
   const uint32_t w4 = w / 4;
   const int64_t y = XcdBandRow(blockIdx.x, h);
   if (y >= int64_t(h)) return;
   const float4* inv = reinterpret_cast<const float4*>(in);
+#pragma unroll 4
   for (uint32_t x4 = threadIdx.x; x4 < w4; x4 += blockDim.x) {
     const size_t i = size_t(y) * w4 + x4;
     float4 t4[5];
