@@ -77,20 +77,25 @@ def test_gpu_iuwt_bit_exact(w, h, n, aliased, include_largest):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("w,h", [(4096, 4096), (1000, 37), (8192, 64)])
+@pytest.mark.parametrize("w,h,n", [(4096, 4096, 6), (1000, 37, 6), (8192, 64, 6),
+                                   (260, 300, 7), (2048, 1500, 8)])
 @pytest.mark.parametrize("include_largest", [True, False])
-def test_gpu_iuwt_fused_rows_equal_four_pass(w, h, include_largest):
-    """The fused decomposition (r06: IuwtDecomposeRows, the intermediate row
-    in LDS, approximation planes alternating instead of copied, float4 tap
-    rows) against the four-pass kernels (RDL_IUWT_FUSED=0), bit for bit, at
-    the C4 size and at widths / heights below the larger spacings; the
-    recomposition is the same kernels either way."""
+@pytest.mark.parametrize("mode", ["2", "3", "1"])
+def test_gpu_iuwt_fused_equal_four_pass(w, h, n, include_largest, mode):
+    """The fused kernels against the four-pass kernels (RDL_IUWT_FUSED=0),
+    bit for bit: mode 2 (the default) the fused row decomposition
+    (IuwtDecomposeRows, the intermediate row in LDS) and the row-chain
+    recomposition (IuwtRecomposeChain: one launch per scale, five filtered
+    rows per chain in LDS), mode 3 the row chains for the decomposition too
+    (IuwtDecomposeChain), mode 1 the fused rows with the four-pass
+    recomposition; at the C4 size, at
+    heights and widths below the larger spacings (d = 63, 127, 255 against 37,
+    64, 260 and 300 rows) and with partial column strips."""
     from rdl_lib import Session
-    n = 6
     img = image(w, h, 77)
     s = Session(0)
     outs = []
-    for fused in ("1", "0"):
+    for fused in (mode, "0"):
         os.environ["RDL_IUWT_FUSED"] = fused
         try:
             d_in, d_scratch = s.array(img), s.array(shape=(h, w))
@@ -106,6 +111,37 @@ def test_gpu_iuwt_fused_rows_equal_four_pass(w, h, include_largest):
         finally:
             del os.environ["RDL_IUWT_FUSED"]
     s.close()
-    assert np.array_equal(bits(outs[0][0]), bits(outs[1][0]))
+    for k in range(n + 1):
+        assert np.array_equal(bits(outs[0][0][k]), bits(outs[1][0][k])), k
     assert np.array_equal(bits(outs[0][1]), bits(outs[1][1]))
     assert np.array_equal(bits(outs[0][2]), bits(img))  # the input is not written
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,h,n", [(4096, 512, 6), (1000, 37, 6), (260, 300, 7), (64, 64, 3)])
+def test_gpu_iuwt_aliased_recurrences_equal_row_kernel(w, h, n):
+    """The aliased decomposition (input as its own scratch, as the IUWT
+    deconvolution calls it): its first horizontal pass is a recursive
+    in-place filter. The recurrence kernel (IuwtHorizontalInPlaceChains, one
+    thread per row and residue, taps in registers) against the
+    one-thread-per-row kernel (RDL_IUWT_FUSED=0), bit for bit, including the
+    overwritten input."""
+    from rdl_lib import Session
+    img = image(w, h, 91)
+    s = Session(0)
+    outs = []
+    for fused in ("2", "0"):
+        os.environ["RDL_IUWT_FUSED"] = fused
+        try:
+            d_in = s.array(img)
+            d_coeffs = s.array(shape=(n + 1, h, w))
+            s.rdl.rdl_iuwt_decompose(s.h, d_in.vp, d_in.vp, w, h, n, d_coeffs.vp, 0)
+            outs.append((d_coeffs.get(), d_in.get()))
+            for x in (d_in, d_coeffs):
+                x.free()
+        finally:
+            del os.environ["RDL_IUWT_FUSED"]
+    s.close()
+    for k in range(n + 1):
+        assert np.array_equal(bits(outs[0][0][k]), bits(outs[1][0][k])), k
+    assert np.array_equal(bits(outs[0][1]), bits(outs[1][1]))
