@@ -71,7 +71,8 @@ struct FastSteps {
  * for pass p (span NS = product of the earlier radices, M = n / (NS R)),
  * entries W_n^{k (q+1) M} at [offset_p + q NS + k], q < R - 1, k < NS;
  * float or double complex, computed in long double. hipMalloc'ed. */
-int MakePassTable(uint32_t n, const RadixList& radix, bool f64, void** out);
+int MakePassTable(uint32_t n, const RadixList& radix, bool f64, void** out,
+                  hipStream_t stream);
 
 const FastColumns* FindFastColumns(uint32_t n, bool f64);
 const FastSteps* FindFastSteps(uint32_t n);
@@ -91,7 +92,7 @@ int FastScalesLaunch(rdl_session* s, const FastSteps* p, const void* in, const v
 int FastStepAInvLaunch(rdl_session* s, const FastSteps* p, const void* in, void* out,
                        const void* ptw_a, uint32_t n_cols);
 /* cos(2 pi j / n), j < n, double (long double on the host) */
-int MakeCosTable(uint32_t n, void** out);
+int MakeCosTable(uint32_t n, void** out, hipStream_t stream);
 /* the real spectrum of a symmetric n x n kernel (n odd) placed at the origin
  * of a w x h plane, float, tiled; a_scratch: (n / 2 + 1) x (w / 2 + 1) doubles */
 int RealKernelLaunch(rdl_session* s, const float* shape, uint32_t n, uint32_t w, uint32_t h,
@@ -136,7 +137,7 @@ int FastRowsForwardLaunch(rdl_session* s, const FastRows* p, const float* in, vo
                           const uint32_t* n_rows, int tiled = 0, const void* twd = nullptr,
                           int all_rows = -1);
 /* the two-level double twiddle base of length `base` (ff::TwdLds layout) */
-int MakeTwiddleBase(uint32_t base, void** out);
+int MakeTwiddleBase(uint32_t base, void** out, hipStream_t stream);
 /* float64 convolution columns (mode 1: forward, x K x s, inverse; row-major
  * input and output) with LDS twiddles and a register-resident K multiply
  * (ff::ColumnsConvD); nullptr where no plan exists or RDL_FFT_CONVD=0. tw:

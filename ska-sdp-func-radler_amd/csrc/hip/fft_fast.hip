@@ -2233,7 +2233,7 @@ int FastRowsForwardLaunch(rdl_session* s, const FastRows* p, const float* in, vo
   return RDL_OK;
 }
 
-int MakeTwiddleBase(uint32_t base, void** out) {
+int MakeTwiddleBase(uint32_t base, void** out, hipStream_t stream) {
   // W_base^{64 i} for i < base / 64, then W_base^i for i < 64, in double
   std::vector<double> host;
   auto put = [&](uint64_t e) {
@@ -2245,8 +2245,7 @@ int MakeTwiddleBase(uint32_t base, void** out) {
   for (uint32_t i = 0; i < base / ff::kTwdLo; ++i) put(uint64_t(i) * ff::kTwdLo);
   for (uint32_t i = 0; i < ff::kTwdLo; ++i) put(i);
   RDL_HIP_CHECK(rdl::DevMalloc(out, host.size() * sizeof(double)));
-  RDL_HIP_CHECK(hipMemcpy(*out, host.data(), host.size() * sizeof(double),
-                          hipMemcpyHostToDevice));
+  RDL_HIP_CHECK(UploadSync(*out, host.data(), host.size() * sizeof(double), stream));
   return RDL_OK;
 }
 
@@ -2305,14 +2304,13 @@ int FastStepAInvLaunch(rdl_session* s, const FastSteps* p, const void* in, void*
   return RDL_OK;
 }
 
-int MakeCosTable(uint32_t n, void** out) {
+int MakeCosTable(uint32_t n, void** out, hipStream_t stream) {
   std::vector<double> host(n);
   for (uint32_t j = 0; j < n; ++j)
     host[j] = double(std::cos(2.0L * 3.14159265358979323846264338327950288L *
                               (long double)j / n));
   RDL_HIP_CHECK(rdl::DevMalloc(out, host.size() * sizeof(double)));
-  RDL_HIP_CHECK(hipMemcpy(*out, host.data(), host.size() * sizeof(double),
-                          hipMemcpyHostToDevice));
+  RDL_HIP_CHECK(UploadSync(*out, host.data(), host.size() * sizeof(double), stream));
   return RDL_OK;
 }
 
@@ -2332,7 +2330,8 @@ int RealKernelLaunch(rdl_session* s, const float* shape, uint32_t n, uint32_t w,
   return RDL_OK;
 }
 
-int MakePassTable(uint32_t n, const RadixList& radix, bool f64, void** out) {
+int MakePassTable(uint32_t n, const RadixList& radix, bool f64, void** out,
+                  hipStream_t stream) {
   std::vector<double> re, im;
   uint32_t ns = 1;
   for (uint32_t p = 0; p < radix.n; ++p) {
@@ -2361,7 +2360,7 @@ int MakePassTable(uint32_t n, const RadixList& radix, bool f64, void** out) {
     }
   }
   RDL_HIP_CHECK(rdl::DevMalloc(out, host.size()));
-  RDL_HIP_CHECK(hipMemcpy(*out, host.data(), host.size(), hipMemcpyHostToDevice));
+  RDL_HIP_CHECK(UploadSync(*out, host.data(), host.size(), stream));
   return RDL_OK;
 }
 

@@ -566,7 +566,7 @@ int MakePlan(rdl_conv* c, uint32_t n, bool f64, rdl::LdsPlan* plan, void** tw) {
     }
   }
   RDL_HIP_CHECK(rdl::DevMalloc(tw, host.size()));
-  RDL_HIP_CHECK(hipMemcpy(*tw, host.data(), host.size(), hipMemcpyHostToDevice));
+  RDL_HIP_CHECK(rdl::UploadSync(*tw, host.data(), host.size(), c->s->stream));
   plan->tw = *tw;
   (void)c;
   return RDL_OK;
@@ -911,14 +911,14 @@ int rdl_conv_create_ex(rdl_session* s, uint32_t width, uint32_t height, int f64,
       c->tiled = c->steps != nullptr;
     }
     if (c->fast_rows)
-      RDL_TRY(rdl::MakePassTable(width / 2, c->fast_rows->radix, c->f64, &c->ptw_row));
+      RDL_TRY(rdl::MakePassTable(width / 2, c->fast_rows->radix, c->f64, &c->ptw_row, c->s->stream));
     if (c->fast_rows && c->fast_rows->inverse_lt)
-      RDL_TRY(rdl::MakeTwiddleBase(width, &c->twd_row));
+      RDL_TRY(rdl::MakeTwiddleBase(width, &c->twd_row, c->s->stream));
     if (c->fast_cols)
-      RDL_TRY(rdl::MakePassTable(height, c->fast_cols->radix, c->f64, &c->ptw_col));
+      RDL_TRY(rdl::MakePassTable(height, c->fast_cols->radix, c->f64, &c->ptw_col, c->s->stream));
     if (c->steps) {
-      RDL_TRY(rdl::MakePassTable(c->steps->n1, c->steps->radix_a, false, &c->ptw_a));
-      RDL_TRY(rdl::MakePassTable(c->steps->n2, c->steps->radix_b, false, &c->ptw_b));
+      RDL_TRY(rdl::MakePassTable(c->steps->n1, c->steps->radix_a, false, &c->ptw_a, c->s->stream));
+      RDL_TRY(rdl::MakePassTable(c->steps->n2, c->steps->radix_b, false, &c->ptw_b, c->s->stream));
     }
   }
   if (want_split && can_split) {
@@ -1271,8 +1271,8 @@ int rdl_conv_real_kernel(rdl_conv* c, const float* h_shape, uint32_t n, void* d_
                     "rdl_conv_real_kernel: the kernel is not symmetric in x and y");
     }
   rdl_session* s = c->s;
-  if (!c->cos_w) RDL_TRY(rdl::MakeCosTable(c->width, &c->cos_w));
-  if (!c->cos_h) RDL_TRY(rdl::MakeCosTable(c->height, &c->cos_h));
+  if (!c->cos_w) RDL_TRY(rdl::MakeCosTable(c->width, &c->cos_w, c->s->stream));
+  if (!c->cos_h) RDL_TRY(rdl::MakeCosTable(c->height, &c->cos_h, c->s->stream));
   const size_t shape_bytes = size_t(n) * n * sizeof(float);
   RDL_TRY(s->EnsureScratch(s->kernel, shape_bytes));
   RDL_HIP_CHECK(hipMemcpyAsync(s->kernel.ptr, h_shape, shape_bytes, hipMemcpyHostToDevice,

@@ -93,6 +93,15 @@ inline hipError_t HostFree(void* p) {
   UntrackBlock(p);
   return hipHostFree(p);
 }
+// A host->device upload on `stream`, waited for: never the null stream.
+// Synchronous null-stream calls (hipMemset / hipMemcpy) made once per
+// session left the 16-stream subimage pool ~21 % slower for the rest of the
+// process (r06 bisection of r05's split joined regression).
+inline hipError_t UploadSync(void* d, const void* h, size_t bytes, hipStream_t stream) {
+  hipError_t e = hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream);
+  if (e != hipSuccess) return e;
+  return hipStreamSynchronize(stream);
+}
 // Coherent pinned host memory the device writes directly (zero-copy): the
 // results a host waits for (peaks, selection counts, loop results) are
 // stored there by the kernel that makes them, so reading one back costs a

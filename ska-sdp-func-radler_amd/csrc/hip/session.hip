@@ -345,6 +345,62 @@ int rdl_device_count(int* count) {
   return RDL_OK;
 }
 
+namespace rdl {
+// Streams come from a per-device pool created with the device's first
+// session (RDL_STREAM_POOL streams, default 40; 0: one fresh stream per
+// request, the earlier behaviour). HIP binds a stream to one of its few
+// hardware queues (GPU_MAX_HW_QUEUES, 4) when the stream is created; the
+// subimage pool's 16 worker sessions created after a long run of another
+// session measured 1.3-2x slower per pass than the same workers created
+// early (r06: bench_legs.py joined,joined_split 9.4 s against 4.7 s), so
+// every session's streams are created together, up front, in one order.
+std::mutex g_stream_mutex;
+std::map<int, std::vector<hipStream_t>> g_stream_free;  // device -> FIFO
+std::map<int, bool> g_stream_made;
+int StreamPoolSize() {
+  const char* e = std::getenv("RDL_STREAM_POOL");
+  return e ? std::max(0, std::atoi(e)) : 40;
+}
+int TakeStream(int device, hipStream_t* out) {
+  const std::lock_guard<std::mutex> lock(g_stream_mutex);
+  auto& v = g_stream_free[device];
+  if (!g_stream_made[device]) {
+    g_stream_made[device] = true;
+    for (int i = 0, n = StreamPoolSize(); i < n; ++i) {
+      hipStream_t st = nullptr;
+      RDL_HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+      v.push_back(st);
+    }
+  }
+  if (v.empty()) {
+    RDL_HIP_CHECK(hipStreamCreateWithFlags(out, hipStreamNonBlocking));
+    return RDL_OK;
+  }
+  *out = v.front();
+  v.erase(v.begin());
+  return RDL_OK;
+}
+// back to the pool (idle: the caller synchronized it), or destroyed
+void GiveStream(int device, hipStream_t st) {
+  if (!st) return;
+  if (StreamPoolSize() == 0) {
+    (void)hipStreamDestroy(st);
+    return;
+  }
+  (void)hipStreamSynchronize(st);
+  const std::lock_guard<std::mutex> lock(g_stream_mutex);
+  g_stream_free[device].push_back(st);
+}
+void DestroyStreamPools() {
+  const std::lock_guard<std::mutex> lock(g_stream_mutex);
+  for (auto& [device, v] : g_stream_free) {
+    (void)hipSetDevice(device);
+    for (hipStream_t st : v) (void)hipStreamDestroy(st);
+    v.clear();
+  }
+}
+}  // namespace rdl
+
 int rdl_session_create(int device, rdl_session** out) {
   RDL_ARG_CHECK(out, "out is NULL");
   RDL_ARG_CHECK(!rdl::ShutDown(), "rdl_shutdown has run");
@@ -364,7 +420,7 @@ int rdl_session_create(int device, rdl_session** out) {
   RDL_HIP_CHECK(hipSetDevice(device));
   auto s = std::make_unique<rdl_session>();
   s->device = device;
-  RDL_HIP_CHECK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+  RDL_TRY(rdl::TakeStream(device, &s->stream));
   s->home = s->stream;
   hipDeviceProp_t prop;
   RDL_HIP_CHECK(hipGetDeviceProperties(&prop, device));
@@ -379,7 +435,12 @@ int rdl_session_create(int device, rdl_session** out) {
   s->cache_on = !(cache && cache[0] == '0');
   s->trace_subminor_phases = trace && trace[0] == '1';  // 2: timing only
   RDL_HIP_CHECK(rdl::DevMalloc(&s->d_small, 1 << 16));
-  RDL_HIP_CHECK(hipMemset(s->d_small, 0, 1 << 16));  // the peak tickets start at 0
+  // the peak tickets start at 0. On the session's own stream: a synchronous
+  // hipMemset here (the null stream, once per session) made the 16-worker
+  // pool's passes 21 % slower for the rest of the process (r05's split joined
+  // regression, 4.6 -> 5.6 s; bisected in r06 to this one call)
+  RDL_HIP_CHECK(hipMemsetAsync(s->d_small, 0, 1 << 16, s->stream));
+  RDL_HIP_CHECK(hipStreamSynchronize(s->stream));
   RDL_HIP_CHECK(rdl::HostMalloc(&s->h_small, 1 << 16));
   if (rdl::ZeroCopyOn()) {  // RDL_ZERO_COPY=0: no mapped host memory at all
     RDL_HIP_CHECK(rdl::MappedMalloc(&s->m_small, &s->m_small_dev, 1 << 16));
@@ -438,10 +499,10 @@ int rdl_session_destroy(rdl_session* s) {
   if (s->h_small) (void)rdl::HostFree(s->h_small);
   if (s->m_small) (void)rdl::HostFree(s->m_small);
   if (s->comm) rdl_comm_destroy(s);
-  if (s->aux) (void)hipStreamDestroy(s->aux);
+  rdl::GiveStream(s->device, s->aux);
   if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);
   if (s->ev_join) (void)hipEventDestroy(s->ev_join);
-  (void)hipStreamDestroy(s->home);
+  rdl::GiveStream(s->device, s->home);
   delete s;
   return RDL_OK;
 }
@@ -477,8 +538,8 @@ int rdl_shutdown(void) {
     }
     if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);
     if (s->ev_join) (void)hipEventDestroy(s->ev_join);
-    if (s->aux) (void)hipStreamDestroy(s->aux);
-    (void)hipStreamDestroy(s->home);
+    rdl::GiveStream(s->device, s->aux);
+    rdl::GiveStream(s->device, s->home);
     s->ev_fork = s->ev_join = nullptr;
     s->aux = s->home = s->stream = nullptr;
     const std::lock_guard<std::mutex> clock(s->cache_mutex);
@@ -489,6 +550,7 @@ int rdl_shutdown(void) {
     // them; every destroy/free entry point is a no-op from here on)
   }
   rdl::ReleaseFftPlans();
+  rdl::DestroyStreamPools();
   // every device block, pinned and mapped host block this library holds:
   // the sessions' caches and scratch, plans' work buffers, sub-minor handles,
   // and the buffers of host objects that outlive the process's last call
@@ -517,7 +579,7 @@ int rdl_session_fork(rdl_session* s) {
   RDL_ARG_CHECK(s->lane == 0, "fork from lane 1");
   if (!s->aux) {
     RDL_HIP_CHECK(hipSetDevice(s->device));
-    RDL_HIP_CHECK(hipStreamCreateWithFlags(&s->aux, hipStreamNonBlocking));
+    RDL_TRY(rdl::TakeStream(s->device, &s->aux));
     RDL_HIP_CHECK(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
     RDL_HIP_CHECK(hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming));
   }
