@@ -680,11 +680,10 @@ def main():
             r.perform(0)
             return rd.gpu.total_iteration_number(r), time.perf_counter() - t
 
-        # split first: its 16 subimage worker sessions are then made before
-        # the 8-channel unsplit runs' allocations. Made after them (with
-        # --tiled-reference 0, the tiled leg's workers are absent), every
-        # kernel family of this leg ran 1.3x longer on the device (r06:
-        # 23.5 vs 17.9 s of kernel time, 9.0 vs 5.6 s a Perform)
+        # split first (kept so the r05-r06 lines compare): before the
+        # per-device stream pool (r06), worker sessions made after the
+        # 8-channel unsplit runs got streams bound to busier hardware queues
+        # and this leg ran 9.4 s instead of 4.6 s (DESIGN.md §5, Round-6 work)
         print("[bench] joined reference, split (warm-up + 1 step) ...", file=sys.stderr,
               flush=True)
         joined_once()
