@@ -6,7 +6,8 @@ without it).
 
     python tools/bench_legs.py joined_split,joined_split,tiled,joined_split [--reps 2]
 
-Legs: headline (8192^2 unsplit), tiled (8192^2 8x8, pool 16), joined (8 x
+Legs: headline (8192^2 unsplit), tiled (8192^2 8x8, pool 16), tiled1 (the
+same with one worker: every kernel dispatched from one thread), joined (8 x
 4096^2 unsplit), joined_split (8 x 4096^2 8x8, pool 16). Every leg runs one
 warm-up Perform, then `--reps` timed ones; per timed Perform the wall clock,
 the components, the host profile's top sections and the device time of every
@@ -51,10 +52,11 @@ def main():
         return cache[kind]
 
     def leg_once(name):
-        if name in ("headline", "tiled"):
+        if name in ("headline", "tiled", "tiled1"):
             psf, dirty = problem("single")
-            grid = 8 if name == "tiled" else 1
-            s = bench.settings_for(rd, 8192, 10 ** 9, 6, thr, grid, 16 if grid > 1 else 1)
+            grid = 1 if name == "headline" else 8
+            pool = 16 if name == "tiled" else 1  # tiled1: one worker (serial)
+            s = bench.settings_for(rd, 8192, 10 ** 9, 6, thr, grid, pool)
             arrays = (psf, dirty.copy(), np.zeros_like(dirty))
             r = rd.Radler(s, *arrays, bench.BEAM_PX * bench.PIXEL_SCALE)
         else:
