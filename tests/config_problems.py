@@ -106,6 +106,10 @@ CONFIGS = {
     # trimming before the first copy-back); `cap` components per subimage
     "p8k": dict(kind="tiled", size=8192, points=2000, blobs=200, threshold=5 * NOISE,
                 max_scales=6, grid=8, cap=300, snapshot=True, pool=16),
+    # p8k run to the threshold (no cap): the bench's tiled_n1 leg itself, its
+    # end state (component count, samples) against the oracle's
+    "p8kt": dict(kind="tiled", size=8192, points=2000, blobs=200, threshold=5 * NOISE,
+                 max_scales=6, grid=8, cap=10 ** 9, snapshot=True, pool=16),
     # t2k split 8 x 8 on the concurrent pool (snapshot schedule), run to the
     # threshold: the component count of a gridded run to threshold against the
     # unsplit run's (the 7x of bench.py's tiled_n1 leg) at a

@@ -554,18 +554,22 @@ def test_t2k8_tiled_to_threshold_component_count():
     multiscale loop to the threshold with its own countdown
     (multiscale_algorithm.cc:249, 363-373; parallel_deconvolution.cc:555-654),
     which is where bench.py's tiled_n1 inflation comes from."""
+    _tiled_to_threshold("t2k8", "unsplit t2k: 14 124")
+
+
+def _tiled_to_threshold(name, note):
     from radler_import import radler as rd
-    fx = fixture("t2k8")
-    tol, _ = end_state_tolerances("t2k8")
-    psfs, dirty = inputs("t2k8", fx)
-    _tiled("t2k8")
-    run = rd.gpu.DeviceRun(settings(rd, "t2k8"), psfs[0], dirty[0], [],
+    fx = fixture(name)
+    tol, _ = end_state_tolerances(name)
+    psfs, dirty = inputs(name, fx)
+    _tiled(name)
+    run = rd.gpu.DeviceRun(settings(rd, name), psfs[0], dirty[0], [],
                            cp.BEAM_PX * cp.PIXEL_SCALE, trace=False)
     r = run.execute()
     n_g, n_o = int(r["iterations"]), int(fx["total_iterations"])
     rel = abs(n_g - n_o) / n_o
-    print(f"t2k8: {n_g} components on the GPU, oracle {n_o} (rel {rel:.3g}, tolerance "
-          f"{tol['components']:.3g}); unsplit t2k: 14 124")
+    print(f"{name}: {n_g} components on the GPU, oracle {n_o} (rel {rel:.3g}, tolerance "
+          f"{tol['components']:.3g}); {note}")
     assert rel <= tol["components"], (n_g, n_o, rel)
     assert bool(r["another_iteration_required"]) == bool(fx["another_iteration_required"])
 
