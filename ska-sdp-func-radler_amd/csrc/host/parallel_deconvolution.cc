@@ -644,20 +644,27 @@ void ParallelDeconvolution::RunSubImagesConcurrently(
   std::vector<size_t> todo;  // the subimages this call runs, in index order
   for (size_t i = 0; i != n_sub; ++i)
     if (!run || (*run)[i]) todo.push_back(i);
-  // RADLER_POOL_QUEUE=1: workers on the main device take subimages from one
-  // queue, the costliest first (the longest-processing-time rule: the
-  // cleaning pass's estimate from the start peaks, as the ranks' LptOwners;
-  // the find-peak pass by area). Off by default: the passes are bound by the
-  // GPU's throughput over the 16 streams, not by the workers' balance, and
-  // the queue measured slower on the box (8192^2 8 x 8 tiled cleaning pass
-  // 3.20-3.25 s round-robin vs 3.33-3.40 s queued, r05). Workers on other
-  // GPUs always keep the fixed assignment (their planes are staged on the
-  // main device before the pass).
+  // The subimages' assignment to the pool's workers (on the main device):
+  //   0: fixed round robin (subimage k on worker k mod W);
+  //   1: one queue, the costliest first (the longest-processing-time rule:
+  //      the cleaning pass's estimate from the start peaks, as the ranks'
+  //      LptOwners; the find-peak pass by area);
+  //   2: one queue in index order (first free worker takes the next).
+  // Default: 1 for image sets of several images (joined channels), 0 for
+  // one image; RADLER_POOL_QUEUE overrides. Measured with the stream pool
+  // (r06, bench_legs.py, one job): 8 x 4096^2 joined split 8 x 8 — 0: 4.61-
+  // 4.63 s, 1: 3.91-4.08 s, 2: 4.15-4.38 s; 8192^2 split 8 x 8 — 0: 4.03-
+  // 4.08 s, 1: 4.17-4.23 s, 2: 4.17-4.46 s. Workers on other GPUs always
+  // keep the fixed assignment (their planes are staged on the main device
+  // before the pass). The result does not depend on the assignment (the
+  // snapshot schedule; tests/test_tiling.py::test_concurrent_pool_queue).
   const char* queue_env = std::getenv("RADLER_POOL_QUEUE");
-  bool all_local = !force_staging && queue_env && queue_env[0] == '1';
+  const int queue_mode =
+      queue_env ? std::atoi(queue_env) : (data_image.Size() > 1 ? 1 : 0);
+  bool all_local = !force_staging && (queue_mode == 1 || queue_mode == 2);
   for (size_t w = 0; w != W; ++w) all_local = all_local && workers_[w]->Device() == main_device;
   std::vector<size_t> order = todo;
-  if (all_local) {
+  if (all_local && queue_mode == 1) {
     const double thr = std::max<double>(algorithms_.front()->Threshold(), 1e-30);
     std::vector<double> cost(n_sub, 0.0);
     for (const size_t i : todo) {

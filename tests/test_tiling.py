@@ -187,3 +187,47 @@ def test_tiled_two_major_iterations(threads):
     """The worker pool and per-subimage algorithms persist across major
     iterations (iteration counts and scale state carry over)."""
     _check_tiled(1, 256, 2, 2, threads=threads, majors=2)
+
+
+@pytest.mark.gpu
+def test_joined_pool_assignment_modes_identical(monkeypatch):
+    """A joined 4-channel set split 3 x 3 on a 4-worker pool: the subimage
+    assignment (RADLER_POOL_QUEUE 0 round robin, 1 cost-ordered queue — the
+    default for image sets of several images — and 2 index-order queue) does
+    not change the result (snapshot schedule): residual, model and
+    iteration count bit-identical over two major iterations."""
+    from radler_import import radler as rd
+    from config_problems import joined_channels
+    pixel = 1.0 / 3600.0 * np.pi / 180.0
+    w = 288
+    freqs = [100e6 + 10e6 * i for i in range(4)]
+    psf, dirty = joined_channels(w, 40, 4, seed=33, frequencies=freqs)
+    outs = []
+    for mode in ("0", None, "2"):
+        if mode is None:
+            monkeypatch.delenv("RADLER_POOL_QUEUE", raising=False)
+        else:
+            monkeypatch.setenv("RADLER_POOL_QUEUE", mode)
+        s = rd.Settings()
+        s.algorithm_type = rd.AlgorithmType.multiscale
+        s.pixel_scale.x = s.pixel_scale.y = pixel
+        s.trimmed_image_width = s.trimmed_image_height = w
+        s.minor_iteration_count = 3000
+        s.absolute_threshold = 2e-3
+        s.major_loop_gain = 0.5
+        s.border_ratio = 0.0
+        s.multiscale.max_scales = 4
+        s.parallel.grid_width = s.parallel.grid_height = 3
+        s.parallel.max_threads = 4
+        res, mod = dirty.copy(), np.zeros_like(dirty)
+        r = rd.Radler(s, psf, res, mod, 2.0 * pixel, n_deconvolution_groups=4,
+                      frequencies=np.array([[f, f] for f in freqs], np.float64),
+                      weights=np.ones(4, np.float64))
+        for major in range(2):
+            r.perform(major)
+        outs.append((res.copy(), mod.copy(), r.iteration_number))
+    for o in outs[1:]:
+        assert np.array_equal(o[0], outs[0][0])
+        assert np.array_equal(o[1], outs[0][1])
+        assert o[2] == outs[0][2]
+    assert outs[0][2] > 0
